@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""bench.py — ed25519 verifies/s on MI355X for the Tendermint commit-verification hot path.
+
+Metric (BASELINE.json): "ed25519 verifies/sec at 1/8 MI355X".  Workload: configs[1],
+"Raw batch of 1M random ed25519 signatures (~120-byte canonical vote sign-bytes)
+on one MI355X" — SURVEY.md §8d C2: 1,048,576 signatures per GPU, each with its
+own key (no key reuse: the generic, worst-case path), CanonicalVote sign-bytes
+messages.  A step = one verification pass over the whole batch, inputs resident
+in HBM (host->device copies are outside the timed region; DESIGN.md gives the
+PCIe-inclusive rate).  At N GPUs every rank verifies its own 1M batch (weak
+scaling, no data-path collective); the per-rank valid counts are summed with one
+int64 all-reduce after the timed region (the tally exchange of SURVEY.md §8e).
+
+Extra JSON fields:
+  roofline      integer-VALU roofline of the verify kernel (HBM traffic ~212 B/verify
+                is negligible; MFMA has no 32x32->64 integer path): achieved
+                v_mad_i64_i32 per second = verifies/s(kernel time) x mads/verify,
+                against the measured device peak of that instruction.
+  cpu_baseline  the C restatement of Go 1.18 crypto/ed25519.Verify (oracle/ed25519_port.c,
+                "port"), single thread (the reference verifies on one goroutine), timed on
+                a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tendermint-fork_amd"))
+
+# v_mad_i64_i32 per verification of the generic (no key cache) kernel, counted from
+# its formulas (DESIGN.md "Roofline"): 64 windows x (16 sq + 27 mul) + table 64 mul +
+# decompression 255 sq + 21 mul + encoding 254 sq + 13 mul; mul = 100, sq = 55 mads;
+# + 188 mad_u64 in the mod-L reduction.
+MADS_PER_VERIFY_GENERIC = 64 * (16 * 55 + 27 * 100) + 64 * 100 + (255 * 55 + 21 * 100) + (254 * 55 + 13 * 100) + 188
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=1 << 20, help="signatures per GPU")
+    ap.add_argument("--cpu-sample", type=int, default=150_000, help="signatures timed on the CPU baseline")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-peak", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from tmed import Engine, lib
+    from tmed.workload import c2_messages, c2_seeds
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    eng = Engine(local_rank)
+    n = args.n
+
+    # ---- synthetic workload (untimed): shard [rank*n, (rank+1)*n) of the C2 stream
+    t_gen = time.time()
+    start = rank * n
+    seeds = c2_seeds(start, n)
+    msgs, offs = c2_messages(start, n)
+    d_seed = torch.from_numpy(seeds).to(dev)
+    d_msg = torch.from_numpy(np.concatenate([msgs, np.zeros(16, np.uint8)])).to(dev)
+    d_off = torch.from_numpy(offs.view(np.int32)).to(dev)
+    d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    d_pub = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    d_out = torch.zeros(n, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    eng.sign_device(d_seed, d_msg, d_off, d_sig, d_pub, n, stream)
+    torch.cuda.synchronize(dev)
+    t_gen = time.time() - t_gen
+
+    def step():
+        eng.verify_device(d_pub, d_sig, d_msg, d_off, d_out, n, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ok_first = int(d_out.sum().item())
+
+    # ---- timed region: K steps between barrier + synchronize
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record()
+        step()
+        evs[i][1].record()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    valid = int(d_out.sum().item())
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tally = torch.tensor([valid, n], dtype=torch.int64, device=dev)
+        dist.all_reduce(tally)  # int64 tally all-reduce
+        valid_all, n_all = int(tally[0].item()), int(tally[1].item())
+    else:
+        valid_all, n_all = valid, n
+    total = n_all * args.steps
+    value = total / elapsed
+
+    result = None
+    if rank == 0:
+        verifies_per_s_kernel = n / (kernel_ms * 1e-3)
+        roof = None
+        if not args.no_peak:
+            import ctypes
+            l = lib()
+            l.tmed_valu_peak.restype = ctypes.c_int
+            l.tmed_valu_peak.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+            g = ctypes.c_double(0)
+            rc = l.tmed_valu_peak(eng._h, 0, ctypes.byref(g))
+            peak = g.value / 1e3 if rc == 0 else None  # Tmad/s
+            achieved = verifies_per_s_kernel * MADS_PER_VERIFY_GENERIC / 1e12
+            roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": round(peak, 3) if peak else None,
+                    "unit": "Tmad/s (v_mad_i64_i32 lane-ops)",
+                    "frac": round(achieved / peak, 4) if peak else None,
+                    "traffic": None,
+                    "mads_per_verify": MADS_PER_VERIFY_GENERIC,
+                    "kernel_ms": round(kernel_ms, 3),
+                    "algorithmic_bytes_per_verify": 32 + 64 + int(offs[-1]) // n + 4 + 1}
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(eng, d_pub, d_sig, msgs, offs, min(args.cpu_sample, n))
+        result = {
+            "metric": "ed25519 verifies/sec at 1/8 MI355X",
+            "value": round(value, 1),
+            "unit": "verifies/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 (GF(2^255-19) radix 2^25.5 limbs, int64 accumulate)",
+            "data": "synthetic (C2: distinct key per signature, CanonicalVote sign-bytes, GPU RFC 8032 signer)",
+            "config": {"workload": "C2: raw batch of %d ed25519 signatures per GPU" % n,
+                       "signatures_per_gpu": n, "avg_msg_bytes": round(int(offs[-1]) / n, 1),
+                       "key_cache": False, "parallelism": "shard-per-gpu x%d" % world},
+            "valid": valid_all, "checked": n_all, "all_valid": valid_all == n_all and ok_first == n,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "setup_s": round(t_gen, 2),
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+    return result
+
+
+def cpu_baseline(eng, d_pub, d_sig, msgs, offs, m):
+    """Single-thread C restatement of the Go verify on the first m tuples (oracle/ed25519_port.c)."""
+    sys.path.insert(0, ROOT)
+    from oracle import port  # cpu_baseline leg only
+    pubs = d_pub[:m].cpu().numpy()
+    sigs = d_sig[:m].cpu().numpy()
+    o = offs[: m + 1].astype(np.uint64)
+    t = time.perf_counter()
+    out = port.verify_batch(pubs, sigs, msgs, o, nthreads=1)
+    dt = time.perf_counter() - t
+    ncores = os.cpu_count() or 1
+    return {"value": round(m / dt, 1), "unit": "verifies/s", "cores": 1, "kind": "port",
+            "sample": "first %d signatures of the same C2 batch, 1 thread, %.1f s; all_valid=%s; host cpu_count=%d"
+                      % (m, dt, bool(out.all()), ncores)}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,138 @@
+/*
+ * tmed25519.h — C ABI of the MI355X batch ed25519 verification engine
+ * (libtmed25519_hip.so, built from tendermint-fork_amd/csrc for gfx950).
+ *
+ * The reference (Tendermint Core v0.34.24, pure Go) has no native boundary on
+ * this path: every signature goes through the Go interface method
+ *     crypto.PubKey.VerifySignature(msg, sig []byte) bool      crypto/crypto.go:25
+ *     -> ed25519.PubKey.VerifySignature                      crypto/ed25519/ed25519.go:148-155
+ * called one at a time from the commit-verification loops
+ *     ValidatorSet.VerifyCommit                              types/validator_set.go:667-714 (call :696)
+ *     ValidatorSet.VerifyCommitLight                         types/validator_set.go:722-765 (call :752)
+ *     ValidatorSet.VerifyCommitLightTrusting                 types/validator_set.go:775-826 (call :813)
+ * This header is what a cgo shim at that seam binds: the
+ * per-signature calls of one commit (or of many commits) become ONE call that
+ * returns a validity byte per tuple, and the shim replays the reference loop
+ * over those bytes, so early exits, error values and tallies are unchanged.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no allocation is handed across the ABI.
+ *   - Return 0 on success, a negative TMED_E* code on failure.  On failure the
+ *     caller must not use out_valid (the Go shim then calls the original Go
+ *     method — never a guessed decision).  Nothing aborts or throws across the ABI.
+ *   - out_valid[i] is 1 iff Go 1.18 crypto/ed25519.Verify would return true for
+ *     (pub[i], msg[i], sig[i]) (and len(sig[i]) == 64): cofactorless, S < L
+ *     strict, permissive A decoding, byte-compared R.
+ *   - All host pointers are only read during the call (cgo pointer rules: the
+ *     library copies what it needs before returning).  A context may be shared
+ *     by concurrent callers: calls on one context are serialised internally.
+ */
+#ifndef TMED25519_H
+#define TMED25519_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TMED_OK 0
+#define TMED_EINVAL (-1)    /* bad argument (null pointer, offsets not monotone, ...) */
+#define TMED_ENODEV (-2)    /* no usable gfx950 device */
+#define TMED_EHIP (-3)      /* HIP runtime error (device lost, launch failure) */
+#define TMED_ENOMEM (-4)    /* device or pinned-host allocation failed */
+#define TMED_ENOKEYSET (-5) /* unknown key-set handle */
+
+typedef struct tmed_ctx tmed_ctx;
+
+/* Number of visible HIP devices (0 when none). */
+int tmed_device_count(void);
+
+/* Create a context bound to HIP device `device` (one process per GPU). */
+int tmed_init(int device, tmed_ctx **out);
+void tmed_destroy(tmed_ctx *ctx);
+const char *tmed_strerror(int code);
+
+/*
+ * Batch verification, host buffers.  Replaces n calls of
+ * ed25519.PubKey.VerifySignature (crypto/ed25519/ed25519.go:148-155).
+ *   pubkeys   n x 32 bytes
+ *   sigs      n x 64 bytes (slot i holds the first sig_lens[i] bytes when sig_lens != NULL)
+ *   sig_lens  NULL (all 64) or n lengths; any length != 64 is rejected
+ *             (ed25519.go:150-152) without touching the device
+ *   msgs      concatenated messages; message i is msgs[msg_off[i] .. msg_off[i+1])
+ *   msg_off   n + 1 non-decreasing offsets
+ *   out_valid n bytes, 0/1
+ */
+int tmed_verify_batch(tmed_ctx *ctx, const uint8_t *pubkeys, const uint8_t *sigs, const uint32_t *sig_lens,
+                      const uint8_t *msgs, const uint32_t *msg_off, size_t n, uint8_t *out_valid);
+
+/*
+ * Same, on device-resident buffers (all pointers are device pointers of the
+ * context's device; stream = hipStream_t or NULL for the context stream).
+ * Asynchronous: completion is ordered on `stream`.  Used when inputs already
+ * live in HBM (bench, multi-commit pipelines).
+ */
+int tmed_verify_batch_device(tmed_ctx *ctx, const uint8_t *d_pubkeys, const uint8_t *d_sigs,
+                             const uint8_t *d_msgs, const uint32_t *d_msg_off, size_t n, uint8_t *d_out_valid,
+                             void *stream);
+
+/*
+ * RFC 8032 signing (crypto/ed25519/ed25519.go:57-60 semantics) used to build
+ * synthetic commits at scale (SURVEY.md §7 "synthetic data volume").
+ * seeds n x 32, outputs sigs n x 64 and pubkeys n x 32.
+ */
+int tmed_sign_batch(tmed_ctx *ctx, const uint8_t *seeds, const uint8_t *msgs, const uint32_t *msg_off, size_t n,
+                    uint8_t *sigs_out, uint8_t *pubkeys_out);
+int tmed_sign_batch_device(tmed_ctx *ctx, const uint8_t *d_seeds, const uint8_t *d_msgs, const uint32_t *d_msg_off,
+                           size_t n, uint8_t *d_sigs_out, uint8_t *d_pubkeys_out, void *stream);
+
+/* Device time (ms) of the last verify/sign launch on this context (HIP events). */
+float tmed_last_kernel_ms(tmed_ctx *ctx);
+
+
+/* ---------------------------------------------------------------- commits */
+
+/*
+ * The per-commit part of a vote's CanonicalVote sign-bytes:
+ * everything Commit.GetVote (types/block.go:784-796) copies from the commit.
+ */
+typedef struct {
+  const char *chain_id;
+  uint32_t chain_id_len;
+  int64_t height;
+  int32_t round;
+  const uint8_t *block_hash; /* 0 or 32 bytes (ValidateHash) */
+  uint32_t block_hash_len;
+  uint32_t psh_total;
+  const uint8_t *psh_hash;   /* 0 or 32 bytes */
+  uint32_t psh_hash_len;
+} tmed_vote_template;
+
+/*
+ * Commit.VoteSignBytes(chainID, idx) for n commit signatures
+ * (types/block.go:807-810 -> types/vote.go:93-101): flags[i] in {1,2,3}
+ * (BlockIDFlag; NULL = all Commit), per-signature timestamp (seconds, nanos).
+ * Writes message i to out[out_off[i] .. out_off[i+1]) when out_cap suffices;
+ * *out_len receives the total size (call with out = NULL to size the buffer,
+ * TMED_ENOMEM when out_cap is too small).  Unknown flags -> TMED_EINVAL
+ * (the reference panics, types/block.go:663).
+ */
+int tmed_vote_sign_bytes(const tmed_vote_template *t, size_t n, const uint8_t *flags, const int64_t *ts_seconds,
+                         const int32_t *ts_nanos, uint8_t *out, size_t out_cap, uint32_t *out_off, size_t *out_len);
+
+/* --------------------------------------------------------- diagnostics */
+
+/*
+ * Integer-VALU peak probe for the roofline: runs a
+ * dependency-free stream of `kind` instructions on every lane of the device
+ * (0 = v_mad_i64_i32, 1 = v_mad_u64_u32, 2 = v_add_u32, 3 = v_mul_lo_u32)
+ * and returns the sustained rate in 1e9 instructions (lane-ops) per second.
+ */
+int tmed_valu_peak(tmed_ctx *ctx, int kind, double *giga_ops_per_s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TMED25519_H */

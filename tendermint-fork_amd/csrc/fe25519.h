@@ -1,0 +1,291 @@
+// fe25519.h — GF(2^255-19) arithmetic for the CDNA4 verify kernels.
+//
+// Replaces the field layer of Go 1.18 crypto/internal/edwards25519/field
+// (third-party to the reference; reached from crypto/ed25519/ed25519.go:154).
+//
+// Representation: 10 signed 32-bit limbs, radix 2^25.5 (limb i weighs
+// 2^ceil(25.5 i); 26 bits for even i, 25 for odd i).  Every limb product is a
+// single v_mad_i64_i32 into a 64-bit accumulator: the radix leaves enough
+// head-room that a column of 10 products (including the x19 wrap and the x2
+// odd-odd factor) never overflows int64, so no carry handling is needed inside
+// a multiplication — only one carry pass per result.
+//
+// Magnitude discipline (checked by tests/test_kernel_host.py on the host build):
+//   "carried" value: |limb| <= ~1.01 * 2^25 (even) / 2^24 (odd)  — every mul/sq output
+//   mul/sq inputs may be sums/differences of up to THREE carried values
+//   (19 * 3.03 * 2^25 < 2^31 keeps the pre-multiplied operand in int32; the
+//   column sum stays below 2^61.2).
+//
+// All functions are __host__ __device__ so that the identical code can be
+// exercised on the CPU by the test-only host build (tests/, never the product).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define TMED_HD __host__ __device__ __forceinline__
+#else
+#define TMED_HD static inline
+#endif
+
+namespace tmed {
+
+struct fe { int32_t v[10]; };
+
+TMED_HD void fe_0(fe &h) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = 0;
+}
+TMED_HD void fe_1(fe &h) { fe_0(h); h.v[0] = 1; }
+TMED_HD void fe_copy(fe &h, const fe &f) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = f.v[i];
+}
+TMED_HD void fe_add(fe &h, const fe &f, const fe &g) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = f.v[i] + g.v[i];
+}
+TMED_HD void fe_sub(fe &h, const fe &f, const fe &g) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = f.v[i] - g.v[i];
+}
+TMED_HD void fe_neg(fe &h, const fe &f) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = -f.v[i];
+}
+// h = b ? g : f   (lane-local select, no branch)
+TMED_HD void fe_select(fe &h, const fe &f, const fe &g, bool b) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = b ? g.v[i] : f.v[i];
+}
+
+// Carry pass over 64-bit column sums -> carried limbs.  Two interleaved chains
+// (0..4 and 4..9) give the scheduler independent work.
+TMED_HD void fe_carry64(fe &out, int64_t h[10]) {
+  int64_t c;
+  c = (h[0] + (int64_t)(1 << 25)) >> 26; h[1] += c; h[0] -= c * ((int64_t)1 << 26);
+  c = (h[4] + (int64_t)(1 << 25)) >> 26; h[5] += c; h[4] -= c * ((int64_t)1 << 26);
+  c = (h[1] + (int64_t)(1 << 24)) >> 25; h[2] += c; h[1] -= c * ((int64_t)1 << 25);
+  c = (h[5] + (int64_t)(1 << 24)) >> 25; h[6] += c; h[5] -= c * ((int64_t)1 << 25);
+  c = (h[2] + (int64_t)(1 << 25)) >> 26; h[3] += c; h[2] -= c * ((int64_t)1 << 26);
+  c = (h[6] + (int64_t)(1 << 25)) >> 26; h[7] += c; h[6] -= c * ((int64_t)1 << 26);
+  c = (h[3] + (int64_t)(1 << 24)) >> 25; h[4] += c; h[3] -= c * ((int64_t)1 << 25);
+  c = (h[7] + (int64_t)(1 << 24)) >> 25; h[8] += c; h[7] -= c * ((int64_t)1 << 25);
+  c = (h[4] + (int64_t)(1 << 25)) >> 26; h[5] += c; h[4] -= c * ((int64_t)1 << 26);
+  c = (h[8] + (int64_t)(1 << 25)) >> 26; h[9] += c; h[8] -= c * ((int64_t)1 << 26);
+  c = (h[9] + (int64_t)(1 << 24)) >> 25; h[0] += c * 19; h[9] -= c * ((int64_t)1 << 25);
+  c = (h[0] + (int64_t)(1 << 25)) >> 26; h[1] += c; h[0] -= c * ((int64_t)1 << 26);
+#pragma unroll
+  for (int i = 0; i < 10; i++) out.v[i] = (int32_t)h[i];
+}
+
+// Re-carry a 32-bit-limb value (e.g. a 2- or 3-sum) into carried form.
+TMED_HD void fe_carry(fe &h, const fe &f) {
+  int64_t t[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) t[i] = f.v[i];
+  fe_carry64(h, t);
+}
+
+// h = f * g  (100 v_mad_i64_i32)
+TMED_HD void fe_mul(fe &h, const fe &f, const fe &g) {
+  int32_t g19[10], f2[10];
+#pragma unroll
+  for (int j = 0; j < 10; j++) g19[j] = (int32_t)(19u * (uint32_t)g.v[j]);
+#pragma unroll
+  for (int i = 0; i < 10; i++) f2[i] = (int32_t)(2u * (uint32_t)f.v[i]);
+  int64_t acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; k++) acc[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+#pragma unroll
+    for (int j = 0; j < 10; j++) {
+      const int k = i + j;
+      const int32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+      const int32_t b = (k >= 10) ? g19[j] : g.v[j];
+      acc[k >= 10 ? k - 10 : k] += (int64_t)a * (int64_t)b;
+    }
+  }
+  fe_carry64(h, acc);
+}
+
+// Column sums of f^2 (55 products).  Pair (i,j), i<=j, carries the coefficient
+// (i<j ? 2 : 1) * (i,j odd ? 2 : 1) * (i+j>=10 ? 19 : 1); the factor 19 (and
+// its companion 2 for odd-odd pairs) is put on the odd-index operand where
+// there is one, so every pre-multiplied operand stays inside int32.
+TMED_HD void fe_sq_acc(int64_t acc[10], const fe &f) {
+  int32_t x2[10], x19[10], x38[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const uint32_t u = (uint32_t)f.v[i];
+    x2[i] = (int32_t)(2u * u); x19[i] = (int32_t)(19u * u); x38[i] = (int32_t)(38u * u);
+  }
+#pragma unroll
+  for (int k = 0; k < 10; k++) acc[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+#pragma unroll
+    for (int j = i; j < 10; j++) {
+      const int k = i + j;
+      const bool wrap = k >= 10;
+      const bool oo = (i & 1) && (j & 1);
+      const bool off = i < j;
+      // operands a (index i) and b (index j)
+      int32_t a = f.v[i], b = f.v[j];
+      if (!wrap) {
+        // coefficient: (off?2:1)*(oo?2:1)  in {1,2,4}
+        if (off && oo) { a = x2[i]; b = x2[j]; }
+        else if (off || oo) { a = x2[i]; }
+      } else {
+        // coefficient: (off?2:1)*(oo?2:1)*19 in {19,38,76}
+        if (off && oo) { a = x2[i]; b = x38[j]; }          // 76 = 2 * 38
+        else if (oo) { b = x38[j]; }                        // i == j odd: 38
+        else if (off) {                                      // 38: 19 on the odd one
+          if (j & 1) { a = x2[i]; b = x19[j]; } else { a = x19[i]; b = x2[j]; }
+        } else { b = x19[j]; }                               // i == j even: 19
+      }
+      acc[wrap ? k - 10 : k] += (int64_t)a * (int64_t)b;
+    }
+  }
+}
+
+TMED_HD void fe_sq(fe &h, const fe &f) {
+  int64_t acc[10];
+  fe_sq_acc(acc, f);
+  fe_carry64(h, acc);
+}
+
+// h = 2 f^2
+TMED_HD void fe_sq2(fe &h, const fe &f) {
+  int64_t acc[10];
+  fe_sq_acc(acc, f);
+#pragma unroll
+  for (int k = 0; k < 10; k++) acc[k] += acc[k];
+  fe_carry64(h, acc);
+}
+
+TMED_HD void fe_sqn(fe &h, const fe &f, int n) {
+  fe_sq(h, f);
+#pragma unroll 1
+  for (int i = 1; i < n; i++) fe_sq(h, h);
+}
+
+// z^(2^250 - 1) and z^11 (shared prefix of the inversion / (p-5)/8 chains)
+TMED_HD void fe_pow250(fe &z250, fe &z11, const fe &z) {
+  fe z2, z9, t, a, b, c;
+  fe_sq(z2, z);
+  fe_sqn(t, z2, 2); fe_mul(z9, t, z);
+  fe_mul(z11, z9, z2);
+  fe_sq(t, z11); fe_mul(a, t, z9);          // a = z^(2^5-1)
+  fe_sqn(t, a, 5); fe_mul(b, t, a);         // b = 2^10-1
+  fe_sqn(t, b, 10); fe_mul(c, t, b);        // c = 2^20-1
+  fe_sqn(t, c, 20); fe_mul(t, t, c);        // 2^40-1
+  fe_sqn(t, t, 10); fe_mul(a, t, b);        // a = 2^50-1
+  fe_sqn(t, a, 50); fe_mul(b, t, a);        // b = 2^100-1
+  fe_sqn(t, b, 100); fe_mul(t, t, b);       // 2^200-1
+  fe_sqn(t, t, 50); fe_mul(z250, t, a);     // 2^250-1
+}
+
+TMED_HD void fe_invert(fe &out, const fe &z) {   // z^(p-2)
+  fe z250, z11, t;
+  fe_pow250(z250, z11, z);
+  fe_sqn(t, z250, 5); fe_mul(out, t, z11);
+}
+
+TMED_HD void fe_pow22523(fe &out, const fe &z) { // z^((p-5)/8)
+  fe z250, z11, t;
+  fe_pow250(z250, z11, z);
+  fe_sqn(t, z250, 2); fe_mul(out, t, z);
+}
+
+// 32 little-endian bytes, held as 8 LE 32-bit words.  Bit 255 is ignored and
+// values >= p are accepted (reduced by the arithmetic), as Go's
+// field.Element.SetBytes.
+TMED_HD void fe_from_words(fe &h, const uint32_t w[8]) {
+  const int off[10] = {0, 26, 51, 77, 102, 128, 153, 179, 204, 230};
+  int64_t t[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const int o = off[i], q = o >> 5, r = o & 31;
+    const uint64_t lo = w[q];
+    const uint64_t hi = (q + 1 < 8) ? (uint64_t)w[q + 1] : 0;
+    const uint64_t x = ((hi << 32) | lo) >> r;
+    const uint32_t mask = (i & 1) ? 0x1ffffffu : 0x3ffffffu;
+    t[i] = (int64_t)(uint32_t)(x & mask);
+  }
+  fe_carry64(h, t);
+}
+
+// Canonical encoding (fully reduced, 0 <= value < p) as 8 LE words.
+TMED_HD void fe_to_words(uint32_t w[8], const fe &f) {
+  int32_t h[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) h[i] = f.v[i];
+  int32_t q = (19 * h[9] + (1 << 24)) >> 25;
+#pragma unroll
+  for (int i = 0; i < 10; i++) q = (h[i] + q) >> ((i & 1) ? 25 : 26);
+  h[0] += 19 * q;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int s = (i & 1) ? 25 : 26;
+    const int32_t c = h[i] >> s;
+    h[i + 1] += c;
+    h[i] -= (int32_t)((uint32_t)c << s);
+  }
+  h[9] -= (int32_t)((uint32_t)(h[9] >> 25) << 25);
+  const int off[10] = {0, 26, 51, 77, 102, 128, 153, 179, 204, 230};
+  uint64_t acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) acc[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const int o = off[i], q2 = o >> 5, r = o & 31;
+    const uint64_t x = (uint64_t)(uint32_t)h[i] << r;
+    acc[q2] |= x & 0xffffffffu;
+    if (q2 + 1 < 8) acc[q2 + 1] |= x >> 32;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = (uint32_t)acc[i];
+}
+
+TMED_HD bool fe_isnegative(const fe &f) {
+  uint32_t w[8];
+  fe_to_words(w, f);
+  return w[0] & 1;
+}
+
+TMED_HD bool fe_iszero(const fe &f) {
+  uint32_t w[8];
+  fe_to_words(w, f);
+  uint32_t a = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) a |= w[i];
+  return a == 0;
+}
+
+TMED_HD bool fe_equal(const fe &f, const fe &g) {
+  fe d;
+  fe_sub(d, f, g);
+  fe_carry(d, d);
+  return fe_iszero(d);
+}
+
+// Constants in carried form.
+TMED_HD void fe_const_d(fe &h) {
+  const int32_t c[10] = {-10913610, 13857413, -15372611, 6949391, 114729, -8787816, -6275908, -3247719, -18696448, -12055116};
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = c[i];
+}
+TMED_HD void fe_const_d2(fe &h) {
+  const int32_t c[10] = {-21827239, -5839606, -30745221, 13898782, 229458, 15978800, -12551817, -6495438, 29715968, 9444199};
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = c[i];
+}
+TMED_HD void fe_const_sqrtm1(fe &h) {
+  const int32_t c[10] = {-32595792, -7943725, 9377950, 3500415, 12389472, -272473, -25146209, -2005654, 326686, 11406482};
+#pragma unroll
+  for (int i = 0; i < 10; i++) h.v[i] = c[i];
+}
+
+}  // namespace tmed

@@ -1,0 +1,260 @@
+// tmed_capi.hip — C ABI (include/tmed25519.h) over the gfx950 kernels.
+//
+// Host runtime: one context per GPU (one process per GPU), a private HIP
+// stream, grow-only device buffers and pinned host staging buffers reused
+// across calls, and a mutex so a context can be shared by concurrent callers
+// (the reference's callers — blocksync, light client, evidence pool — run on
+// different goroutines; ValidatorSet itself is not goroutine-safe,
+// types/validator_set.go:49, so no shared mutable state crosses the seam).
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+
+#include "../../include/tmed25519.h"
+#include "kernels.h"
+
+using namespace tmed;
+
+namespace {
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes + bytes / 4 + 256;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct HostBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes + bytes / 4 + 256;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+int map_err(hipError_t e) {
+  if (e == hipSuccess) return TMED_OK;
+  if (e == hipErrorOutOfMemory) return TMED_ENOMEM;
+  return TMED_EHIP;
+}
+
+}  // namespace
+
+struct tmed_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  float last_ms = 0.f;
+  std::mutex mu;
+  ge_niels *d_btab = nullptr;
+  int4 *d_slab = nullptr;
+  uint32_t slab_slots = 0;
+  DevBuf d_a, d_b, d_msg, d_off, d_out, d_c;
+  HostBuf h_a, h_b, h_msg, h_off, h_out, h_c;
+};
+
+extern "C" {
+
+int tmed_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+const char *tmed_strerror(int code) {
+  switch (code) {
+    case TMED_OK: return "ok";
+    case TMED_EINVAL: return "invalid argument";
+    case TMED_ENODEV: return "no usable gfx950 HIP device";
+    case TMED_EHIP: return "HIP runtime error";
+    case TMED_ENOMEM: return "out of memory";
+    case TMED_ENOKEYSET: return "unknown key-set handle";
+    default: return "unknown error";
+  }
+}
+
+int tmed_init(int device, tmed_ctx **out) {
+  if (!out) return TMED_EINVAL;
+  *out = nullptr;
+  int ndev = tmed_device_count();
+  if (device < 0 || device >= ndev) return TMED_ENODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return TMED_EHIP;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return TMED_ENODEV;  // code objects are gfx950-only
+  if (hipSetDevice(device) != hipSuccess) return TMED_EHIP;
+  tmed_ctx *c = new tmed_ctx();
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  ge_niels bt[9];
+  host_build_btab(bt);
+  if (e == hipSuccess) e = hipMalloc((void **)&c->d_btab, sizeof(bt));
+  if (e == hipSuccess) e = hipMemcpy(c->d_btab, bt, sizeof(bt), hipMemcpyHostToDevice);
+  // Lane slots for the per-lane tables: 4x the resident lanes of 256 CUs at
+  // 8 waves/CU is plenty for the grid-stride loop (~377 MB of HBM).
+  c->slab_slots = 1024 * kThreadsPerBlock;
+  if (e == hipSuccess) e = hipMalloc((void **)&c->d_slab, (size_t)c->slab_slots * kSlabSlotBytes);
+  if (e != hipSuccess) {
+    tmed_destroy(c);
+    return map_err(e);
+  }
+  *out = c;
+  return TMED_OK;
+}
+
+void tmed_destroy(tmed_ctx *c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  for (DevBuf *b : {&c->d_a, &c->d_b, &c->d_msg, &c->d_off, &c->d_out, &c->d_c}) b->release();
+  for (HostBuf *b : {&c->h_a, &c->h_b, &c->h_msg, &c->h_off, &c->h_out, &c->h_c}) b->release();
+  if (c->d_slab) hipFree(c->d_slab);
+  if (c->d_btab) hipFree(c->d_btab);
+  if (c->ev0) hipEventDestroy(c->ev0);
+  if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+float tmed_last_kernel_ms(tmed_ctx *c) { return c ? c->last_ms : 0.f; }
+
+int tmed_verify_batch_device(tmed_ctx *c, const uint8_t *d_pub, const uint8_t *d_sig, const uint8_t *d_msgs,
+                             const uint32_t *d_off, size_t n, uint8_t *d_out, void *stream) {
+  if (!c) return TMED_EINVAL;
+  if (n == 0) return TMED_OK;
+  if (!d_pub || !d_sig || !d_msgs || !d_off || !d_out || n > 0xffffffffu) return TMED_EINVAL;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipSetDevice(c->device);
+  hipError_t e = launch_verify(d_pub, d_sig, d_msgs, d_off, (uint32_t)n, d_out, c->d_slab, c->slab_slots,
+                               c->d_btab, s);
+  return map_err(e);
+}
+
+int tmed_sign_batch_device(tmed_ctx *c, const uint8_t *d_seeds, const uint8_t *d_msgs, const uint32_t *d_off,
+                           size_t n, uint8_t *d_sig_out, uint8_t *d_pub_out, void *stream) {
+  if (!c) return TMED_EINVAL;
+  if (n == 0) return TMED_OK;
+  if (!d_seeds || !d_msgs || !d_off || !d_sig_out || !d_pub_out || n > 0xffffffffu) return TMED_EINVAL;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipSetDevice(c->device);
+  return map_err(launch_sign(d_seeds, d_msgs, d_off, (uint32_t)n, d_sig_out, d_pub_out, c->d_slab,
+                             c->slab_slots, c->d_btab, s));
+}
+
+static int check_offsets(const uint32_t *off, size_t n) {
+  for (size_t i = 0; i < n; i++)
+    if (off[i + 1] < off[i]) return TMED_EINVAL;
+  return TMED_OK;
+}
+
+int tmed_verify_batch(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, const uint32_t *sig_lens,
+                      const uint8_t *msgs, const uint32_t *off, size_t n, uint8_t *out) {
+  if (!c || !out) return TMED_EINVAL;
+  if (n == 0) return TMED_OK;
+  if (!pub || !sig || !off || n > 0xffffffffu) return TMED_EINVAL;
+  if (check_offsets(off, n) != TMED_OK) return TMED_EINVAL;
+  const size_t mbytes = off[n];
+  if (mbytes && !msgs) return TMED_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  hipSetDevice(c->device);
+  hipError_t e = hipSuccess;
+  const size_t moff_bytes = (n + 1) * 4;
+  for (auto &pr : {std::make_pair(&c->d_a, n * 32), std::make_pair(&c->d_b, n * 64),
+                   std::make_pair(&c->d_msg, mbytes + 16), std::make_pair(&c->d_off, moff_bytes),
+                   std::make_pair(&c->d_out, n)})
+    if (e == hipSuccess) e = pr.first->ensure(pr.second);
+  for (auto &pr : {std::make_pair(&c->h_a, n * 32), std::make_pair(&c->h_b, n * 64),
+                   std::make_pair(&c->h_msg, mbytes + 16), std::make_pair(&c->h_off, moff_bytes),
+                   std::make_pair(&c->h_out, n)})
+    if (e == hipSuccess) e = pr.first->ensure(pr.second);
+  if (e != hipSuccess) return map_err(e);
+  // Stage into pinned memory (the caller's buffers may be GC-managed Go memory).
+  memcpy(c->h_a.p, pub, n * 32);
+  memcpy(c->h_b.p, sig, n * 64);
+  if (mbytes) memcpy(c->h_msg.p, msgs, mbytes);
+  memcpy(c->h_off.p, off, moff_bytes);
+  hipStream_t s = c->stream;
+  e = hipMemcpyAsync(c->d_a.p, c->h_a.p, n * 32, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->d_b.p, c->h_b.p, n * 64, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && mbytes) e = hipMemcpyAsync(c->d_msg.p, c->h_msg.p, mbytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->d_off.p, c->h_off.p, moff_bytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipEventRecord(c->ev0, s);
+  if (e == hipSuccess)
+    e = launch_verify((const uint8_t *)c->d_a.p, (const uint8_t *)c->d_b.p, (const uint8_t *)c->d_msg.p,
+                      (const uint32_t *)c->d_off.p, (uint32_t)n, (uint8_t *)c->d_out.p, c->d_slab, c->slab_slots,
+                      c->d_btab, s);
+  if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, n, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return map_err(e);
+  hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
+  memcpy(out, c->h_out.p, n);
+  if (sig_lens)
+    for (size_t i = 0; i < n; i++)
+      if (sig_lens[i] != 64) out[i] = 0;  // crypto/ed25519/ed25519.go:150-152
+  return TMED_OK;
+}
+
+int tmed_sign_batch(tmed_ctx *c, const uint8_t *seeds, const uint8_t *msgs, const uint32_t *off, size_t n,
+                    uint8_t *sigs_out, uint8_t *pubs_out) {
+  if (!c || !sigs_out || !pubs_out) return TMED_EINVAL;
+  if (n == 0) return TMED_OK;
+  if (!seeds || !off || n > 0xffffffffu) return TMED_EINVAL;
+  if (check_offsets(off, n) != TMED_OK) return TMED_EINVAL;
+  const size_t mbytes = off[n];
+  if (mbytes && !msgs) return TMED_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  hipSetDevice(c->device);
+  hipError_t e = hipSuccess;
+  const size_t moff_bytes = (n + 1) * 4;
+  for (auto &pr : {std::make_pair(&c->d_a, n * 32), std::make_pair(&c->d_b, n * 64),
+                   std::make_pair(&c->d_msg, mbytes + 16), std::make_pair(&c->d_off, moff_bytes),
+                   std::make_pair(&c->d_c, n * 32)})
+    if (e == hipSuccess) e = pr.first->ensure(pr.second);
+  if (e != hipSuccess) return map_err(e);
+  hipStream_t s = c->stream;
+  e = hipMemcpyAsync(c->d_a.p, seeds, n * 32, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && mbytes) e = hipMemcpyAsync(c->d_msg.p, msgs, mbytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->d_off.p, off, moff_bytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipEventRecord(c->ev0, s);
+  if (e == hipSuccess)
+    e = launch_sign((const uint8_t *)c->d_a.p, (const uint8_t *)c->d_msg.p, (const uint32_t *)c->d_off.p,
+                    (uint32_t)n, (uint8_t *)c->d_b.p, (uint8_t *)c->d_c.p, c->d_slab, c->slab_slots, c->d_btab, s);
+  if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(sigs_out, c->d_b.p, n * 64, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(pubs_out, c->d_c.p, n * 32, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return map_err(e);
+  hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
+  return TMED_OK;
+}
+
+}  // extern "C"

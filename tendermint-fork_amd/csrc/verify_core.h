@@ -1,0 +1,208 @@
+// verify_core.h — one ed25519 verification (or signature) per lane.
+//
+// Restates, for the GPU, the decision procedure of the reference's hot path:
+//   crypto/ed25519/ed25519.go:148-155 PubKey.VerifySignature
+//   -> golang.org/x/crypto v0.1.0 (go.mod:44) -> Go 1.18 crypto/ed25519.Verify
+// (SURVEY.md §8a row V0):
+//   sig[63] & 0xE0 -> reject; A = SetBytes(pub) (permissive); k = SHA-512(R||A||M) mod L;
+//   S >= L -> reject; R' = [k](-A) + [S]B (cofactorless); accept iff enc(R') == R bytes.
+// (len(sig) != 64 is decided on the host, before a tuple reaches the device.)
+//
+// SIMT shape: the double-scalar multiplication is a Straus interleave with
+// FIXED signed radix-16 windows for both scalars (64 windows: 4 doublings, one
+// cached add from the per-lane table of -A, one niels add from the shared B
+// table).  Unlike the reference's wNAF (whose data-dependent add positions
+// would make every lane of a 64-wide wave pay for every other lane's adds),
+// every lane runs exactly the same instruction stream; digit 0 adds the
+// identity, which the complete formulas handle exactly.
+#pragma once
+#include "ge25519.h"
+#include "sc25519.h"
+#include "sha512.h"
+
+namespace tmed {
+
+// Per-lane variable-base table access.  T must provide
+//   void store(int j, const ge_cached&)  and  void load(int j, ge_cached&)
+// for j in [0, 8] (j = 0 is the identity).  The device implementation lives in a
+// global-memory slab (per-lane tables are 1.4 KB: too large for LDS at useful
+// occupancy); the host test build uses a local array.
+template <class T>
+TMED_HD void build_table_negA(T &tab, const ge_p3 &A) {
+  ge_p3 nA;  // -A
+  fe_neg(nA.X, A.X); fe_copy(nA.Y, A.Y); fe_copy(nA.Z, A.Z); fe_neg(nA.T, A.T);
+  ge_cached c, c1;
+  ge_cached_0(c);
+  tab.store(0, c);
+  ge_p3_to_cached(c1, nA);
+  tab.store(1, c1);
+  ge_p3 cur = nA;
+  ge_p1p1 t;
+#pragma unroll 1
+  for (int j = 2; j <= 8; j++) {
+    ge_add_cached(t, cur, c1, false);
+    ge_p1p1_to_p3(cur, t);
+    ge_p3_to_cached(c, cur);
+    tab.store(j, c);
+  }
+}
+
+// out = [k](-A) + [S]B  using the per-lane table of (-A) multiples and the
+// shared niels table of B multiples.
+template <class T, class BT>
+TMED_HD void double_scalarmult(ge_p2 &out, const uint32_t k[8], const uint32_t s[8], T &tab, const BT &btab) {
+  uint32_t kr[8], sr[8];
+  sc_recode16(kr, k);
+  sc_recode16(sr, s);
+  ge_p2 q;
+  ge_p2_0(q);
+  ge_p1p1 t;
+  ge_p3 r;
+#pragma unroll 1
+  for (int j = 0; j < 8; j++) {
+    uint32_t kc = kr[7], sc = sr[7];
+#pragma unroll
+    for (int m = 7; m > 0; m--) { kr[m] = kr[m - 1]; sr[m] = sr[m - 1]; }
+#pragma unroll 1
+    for (int i = 0; i < 8; i++) {
+      const int da = (int)(kc >> 28) - 8;
+      const int db = (int)(sc >> 28) - 8;
+      kc <<= 4;
+      sc <<= 4;
+      // q = 16 * q
+#pragma unroll 1
+      for (int d = 0; d < 3; d++) {
+        ge_p2_dbl(t, q);
+        ge_p1p1_to_p2(q, t);
+      }
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p3(r, t);
+      // + da * (-A)
+      ge_cached ca;
+      tab.load(da < 0 ? -da : da, ca);
+      ge_add_cached(t, r, ca, da < 0);
+      ge_p1p1_to_p3(r, t);
+      // + db * B
+      ge_niels nb;
+      btab.load(db < 0 ? -db : db, nb);
+      ge_madd_niels(t, r, nb, db < 0);
+      ge_p1p1_to_p2(q, t);
+    }
+  }
+  out = q;
+}
+
+// Load 8 LE 32-bit words from 32 bytes.
+TMED_HD void load_words8(uint32_t w[8], const uint8_t *p) {
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    w[i] = (uint32_t)p[4 * i] | ((uint32_t)p[4 * i + 1] << 8) | ((uint32_t)p[4 * i + 2] << 16) |
+           ((uint32_t)p[4 * i + 3] << 24);
+}
+
+// One verification.  pubw: 8 words of A; sigw: 16 words (R = 0..7, S = 8..15).
+template <class T, class BT>
+TMED_HD bool verify_one(const uint32_t pubw[8], const uint32_t sigw[16], const uint8_t *msg, uint32_t mlen,
+                        T &tab, const BT &btab) {
+  bool ok = (sigw[15] & 0xE0000000u) == 0;        // sig[63] & 0xE0
+  const uint32_t *S = sigw + 8;
+  ok = ok && sc_is_canonical(S);                  // Scalar.SetCanonicalBytes
+  ge_p3 A;
+  ok = ge_frombytes_go(A, pubw) && ok;            // Point.SetBytes (identity on failure)
+  uint32_t h[16], k[8];
+  sha512_stream(h, sigw, pubw, 64, msg, mlen);     // SHA-512(R || A || M)
+  sc_reduce512(k, h);                              // Scalar.SetUniformBytes
+  uint32_t s[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = ok ? S[i] : 0u;  // keep S < 2^255 for the recoding
+  build_table_negA(tab, A);
+  ge_p2 R;
+  double_scalarmult(R, k, s, tab, btab);
+  uint32_t enc[8];
+  ge_tobytes(enc, R.X, R.Y, R.Z);
+  uint32_t diff = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) diff |= enc[i] ^ sigw[i];
+  return ok && diff == 0;
+}
+
+// [s]B for s < 2^255 via the same window schedule (k = 0 uses the identity
+// table; used by the signer and key generation only).
+template <class T, class BT>
+TMED_HD void scalarmult_base(uint32_t enc[8], const uint32_t s[8], T &tab, const BT &btab) {
+  uint32_t zero[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) zero[i] = 0;
+  ge_p3 id;
+  ge_p3_0(id);
+  build_table_negA(tab, id);
+  ge_p2 R;
+  double_scalarmult(R, zero, s, tab, btab);
+  ge_tobytes(enc, R.X, R.Y, R.Z);
+}
+
+// RFC 8032 signing (crypto/ed25519/ed25519.go:57-60 -> Go ed25519.Sign):
+//   h = SHA-512(seed); a = clamp(h[0:32]) mod L; A = [a]B;
+//   r = SHA-512(h[32:64] || M) mod L; R = [r]B; k = SHA-512(R || A || M) mod L; S = r + k a.
+template <class T, class BT>
+TMED_HD void sign_one(uint32_t sig[16], uint32_t pub[8], const uint32_t seed[8], const uint8_t *msg,
+                      uint32_t mlen, T &tab, const BT &btab) {
+  uint32_t h[16], zero[8], a[8], x[16], r[8], k[8], s[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) zero[i] = 0;
+  sha512_stream(h, seed, zero, 32, msg, 0);
+  h[0] &= 0xfffffff8u;
+  h[7] &= 0x7fffffffu;
+  h[7] |= 0x40000000u;
+#pragma unroll
+  for (int i = 0; i < 16; i++) x[i] = i < 8 ? h[i] : 0u;
+  sc_reduce512(a, x);
+  scalarmult_base(pub, a, tab, btab);
+  uint32_t prefix[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) prefix[i] = h[8 + i];
+  sha512_stream(x, prefix, zero, 32, msg, mlen);
+  sc_reduce512(r, x);
+  scalarmult_base(sig, r, tab, btab);
+  sha512_stream(x, sig, pub, 64, msg, mlen);
+  sc_reduce512(k, x);
+  sc_muladd(s, k, a, r);
+#pragma unroll
+  for (int i = 0; i < 8; i++) sig[8 + i] = s[i];
+}
+
+// Host-side construction of the shared B table (j*B, j = 0..8, niels form),
+// using the same field code.  Run once per context.
+TMED_HD void build_btab_niels(ge_niels out[9]) {
+  // B = (x, 4/5), x even
+  uint32_t byw[8];
+  const uint8_t by[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
+                          0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
+                          0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
+  load_words8(byw, by);
+  ge_p3 B;
+  ge_frombytes_go(B, byw);
+  ge_niels_0(out[0]);
+  ge_p3 cur = B;
+  ge_cached cb;
+  ge_p3_to_cached(cb, B);
+  ge_p1p1 t;
+  fe d2;
+  fe_const_d2(d2);
+  for (int j = 1; j <= 8; j++) {
+    if (j > 1) {
+      ge_add_cached(t, cur, cb, false);
+      ge_p1p1_to_p3(cur, t);
+    }
+    fe zi, x, y, xy;
+    fe_invert(zi, cur.Z);
+    fe_mul(x, cur.X, zi);
+    fe_mul(y, cur.Y, zi);
+    fe_add(out[j].YpX, y, x); fe_carry(out[j].YpX, out[j].YpX);
+    fe_sub(out[j].YmX, y, x); fe_carry(out[j].YmX, out[j].YmX);
+    fe_mul(xy, x, y);
+    fe_mul(out[j].XY2d, xy, d2);
+  }
+}
+
+}  // namespace tmed

@@ -1,0 +1,68 @@
+"""Loader for the gfx950 engine library (libtmed25519_hip.so) — fails loudly.
+
+There is no CPU fallback in the product: if the library is missing, or no
+gfx950 device is present, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libtmed25519_hip.so")
+
+TMED_OK = 0
+TMED_EINVAL = -1
+TMED_ENODEV = -2
+TMED_EHIP = -3
+TMED_ENOMEM = -4
+TMED_ENOKEYSET = -5
+
+_lib = None
+
+
+class TmedError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        msg = lib().tmed_strerror(code).decode() if _lib is not None else str(code)
+        super().__init__("%s: %s (code %d)" % (what or "tmed", msg, code))
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("tmed: %s is missing — run __graft_entry__.build() (hipcc --offload-arch=gfx950); "
+                          "there is no CPU fallback" % LIB_PATH)
+    l = ctypes.CDLL(LIB_PATH)
+    P, SZ, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    l.tmed_device_count.restype = I
+    l.tmed_device_count.argtypes = []
+    l.tmed_init.restype = I
+    l.tmed_init.argtypes = [I, ctypes.POINTER(P)]
+    l.tmed_destroy.restype = None
+    l.tmed_destroy.argtypes = [P]
+    l.tmed_strerror.restype = ctypes.c_char_p
+    l.tmed_strerror.argtypes = [I]
+    l.tmed_verify_batch.restype = I
+    l.tmed_verify_batch.argtypes = [P, P, P, P, P, P, SZ, P]
+    l.tmed_verify_batch_device.restype = I
+    l.tmed_verify_batch_device.argtypes = [P, P, P, P, P, SZ, P, P]
+    l.tmed_sign_batch.restype = I
+    l.tmed_sign_batch.argtypes = [P, P, P, P, SZ, P, P]
+    l.tmed_sign_batch_device.restype = I
+    l.tmed_sign_batch_device.argtypes = [P, P, P, P, SZ, P, P, P]
+    l.tmed_last_kernel_ms.restype = ctypes.c_float
+    l.tmed_last_kernel_ms.argtypes = [P]
+    _lib = l
+    return l
+
+
+# Every symbol include/tmed25519.h declares (checked by the CPU test suite).
+EXPORTED_SYMBOLS = [
+    "tmed_device_count", "tmed_init", "tmed_destroy", "tmed_strerror",
+    "tmed_verify_batch", "tmed_verify_batch_device",
+    "tmed_sign_batch", "tmed_sign_batch_device", "tmed_last_kernel_ms",
+    "tmed_vote_sign_bytes", "tmed_valu_peak",
+]

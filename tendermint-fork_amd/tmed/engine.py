@@ -1,0 +1,121 @@
+"""Host-side handle on one GPU: batch verify / sign through the C ABI.
+
+Mirrors the per-signature contract of ``ed25519.PubKey.VerifySignature``
+(reference ``crypto/ed25519/ed25519.go:148-155``) for whole batches: each
+output byte is exactly the bool the reference would return.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import numpy as np
+
+from ._native import TMED_OK, TmedError, lib
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def pack_messages(msgs: Sequence[bytes]):
+    """Concatenate messages -> (flat u8 array, u32 offsets[n+1])."""
+    lens = np.fromiter((len(m) for m in msgs), dtype=np.int64, count=len(msgs))
+    off = np.zeros(len(msgs) + 1, dtype=np.int64)
+    np.cumsum(lens, out=off[1:])
+    if off[-1] >= 2**32:
+        raise ValueError("message batch exceeds 4 GiB")
+    flat = np.frombuffer(b"".join(msgs), dtype=np.uint8) if off[-1] else np.zeros(1, np.uint8)
+    return flat, off.astype(np.uint32)
+
+
+class Engine:
+    """One context on one HIP device (one process per GPU)."""
+
+    def __init__(self, device: int = 0):
+        l = lib()
+        if l.tmed_device_count() <= device:
+            raise TmedError(-2, "tmed_init(device=%d)" % device)
+        h = ctypes.c_void_p()
+        rc = l.tmed_init(device, ctypes.byref(h))
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_init(device=%d)" % device)
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().tmed_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- host buffers -------------------------------------------------------
+    def verify_arrays(self, pubs: np.ndarray, sigs: np.ndarray, msgs: np.ndarray, offs: np.ndarray,
+                      sig_lens: np.ndarray | None = None) -> np.ndarray:
+        n = pubs.shape[0]
+        out = np.zeros(n, dtype=np.uint8)
+        if n == 0:
+            return out
+        pubs = np.ascontiguousarray(pubs, dtype=np.uint8).reshape(n, 32)
+        sigs = np.ascontiguousarray(sigs, dtype=np.uint8).reshape(n, 64)
+        msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint32)
+        sl = None if sig_lens is None else np.ascontiguousarray(sig_lens, dtype=np.uint32)
+        rc = lib().tmed_verify_batch(self._h, _p(pubs), _p(sigs), None if sl is None else _p(sl), _p(msgs),
+                                     _p(offs), n, _p(out))
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_verify_batch")
+        return out
+
+    def verify_batch(self, pubs: Sequence[bytes], msgs: Sequence[bytes], sigs: Sequence[bytes]) -> np.ndarray:
+        """Decisions for (pub[i], msg[i], sig[i]); sigs of any length (len != 64 -> 0)."""
+        n = len(pubs)
+        pa = np.zeros((n, 32), np.uint8)
+        sa = np.zeros((n, 64), np.uint8)
+        sl = np.zeros(n, np.uint32)
+        for i in range(n):
+            if len(pubs[i]) != 32:
+                raise ValueError("ed25519: bad public key length %d" % len(pubs[i]))  # Go panics here
+            pa[i] = np.frombuffer(pubs[i], np.uint8)
+            s = sigs[i][:64]
+            sa[i, :len(s)] = np.frombuffer(s, np.uint8) if s else 0
+            sl[i] = len(sigs[i])
+        flat, off = pack_messages(list(msgs))
+        return self.verify_arrays(pa, sa, flat, off, sl)
+
+    def sign_arrays(self, seeds: np.ndarray, msgs: np.ndarray, offs: np.ndarray):
+        n = seeds.shape[0]
+        sigs = np.zeros((n, 64), np.uint8)
+        pubs = np.zeros((n, 32), np.uint8)
+        if n == 0:
+            return sigs, pubs
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint8)
+        msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint32)
+        rc = lib().tmed_sign_batch(self._h, _p(seeds), _p(msgs), _p(offs), n, _p(sigs), _p(pubs))
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_sign_batch")
+        return sigs, pubs
+
+    # ---- device-resident (torch tensors on this device) ----------------------
+    def verify_device(self, d_pub, d_sig, d_msg, d_off, d_out, n: int, stream=None) -> None:
+        s = ctypes.c_void_p(stream) if stream else None
+        rc = lib().tmed_verify_batch_device(self._h, d_pub.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
+                                            d_off.data_ptr(), n, d_out.data_ptr(), s)
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_verify_batch_device")
+
+    def sign_device(self, d_seed, d_msg, d_off, d_sig_out, d_pub_out, n: int, stream=None) -> None:
+        s = ctypes.c_void_p(stream) if stream else None
+        rc = lib().tmed_sign_batch_device(self._h, d_seed.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(), n,
+                                          d_sig_out.data_ptr(), d_pub_out.data_ptr(), s)
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_sign_batch_device")
+
+    def last_kernel_ms(self) -> float:
+        return float(lib().tmed_last_kernel_ms(self._h))

@@ -1,0 +1,40 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "tendermint-fork_amd")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) device")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+@pytest.fixture(scope="session")
+def hostsim():
+    """TEST-ONLY CPU build of the kernel source (tests/native/hostsim.cpp)."""
+    import ctypes
+    d = os.path.join(ROOT, "tests", "native")
+    subprocess.check_call(["make", "-s", "-C", d])
+    return ctypes.CDLL(os.path.join(d, "libhostsim.so"))
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "ed25519_vectors.json")) as f:
+        return json.load(f)["vectors"]
+
+
+@pytest.fixture(scope="session")
+def engine():
+    from tmed import Engine
+    e = Engine(0)
+    yield e
+    e.close()

@@ -1,0 +1,108 @@
+// hostsim.cpp — TEST-ONLY host build of the device verify/sign code.
+//
+// Compiles tendermint-fork_amd/csrc/verify_core.h (the exact source the HIP
+// kernels run) for the CPU with g++, so that the kernel arithmetic can be
+// checked against the oracle in a container without a GPU.  Never part of the
+// product: the product library (libtmed25519_hip.so) has no CPU path.
+#include <stdint.h>
+#include <string.h>
+#include "verify_core.h"
+
+using namespace tmed;
+
+namespace {
+struct HostTab {
+  ge_cached e[9];
+  void store(int j, const ge_cached &c) { e[j] = c; }
+  void load(int j, ge_cached &c) const { c = e[j]; }
+};
+struct HostBTab {
+  ge_niels e[9];
+  void load(int j, ge_niels &n) const { n = e[j]; }
+};
+HostBTab &btab() {
+  static HostBTab t;
+  static bool init = false;
+  if (!init) { build_btab_niels(t.e); init = true; }
+  return t;
+}
+}  // namespace
+
+extern "C" {
+
+void hostsim_verify_batch(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
+                          size_t n, uint8_t *out) {
+  HostBTab &bt = btab();
+#pragma omp parallel for schedule(dynamic, 16)
+  for (long i = 0; i < (long)n; i++) {
+    HostTab tab;
+    uint32_t pw[8], sw[16];
+    load_words8(pw, pub + 32 * i);
+    load_words8(sw, sig + 64 * i);
+    load_words8(sw + 8, sig + 64 * i + 32);
+    out[i] = verify_one(pw, sw, msgs + off[i], off[i + 1] - off[i], tab, bt) ? 1 : 0;
+  }
+}
+
+void hostsim_sign_batch(const uint8_t *seeds, const uint8_t *msgs, const uint32_t *off, size_t n,
+                        uint8_t *sig_out, uint8_t *pub_out) {
+  HostBTab &bt = btab();
+#pragma omp parallel for schedule(dynamic, 16)
+  for (long i = 0; i < (long)n; i++) {
+    HostTab tab;
+    uint32_t seed[8], sg[16], pb[8];
+    load_words8(seed, seeds + 32 * i);
+    sign_one(sg, pb, seed, msgs + off[i], off[i + 1] - off[i], tab, bt);
+    for (int w = 0; w < 16; w++) for (int b = 0; b < 4; b++) sig_out[64 * i + 4 * w + b] = (uint8_t)(sg[w] >> (8 * b));
+    for (int w = 0; w < 8; w++) for (int b = 0; b < 4; b++) pub_out[32 * i + 4 * w + b] = (uint8_t)(pb[w] >> (8 * b));
+  }
+}
+
+// Field-level probes: inputs/outputs are 32-byte LE encodings.
+static void to_bytes(uint8_t *o, const uint32_t w[8]) { for (int i = 0; i < 32; i++) o[i] = (uint8_t)(w[i / 4] >> (8 * (i % 4))); }
+
+void hostsim_fe_op(int op, const uint8_t *a, const uint8_t *b, uint8_t *out) {
+  uint32_t wa[8], wb[8], wo[8];
+  load_words8(wa, a); load_words8(wb, b);
+  fe fa, fb, fo;
+  fe_from_words(fa, wa); fe_from_words(fb, wb);
+  switch (op) {
+    case 0: fe_mul(fo, fa, fb); break;
+    case 1: fe_sq(fo, fa); break;
+    case 2: fe_invert(fo, fa); break;
+    case 3: fe_pow22523(fo, fa); break;
+    case 4: fe_add(fo, fa, fb); fe_carry(fo, fo); break;
+    case 5: fe_sub(fo, fa, fb); fe_carry(fo, fo); break;
+    case 6: fe_sq2(fo, fa); break;
+    case 7: { fe t; fe_add(t, fa, fb); fe_add(t, t, fa); fe_mul(fo, t, t); break; }  // 3-sum input
+    case 8: { fe t; fe_add(t, fa, fb); fe_add(t, t, fa); fe_sq(fo, t); break; }
+    default: fe_copy(fo, fa);
+  }
+  fe_to_words(wo, fo);
+  to_bytes(out, wo);
+}
+
+int hostsim_decode(const uint8_t *p, uint8_t *out_enc) {
+  uint32_t w[8], e[8];
+  load_words8(w, p);
+  ge_p3 A;
+  bool ok = ge_frombytes_go(A, w);
+  ge_tobytes(e, A.X, A.Y, A.Z);
+  to_bytes(out_enc, e);
+  return ok ? 1 : 0;
+}
+
+void hostsim_sha512(const uint8_t *m, uint32_t n, uint8_t *out) {
+  uint32_t z[8] = {0}, h[16];
+  sha512_stream(h, z, z, 0, m, n);
+  for (int i = 0; i < 64; i++) out[i] = (uint8_t)(h[i / 4] >> (8 * (i % 4)));
+}
+
+void hostsim_sc_reduce(const uint8_t *h64, uint8_t *out) {
+  uint32_t x[16], r[8];
+  for (int i = 0; i < 16; i++) x[i] = (uint32_t)h64[4 * i] | ((uint32_t)h64[4 * i + 1] << 8) | ((uint32_t)h64[4 * i + 2] << 16) | ((uint32_t)h64[4 * i + 3] << 24);
+  sc_reduce512(r, x);
+  to_bytes(out, r);
+}
+
+}  // extern "C"

@@ -1,0 +1,122 @@
+"""GPU parity: the gfx950 kernels through the C ABI vs the oracle (bit-exact decisions)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import ed25519_go as E
+from oracle import port
+
+pytestmark = pytest.mark.gpu
+
+
+def test_golden_vectors(engine, golden):
+    pubs = [bytes.fromhex(v["pub"]) for v in golden]
+    msgs = [bytes.fromhex(v["msg"]) for v in golden]
+    sigs = [bytes.fromhex(v["sig"]) for v in golden]
+    out = engine.verify_batch(pubs, msgs, sigs)
+    exp = np.array([v["valid"] for v in golden], np.uint8)
+    bad = [golden[i]["class"] for i in np.nonzero(out != exp)[0]]
+    assert not bad, bad
+    assert exp.sum() > 600 and (exp == 0).sum() > 500
+
+
+def _random_batch(n, seed, mlen=(0, 300)):
+    rng = np.random.default_rng(seed)
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    lens = rng.integers(mlen[0], mlen[1], n)
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    msgs = rng.integers(0, 256, int(offs[-1]) + 16, dtype=np.uint8)
+    return rng, seeds, msgs, offs
+
+
+def test_sign_kernel_matches_oracle(engine):
+    rng, seeds, msgs, offs = _random_batch(3000, 1)
+    sigs, pubs = engine.sign_arrays(seeds, msgs, offs.astype(np.uint32))
+    esig, epub = port.sign_batch(seeds, msgs, offs, 8)
+    assert (sigs == esig).all() and (pubs == epub).all()
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 257, 1000])
+def test_batch_sizes(engine, n):
+    rng, seeds, msgs, offs = _random_batch(n, 100 + n)
+    sigs, pubs = port.sign_batch(seeds, msgs, offs, 8)
+    sigs[::3, 5] ^= 0x10
+    out = engine.verify_arrays(pubs, sigs, msgs, offs.astype(np.uint32))
+    exp = port.verify_batch(pubs, sigs, msgs, offs, 8)
+    assert (out == exp).all()
+
+
+def test_c5_adversarial_mix(engine):
+    """C5: 1% invalid / non-canonical / small-order edge cases mixed into a valid batch (seed 0x5EED)."""
+    n = 100_000
+    rng, seeds, msgs, offs = _random_batch(n, 0x5EED, (100, 130))
+    sigs, pubs = engine.sign_arrays(seeds, msgs, offs.astype(np.uint32))
+    idx = rng.choice(n, n // 100, replace=False)
+    small = [E.encode(p) for p in E.small_order_points()]
+    for j, i in enumerate(idx):
+        k = j % 6
+        if k == 0:
+            sigs[i, rng.integers(0, 64)] ^= 1 << rng.integers(0, 8)       # bit flip
+        elif k == 1:
+            S = int.from_bytes(sigs[i, 32:].tobytes(), "little") + E.L   # S + L
+            sigs[i, 32:] = np.frombuffer(S.to_bytes(32, "little"), np.uint8)
+        elif k == 2:
+            pubs[i] = np.frombuffer(small[j % 8], np.uint8)               # small-order A
+        elif k == 3:
+            sigs[i, :32] = np.frombuffer(small[j % 8], np.uint8)          # small-order R
+        elif k == 4:
+            y = (int(rng.integers(0, 19)) + E.P).to_bytes(32, "little")   # non-canonical A (y >= p)
+            pubs[i] = np.frombuffer(y, np.uint8)
+        else:
+            sigs[i, 31] ^= 0x80                                            # R sign flip
+    out = engine.verify_arrays(pubs, sigs, msgs, offs.astype(np.uint32))
+    exp = port.verify_batch(pubs, sigs, msgs, offs, 16)
+    assert int((out != exp).sum()) == 0
+    assert exp.sum() <= n - len(idx) + 16
+
+
+def test_full_size_property(engine):
+    """BASELINE size (1,048,576): GPU-signed batch verifies all-valid; a bit flip in every
+    signature flips every decision (size-independent property); a sample is checked by the port."""
+    import torch
+    from tmed.workload import c2_messages, c2_seeds
+    n = 1 << 20
+    seeds = c2_seeds(0, n)
+    msgs, offs = c2_messages(0, n)
+    dev = torch.device("cuda", 0)
+    d_seed = torch.from_numpy(seeds).to(dev)
+    d_msg = torch.from_numpy(np.concatenate([msgs, np.zeros(16, np.uint8)])).to(dev)
+    d_off = torch.from_numpy(offs.view(np.int32)).to(dev)
+    d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    d_pub = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    d_out = torch.zeros(n, dtype=torch.uint8, device=dev)
+    engine.sign_device(d_seed, d_msg, d_off, d_sig, d_pub, n)
+    engine.verify_device(d_pub, d_sig, d_msg, d_off, d_out, n)
+    torch.cuda.synchronize()
+    assert int(d_out.sum().item()) == n
+    d_sig[:, 40] ^= 1
+    engine.verify_device(d_pub, d_sig, d_msg, d_off, d_out, n)
+    torch.cuda.synchronize()
+    assert int(d_out.sum().item()) == 0
+    d_sig[:, 40] ^= 1
+    m = 4096
+    sl = slice(n - m, n)
+    exp = port.verify_batch(d_pub[sl].cpu().numpy(), d_sig[sl].cpu().numpy(), msgs,
+                            offs[n - m:].astype(np.uint64), 16)
+    assert exp.all()
+    assert d_sig[sl].cpu().numpy().tobytes() == port.sign_batch(seeds[n - m:], msgs, offs[n - m:].astype(np.uint64), 16)[0].tobytes()
+
+
+def test_product_signbytes_match_oracle():
+    from oracle.signbytes import vote_sign_bytes as ovsb
+    from tmed.signbytes import vote_sign_bytes as pvsb
+    rng = np.random.default_rng(4)
+    for i in range(300):
+        bid = None if i % 5 == 0 else (rng.bytes(32), int(rng.integers(0, 2**32)), rng.bytes(32))
+        ts = (int(rng.integers(-2**40, 2**40)), int(rng.integers(0, 10**9)))
+        h, r = int(rng.integers(0, 2**62)), int(rng.integers(-2**31, 2**31))
+        cid = "c" * int(rng.integers(0, 51))
+        flag = 3 if bid is None else 2
+        assert pvsb(cid, h, r, bid, ts, flag) == ovsb(cid, 2, h, r, bid if flag == 2 else None, ts)

@@ -1,0 +1,106 @@
+"""The exact kernel source (tendermint-fork_amd/csrc/*.h) compiled for the CPU
+(tests/native/hostsim.cpp, test-only) against the oracle — catches arithmetic
+bugs without a GPU.  The GPU parity proper is tests/test_gpu_verify.py."""
+import ctypes
+import hashlib
+import random
+
+import numpy as np
+
+from oracle import ed25519_go as E
+from oracle import port
+
+VP = ctypes.c_void_p
+
+
+def _p(a):
+    return a.ctypes.data_as(VP)
+
+
+def _fe(l, op, a, b):
+    o = ctypes.create_string_buffer(32)
+    l.hostsim_fe_op(op, a.to_bytes(32, "little"), b.to_bytes(32, "little"), o)
+    return int.from_bytes(o.raw, "little")
+
+
+def test_field_ops_vs_bigint(hostsim):
+    P = E.P
+    rng = random.Random(11)
+    edge = [0, 1, 2, 19, P - 1, P, P + 1, P + 18, 2**255 - 1, 2**255 - 20, 2**254, 2**26 - 1, 2**51]
+    vals = edge + [rng.randrange(2**255) for _ in range(120)]
+    for a in vals:
+        for b in edge[:6] + [rng.randrange(2**255)]:
+            A, B = a % P, b % P
+            exp = {0: A * B % P, 1: A * A % P, 2: pow(A, P - 2, P), 3: pow(A, (P - 5) // 8, P), 4: (A + B) % P,
+                   5: (A - B) % P, 6: 2 * A * A % P, 7: (2 * A + B) ** 2 % P, 8: (2 * A + B) ** 2 % P}
+            for op, e in exp.items():
+                assert _fe(hostsim, op, a, b) == e, (op, hex(a), hex(b))
+
+
+def test_sha512_and_reduce(hostsim):
+    rng = random.Random(5)
+    for n in [0, 1, 17, 111, 112, 113, 127, 128, 129, 200, 239, 240, 241, 300, 400]:
+        m = bytes(rng.randrange(256) for _ in range(n))
+        o = ctypes.create_string_buffer(64)
+        hostsim.hostsim_sha512(m, n, o)
+        assert o.raw == hashlib.sha512(m).digest()
+        r = ctypes.create_string_buffer(32)
+        hostsim.hostsim_sc_reduce(o.raw, r)
+        assert int.from_bytes(r.raw, "little") == int.from_bytes(o.raw, "little") % E.L
+    for x in [b"\xff" * 64, bytes(64), E.L.to_bytes(64, "little"), (E.L - 1).to_bytes(64, "little"),
+              (2 * E.L).to_bytes(64, "little"), (E.L * (2**259 - 1)).to_bytes(64, "little")]:
+        r = ctypes.create_string_buffer(32)
+        hostsim.hostsim_sc_reduce(x, r)
+        assert int.from_bytes(r.raw, "little") == int.from_bytes(x, "little") % E.L
+
+
+def test_decode_matches_go_rule(hostsim):
+    rng = random.Random(9)
+    cands = [bytes(32), bytes(31) + b"\x80"] + [rng.randbytes(32) for _ in range(80)]
+    cands += [E.encode(q) for q in E.small_order_points()]
+    cands += [(y + E.P).to_bytes(32, "little") for y in range(19)]
+    for p in cands:
+        o = ctypes.create_string_buffer(32)
+        ok = hostsim.hostsim_decode(p, o)
+        pt = E.decode(p)
+        assert bool(ok) == (pt is not None), p.hex()
+        if pt is not None:
+            assert o.raw == E.encode(pt)
+
+
+def _verify(l, pubs, sigs, msgs, offs):
+    n = len(pubs)
+    out = np.zeros(n, np.uint8)
+    l.hostsim_verify_batch(_p(pubs), _p(sigs), _p(msgs), _p(offs), ctypes.c_size_t(n), _p(out))
+    return out
+
+
+def test_golden_vectors_hostsim(hostsim, golden):
+    vs = [v for v in golden if len(v["sig"]) == 128]
+    pubs = np.array([np.frombuffer(bytes.fromhex(v["pub"]), np.uint8) for v in vs])
+    sigs = np.array([np.frombuffer(bytes.fromhex(v["sig"]), np.uint8) for v in vs])
+    ms = [bytes.fromhex(v["msg"]) for v in vs]
+    offs = np.zeros(len(vs) + 1, np.uint32)
+    offs[1:] = np.cumsum([len(m) for m in ms])
+    msgs = np.frombuffer(b"".join(ms) + b"\0", np.uint8)
+    out = _verify(hostsim, pubs, sigs, msgs, offs)
+    exp = np.array([v["valid"] for v in vs], np.uint8)
+    bad = [vs[i]["class"] for i in np.nonzero(out != exp)[0]]
+    assert not bad, bad
+
+
+def test_sign_matches_oracle(hostsim):
+    rng = np.random.default_rng(2)
+    n = 96
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    lens = rng.integers(0, 260, n)
+    offs = np.zeros(n + 1, np.uint32)
+    offs[1:] = np.cumsum(lens)
+    msgs = rng.integers(0, 256, int(offs[-1]) + 1, dtype=np.uint8)
+    sig = np.zeros((n, 64), np.uint8)
+    pub = np.zeros((n, 32), np.uint8)
+    hostsim.hostsim_sign_batch(_p(seeds), _p(msgs), _p(offs), ctypes.c_size_t(n), _p(sig), _p(pub))
+    for i in range(n):
+        m = msgs[offs[i]:offs[i + 1]].tobytes()
+        assert sig[i].tobytes() == port.sign(seeds[i].tobytes(), m)
+        assert pub[i].tobytes() == port.pubkey_from_seed(seeds[i].tobytes())

@@ -1,0 +1,138 @@
+"""Pin the ed25519 oracle: RFC 8032 vectors, OpenSSL 3 cross-check, big-int vs C restatement."""
+import ctypes
+import ctypes.util
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+from oracle import ed25519_go as E
+from oracle import port
+
+RFC = [
+    ("9d61b19deffd5a60ba844af492ec2cc44449c5697b326919703bac031cae7f60",
+     "d75a980182b10ab7d54bfed3c964073a0ee172f3daa62325af021a68f707511a", "",
+     "e5564300c360ac729086e2cc806e828a84877f1eb8e5d974d873e065224901555fb8821590a33bacc61e39701cf9b46bd25bf5f0595bbe24655141438e7a100b"),
+    ("4ccd089b28ff96da9db6c346ec114e0f5b8a319f35aba624da8cf6ed4fb8a6fb",
+     "3d4017c3e843895a92b70aa74d1b7ebc9c982ccf2ec4968cc0cd55f12af4660c", "72",
+     "92a009a9f0d4cab8720e820b5f642540a2b27b5416503f8fb3762223ebdb69da085ac1e43e15996e458f3613d0f11d8c387b2eaeb4302aeeb00d291612bb0c00"),
+]
+
+
+@pytest.mark.parametrize("sk,pk,msg,sig", RFC)
+def test_rfc8032_vectors(sk, pk, msg, sig):
+    sk, pk, msg, sig = map(bytes.fromhex, (sk, pk, msg, sig))
+    assert E.pubkey_from_seed(sk) == pk
+    assert E.sign(sk, msg) == sig
+    assert E.verify(pk, msg, sig)
+    assert port.pubkey_from_seed(sk) == pk and port.sign(sk, msg) == sig and port.verify(pk, msg, sig)
+
+
+def _openssl():
+    name = ctypes.util.find_library("crypto") or "libcrypto.so.3"
+    try:
+        lc = ctypes.CDLL(name)
+    except OSError:
+        pytest.skip("libcrypto not available")
+    P = ctypes.c_void_p
+    lc.EVP_PKEY_new_raw_public_key.restype = P
+    lc.EVP_PKEY_new_raw_public_key.argtypes = [ctypes.c_int, P, P, ctypes.c_size_t]
+    lc.EVP_PKEY_new_raw_private_key.restype = P
+    lc.EVP_PKEY_new_raw_private_key.argtypes = [ctypes.c_int, P, P, ctypes.c_size_t]
+    lc.EVP_MD_CTX_new.restype = P
+    lc.EVP_MD_CTX_free.argtypes = [P]
+    lc.EVP_PKEY_free.argtypes = [P]
+    lc.EVP_DigestVerifyInit.argtypes = [P, P, P, P, P]
+    lc.EVP_DigestVerify.argtypes = [P, P, ctypes.c_size_t, P, ctypes.c_size_t]
+    lc.EVP_DigestSignInit.argtypes = [P, P, P, P, P]
+    lc.EVP_DigestSign.argtypes = [P, P, P, P, ctypes.c_size_t]
+    return lc
+
+
+def ossl_verify(lc, pub, msg, sig):
+    k = lc.EVP_PKEY_new_raw_public_key(1087, None, pub, 32)
+    if not k:
+        return False
+    c = lc.EVP_MD_CTX_new()
+    lc.EVP_DigestVerifyInit(c, None, None, None, k)
+    r = lc.EVP_DigestVerify(c, sig, len(sig), msg, len(msg))
+    lc.EVP_MD_CTX_free(c)
+    lc.EVP_PKEY_free(k)
+    return r == 1
+
+
+def ossl_sign(lc, seed, msg):
+    k = lc.EVP_PKEY_new_raw_private_key(1087, None, seed, 32)
+    c = lc.EVP_MD_CTX_new()
+    lc.EVP_DigestSignInit(c, None, None, None, k)
+    out = ctypes.create_string_buffer(64)
+    ln = ctypes.c_size_t(64)
+    assert lc.EVP_DigestSign(c, out, ctypes.byref(ln), msg, len(msg)) == 1
+    lc.EVP_MD_CTX_free(c)
+    lc.EVP_PKEY_free(k)
+    return out.raw
+
+
+def test_openssl_cross_check_random():
+    """Independent implementation agrees on random valid/invalid tuples (non-edge cases only)."""
+    lc = _openssl()
+    rng = random.Random(7)
+    for i in range(150):
+        seed = rng.randbytes(32)
+        msg = rng.randbytes(rng.randrange(0, 300))
+        sig = E.sign(seed, msg)
+        assert sig == ossl_sign(lc, seed, msg)
+        pub = E.pubkey_from_seed(seed)
+        for mut in range(3):
+            s = bytearray(sig)
+            m = msg
+            if mut == 1:
+                s[rng.randrange(64)] ^= 1 << rng.randrange(8)
+            if mut == 2:
+                m = msg + b"!"
+            s = bytes(s)
+            if int.from_bytes(s[32:], "little") >= E.L:
+                continue  # OpenSSL 3 also rejects, but keep to the non-edge domain
+            assert E.verify(pub, m, s) == ossl_verify(lc, pub, m, s)
+
+
+def test_golden_matches_both_restatements(golden):
+    bad = []
+    for v in golden:
+        pub, msg, sig = bytes.fromhex(v["pub"]), bytes.fromhex(v["msg"]), bytes.fromhex(v["sig"])
+        exp = v["valid"]
+        if E.verify(pub, msg, sig) != exp:
+            bad.append(("py", v["class"]))
+        if port.verify(pub, msg, sig) != exp:
+            bad.append(("c", v["class"]))
+    assert not bad
+
+
+def test_go_edge_semantics():
+    """Spot checks of the Go 1.18 rule: derived, not reference-pinned."""
+    seed = hashlib.sha256(b"edge").digest()
+    pub = E.pubkey_from_seed(seed)
+    msg = b"m"
+    sig = E.sign(seed, msg)
+    S = int.from_bytes(sig[32:], "little")
+    assert not E.verify(pub, msg, sig[:32] + (S + E.L).to_bytes(32, "little"))  # S >= L strict
+    assert not E.verify(pub, msg, sig[:63])                                         # len != 64
+    # x = 0 with the sign bit set decodes (permissive A)
+    assert E.decode(bytes(31) + b"\x80") is not None
+    # y >= p aliases decode to the reduced point
+    one_p = (1 + E.P).to_bytes(32, "little")
+    assert E.decode(one_p) is not None and E.pt_equal(E.decode(one_p), E.IDENTITY)
+
+
+def test_port_batch_threads_agree():
+    rng = np.random.default_rng(3)
+    n = 512
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    msgs = rng.integers(0, 256, n * 120, dtype=np.uint8)
+    offs = (np.arange(n + 1) * 120).astype(np.uint64)
+    sigs, pubs = port.sign_batch(seeds, msgs, offs, 4)
+    sigs[::5, 3] ^= 4
+    a = port.verify_batch(pubs, sigs, msgs, offs, 1)
+    b = port.verify_batch(pubs, sigs, msgs, offs, 4)
+    assert (a == b).all() and a.sum() == n - len(range(0, n, 5))
