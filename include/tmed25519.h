@@ -132,6 +132,100 @@ int tmed_vote_sign_bytes(const tmed_vote_template *t, size_t n, const uint8_t *f
  */
 int tmed_valu_peak(tmed_ctx *ctx, int kind, double *giga_ops_per_s);
 
+/* ------------------------------------------------------- commit seam (C++) */
+
+/* BlockID as compared by BlockID.Equals (types/block.go:1170-1173). */
+typedef struct {
+  const uint8_t *hash;
+  uint32_t hash_len;
+  uint32_t psh_total;
+  const uint8_t *psh_hash;
+  uint32_t psh_hash_len;
+} tmed_block_id;
+
+/* ValidatorSet (types/validator_set.go:51-58), index order = commit order. */
+typedef struct {
+  size_t n;
+  const uint8_t *pubkeys;   /* n x 32 (ed25519 keys; other key types stay on the Go path) */
+  const int64_t *powers;    /* n voting powers */
+  const uint8_t *addresses; /* n x 20, PubKey.Address(); needed by LightTrusting only (may be NULL otherwise) */
+  int64_t total_power;      /* vals.TotalVotingPower() (its panics stay in Go, :298-321) */
+} tmed_valset;
+
+/* Commit + CommitSigs (types/block.go:575-634, 737-752). */
+typedef struct {
+  int64_t height;
+  int32_t round;
+  tmed_block_id block_id;
+  size_t n_sigs;
+  const uint8_t *flags;       /* BlockIDFlag per signature: 1 Absent, 2 Commit, 3 Nil */
+  const uint8_t *addresses;   /* n_sigs x 20 ValidatorAddress (LightTrusting only; may be NULL otherwise) */
+  const int64_t *ts_seconds;  /* Timestamp.Unix() */
+  const int32_t *ts_nanos;    /* Timestamp.Nanosecond() */
+  const uint8_t *sigs;        /* n_sigs x 64 (first sig_lens[i] bytes meaningful) */
+  const uint32_t *sig_lens;   /* NULL = all 64 */
+} tmed_commit;
+
+#define TMED_MODE_COMMIT 0         /* ValidatorSet.VerifyCommit              :667-714 */
+#define TMED_MODE_LIGHT 1          /* ValidatorSet.VerifyCommitLight         :722-765 */
+#define TMED_MODE_LIGHT_TRUSTING 2 /* ValidatorSet.VerifyCommitLightTrusting :775-826 */
+
+typedef struct {
+  int mode;
+  const char *chain_id;
+  uint32_t chain_id_len;
+  const tmed_valset *vals;
+  const tmed_block_id *block_id; /* COMMIT / LIGHT: expected BlockID */
+  int64_t height;                /* COMMIT / LIGHT: expected height */
+  const tmed_commit *commit;
+  int64_t trust_num, trust_den;  /* LIGHT_TRUSTING: tmmath.Fraction (libs/math/fraction.go:11-18) */
+} tmed_commit_request;
+
+/* Outcome codes: the reference's return value, to be formatted by the caller exactly as Go does. */
+#define TMED_COMMIT_OK 0
+#define TMED_COMMIT_WRONG_SET_SIZE 1   /* ErrInvalidCommitSignatures{expected, actual} (types/errors.go:32-41) */
+#define TMED_COMMIT_WRONG_HEIGHT 2     /* ErrInvalidCommitHeight{expected, actual} (types/errors.go:21-30) */
+#define TMED_COMMIT_WRONG_BLOCK_ID 3   /* "invalid commit -- wrong block ID: want %v, got %v" */
+#define TMED_COMMIT_WRONG_SIGNATURE 4  /* "wrong signature (#%d): %X" (idx) */
+#define TMED_COMMIT_NOT_ENOUGH_POWER 5 /* ErrNotEnoughVotingPowerSigned{got, needed} (:856-863) */
+#define TMED_COMMIT_DOUBLE_VOTE 6      /* "double vote from %v (%d and %d)" (val_idx, idx_first, idx) */
+#define TMED_COMMIT_ZERO_DENOMINATOR 7 /* "trustLevel has zero Denominator" */
+#define TMED_COMMIT_OVERFLOW 8         /* "int64 overflow while calculating voting power needed..." */
+
+typedef struct {
+  int code;
+  int64_t got, needed;     /* NOT_ENOUGH_POWER */
+  int64_t expected, actual;/* WRONG_SET_SIZE / WRONG_HEIGHT */
+  int32_t idx;             /* WRONG_SIGNATURE index; DOUBLE_VOTE second index */
+  int32_t idx_first;       /* DOUBLE_VOTE first index */
+  int32_t val_idx;         /* DOUBLE_VOTE validator index */
+  uint32_t verified;       /* signatures sent to the device for this request */
+} tmed_commit_result;
+
+/*
+ * Verify n commit requests with ONE device batch: run the reference prechecks,
+ * collect the signatures each loop would reach (all non-absent for COMMIT; the
+ * ForBlock prefix up to the >2/3 (resp. trust-level) crossing for LIGHT /
+ * LIGHT_TRUSTING, stopping at a double vote), build their CanonicalVote
+ * sign-bytes, verify them on the GPU, then replay each reference loop over the
+ * validity bits — same first-error index, same early exit, same Got/Needed.
+ * TMED_EINVAL for inputs on which the reference panics (unknown BlockIDFlag,
+ * malformed hashes): the caller must take the original code path.
+ */
+int tmed_verify_commits(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, tmed_commit_result *out);
+
+/*
+ * The same seam with the batch verifier supplied by the caller (same contract
+ * as tmed_verify_batch; return 0 on success).  tmed_verify_commits is this
+ * with the context's GPU verifier.  Lets a host integrate its own verifier
+ * (e.g. the Go shim's fallback is the original Go method, not this) and lets
+ * the CPU test-suite check the plan/replay logic against the oracle.
+ */
+typedef int (*tmed_batch_verify_fn)(void *user, const uint8_t *pubkeys, const uint8_t *sigs, const uint32_t *sig_lens,
+                                    const uint8_t *msgs, const uint32_t *msg_off, size_t n, uint8_t *out_valid);
+int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out,
+                             tmed_batch_verify_fn verify, void *user);
+
 #ifdef __cplusplus
 }
 #endif

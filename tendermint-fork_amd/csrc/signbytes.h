@@ -1,0 +1,25 @@
+// signbytes.h — per-commit CanonicalVote encoder (see signbytes.hip for the layout + citations).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/tmed25519.h"
+
+namespace tmed {
+
+// Everything but the per-vote flag/timestamp is encoded once per commit.
+struct VoteEncoder {
+  uint8_t pre[32];
+  int pre_len = 0;
+  uint8_t bid[160];
+  int bid_body = 0, bid_field = 0;
+  const char *cid = nullptr;
+  uint32_t cid_len = 0;
+  int cid_field = 0;
+
+  int init(const tmed_vote_template *t);
+  size_t size(int flag, int64_t sec, int32_t nanos) const;
+  uint8_t *write(uint8_t *out, int flag, int64_t sec, int32_t nanos) const;
+};
+
+}  // namespace tmed

@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include "../../include/tmed25519.h"
+#include "signbytes.h"
 
 namespace {
 
@@ -34,62 +35,79 @@ inline uint8_t *put_le64(uint8_t *p, uint64_t v) {
   return p;
 }
 
-// Encoded CanonicalBlockID body (without its tag/len); returns length or 0 when the BlockID is zero.
-int block_id_body(const tmed_vote_template *t, uint8_t *buf) {
+}  // namespace
+
+namespace tmed {
+
+int VoteEncoder::init(const tmed_vote_template *t) {
+  if (!t) return TMED_EINVAL;
+  if ((t->block_hash_len != 0 && t->block_hash_len != 32) || (t->psh_hash_len != 0 && t->psh_hash_len != 32))
+    return TMED_EINVAL;  // ValidateHash: BlockIDFromProto would panic (types/canonical.go:19-22)
+  if (t->chain_id_len && !t->chain_id) return TMED_EINVAL;
+  uint8_t *p = pre;
+  *p++ = 0x08; *p++ = 0x02;  // SignedMsgType Precommit (Commit.GetVote, types/block.go:787)
+  if (t->height != 0) { *p++ = 0x11; p = put_le64(p, (uint64_t)t->height); }
+  if (t->round != 0) { *p++ = 0x19; p = put_le64(p, (uint64_t)(int64_t)t->round); }
+  pre_len = (int)(p - pre);
+  // CanonicalBlockID body; a zero BlockID is omitted (CanonicalizeBlockID -> nil)
   const bool zero = t->block_hash_len == 0 && t->psh_total == 0 && t->psh_hash_len == 0;
-  if (zero) return 0;
-  uint8_t psh[64];
-  uint8_t *q = psh;
-  if (t->psh_total != 0) { *q++ = 0x08; q = put_uvarint(q, t->psh_total); }
-  if (t->psh_hash_len > 0) { *q++ = 0x12; q = put_uvarint(q, t->psh_hash_len); memcpy(q, t->psh_hash, t->psh_hash_len); q += t->psh_hash_len; }
-  const int psh_len = (int)(q - psh);
-  uint8_t *p = buf;
-  if (t->block_hash_len > 0) { *p++ = 0x0a; p = put_uvarint(p, t->block_hash_len); memcpy(p, t->block_hash, t->block_hash_len); p += t->block_hash_len; }
-  *p++ = 0x12; p = put_uvarint(p, (uint64_t)psh_len); memcpy(p, psh, psh_len); p += psh_len;
-  return (int)(p - buf);
+  bid_body = 0;
+  if (!zero) {
+    uint8_t psh[64];
+    uint8_t *q = psh;
+    if (t->psh_total != 0) { *q++ = 0x08; q = put_uvarint(q, t->psh_total); }
+    if (t->psh_hash_len > 0) { *q++ = 0x12; q = put_uvarint(q, t->psh_hash_len); memcpy(q, t->psh_hash, t->psh_hash_len); q += t->psh_hash_len; }
+    const int psh_len = (int)(q - psh);
+    uint8_t *b = bid;
+    if (t->block_hash_len > 0) { *b++ = 0x0a; b = put_uvarint(b, t->block_hash_len); memcpy(b, t->block_hash, t->block_hash_len); b += t->block_hash_len; }
+    *b++ = 0x12; b = put_uvarint(b, (uint64_t)psh_len); memcpy(b, psh, psh_len); b += psh_len;
+    bid_body = (int)(b - bid);
+  }
+  bid_field = bid_body ? 1 + uvarint_len((uint64_t)bid_body) + bid_body : 0;
+  cid = t->chain_id;
+  cid_len = t->chain_id_len;
+  cid_field = cid_len ? 1 + uvarint_len(cid_len) + (int)cid_len : 0;
+  return TMED_OK;
 }
 
-}  // namespace
+size_t VoteEncoder::size(int flag, int64_t sec, int32_t nanos) const {
+  const uint64_t s = (uint64_t)sec, n = (uint64_t)(int64_t)nanos;
+  const int ts_body = (s ? 1 + uvarint_len(s) : 0) + (n ? 1 + uvarint_len(n) : 0);
+  const int body = pre_len + (flag == 2 ? bid_field : 0) + 1 + uvarint_len((uint64_t)ts_body) + ts_body + cid_field;
+  return (size_t)uvarint_len((uint64_t)body) + body;
+}
+
+uint8_t *VoteEncoder::write(uint8_t *w, int flag, int64_t sec, int32_t nanos) const {
+  const uint64_t s = (uint64_t)sec, n = (uint64_t)(int64_t)nanos;
+  const int ts_body = (s ? 1 + uvarint_len(s) : 0) + (n ? 1 + uvarint_len(n) : 0);
+  const bool with_bid = flag == 2;  // BlockIDFlagCommit -> commit BlockID; Absent/Nil -> zero BlockID
+  const int body = pre_len + (with_bid ? bid_field : 0) + 1 + uvarint_len((uint64_t)ts_body) + ts_body + cid_field;
+  w = put_uvarint(w, (uint64_t)body);
+  memcpy(w, pre, pre_len); w += pre_len;
+  if (with_bid && bid_body) { *w++ = 0x22; w = put_uvarint(w, (uint64_t)bid_body); memcpy(w, bid, bid_body); w += bid_body; }
+  *w++ = 0x2a; w = put_uvarint(w, (uint64_t)ts_body);
+  if (s) { *w++ = 0x08; w = put_uvarint(w, s); }
+  if (n) { *w++ = 0x10; w = put_uvarint(w, n); }
+  if (cid_len) { *w++ = 0x32; w = put_uvarint(w, cid_len); memcpy(w, cid, cid_len); w += cid_len; }
+  return w;
+}
+
+}  // namespace tmed
 
 extern "C" int tmed_vote_sign_bytes(const tmed_vote_template *t, size_t n, const uint8_t *flags,
                                     const int64_t *ts_seconds, const int32_t *ts_nanos, uint8_t *out,
                                     size_t out_cap, uint32_t *out_off, size_t *out_len) {
   if (!t || (n && (!ts_seconds || !ts_nanos || !out_off))) return TMED_EINVAL;
-  if ((t->block_hash_len != 0 && t->block_hash_len != 32) || (t->psh_hash_len != 0 && t->psh_hash_len != 32))
-    return TMED_EINVAL;  // ValidateHash: BlockIDFromProto would panic (types/canonical.go:19-22)
-  if (t->chain_id_len && !t->chain_id) return TMED_EINVAL;
-  // prefix: type, height, round (identical for every vote of the commit)
-  uint8_t pre[32];
-  uint8_t *p = pre;
-  *p++ = 0x08; *p++ = 0x02;  // SignedMsgType Precommit (GetVote, types/block.go:787)
-  if (t->height != 0) { *p++ = 0x11; p = put_le64(p, (uint64_t)t->height); }
-  if (t->round != 0) { *p++ = 0x19; p = put_le64(p, (uint64_t)(int64_t)t->round); }
-  const int pre_len = (int)(p - pre);
-  uint8_t bid[160];
-  const int bid_body = block_id_body(t, bid);
-  const int bid_field = bid_body ? 1 + uvarint_len((uint64_t)bid_body) + bid_body : 0;
-  const int cid_field = t->chain_id_len ? 1 + uvarint_len(t->chain_id_len) + (int)t->chain_id_len : 0;
+  tmed::VoteEncoder enc;
+  int rc = enc.init(t);
+  if (rc != TMED_OK) return rc;
   size_t pos = 0;
   for (size_t i = 0; i < n; i++) {
-    const uint8_t f = flags ? flags[i] : 2;
+    const int f = flags ? flags[i] : 2;
     if (f < 1 || f > 3) return TMED_EINVAL;  // CommitSig.BlockID panics on unknown flags (types/block.go:663)
-    const bool with_bid = (f == 2);          // BlockIDFlagCommit -> commit BlockID, else zero BlockID
-    const uint64_t sec = (uint64_t)ts_seconds[i];
-    const uint64_t nan = (uint64_t)(int64_t)ts_nanos[i];
-    const int ts_body = (sec ? 1 + uvarint_len(sec) : 0) + (nan ? 1 + uvarint_len(nan) : 0);
-    const int body = pre_len + (with_bid ? bid_field : 0) + 1 + uvarint_len((uint64_t)ts_body) + ts_body + cid_field;
-    const size_t total = (size_t)uvarint_len((uint64_t)body) + body;
+    const size_t total = enc.size(f, ts_seconds[i], ts_nanos[i]);
     out_off[i] = (uint32_t)pos;
-    if (out && pos + total <= out_cap) {
-      uint8_t *w = out + pos;
-      w = put_uvarint(w, (uint64_t)body);
-      memcpy(w, pre, pre_len); w += pre_len;
-      if (with_bid) { *w++ = 0x22; w = put_uvarint(w, (uint64_t)bid_body); memcpy(w, bid, bid_body); w += bid_body; }
-      *w++ = 0x2a; w = put_uvarint(w, (uint64_t)ts_body);
-      if (sec) { *w++ = 0x08; w = put_uvarint(w, sec); }
-      if (nan) { *w++ = 0x10; w = put_uvarint(w, nan); }
-      if (t->chain_id_len) { *w++ = 0x32; w = put_uvarint(w, t->chain_id_len); memcpy(w, t->chain_id, t->chain_id_len); w += t->chain_id_len; }
-    }
+    if (out && pos + total <= out_cap) enc.write(out + pos, f, ts_seconds[i], ts_nanos[i]);
     pos += total;
     if (pos > 0xffffffffu) return TMED_EINVAL;
   }

@@ -64,5 +64,5 @@ EXPORTED_SYMBOLS = [
     "tmed_device_count", "tmed_init", "tmed_destroy", "tmed_strerror",
     "tmed_verify_batch", "tmed_verify_batch_device",
     "tmed_sign_batch", "tmed_sign_batch_device", "tmed_last_kernel_ms",
-    "tmed_vote_sign_bytes", "tmed_valu_peak",
+    "tmed_vote_sign_bytes", "tmed_valu_peak", "tmed_verify_commits", "tmed_verify_commits_with",
 ]

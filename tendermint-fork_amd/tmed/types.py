@@ -1,0 +1,317 @@
+"""Host mirror of the reference's commit types and the VerifyCommit* seam.
+
+Python mirror of ``types.ValidatorSet.VerifyCommit``, ``VerifyCommitLight`` and
+``VerifyCommitLightTrusting`` (reference ``types/validator_set.go:667-826``)
+over the C ABI ``tmed_verify_commits`` (C++ plan/replay in
+``csrc/commit.hip``): same argument meaning, same return convention (``None``
+or an error value whose ``str()`` is Go's ``err.Error()``), same error types
+(``ErrInvalidCommitSignatures``, ``ErrInvalidCommitHeight``,
+``ErrNotEnoughVotingPowerSigned`` are what ``light/verifier.go:60-61`` and
+``light/client.go:746`` type-switch on).  Batches of commits go to the GPU in
+one launch via :func:`verify_commits`.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from ._native import TMED_OK, TmedError, lib
+
+FLAG_ABSENT, FLAG_COMMIT, FLAG_NIL = 1, 2, 3        # types/block.go:577-584
+MODE_COMMIT, MODE_LIGHT, MODE_LIGHT_TRUSTING = 0, 1, 2
+MAX_INT64 = (1 << 63) - 1
+MAX_TOTAL_VOTING_POWER = MAX_INT64 // 8            # types/validator_set.go:25
+ZERO_TIME = (-62135596800, 0)
+
+
+def _hexu(b: bytes) -> str:
+    return bytes(b).hex().upper()
+
+
+def address_of(pub: bytes) -> bytes:
+    """ed25519 PubKey.Address = SHA-256(pub)[:20] (crypto/ed25519/ed25519.go:136-141)."""
+    return hashlib.sha256(pub).digest()[:20]
+
+
+# --------------------------------------------------------------------------- types
+
+@dataclass
+class BlockID:
+    hash: bytes = b""
+    psh_total: int = 0
+    psh_hash: bytes = b""
+
+    def equals(self, o: "BlockID") -> bool:
+        return self.hash == o.hash and self.psh_total == o.psh_total and self.psh_hash == o.psh_hash
+
+    def __str__(self):  # types/block.go:1217-1219 (+ PartSetHeader.String, part_set.go:103-105)
+        return "%s:%d:%s" % (_hexu(self.hash), self.psh_total, _hexu((bytes(self.psh_hash[:6]) + bytes(6))[:6]))
+
+
+@dataclass
+class CommitSig:
+    flag: int
+    address: bytes = b""
+    timestamp: tuple = ZERO_TIME
+    signature: bytes = b""
+
+
+@dataclass
+class Commit:
+    height: int
+    round: int
+    block_id: BlockID
+    signatures: List[CommitSig]
+
+
+@dataclass
+class Validator:
+    pub_key: bytes
+    voting_power: int
+    proposer_priority: int = 0
+    address: bytes = b""
+
+    def __post_init__(self):
+        if not self.address:
+            self.address = address_of(self.pub_key)
+
+    def __str__(self):  # types/validator.go:92-101
+        return "Validator{%s PubKeyEd25519{%s} VP:%d A:%d}" % (
+            _hexu(self.address), _hexu(self.pub_key), self.voting_power, self.proposer_priority)
+
+
+@dataclass
+class ValidatorSet:
+    validators: List[Validator]
+    _total: int = field(default=0, repr=False)
+    _packed: Optional[tuple] = field(default=None, repr=False)
+
+    def size(self) -> int:
+        return len(self.validators)
+
+    def total_voting_power(self) -> int:  # types/validator_set.go:298-321
+        if self._total == 0:
+            s = 0
+            for v in self.validators:
+                s = min(s + v.voting_power, MAX_INT64)
+                if s > MAX_TOTAL_VOTING_POWER:
+                    raise RuntimeError("Total voting power should be guarded to not exceed %d; got: %d"
+                                       % (MAX_TOTAL_VOTING_POWER, s))
+            self._total = s
+        return self._total
+
+    def packed(self):
+        if self._packed is None:
+            n = len(self.validators)
+            pubs = np.zeros((max(n, 1), 32), np.uint8)
+            addrs = np.zeros((max(n, 1), 20), np.uint8)
+            for i, v in enumerate(self.validators):
+                if len(v.pub_key) != 32:
+                    raise ValueError("not an ed25519 key: the reference path handles it")
+                pubs[i] = np.frombuffer(v.pub_key, np.uint8)
+                addrs[i] = np.frombuffer(v.address, np.uint8)
+            powers = np.array([v.voting_power for v in self.validators] or [0], np.int64)
+            self._packed = (pubs, powers, addrs)
+        return self._packed
+
+    # reference method names
+    def verify_commit(self, engine, chain_id: str, block_id: BlockID, height: int, commit: Commit):
+        return verify_commits(engine, [(MODE_COMMIT, self, chain_id, block_id, height, commit, 0, 0)])[0]
+
+    def verify_commit_light(self, engine, chain_id: str, block_id: BlockID, height: int, commit: Commit):
+        return verify_commits(engine, [(MODE_LIGHT, self, chain_id, block_id, height, commit, 0, 0)])[0]
+
+    def verify_commit_light_trusting(self, engine, chain_id: str, commit: Commit, num: int, den: int):
+        return verify_commits(engine, [(MODE_LIGHT_TRUSTING, self, chain_id, None, 0, commit, num, den)])[0]
+
+
+# --------------------------------------------------------------------------- errors
+
+class GoError:
+    def __init__(self, msg: str):
+        self.msg = msg
+
+    def __str__(self):
+        return self.msg
+
+    def __repr__(self):
+        return "%s(%r)" % (type(self).__name__, self.msg)
+
+    def __eq__(self, o):
+        return type(self).__name__ == type(o).__name__ and str(self) == str(o)
+
+
+class ErrInvalidCommitSignatures(GoError):  # types/errors.go:32-41
+    def __init__(self, expected, actual):
+        self.expected, self.actual = expected, actual
+        super().__init__("Invalid commit -- wrong set size: %d vs %d" % (expected, actual))
+
+
+class ErrInvalidCommitHeight(GoError):  # types/errors.go:21-30
+    def __init__(self, expected, actual):
+        self.expected, self.actual = expected, actual
+        super().__init__("Invalid commit -- wrong height: %d vs %d" % (expected, actual))
+
+
+class ErrNotEnoughVotingPowerSigned(GoError):  # types/validator_set.go:856-863
+    def __init__(self, got, needed):
+        self.got, self.needed = got, needed
+        super().__init__("invalid commit -- insufficient voting power: got %d, needed more than %d" % (got, needed))
+
+
+# --------------------------------------------------------------------------- ABI structs
+
+class _BlockIDC(ctypes.Structure):
+    _fields_ = [("hash", ctypes.c_void_p), ("hash_len", ctypes.c_uint32), ("psh_total", ctypes.c_uint32),
+                ("psh_hash", ctypes.c_void_p), ("psh_hash_len", ctypes.c_uint32)]
+
+
+class _ValsetC(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_size_t), ("pubkeys", ctypes.c_void_p), ("powers", ctypes.c_void_p),
+                ("addresses", ctypes.c_void_p), ("total_power", ctypes.c_int64)]
+
+
+class _CommitC(ctypes.Structure):
+    _fields_ = [("height", ctypes.c_int64), ("round", ctypes.c_int32), ("block_id", _BlockIDC),
+                ("n_sigs", ctypes.c_size_t), ("flags", ctypes.c_void_p), ("addresses", ctypes.c_void_p),
+                ("ts_seconds", ctypes.c_void_p), ("ts_nanos", ctypes.c_void_p), ("sigs", ctypes.c_void_p),
+                ("sig_lens", ctypes.c_void_p)]
+
+
+class _RequestC(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int), ("chain_id", ctypes.c_char_p), ("chain_id_len", ctypes.c_uint32),
+                ("vals", ctypes.POINTER(_ValsetC)), ("block_id", ctypes.POINTER(_BlockIDC)),
+                ("height", ctypes.c_int64), ("commit", ctypes.POINTER(_CommitC)),
+                ("trust_num", ctypes.c_int64), ("trust_den", ctypes.c_int64)]
+
+
+class _ResultC(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_int), ("got", ctypes.c_int64), ("needed", ctypes.c_int64),
+                ("expected", ctypes.c_int64), ("actual", ctypes.c_int64), ("idx", ctypes.c_int32),
+                ("idx_first", ctypes.c_int32), ("val_idx", ctypes.c_int32), ("verified", ctypes.c_uint32)]
+
+
+VERIFY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
+
+
+def _bind():
+    l = lib()
+    if l.tmed_verify_commits.argtypes is None:
+        l.tmed_verify_commits.restype = ctypes.c_int
+        l.tmed_verify_commits.argtypes = [ctypes.c_void_p, ctypes.POINTER(_RequestC), ctypes.c_size_t,
+                                          ctypes.POINTER(_ResultC)]
+        l.tmed_verify_commits_with.restype = ctypes.c_int
+        l.tmed_verify_commits_with.argtypes = [ctypes.POINTER(_RequestC), ctypes.c_size_t,
+                                               ctypes.POINTER(_ResultC), VERIFY_FN, ctypes.c_void_p]
+    return l
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _block_id_c(b: BlockID, keep):
+    h, ph = bytes(b.hash), bytes(b.psh_hash)
+    keep.extend([h, ph])
+    return _BlockIDC(ctypes.cast(ctypes.c_char_p(h), ctypes.c_void_p), len(h), b.psh_total,
+                     ctypes.cast(ctypes.c_char_p(ph), ctypes.c_void_p), len(ph))
+
+
+def _commit_c(c: Commit, keep):
+    n = len(c.signatures)
+    m = max(n, 1)
+    flags = np.zeros(m, np.uint8)
+    addrs = np.zeros((m, 20), np.uint8)
+    sec = np.zeros(m, np.int64)
+    nan = np.zeros(m, np.int32)
+    sigs = np.zeros((m, 64), np.uint8)
+    lens = np.zeros(m, np.uint32)
+    for i, cs in enumerate(c.signatures):
+        flags[i] = cs.flag
+        if len(cs.address) == 20:
+            addrs[i] = np.frombuffer(cs.address, np.uint8)
+        sec[i], nan[i] = cs.timestamp
+        s = cs.signature[:64]
+        if s:
+            sigs[i, :len(s)] = np.frombuffer(s, np.uint8)
+        lens[i] = len(cs.signature)
+    keep.extend([flags, addrs, sec, nan, sigs, lens])
+    return _CommitC(c.height, c.round, _block_id_c(c.block_id, keep), n, _ptr(flags), _ptr(addrs), _ptr(sec),
+                    _ptr(nan), _ptr(sigs), _ptr(lens))
+
+
+def _to_error(code, r: _ResultC, vals: ValidatorSet, block_id, commit: Commit):
+    if code == 0:
+        return None
+    if code == 1:
+        return ErrInvalidCommitSignatures(r.expected, r.actual)
+    if code == 2:
+        return ErrInvalidCommitHeight(r.expected, r.actual)
+    if code == 3:
+        return GoError("invalid commit -- wrong block ID: want %s, got %s" % (block_id, commit.block_id))
+    if code == 4:
+        return GoError("wrong signature (#%d): %s" % (r.idx, _hexu(commit.signatures[r.idx].signature)))
+    if code == 5:
+        return ErrNotEnoughVotingPowerSigned(r.got, r.needed)
+    if code == 6:
+        return GoError("double vote from %s (%d and %d)" % (vals.validators[r.val_idx], r.idx_first, r.idx))
+    if code == 7:
+        return GoError("trustLevel has zero Denominator")
+    if code == 8:
+        return GoError("int64 overflow while calculating voting power needed. please provide smaller trustLevel numerator")
+    raise RuntimeError("tmed: unknown commit outcome %d" % code)
+
+
+def verify_commits(engine, requests: Sequence[tuple], verifier=None, stats: Optional[list] = None):
+    """Verify many commits with one device batch.
+
+    requests: (mode, ValidatorSet, chain_id, BlockID|None, height, Commit, trust_num, trust_den).
+    verifier: None -> the engine's GPU path (tmed_verify_commits); otherwise a Python callable
+    ``(pubs, sigs, lens, msgs, offs) -> uint8 array`` (used by the CPU test-suite with the oracle).
+    Returns one Go-style error (or None) per request.
+    """
+    l = _bind()
+    keep = []
+    n = len(requests)
+    reqs = (_RequestC * max(n, 1))()
+    for q, (mode, vals, chain_id, block_id, height, commit, num, den) in enumerate(requests):
+        pubs, powers, addrs = vals.packed()
+        vs = _ValsetC(len(vals.validators), _ptr(pubs), _ptr(powers), _ptr(addrs), vals.total_voting_power())
+        cc = _commit_c(commit, keep)
+        cid = chain_id.encode()
+        bid = _block_id_c(block_id, keep) if block_id is not None else None
+        keep.extend([vs, cc, cid, bid])
+        reqs[q] = _RequestC(mode, cid, len(cid), ctypes.pointer(vs),
+                            ctypes.pointer(bid) if bid is not None else None, height, ctypes.pointer(cc), num, den)
+    res = (_ResultC * max(n, 1))()
+    if verifier is None:
+        rc = l.tmed_verify_commits(engine._h, reqs, n, res)
+    else:
+        def cb(user, pubs, sigs, lens, msgs, offs, m, out):
+            try:
+                P = ctypes.POINTER(ctypes.c_uint8)
+                pa = np.ctypeslib.as_array(ctypes.cast(pubs, P), (m * 32,)).reshape(m, 32)
+                sa = np.ctypeslib.as_array(ctypes.cast(sigs, P), (m * 64,)).reshape(m, 64)
+                la = np.ctypeslib.as_array(ctypes.cast(lens, ctypes.POINTER(ctypes.c_uint32)), (m,))
+                oa = np.ctypeslib.as_array(ctypes.cast(offs, ctypes.POINTER(ctypes.c_uint32)), (m + 1,))
+                ma = np.ctypeslib.as_array(ctypes.cast(msgs, P), (int(oa[-1]) + 1,))
+                dec = verifier(pa.copy(), sa.copy(), la.copy(), ma.copy(), oa.copy())
+                np.ctypeslib.as_array(ctypes.cast(out, P), (m,))[:] = dec
+                return 0
+            except Exception:  # never raise across the ABI
+                return -3
+        fn = VERIFY_FN(cb)
+        rc = l.tmed_verify_commits_with(reqs, n, res, fn, None)
+    if rc != TMED_OK:
+        raise TmedError(rc, "tmed_verify_commits")
+    out = []
+    for q, (mode, vals, chain_id, block_id, height, commit, num, den) in enumerate(requests):
+        out.append(_to_error(res[q].code, res[q], vals, block_id, commit))
+        if stats is not None:
+            stats.append(int(res[q].verified))
+    return out
