@@ -92,6 +92,24 @@ int tmed_sign_batch_device(tmed_ctx *ctx, const uint8_t *d_seeds, const uint8_t 
 float tmed_last_kernel_ms(tmed_ctx *ctx);
 
 
+/* ------------------------------------------------------- key-set cache */
+
+/*
+ * Decode a validator set's keys once (Point.SetBytes rule) and build a
+ * signed radix-256 comb of -A per key in HBM.  Signatures
+ * are then verified by key index: 64 mixed additions, no doublings, no per-
+ * signature decompression.  Decisions are identical to tmed_verify_batch.
+ * Callers key the handle by ValidatorSet.Hash() (types/validator_set.go:347-353).
+ */
+int tmed_keyset_load(tmed_ctx *ctx, const uint8_t *pubkeys, size_t n, uint64_t *handle);
+int tmed_keyset_free(tmed_ctx *ctx, uint64_t handle);
+int tmed_verify_batch_keyset(tmed_ctx *ctx, uint64_t handle, const uint32_t *val_idx, const uint8_t *sigs,
+                             const uint32_t *sig_lens, const uint8_t *msgs, const uint32_t *msg_off, size_t n,
+                             uint8_t *out_valid);
+int tmed_verify_batch_keyset_device(tmed_ctx *ctx, uint64_t handle, const uint32_t *d_val_idx, const uint8_t *d_sigs,
+                                    const uint8_t *d_msgs, const uint32_t *d_msg_off, size_t n, uint8_t *d_out_valid,
+                                    void *stream);
+
 /* ---------------------------------------------------------------- commits */
 
 /*

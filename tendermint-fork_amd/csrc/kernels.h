@@ -23,4 +23,24 @@ hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t
 
 void host_build_btab(ge_niels out[9]);
 
+// ---- fixed-base combs (key cache) -------------------------------
+// Signed radix-256 comb of a point P: entry [w][j] = j * 256^w * P (niels, affine),
+// w = 0..31, j = 0..128 (j = 0 is the identity), 128 B per entry (30 limbs + pad).
+// [k]P = sum_w comb[w][d_w] with d_w = byte_w(k + 0x80...80) - 128 in [-128, 127]:
+// 32 mixed additions and no doublings.
+constexpr int kCombWindows = 32;
+constexpr int kCombEntries = 129;
+constexpr int kCombEntryInt4 = 8;  // 128 B
+constexpr size_t kCombBytesPerKey = (size_t)kCombWindows * kCombEntries * kCombEntryInt4 * 16;
+
+// bases[key][w] = 256^w * (negate ? -A : A) as p3 (40 limbs); ok[key] = decode accepted.
+hipError_t launch_comb_bases(const uint8_t *pubs, uint32_t n, int negate, uint8_t *ok, int32_t *bases,
+                             hipStream_t stream);
+// comb[key] from bases[key] (n * 32 workgroups of 128 lanes).
+hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStream_t stream);
+// Key-cached verification: key index per signature into a keyset.
+hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
+                                const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
+                                const uint32_t *off, uint32_t n, uint8_t *out, hipStream_t stream);
+
 }  // namespace tmed

@@ -145,4 +145,124 @@ hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t
 
 void host_build_btab(ge_niels out[9]) { build_btab_niels(out); }
 
+// ============================================================ fixed-base combs
+
+__device__ __forceinline__ void p3_store(int32_t *dst, const ge_p3 &p) {
+  const fe *fs[4] = {&p.X, &p.Y, &p.Z, &p.T};
+#pragma unroll
+  for (int f = 0; f < 40; f++) dst[f] = fs[f / 10]->v[f % 10];
+}
+__device__ __forceinline__ void p3_load(ge_p3 &p, const int32_t *src) {
+  fe *fs[4] = {&p.X, &p.Y, &p.Z, &p.T};
+#pragma unroll
+  for (int f = 0; f < 40; f++) fs[f / 10]->v[f % 10] = src[f];
+}
+
+__global__ __launch_bounds__(64) void comb_bases_kernel(const uint8_t *__restrict__ pubs, uint32_t n, int negate,
+                                                       uint8_t *__restrict__ ok_out, int32_t *__restrict__ bases) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t pw[8];
+  load_row_words(pw, pubs + 32 * (size_t)i, 2);
+  ge_p3 P;
+  const bool ok = ge_frombytes_go(P, pw);
+  ok_out[i] = ok ? 1 : 0;
+  if (negate) { fe_neg(P.X, P.X); fe_neg(P.T, P.T); }
+#pragma unroll 1
+  for (int w = 0; w < kCombWindows; w++) {
+    p3_store(bases + ((size_t)i * kCombWindows + w) * 40, P);
+    ge_mul256(P);
+  }
+}
+
+__device__ __forceinline__ void niels_store(int4 *dst, const ge_niels &e) {
+  const fe *fs[3] = {&e.YpX, &e.YmX, &e.XY2d};
+#pragma unroll
+  for (int q = 0; q < kCombEntryInt4; q++) {
+    int32_t w[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int f = 4 * q + c;
+      w[c] = f < 30 ? fs[f / 10]->v[f % 10] : 0;
+    }
+    dst[q] = make_int4(w[0], w[1], w[2], w[3]);
+  }
+}
+__device__ __forceinline__ void niels_load(ge_niels &e, const int4 *src) {
+  fe *fs[3] = {&e.YpX, &e.YmX, &e.XY2d};
+#pragma unroll
+  for (int q = 0; q < kCombEntryInt4; q++) {
+    const int4 v = src[q];
+    const int32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int f = 4 * q + c;
+      if (f < 30) fs[f / 10]->v[f % 10] = w[c];
+    }
+  }
+}
+
+// One workgroup per (key, window); lane j computes (j+1) * base (verify_core.h comb_entry).
+__global__ __launch_bounds__(128) void comb_fill_kernel(const int32_t *__restrict__ bases, uint32_t n,
+                                                       int4 *__restrict__ comb) {
+  const uint32_t kw = blockIdx.x;  // key * 32 + window
+  const uint32_t j = threadIdx.x + 1;  // 1..128
+  ge_p3 P;
+  p3_load(P, bases + (size_t)kw * 40);
+  ge_niels e;
+  comb_entry(e, P, j);
+  int4 *row = comb + (size_t)kw * kCombEntries * kCombEntryInt4;
+  niels_store(row + (size_t)j * kCombEntryInt4, e);
+  if (threadIdx.x == 0) {
+    ge_niels id;
+    ge_niels_0(id);
+    niels_store(row, id);
+  }
+}
+
+struct GlobalComb {
+  const int4 *base;  // 32 windows x 129 entries x 8 int4
+  __device__ __forceinline__ void load(int w, int j, ge_niels &e) const {
+    niels_load(e, base + ((size_t)w * kCombEntries + j) * kCombEntryInt4);
+  }
+};
+
+__global__ __launch_bounds__(kThreadsPerBlock) void verify_keyset_kernel(
+    const uint32_t *__restrict__ val_idx, const uint8_t *__restrict__ key_pub, const uint8_t *__restrict__ key_ok,
+    const int4 *__restrict__ acomb, const int4 *__restrict__ bcomb, const uint8_t *__restrict__ sig,
+    const uint8_t *__restrict__ msgs, const uint32_t *__restrict__ off, uint32_t n, uint8_t *__restrict__ out) {
+  const GlobalComb bc{bcomb};
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t v = val_idx[i];
+    uint32_t pw[8], sw[16];
+    load_row_words(pw, key_pub + 32 * (size_t)v, 2);
+    load_row_words(sw, sig + 64 * (size_t)i, 4);
+    const uint32_t o0 = off[i], o1 = off[i + 1];
+    const GlobalComb ac{acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4};
+    out[i] = verify_one_comb(pw, key_ok[v] != 0, sw, msgs + o0, o1 - o0, ac, bc) ? 1 : 0;
+  }
+}
+
+hipError_t launch_comb_bases(const uint8_t *pubs, uint32_t n, int negate, uint8_t *ok, int32_t *bases,
+                             hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(comb_bases_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, pubs, n, negate, ok, bases);
+  return hipGetLastError();
+}
+
+hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(comb_fill_kernel, dim3(n * kCombWindows), dim3(128), 0, stream, bases, n, comb);
+  return hipGetLastError();
+}
+
+hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
+                                const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
+                                const uint32_t *off, uint32_t n, uint8_t *out, hipStream_t stream) {
+  const uint32_t grid = grid_for(n, 4096);
+  hipLaunchKernelGGL(verify_keyset_kernel, dim3(grid), dim3(kThreadsPerBlock), 0, stream, val_idx, key_pub, key_ok,
+                     acomb, bcomb, sig, msgs, off, n, out);
+  return hipGetLastError();
+}
+
 }  // namespace tmed

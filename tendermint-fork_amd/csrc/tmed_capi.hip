@@ -15,70 +15,9 @@
 #include "../../include/tmed25519.h"
 #include "kernels.h"
 
+#include "ctx.h"
+
 using namespace tmed;
-
-namespace {
-
-struct DevBuf {
-  void *p = nullptr;
-  size_t cap = 0;
-  hipError_t ensure(size_t bytes) {
-    if (bytes <= cap) return hipSuccess;
-    if (p) hipFree(p);
-    p = nullptr;
-    cap = 0;
-    size_t want = bytes + bytes / 4 + 256;
-    hipError_t e = hipMalloc(&p, want);
-    if (e == hipSuccess) cap = want;
-    return e;
-  }
-  void release() {
-    if (p) hipFree(p);
-    p = nullptr;
-    cap = 0;
-  }
-};
-
-struct HostBuf {
-  void *p = nullptr;
-  size_t cap = 0;
-  hipError_t ensure(size_t bytes) {
-    if (bytes <= cap) return hipSuccess;
-    if (p) hipHostFree(p);
-    p = nullptr;
-    cap = 0;
-    size_t want = bytes + bytes / 4 + 256;
-    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
-    if (e == hipSuccess) cap = want;
-    return e;
-  }
-  void release() {
-    if (p) hipHostFree(p);
-    p = nullptr;
-    cap = 0;
-  }
-};
-
-int map_err(hipError_t e) {
-  if (e == hipSuccess) return TMED_OK;
-  if (e == hipErrorOutOfMemory) return TMED_ENOMEM;
-  return TMED_EHIP;
-}
-
-}  // namespace
-
-struct tmed_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  float last_ms = 0.f;
-  std::mutex mu;
-  ge_niels *d_btab = nullptr;
-  int4 *d_slab = nullptr;
-  uint32_t slab_slots = 0;
-  DevBuf d_a, d_b, d_msg, d_off, d_out, d_c;
-  HostBuf h_a, h_b, h_msg, h_off, h_out, h_c;
-};
 
 extern "C" {
 
@@ -122,9 +61,22 @@ int tmed_init(int device, tmed_ctx **out) {
   // 8 waves/CU is plenty for the grid-stride loop (~377 MB of HBM).
   c->slab_slots = 1024 * kThreadsPerBlock;
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_slab, (size_t)c->slab_slots * kSlabSlotBytes);
-  if (e != hipSuccess) {
+  // Shared signed radix-256 comb of +B (528 KB, L2-resident) for the key-cached path.
+  uint8_t *d_bpub = nullptr, *d_bok = nullptr;
+  const uint8_t benc[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
+                            0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
+                            0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
+  if (e == hipSuccess) e = hipMalloc((void **)&c->d_bcomb, kCombBytesPerKey);
+  if (e == hipSuccess) e = hipMalloc((void **)&d_bpub, 32);
+  if (e == hipSuccess) e = hipMalloc((void **)&d_bok, 1);
+  if (e == hipSuccess) e = hipMemcpy(d_bpub, benc, 32, hipMemcpyHostToDevice);
+  int rc = map_err(e);
+  if (rc == TMED_OK) rc = build_comb(c, d_bpub, 1, /*negate=*/0, d_bok, c->d_bcomb);
+  if (d_bpub) (void)hipFree(d_bpub);
+  if (d_bok) (void)hipFree(d_bok);
+  if (rc != TMED_OK) {
     tmed_destroy(c);
-    return map_err(e);
+    return rc;
   }
   *out = c;
   return TMED_OK;
@@ -136,6 +88,9 @@ void tmed_destroy(tmed_ctx *c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   for (DevBuf *b : {&c->d_a, &c->d_b, &c->d_msg, &c->d_off, &c->d_out, &c->d_c}) b->release();
   for (HostBuf *b : {&c->h_a, &c->h_b, &c->h_msg, &c->h_off, &c->h_out, &c->h_c}) b->release();
+  for (auto &kv : c->keysets) free_keyset(kv.second);
+  c->keysets.clear();
+  if (c->d_bcomb) hipFree(c->d_bcomb);
   if (c->d_slab) hipFree(c->d_slab);
   if (c->d_btab) hipFree(c->d_btab);
   if (c->ev0) hipEventDestroy(c->ev0);

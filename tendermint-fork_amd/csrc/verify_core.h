@@ -171,6 +171,123 @@ TMED_HD void sign_one(uint32_t sig[16], uint32_t pub[8], const uint32_t seed[8],
   for (int i = 0; i < 8; i++) sig[8 + i] = s[i];
 }
 
+// ------------------------------------------------------------------ combs
+// Signed radix-256 comb (key cache): entry [w][j] = j * 256^w * P
+// in affine niels form, j = 0..128.  [k]P = sum_w entry[w][d_w] with
+// d_w = byte_w(k + 0x8080...80) - 128: 32 mixed additions, no doublings.
+
+// P <- 256 * P
+TMED_HD void ge_mul256(ge_p3 &P) {
+  ge_p1p1 t;
+  ge_p2 q;
+  ge_p3_to_p2(q, P);
+#pragma unroll 1
+  for (int d = 0; d < 7; d++) { ge_p2_dbl(t, q); ge_p1p1_to_p2(q, t); }
+  ge_p2_dbl(t, q);
+  ge_p1p1_to_p3(P, t);
+}
+
+// out = j * base (j in 1..255) in niels form; branch-free double-and-add.
+TMED_HD void comb_entry(ge_niels &out, const ge_p3 &base, uint32_t j) {
+  ge_cached cP;
+  ge_p3_to_cached(cP, base);
+  ge_p3 acc, sum;
+  ge_p3_0(acc);
+  ge_p1p1 t;
+  ge_p2 q;
+#pragma unroll 1
+  for (int b = 7; b >= 0; b--) {
+    ge_p3_to_p2(q, acc);
+    ge_p2_dbl(t, q);
+    ge_p1p1_to_p3(acc, t);
+    ge_add_cached(t, acc, cP, false);
+    ge_p1p1_to_p3(sum, t);
+    const bool bit = (j >> b) & 1;
+    fe_select(acc.X, acc.X, sum.X, bit);
+    fe_select(acc.Y, acc.Y, sum.Y, bit);
+    fe_select(acc.Z, acc.Z, sum.Z, bit);
+    fe_select(acc.T, acc.T, sum.T, bit);
+  }
+  fe zi, x, y, xy, d2;
+  fe_const_d2(d2);
+  fe_invert(zi, acc.Z);
+  fe_mul(x, acc.X, zi);
+  fe_mul(y, acc.Y, zi);
+  fe_add(out.YpX, y, x); fe_carry(out.YpX, out.YpX);
+  fe_sub(out.YmX, y, x); fe_carry(out.YmX, out.YmX);
+  fe_mul(xy, x, y);
+  fe_mul(out.XY2d, xy, d2);
+}
+
+// Signed radix-256 recoding: r = k + 0x8080...80; digit w = byte_w(r) - 128 (k < 2^255).
+TMED_HD void sc_recode256(uint32_t r[8], const uint32_t k[8]) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t t = (uint64_t)k[i] + 0x80808080u + c;
+    r[i] = (uint32_t)t;
+    c = t >> 32;
+  }
+}
+
+// e <- sign(d) * entry(|d|): -(y+x, y-x, 2dxy) = (y-x, y+x, -2dxy)
+TMED_HD void niels_apply_sign(ge_niels &e, bool neg) {
+  fe t;
+  fe_copy(t, e.YpX);
+  fe_select(e.YpX, e.YpX, e.YmX, neg);
+  fe_select(e.YmX, e.YmX, t, neg);
+  fe_neg(t, e.XY2d);
+  fe_select(e.XY2d, e.XY2d, t, neg);
+}
+
+// Key-cached verification: [k](-A) from the key's comb, [S]B from the shared comb.
+// AC/BC provide  void load(int window, int j, ge_niels&) const  for j in 0..128.
+template <class AC, class BC>
+TMED_HD bool verify_one_comb(const uint32_t pubw[8], bool key_ok, const uint32_t sigw[16], const uint8_t *msg,
+                             uint32_t mlen, const AC &acomb, const BC &bcomb) {
+  bool ok = key_ok && (sigw[15] & 0xE0000000u) == 0;
+  ok = ok && sc_is_canonical(sigw + 8);
+  uint32_t h[16], k[8], s[8], kr[8], sr[8];
+  sha512_stream(h, sigw, pubw, 64, msg, mlen);
+  sc_reduce512(k, h);
+#pragma unroll
+  for (int w = 0; w < 8; w++) s[w] = ok ? sigw[8 + w] : 0u;
+  sc_recode256(kr, k);
+  sc_recode256(sr, s);
+  ge_p3 acc;
+  ge_p3_0(acc);
+  ge_p1p1 t;
+  ge_niels e;
+#pragma unroll 1
+  for (int wd = 0; wd < 8; wd++) {
+    uint32_t kc = kr[0], scur = sr[0];
+#pragma unroll
+    for (int m = 0; m < 7; m++) { kr[m] = kr[m + 1]; sr[m] = sr[m + 1]; }
+#pragma unroll 1
+    for (int b = 0; b < 4; b++) {
+      const int w = wd * 4 + b;
+      const int da = (int)(kc & 0xffu) - 128;
+      const int db = (int)(scur & 0xffu) - 128;
+      kc >>= 8;
+      scur >>= 8;
+      acomb.load(w, da < 0 ? -da : da, e);
+      niels_apply_sign(e, da < 0);
+      ge_madd_niels(t, acc, e, false);
+      ge_p1p1_to_p3(acc, t);
+      bcomb.load(w, db < 0 ? -db : db, e);
+      niels_apply_sign(e, db < 0);
+      ge_madd_niels(t, acc, e, false);
+      ge_p1p1_to_p3(acc, t);
+    }
+  }
+  uint32_t enc[8];
+  ge_tobytes(enc, acc.X, acc.Y, acc.Z);
+  uint32_t diff = 0;
+#pragma unroll
+  for (int w = 0; w < 8; w++) diff |= enc[w] ^ sigw[w];
+  return ok && diff == 0;
+}
+
 // Host-side construction of the shared B table (j*B, j = 0..8, niels form),
 // using the same field code.  Run once per context.
 TMED_HD void build_btab_niels(ge_niels out[9]) {

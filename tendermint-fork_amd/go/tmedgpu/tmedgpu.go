@@ -1,0 +1,219 @@
+// Package tmedgpu is the reference-side cgo binding of libtmed25519_hip.so
+// (include/tmed25519.h) for Tendermint Core v0.34.24.
+//
+// It is NOT compiled in this repository (no Go toolchain in the build image);
+// it is the shim a maintainer adds under github.com/tendermint/tendermint/crypto/
+// to route the commit-verification loops to the GPU.  See INTEGRATION.md.
+//
+// Seam (SURVEY.md §8b): ValidatorSet.VerifyCommit / VerifyCommitLight /
+// VerifyCommitLightTrusting (types/validator_set.go:667-826) call
+// VerifyCommitsGPU instead of looping over crypto.PubKey.VerifySignature
+// (crypto/ed25519/ed25519.go:148-155).  Any error returned here means "take the
+// original Go path": the caller never guesses a decision.
+package tmedgpu
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../lib -ltmed25519_hip -Wl,-rpath,${SRCDIR}/../../lib
+#include <stdlib.h>
+#include "tmed25519.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"sync"
+	"unsafe"
+)
+
+// Engine wraps one tmed_ctx (one per GPU; safe for concurrent use: the
+// library serialises calls on a context).
+type Engine struct{ ctx *C.tmed_ctx }
+
+var (
+	once    sync.Once
+	defEng  *Engine
+	initErr error
+)
+
+// Default returns the process-wide engine on device 0 (or the init error).
+func Default() (*Engine, error) {
+	once.Do(func() {
+		var ctx *C.tmed_ctx
+		if rc := C.tmed_init(0, &ctx); rc != 0 {
+			initErr = errors.New(C.GoString(C.tmed_strerror(rc)))
+			return
+		}
+		defEng = &Engine{ctx: ctx}
+	})
+	return defEng, initErr
+}
+
+// Mode selects the reference loop being replaced.
+type Mode int
+
+const (
+	ModeCommit         Mode = C.TMED_MODE_COMMIT
+	ModeLight          Mode = C.TMED_MODE_LIGHT
+	ModeLightTrusting  Mode = C.TMED_MODE_LIGHT_TRUSTING
+)
+
+// Outcome codes (see tmed25519.h); the caller formats the same errors Go does.
+const (
+	OK              = C.TMED_COMMIT_OK
+	WrongSetSize    = C.TMED_COMMIT_WRONG_SET_SIZE
+	WrongHeight     = C.TMED_COMMIT_WRONG_HEIGHT
+	WrongBlockID    = C.TMED_COMMIT_WRONG_BLOCK_ID
+	WrongSignature  = C.TMED_COMMIT_WRONG_SIGNATURE
+	NotEnoughPower  = C.TMED_COMMIT_NOT_ENOUGH_POWER
+	DoubleVote      = C.TMED_COMMIT_DOUBLE_VOTE
+	ZeroDenominator = C.TMED_COMMIT_ZERO_DENOMINATOR
+	Overflow        = C.TMED_COMMIT_OVERFLOW
+)
+
+// ValSet / CommitData are flat copies of types.ValidatorSet / types.Commit
+// (filled by the caller in package types, which owns those types).
+type ValSet struct {
+	PubKeys    []byte  // n x 32
+	Powers     []int64 // n
+	Addresses  []byte  // n x 20
+	TotalPower int64
+}
+
+type BlockID struct {
+	Hash     []byte
+	PSHTotal uint32
+	PSHHash  []byte
+}
+
+type CommitData struct {
+	Height    int64
+	Round     int32
+	BlockID   BlockID
+	Flags     []byte  // BlockIDFlag per signature
+	Addresses []byte  // n x 20
+	TsSeconds []int64
+	TsNanos   []int32
+	Sigs      []byte // n x 64 (zero padded)
+	SigLens   []uint32
+}
+
+type Request struct {
+	Mode       Mode
+	ChainID    string
+	Vals       *ValSet
+	BlockID    *BlockID
+	Height     int64
+	Commit     *CommitData
+	TrustNum   int64
+	TrustDen   int64
+}
+
+type Result struct {
+	Code                   int
+	Got, Needed            int64
+	Expected, Actual       int64
+	Idx, IdxFirst, ValIdx  int32
+}
+
+// cgo pointer rules (Go 1.18: no runtime.Pinner): C memory must not hold Go
+// pointers, so every input is copied into one C arena for the duration of the
+// call (~200 B per signature, negligible next to the verification).  The
+// library itself copies into pinned buffers before launching.
+type arena struct{ ptrs []unsafe.Pointer }
+
+func (a *arena) bytes(b []byte) *C.uint8_t {
+	if len(b) == 0 {
+		return nil
+	}
+	p := C.CBytes(b)
+	a.ptrs = append(a.ptrs, p)
+	return (*C.uint8_t)(p)
+}
+
+func (a *arena) alloc(sz uintptr) unsafe.Pointer {
+	p := C.malloc(C.size_t(sz))
+	a.ptrs = append(a.ptrs, p)
+	return p
+}
+
+func (a *arena) i64(v []int64) *C.int64_t {
+	if len(v) == 0 {
+		return nil
+	}
+	p := a.alloc(uintptr(len(v)) * 8)
+	copy((*[1 << 30]int64)(p)[:len(v):len(v)], v)
+	return (*C.int64_t)(p)
+}
+
+func (a *arena) i32(v []int32) *C.int32_t {
+	if len(v) == 0 {
+		return nil
+	}
+	p := a.alloc(uintptr(len(v)) * 4)
+	copy((*[1 << 30]int32)(p)[:len(v):len(v)], v)
+	return (*C.int32_t)(p)
+}
+
+func (a *arena) u32(v []uint32) *C.uint32_t {
+	if len(v) == 0 {
+		return nil
+	}
+	p := a.alloc(uintptr(len(v)) * 4)
+	copy((*[1 << 30]uint32)(p)[:len(v):len(v)], v)
+	return (*C.uint32_t)(p)
+}
+
+func (a *arena) free() {
+	for _, p := range a.ptrs {
+		C.free(p)
+	}
+}
+
+func (a *arena) blockID(b *BlockID) C.tmed_block_id {
+	return C.tmed_block_id{hash: a.bytes(b.Hash), hash_len: C.uint32_t(len(b.Hash)), psh_total: C.uint32_t(b.PSHTotal),
+		psh_hash: a.bytes(b.PSHHash), psh_hash_len: C.uint32_t(len(b.PSHHash))}
+}
+
+// VerifyCommits verifies many commits with ONE device batch.
+func (e *Engine) VerifyCommits(reqs []Request) ([]Result, error) {
+	n := len(reqs)
+	if n == 0 {
+		return nil, nil
+	}
+	var a arena
+	defer a.free()
+	creqs := (*[1 << 26]C.tmed_commit_request)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_commit_request{})))[:n:n]
+	vs := (*[1 << 26]C.tmed_valset)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_valset{})))[:n:n]
+	cs := (*[1 << 26]C.tmed_commit)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_commit{})))[:n:n]
+	bids := (*[1 << 26]C.tmed_block_id)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_block_id{})))[:n:n]
+	for i := range reqs {
+		r := &reqs[i]
+		vs[i] = C.tmed_valset{n: C.size_t(len(r.Vals.Powers)), pubkeys: a.bytes(r.Vals.PubKeys),
+			powers: a.i64(r.Vals.Powers), addresses: a.bytes(r.Vals.Addresses), total_power: C.int64_t(r.Vals.TotalPower)}
+		c := r.Commit
+		cs[i] = C.tmed_commit{height: C.int64_t(c.Height), round: C.int32_t(c.Round), block_id: a.blockID(&c.BlockID),
+			n_sigs: C.size_t(len(c.Flags)), flags: a.bytes(c.Flags), addresses: a.bytes(c.Addresses),
+			ts_seconds: a.i64(c.TsSeconds), ts_nanos: a.i32(c.TsNanos), sigs: a.bytes(c.Sigs), sig_lens: a.u32(c.SigLens)}
+		bids[i] = C.tmed_block_id{}
+		if r.BlockID != nil {
+			bids[i] = a.blockID(r.BlockID)
+		}
+		cid := C.CString(r.ChainID)
+		a.ptrs = append(a.ptrs, unsafe.Pointer(cid))
+		creqs[i] = C.tmed_commit_request{mode: C.int(r.Mode), chain_id: cid, chain_id_len: C.uint32_t(len(r.ChainID)),
+			vals: &vs[i], block_id: &bids[i], height: C.int64_t(r.Height), commit: &cs[i],
+			trust_num: C.int64_t(r.TrustNum), trust_den: C.int64_t(r.TrustDen)}
+	}
+	res := make([]C.tmed_commit_result, n)
+	if rc := C.tmed_verify_commits(e.ctx, &creqs[0], C.size_t(n), &res[0]); rc != 0 {
+		return nil, errors.New(C.GoString(C.tmed_strerror(rc)))
+	}
+	out := make([]Result, n)
+	for i := range res {
+		out[i] = Result{Code: int(res[i].code), Got: int64(res[i].got), Needed: int64(res[i].needed),
+			Expected: int64(res[i].expected), Actual: int64(res[i].actual), Idx: int32(res[i].idx),
+			IdxFirst: int32(res[i].idx_first), ValIdx: int32(res[i].val_idx)}
+	}
+	return out, nil
+}

@@ -53,6 +53,14 @@ def lib() -> ctypes.CDLL:
     l.tmed_sign_batch.argtypes = [P, P, P, P, SZ, P, P]
     l.tmed_sign_batch_device.restype = I
     l.tmed_sign_batch_device.argtypes = [P, P, P, P, SZ, P, P, P]
+    l.tmed_keyset_load.restype = I
+    l.tmed_keyset_load.argtypes = [P, P, SZ, ctypes.POINTER(ctypes.c_uint64)]
+    l.tmed_keyset_free.restype = I
+    l.tmed_keyset_free.argtypes = [P, ctypes.c_uint64]
+    l.tmed_verify_batch_keyset.restype = I
+    l.tmed_verify_batch_keyset.argtypes = [P, ctypes.c_uint64, P, P, P, P, P, SZ, P]
+    l.tmed_verify_batch_keyset_device.restype = I
+    l.tmed_verify_batch_keyset_device.argtypes = [P, ctypes.c_uint64, P, P, P, P, SZ, P, P]
     l.tmed_last_kernel_ms.restype = ctypes.c_float
     l.tmed_last_kernel_ms.argtypes = [P]
     _lib = l
@@ -65,4 +73,5 @@ EXPORTED_SYMBOLS = [
     "tmed_verify_batch", "tmed_verify_batch_device",
     "tmed_sign_batch", "tmed_sign_batch_device", "tmed_last_kernel_ms",
     "tmed_vote_sign_bytes", "tmed_valu_peak", "tmed_verify_commits", "tmed_verify_commits_with",
+    "tmed_keyset_load", "tmed_keyset_free", "tmed_verify_batch_keyset", "tmed_verify_batch_keyset_device",
 ]

@@ -117,5 +117,43 @@ class Engine:
         if rc != TMED_OK:
             raise TmedError(rc, "tmed_sign_batch_device")
 
+    # ---- key-set cache (per validator set) ----------------------------------
+    def keyset_load(self, pubs: np.ndarray) -> int:
+        pubs = np.ascontiguousarray(pubs, dtype=np.uint8).reshape(-1, 32)
+        h = ctypes.c_uint64(0)
+        rc = lib().tmed_keyset_load(self._h, _p(pubs), pubs.shape[0], ctypes.byref(h))
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_keyset_load")
+        return h.value
+
+    def keyset_free(self, handle: int) -> None:
+        rc = lib().tmed_keyset_free(self._h, handle)
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_keyset_free")
+
+    def verify_keyset_arrays(self, handle: int, val_idx: np.ndarray, sigs: np.ndarray, msgs: np.ndarray,
+                             offs: np.ndarray, sig_lens: np.ndarray | None = None) -> np.ndarray:
+        n = val_idx.shape[0]
+        out = np.zeros(n, dtype=np.uint8)
+        if n == 0:
+            return out
+        vi = np.ascontiguousarray(val_idx, dtype=np.uint32)
+        sigs = np.ascontiguousarray(sigs, dtype=np.uint8).reshape(n, 64)
+        msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint32)
+        sl = None if sig_lens is None else np.ascontiguousarray(sig_lens, dtype=np.uint32)
+        rc = lib().tmed_verify_batch_keyset(self._h, handle, _p(vi), _p(sigs), None if sl is None else _p(sl),
+                                            _p(msgs), _p(offs), n, _p(out))
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_verify_batch_keyset")
+        return out
+
+    def verify_keyset_device(self, handle: int, d_val_idx, d_sig, d_msg, d_off, d_out, n: int, stream=None) -> None:
+        s = ctypes.c_void_p(stream) if stream else None
+        rc = lib().tmed_verify_batch_keyset_device(self._h, handle, d_val_idx.data_ptr(), d_sig.data_ptr(),
+                                                   d_msg.data_ptr(), d_off.data_ptr(), n, d_out.data_ptr(), s)
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_verify_batch_keyset_device")
+
     def last_kernel_ms(self) -> float:
         return float(lib().tmed_last_kernel_ms(self._h))

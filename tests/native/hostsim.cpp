@@ -6,6 +6,8 @@
 // product: the product library (libtmed25519_hip.so) has no CPU path.
 #include <stdint.h>
 #include <string.h>
+
+#include <vector>
 #include "verify_core.h"
 
 using namespace tmed;
@@ -55,6 +57,60 @@ void hostsim_sign_batch(const uint8_t *seeds, const uint8_t *msgs, const uint32_
     sign_one(sg, pb, seed, msgs + off[i], off[i + 1] - off[i], tab, bt);
     for (int w = 0; w < 16; w++) for (int b = 0; b < 4; b++) sig_out[64 * i + 4 * w + b] = (uint8_t)(sg[w] >> (8 * b));
     for (int w = 0; w < 8; w++) for (int b = 0; b < 4; b++) pub_out[32 * i + 4 * w + b] = (uint8_t)(pb[w] >> (8 * b));
+  }
+}
+
+// Key-cached (comb) verification on the host: builds every comb with the kernel's
+// comb_entry/ge_mul256 and runs verify_one_comb.
+struct HostComb {
+  std::vector<ge_niels> e;  // 32 x 129
+  void load(int w, int j, ge_niels &out) const { out = e[(size_t)w * 129 + j]; }
+};
+
+static void build_host_comb(HostComb &c, const uint32_t pw[8], bool negate, bool *ok) {
+  ge_p3 P;
+  *ok = ge_frombytes_go(P, pw);
+  if (negate) { fe_neg(P.X, P.X); fe_neg(P.T, P.T); }
+  c.e.resize(32 * 129);
+  for (int w = 0; w < 32; w++) {
+    ge_niels_0(c.e[(size_t)w * 129]);
+#pragma omp parallel for
+    for (int j = 1; j <= 128; j++) comb_entry(c.e[(size_t)w * 129 + j], P, (uint32_t)j);
+    ge_mul256(P);
+  }
+}
+
+void hostsim_verify_comb_batch(const uint8_t *keys, size_t nkeys, const uint32_t *key_idx, const uint8_t *sig,
+                               const uint8_t *msgs, const uint32_t *off, size_t n, uint8_t *out) {
+  static HostComb bcomb;
+  static bool binit = false;
+  if (!binit) {
+    uint32_t bw[8];
+    const uint8_t by[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
+                            0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
+                            0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
+    load_words8(bw, by);
+    bool ok;
+    build_host_comb(bcomb, bw, false, &ok);
+    binit = true;
+  }
+  std::vector<HostComb> ac(nkeys);
+  std::vector<uint8_t> kok(nkeys);
+  for (size_t k = 0; k < nkeys; k++) {
+    uint32_t pw[8];
+    load_words8(pw, keys + 32 * k);
+    bool ok;
+    build_host_comb(ac[k], pw, true, &ok);
+    kok[k] = ok;
+  }
+#pragma omp parallel for schedule(dynamic, 8)
+  for (long i = 0; i < (long)n; i++) {
+    uint32_t pw[8], sw[16];
+    const uint32_t v = key_idx[i];
+    load_words8(pw, keys + 32 * v);
+    load_words8(sw, sig + 64 * i);
+    load_words8(sw + 8, sig + 64 * i + 32);
+    out[i] = verify_one_comb(pw, kok[v] != 0, sw, msgs + off[i], off[i + 1] - off[i], ac[v], bcomb) ? 1 : 0;
   }
 }
 

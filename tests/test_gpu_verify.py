@@ -120,3 +120,42 @@ def test_product_signbytes_match_oracle():
         cid = "c" * int(rng.integers(0, 51))
         flag = 3 if bid is None else 2
         assert pvsb(cid, h, r, bid, ts, flag) == ovsb(cid, 2, h, r, bid if flag == 2 else None, ts)
+
+
+def test_keyset_golden_and_random(engine, golden):
+    """Key-cached comb path == generic path == oracle, on golden tuples grouped by key."""
+    vs = [v for v in golden if len(v["sig"]) == 128]
+    keys = sorted({v["pub"] for v in vs})
+    kidx = {k: i for i, k in enumerate(keys)}
+    karr = np.array([np.frombuffer(bytes.fromhex(k), np.uint8) for k in keys])
+    h = engine.keyset_load(karr)
+    try:
+        idx = np.array([kidx[v["pub"]] for v in vs], np.uint32)
+        sigs = np.array([np.frombuffer(bytes.fromhex(v["sig"]), np.uint8) for v in vs])
+        ms = [bytes.fromhex(v["msg"]) for v in vs]
+        offs = np.zeros(len(vs) + 1, np.uint32)
+        offs[1:] = np.cumsum([len(m) for m in ms])
+        msgs = np.frombuffer(b"".join(ms) + b"\0" * 16, np.uint8)
+        out = engine.verify_keyset_arrays(h, idx, sigs, msgs, offs)
+        exp = np.array([v["valid"] for v in vs], np.uint8)
+        assert (out == exp).all(), [vs[i]["class"] for i in np.nonzero(out != exp)[0]][:10]
+    finally:
+        engine.keyset_free(h)
+    # a 175-key set signing 20 commits' worth of votes, 1% corrupted
+    rng, seeds, msgs, offs = _random_batch(175, 77, (110, 125))
+    _, pubs = port.sign_batch(seeds, msgs, offs, 8)
+    h = engine.keyset_load(pubs)
+    try:
+        n = 3500
+        vi = rng.integers(0, 175, n).astype(np.uint32)
+        lens = rng.integers(100, 160, n)
+        o2 = np.zeros(n + 1, np.uint64)
+        o2[1:] = np.cumsum(lens)
+        m2 = rng.integers(0, 256, int(o2[-1]) + 16, dtype=np.uint8)
+        sig2, _ = port.sign_batch(seeds[vi], m2, o2, 8)
+        sig2[::97, 7] ^= 2
+        out = engine.verify_keyset_arrays(h, vi, sig2, m2, o2.astype(np.uint32))
+        exp = port.verify_batch(pubs[vi], sig2, m2, o2, 8)
+        assert (out == exp).all() and exp.sum() == n - len(range(0, n, 97))
+    finally:
+        engine.keyset_free(h)

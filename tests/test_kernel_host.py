@@ -104,3 +104,25 @@ def test_sign_matches_oracle(hostsim):
         m = msgs[offs[i]:offs[i + 1]].tobytes()
         assert sig[i].tobytes() == port.sign(seeds[i].tobytes(), m)
         assert pub[i].tobytes() == port.pubkey_from_seed(seeds[i].tobytes())
+
+
+def test_comb_path_hostsim(hostsim, golden):
+    """Key-cached (radix-256 comb) verification, host build of the kernel code, vs the oracle:
+    golden tuples grouped by key (incl. small-order, non-canonical and undecodable keys)."""
+    vs = [v for v in golden if len(v["sig"]) == 128][::4]
+    keys = sorted({v["pub"] for v in vs})[:40]
+    vs = [v for v in vs if v["pub"] in keys]
+    kidx = {k: i for i, k in enumerate(keys)}
+    karr = np.array([np.frombuffer(bytes.fromhex(k), np.uint8) for k in keys])
+    idx = np.array([kidx[v["pub"]] for v in vs], np.uint32)
+    sigs = np.array([np.frombuffer(bytes.fromhex(v["sig"]), np.uint8) for v in vs])
+    ms = [bytes.fromhex(v["msg"]) for v in vs]
+    offs = np.zeros(len(vs) + 1, np.uint32)
+    offs[1:] = np.cumsum([len(m) for m in ms])
+    msgs = np.frombuffer(b"".join(ms) + b"\0", np.uint8)
+    out = np.zeros(len(vs), np.uint8)
+    hostsim.hostsim_verify_comb_batch(_p(karr), ctypes.c_size_t(len(keys)), _p(idx), _p(sigs), _p(msgs), _p(offs),
+                                      ctypes.c_size_t(len(vs)), _p(out))
+    exp = np.array([v["valid"] for v in vs], np.uint8)
+    assert (out == exp).all(), [vs[i]["class"] for i in np.nonzero(out != exp)[0]]
+    assert exp.sum() > 10 and (exp == 0).sum() > 10

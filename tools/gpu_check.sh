@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU-box session: parity tests, bench, kernel-trace profile.  Every GPU step has its
+# own time limit; a fault/abort/timeout (124/134/137/139) ends the session there.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+OUT=gpurun_out
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+nproc > $OUT/nproc.txt; lscpu > $OUT/lscpu.txt 2>&1; (which go || echo "no go") >> $OUT/nproc.txt 2>&1
+STEPS="${*:-tests bench prof}"
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 900 python -m pytest tests -x -q -m gpu > $OUT/gpu_tests.log 2>&1; rc=$?
+      echo "tests rc=$rc" | tee -a $OUT/gpu_tests.log ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?
+      echo "smoke rc=$rc" | tee -a $OUT/smoke.log ;;
+    bench)
+      timeout -k 10 600 python bench.py > $OUT/bench.log 2>&1; rc=$?
+      echo "bench rc=$rc" | tee -a $OUT/bench.log; tail -1 $OUT/bench.log ;;
+    prof)
+      cd /tmp && export TMPDIR=/tmp
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1; rc=$?
+      cd $GRAFT_REPO_ROOT; echo "prof rc=$rc" | tee -a $OUT/prof.log ;;
+    *) echo "unknown step $s"; rc=0 ;;
+  esac
+  if fatal $rc; then echo "fatal rc=$rc in $s; stopping"; exit $rc; fi
+done
+exit 0
