@@ -84,7 +84,10 @@ def main():
     d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
     d_pub = torch.empty((n, 32), dtype=torch.uint8, device=dev)
     d_out = torch.zeros(n, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    # a dedicated (non-null) stream: the kernels and the timing events share it
+    torch_stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(torch_stream)
+    stream = torch_stream.cuda_stream
     eng.sign_device(d_seed, d_msg, d_off, d_sig, d_pub, n, stream)
     torch.cuda.synchronize(dev)
     t_gen = time.time() - t_gen

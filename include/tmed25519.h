@@ -145,7 +145,8 @@ int tmed_vote_sign_bytes(const tmed_vote_template *t, size_t n, const uint8_t *f
 /*
  * Integer-VALU peak probe for the roofline: runs a
  * dependency-free stream of `kind` instructions on every lane of the device
- * (0 = v_mad_i64_i32, 1 = v_mad_u64_u32, 2 = v_add_u32, 3 = v_mul_lo_u32)
+ * (0 v_mad_i64_i32, 1 v_mad_u64_u32, 2 v_add_u32, 3 v_mul_lo_u32, 4 v_ashrrev_i64,
+ * 5 v_lshl_add_u64, 6 v_lshl_add_u32, 7 v_add_co_u32+v_addc_co_u32)
  * and returns the sustained rate in 1e9 instructions (lane-ops) per second.
  */
 int tmed_valu_peak(tmed_ctx *ctx, int kind, double *giga_ops_per_s);
@@ -168,6 +169,7 @@ typedef struct {
   const int64_t *powers;    /* n voting powers */
   const uint8_t *addresses; /* n x 20, PubKey.Address(); needed by LightTrusting only (may be NULL otherwise) */
   int64_t total_power;      /* vals.TotalVotingPower() (its panics stay in Go, :298-321) */
+  uint64_t keyset;          /* 0, or a tmed_keyset_load handle of exactly these pubkeys (key-cached path) */
 } tmed_valset;
 
 /* Commit + CommitSigs (types/block.go:575-634, 737-752). */

@@ -16,6 +16,7 @@
 //      exit, Got/Needed and error kinds come out identical by construction.
 #include <string.h>
 
+#include <functional>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -87,9 +88,17 @@ int check_request(const tmed_commit_request &r) {
 
 }  // namespace
 
-extern "C" int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out,
-                                        tmed_batch_verify_fn verify, void *user) {
-  if (!verify || (n && (!reqs || !out))) return TMED_EINVAL;
+// Flattened candidates of one seam call.
+struct CandBatch {
+  size_t m = 0;
+  std::vector<uint8_t> pubs, sigs, msgs;
+  std::vector<uint32_t> lens, offs, val_idx;
+  std::vector<uint64_t> keyset;
+};
+using BatchVerifier = std::function<int(const CandBatch &, uint8_t *valid)>;
+
+static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, const BatchVerifier &verify) {
+  if (n && (!reqs || !out)) return TMED_EINVAL;
   std::vector<Plan> plans(n);
   std::vector<Cand> cands;
   for (size_t q = 0; q < n; q++) {
@@ -161,8 +170,16 @@ extern "C" int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t 
   const size_t m = cands.size();
   std::vector<uint8_t> valid(m, 0);
   if (m) {
-    std::vector<uint8_t> pubs(m * 32), sigs(m * 64);
-    std::vector<uint32_t> lens(m), offs(m + 1);
+    CandBatch cb;
+    cb.m = m;
+    cb.pubs.resize(m * 32);
+    cb.sigs.resize(m * 64);
+    cb.lens.resize(m);
+    cb.offs.resize(m + 1);
+    cb.val_idx.resize(m);
+    cb.keyset.resize(m);
+    std::vector<uint8_t> &pubs = cb.pubs, &sigs = cb.sigs;
+    std::vector<uint32_t> &lens = cb.lens, &offs = cb.offs;
     std::vector<tmed::VoteEncoder> enc(n);
     for (size_t q = 0; q < n; q++) {
       if (plans[q].decided) continue;
@@ -188,7 +205,8 @@ extern "C" int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t 
       if (total > 0xffffffffu) return TMED_EINVAL;
     }
     offs[m] = (uint32_t)total;
-    std::vector<uint8_t> msgs(total + 16);
+    cb.msgs.resize(total + 16);
+    std::vector<uint8_t> &msgs = cb.msgs;
     for (size_t k = 0; k < m; k++) {
       const Cand &cd = cands[k];
       const tmed_commit_request &r = reqs[cd.req];
@@ -199,8 +217,10 @@ extern "C" int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t 
       const uint32_t sl = c.sig_lens ? c.sig_lens[i] : 64;
       memcpy(&sigs[k * 64], c.sigs + 64 * i, sl < 64 ? sl : 64);
       lens[k] = sl;
+      cb.val_idx[k] = (uint32_t)cd.val_idx;
+      cb.keyset[k] = r.vals->keyset;
     }
-    int rc = verify(user, pubs.data(), sigs.data(), lens.data(), msgs.data(), offs.data(), m, valid.data());
+    int rc = verify(cb, valid.data());
     if (rc != TMED_OK) return rc;
   }
 
@@ -262,13 +282,55 @@ extern "C" int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t 
   return TMED_OK;
 }
 
-static int ctx_verify(void *user, const uint8_t *pubs, const uint8_t *sigs, const uint32_t *lens, const uint8_t *msgs,
-                      const uint32_t *offs, size_t m, uint8_t *out) {
-  return tmed_verify_batch((tmed_ctx *)user, pubs, sigs, lens, msgs, offs, m, out);
+extern "C" int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out,
+                                        tmed_batch_verify_fn verify, void *user) {
+  if (!verify) return TMED_EINVAL;
+  return run_seam(reqs, n, out, [&](const CandBatch &cb, uint8_t *valid) {
+    return verify(user, cb.pubs.data(), cb.sigs.data(), cb.lens.data(), cb.msgs.data(), cb.offs.data(), cb.m, valid);
+  });
+}
+
+// GPU verifier: candidates of validator sets with a key-set handle go through the
+// key-cached kernel (one launch per distinct key set), the rest through the generic one.
+static int ctx_verify(tmed_ctx *ctx, const CandBatch &cb, uint8_t *valid) {
+  std::unordered_map<uint64_t, std::vector<uint32_t>> groups;
+  for (size_t k = 0; k < cb.m; k++) groups[cb.keyset[k]].push_back((uint32_t)k);
+  if (groups.size() == 1 && groups.begin()->first == 0)
+    return tmed_verify_batch(ctx, cb.pubs.data(), cb.sigs.data(), cb.lens.data(), cb.msgs.data(), cb.offs.data(),
+                             cb.m, valid);
+  for (auto &g : groups) {
+    const std::vector<uint32_t> &ix = g.second;
+    const size_t m = ix.size();
+    std::vector<uint8_t> pubs(m * 32), sigs(m * 64), msgs, out(m);
+    std::vector<uint32_t> lens(m), offs(m + 1), vidx(m);
+    size_t total = 0;
+    for (size_t j = 0; j < m; j++) total += cb.offs[ix[j] + 1] - cb.offs[ix[j]];
+    msgs.resize(total + 16);
+    total = 0;
+    for (size_t j = 0; j < m; j++) {
+      const uint32_t k = ix[j];
+      memcpy(&pubs[j * 32], &cb.pubs[k * 32], 32);
+      memcpy(&sigs[j * 64], &cb.sigs[k * 64], 64);
+      lens[j] = cb.lens[k];
+      vidx[j] = cb.val_idx[k];
+      const uint32_t len = cb.offs[k + 1] - cb.offs[k];
+      offs[j] = (uint32_t)total;
+      memcpy(&msgs[total], &cb.msgs[cb.offs[k]], len);
+      total += len;
+    }
+    offs[m] = (uint32_t)total;
+    int rc = g.first == 0
+                 ? tmed_verify_batch(ctx, pubs.data(), sigs.data(), lens.data(), msgs.data(), offs.data(), m, out.data())
+                 : tmed_verify_batch_keyset(ctx, g.first, vidx.data(), sigs.data(), lens.data(), msgs.data(),
+                                            offs.data(), m, out.data());
+    if (rc != TMED_OK) return rc;
+    for (size_t j = 0; j < m; j++) valid[ix[j]] = out[j];
+  }
+  return TMED_OK;
 }
 
 extern "C" int tmed_verify_commits(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
                                    tmed_commit_result *out) {
   if (!ctx) return TMED_EINVAL;
-  return tmed_verify_commits_with(reqs, n, out, ctx_verify, ctx);
+  return run_seam(reqs, n, out, [&](const CandBatch &cb, uint8_t *valid) { return ctx_verify(ctx, cb, valid); });
 }

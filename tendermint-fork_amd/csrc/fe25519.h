@@ -32,6 +32,29 @@ namespace tmed {
 
 struct fe { int32_t v[10]; };
 
+// x*19 and x*38 as two full-rate v_lshl_add_u32 (LLVM would otherwise fold the
+// shift-adds back into v_mul_lo_u32, a multi-pass op on CDNA).
+TMED_HD int32_t mul19(int32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t t, r;
+  asm("v_lshl_add_u32 %0, %1, 4, %1" : "=v"(t) : "v"(x));      // 17x
+  asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(r) : "v"(x), "v"(t));  // 19x
+  return (int32_t)r;
+#else
+  return (int32_t)(19u * (uint32_t)x);
+#endif
+}
+TMED_HD int32_t mul38(int32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t t, r;
+  asm("v_lshl_add_u32 %0, %1, 4, %1" : "=v"(t) : "v"(x));      // 17x
+  asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(r) : "v"(x), "v"(t));  // 19x
+  return (int32_t)(r << 1);
+#else
+  return (int32_t)(38u * (uint32_t)x);
+#endif
+}
+
 TMED_HD void fe_0(fe &h) {
 #pragma unroll
   for (int i = 0; i < 10; i++) h.v[i] = 0;
@@ -91,7 +114,7 @@ TMED_HD void fe_carry(fe &h, const fe &f) {
 TMED_HD void fe_mul(fe &h, const fe &f, const fe &g) {
   int32_t g19[10], f2[10];
 #pragma unroll
-  for (int j = 0; j < 10; j++) g19[j] = (int32_t)(19u * (uint32_t)g.v[j]);
+  for (int j = 0; j < 10; j++) g19[j] = mul19(g.v[j]);
 #pragma unroll
   for (int i = 0; i < 10; i++) f2[i] = (int32_t)(2u * (uint32_t)f.v[i]);
   int64_t acc[10];
@@ -119,7 +142,7 @@ TMED_HD void fe_sq_acc(int64_t acc[10], const fe &f) {
 #pragma unroll
   for (int i = 0; i < 10; i++) {
     const uint32_t u = (uint32_t)f.v[i];
-    x2[i] = (int32_t)(2u * u); x19[i] = (int32_t)(19u * u); x38[i] = (int32_t)(38u * u);
+    x2[i] = (int32_t)(2u * u); x19[i] = mul19(f.v[i]); x38[i] = mul38(f.v[i]);
   }
 #pragma unroll
   for (int k = 0; k < 10; k++) acc[k] = 0;

@@ -1,10 +1,11 @@
-// microbench.hip — integer-VALU peak probe used as the roofline denominator.
+// microbench.hip — integer-VALU peak probes (roofline denominator and cost model).
 //
 // the verify kernel is bound by 32x32->64 integer multiply-adds;
-// "peak_mad_rate = measured v_mad_u64_u32 throughput from a gfx950
-// microbenchmark".  Each lane runs 16 independent accumulation chains (enough
-// ILP to hide the dependent latency) for `iters` iterations; the result is
-// folded into one store so nothing is dead-code-eliminated.
+// "peak_mad_rate = measured v_mad throughput from a gfx950 microbenchmark".
+// Each lane runs 16 independent chains of ONE instruction (inline asm, so the
+// compiler cannot fold or re-select it) for `iters` x 8 steps.  The same probe,
+// run for the other instructions the field arithmetic emits, gives the per-
+// instruction issue cost used in DESIGN.md's cost model.
 #include <hip/hip_runtime.h>
 
 #include "../../include/tmed25519.h"
@@ -15,69 +16,86 @@ constexpr int kChains = 16;
 constexpr int kUnroll = 8;
 
 template <int KIND>
+__device__ __forceinline__ void step(uint64_t &x, uint32_t b) {
+  uint32_t lo = (uint32_t)x;
+  if constexpr (KIND == 0) asm volatile("v_mad_i64_i32 %0, vcc, %1, %2, %0" : "+v"(x) : "v"(lo), "v"(b) : "vcc");
+  if constexpr (KIND == 1) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(x) : "v"(lo), "v"(b) : "vcc");
+  if constexpr (KIND == 2) { asm volatile("v_add_u32 %0, %0, %1" : "+v"(lo) : "v"(b)); x = lo; }
+  if constexpr (KIND == 3) { asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(lo) : "v"(b)); x = lo; }
+  if constexpr (KIND == 4) asm volatile("v_ashrrev_i64 %0, 3, %0" : "+v"(x));
+  if constexpr (KIND == 5) asm volatile("v_lshl_add_u64 %0, %0, 2, %0" : "+v"(x));
+  if constexpr (KIND == 6) { asm volatile("v_lshl_add_u32 %0, %0, 4, %1" : "+v"(lo) : "v"(b)); x = lo; }
+  if constexpr (KIND == 7) asm volatile("v_add_co_u32 %0, vcc, %0, %1\n\tv_addc_co_u32 %2, vcc, 0, %2, vcc"
+                                        : "+v"(lo), "+v"(b), "+v"(lo) :: "vcc");
+}
+
+template <int KIND>
 __global__ __launch_bounds__(256) void valu_probe(uint32_t iters, uint32_t seed, uint64_t *sink) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t a = seed ^ t, b = seed * 2654435761u + t;
-  int64_t si[kChains];
-  uint64_t su[kChains];
-  uint32_t s32[kChains];
+  const uint32_t b = seed * 2654435761u + t;
+  uint64_t s[kChains];
 #pragma unroll
-  for (int c = 0; c < kChains; c++) { si[c] = c + t; su[c] = c ^ t; s32[c] = c * t; }
+  for (int c = 0; c < kChains; c++) s[c] = (uint64_t)(c + 1) * 0x9E3779B97F4A7C15ull ^ t;
   for (uint32_t i = 0; i < iters; i++) {
 #pragma unroll
     for (int u = 0; u < kUnroll; u++) {
 #pragma unroll
-      for (int c = 0; c < kChains; c++) {
-        if (KIND == 0) si[c] = (int64_t)(int32_t)si[c] * (int64_t)(int32_t)b + si[c];
-        if (KIND == 1) su[c] = (uint64_t)(uint32_t)su[c] * (uint64_t)b + su[c];
-        if (KIND == 2) s32[c] = s32[c] + s32[c ^ 1];
-        if (KIND == 3) s32[c] = s32[c] * s32[c ^ 1];
-      }
+      for (int c = 0; c < kChains; c++) step<KIND>(s[c], b);
     }
-    asm volatile("" : "+v"(b));  // keep the operands live & opaque
   }
   uint64_t acc = 0;
 #pragma unroll
-  for (int c = 0; c < kChains; c++) acc += (uint64_t)si[c] + su[c] + s32[c];
+  for (int c = 0; c < kChains; c++) acc += s[c];
   if (acc == 0x1234567890abcdefull) sink[0] = acc;
+}
+
+template <int KIND>
+void launch_probe(uint32_t blocks, uint32_t it, uint64_t *sink) {
+  hipLaunchKernelGGL(valu_probe<KIND>, dim3(blocks), dim3(256), 0, 0, it, 7u, sink);
 }
 
 }  // namespace
 
+// kind: 0 v_mad_i64_i32, 1 v_mad_u64_u32, 2 v_add_u32, 3 v_mul_lo_u32, 4 v_ashrrev_i64,
+//       5 v_lshl_add_u64, 6 v_lshl_add_u32, 7 v_add_co_u32+v_addc_co_u32 (counted as 2)
 extern "C" int tmed_valu_peak(tmed_ctx *ctx, int kind, double *gops) {
   (void)ctx;
-  if (!gops || kind < 0 || kind > 3) return TMED_EINVAL;
+  if (!gops || kind < 0 || kind > 7) return TMED_EINVAL;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return TMED_EHIP;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return TMED_EHIP;
   uint64_t *sink = nullptr;
   if (hipMalloc(&sink, 8) != hipSuccess) return TMED_ENOMEM;
-  const uint32_t blocks = prop.multiProcessorCount * 8;  // 8 waves of 256 lanes per CU... 2048 threads/CU
-  const uint32_t iters = 4096;
-  hipEvent_t e0, e1;
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
+  const uint32_t blocks = prop.multiProcessorCount * 8;  // 8 x 256 lanes per CU (8 waves/SIMD)
+  const uint32_t iters = 2048;
   auto launch = [&](uint32_t it) {
     switch (kind) {
-      case 0: hipLaunchKernelGGL(valu_probe<0>, dim3(blocks), dim3(256), 0, 0, it, 7u, sink); break;
-      case 1: hipLaunchKernelGGL(valu_probe<1>, dim3(blocks), dim3(256), 0, 0, it, 7u, sink); break;
-      case 2: hipLaunchKernelGGL(valu_probe<2>, dim3(blocks), dim3(256), 0, 0, it, 7u, sink); break;
-      default: hipLaunchKernelGGL(valu_probe<3>, dim3(blocks), dim3(256), 0, 0, it, 7u, sink); break;
+      case 0: launch_probe<0>(blocks, it, sink); break;
+      case 1: launch_probe<1>(blocks, it, sink); break;
+      case 2: launch_probe<2>(blocks, it, sink); break;
+      case 3: launch_probe<3>(blocks, it, sink); break;
+      case 4: launch_probe<4>(blocks, it, sink); break;
+      case 5: launch_probe<5>(blocks, it, sink); break;
+      case 6: launch_probe<6>(blocks, it, sink); break;
+      default: launch_probe<7>(blocks, it, sink); break;
     }
   };
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
   launch(64);  // warm
-  hipEventRecord(e0, 0);
+  (void)hipEventRecord(e0, 0);
   launch(iters);
-  hipEventRecord(e1, 0);
+  (void)hipEventRecord(e1, 0);
   hipError_t e = hipEventSynchronize(e1);
   float ms = 0.f;
   if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  hipFree(sink);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(sink);
   if (e != hipSuccess) return TMED_EHIP;
-  const double ops = (double)blocks * 256.0 * iters * kUnroll * kChains;
+  const double ops = (double)blocks * 256.0 * iters * kUnroll * kChains * (kind == 7 ? 2 : 1);
   *gops = ops / (ms * 1e-3) / 1e9;
   return TMED_OK;
 }

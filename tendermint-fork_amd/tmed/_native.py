@@ -32,6 +32,14 @@ def lib() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: when PyTorch-ROCm is present its bundled
+    # libamdhip64.so.7 must be the one loaded (our NEEDED libamdhip64.so.7 then
+    # binds to it).  Loading ours first would pull /opt/rocm's copy and a second
+    # runtime would appear when torch loads, which cannot see the GPUs.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError("tmed: %s is missing — run __graft_entry__.build() (hipcc --offload-arch=gfx950); "
                           "there is no CPU fallback" % LIB_PATH)

@@ -37,11 +37,11 @@ def scenarios(seed=1, count=60):
                 kind = rng.randrange(3)
                 if kind == 0:
                     resign(cm, i, seeds[i], "other-chain")
-                elif kind == 1:
+                elif kind == 1 and cm.signatures[i].signature:
                     s = bytearray(cm.signatures[i].signature)
-                    s[rng.randrange(64)] ^= 1
+                    s[rng.randrange(len(s))] ^= 1
                     cm.signatures[i].signature = bytes(s)
-                else:
+                elif kind == 2:
                     cm.signatures[i].signature = cm.signatures[i].signature[:rng.randrange(64)]
         mode = rng.randrange(3)
         want_bid, want_h = bid, h

@@ -23,6 +23,21 @@ for s in $STEPS; do
       cd /tmp && export TMPDIR=/tmp
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1; rc=$?
       cd $GRAFT_REPO_ROOT; echo "prof rc=$rc" | tee -a $OUT/prof.log ;;
+    probe)
+      timeout -k 10 300 python tools/probe_valu.py > $OUT/probe_valu.json 2>$OUT/probe_valu.err; rc=$?
+      echo "probe rc=$rc"; cat $OUT/probe_valu.json ;;
+    counters)
+      timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1; rc=$? ;;
+    pmc)
+      cd /tmp && export TMPDIR=/tmp
+      rc=0
+      for ctr in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE" "SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES"; do
+        tag=$(echo $ctr | tr ' ' '_')
+        timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$OUT/pmc_$tag -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-peak > $GRAFT_REPO_ROOT/$OUT/pmc_$tag.log 2>&1; rc=$?
+        echo "pmc $ctr rc=$rc" | tee -a $GRAFT_REPO_ROOT/$OUT/pmc.log
+        if fatal $rc; then break; fi
+      done
+      cd $GRAFT_REPO_ROOT ;;
     *) echo "unknown step $s"; rc=0 ;;
   esac
   if fatal $rc; then echo "fatal rc=$rc in $s; stopping"; exit $rc; fi
