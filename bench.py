@@ -33,11 +33,15 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "tendermint-fork_amd"))
 
-# v_mad_i64_i32 per verification of the generic (no key cache) kernel, counted from
-# its formulas (DESIGN.md "Roofline"): 64 windows x (16 sq + 27 mul) + table 64 mul +
-# decompression 255 sq + 21 mul + encoding 254 sq + 13 mul; mul = 100, sq = 55 mads;
-# + 188 mad_u64 in the mod-L reduction.
-MADS_PER_VERIFY_GENERIC = 64 * (16 * 55 + 27 * 100) + 64 * 100 + (255 * 55 + 21 * 100) + (254 * 55 + 13 * 100) + 188
+# v_mad_i64_i32 per verification of the generic (no key cache) kernel, counted from its
+# formulas (DESIGN.md "Roofline"); field mul = 100 mads, square = 55 (radix 2^25.5).
+MUL, SQ = 100, 55
+MADS_STRAUS = 32 * (32 * SQ + 47 * MUL)     # 32 x (8 dbl + 2 cached adds (-A) + 1 niels add (B))
+MADS_TABLE = 64 * MUL                        # 1..8 x (-A), cached form
+MADS_DECODE = 255 * SQ + 21 * MUL + MUL      # Point.SetBytes (sqrt-ratio chain) + T = XY
+MADS_ENCODE = 254 * SQ + 13 * MUL            # inversion + canonical encoding of R'
+MADS_SCALAR = 188                            # mod-L Barrett (v_mad_u64_u32)
+MADS_PER_VERIFY_GENERIC = MADS_STRAUS + MADS_TABLE + MADS_DECODE + MADS_ENCODE + MADS_SCALAR
 
 
 def parse():

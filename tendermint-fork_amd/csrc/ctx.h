@@ -80,6 +80,7 @@ struct tmed_ctx {
   tmed::ge_niels *d_btab = nullptr;
   int4 *d_bcomb = nullptr;  // signed radix-256 comb of +B (shared)
   int4 *d_slab = nullptr;
+  int4 *d_prep = nullptr;
   uint32_t slab_slots = 0;
   tmed::DevBuf d_a, d_b, d_msg, d_off, d_out, d_c;
   tmed::HostBuf h_a, h_b, h_msg, h_off, h_out, h_c;

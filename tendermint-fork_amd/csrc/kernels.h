@@ -15,13 +15,17 @@ constexpr uint32_t kSlabSlotBytes = 9 * 160;
 
 hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                          uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
-                         hipStream_t stream);
+                         int4 *prep, hipStream_t stream);
 
 hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t *off, uint32_t n, uint8_t *sig_out,
                        uint8_t *pub_out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
                        hipStream_t stream);
 
-void host_build_btab(ge_niels out[9]);
+// Shared fixed-base table j*B, j = 0..128 (niels), staged in LDS by the kernels.
+constexpr int kBTabSize = 129;
+// prep hand-off bytes per signature slot (k, s, A.x, A.y, ok)
+constexpr uint32_t kPrepSlotBytes = 160;
+void host_build_btab(ge_niels out[129]);
 
 // ---- fixed-base combs (key cache) -------------------------------
 // Signed radix-256 comb of a point P: entry [w][j] = j * 256^w * P (niels, affine),
@@ -41,6 +45,7 @@ hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStr
 // Key-cached verification: key index per signature into a keyset.
 hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
                                 const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
-                                const uint32_t *off, uint32_t n, uint8_t *out, hipStream_t stream);
+                                const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
+                                hipStream_t stream);
 
 }  // namespace tmed

@@ -55,6 +55,50 @@ struct LdsBTab {
   __device__ __forceinline__ void load(int j, ge_niels &n) const { n = t[j]; }
 };
 
+constexpr int kBTabEntries = 129;  // j*B, j = 0..128 (niels) — 15.5 KB of LDS
+
+__device__ __forceinline__ void stage_btab(ge_niels *sbt, const ge_niels *btab_g) {
+  int32_t *dst = reinterpret_cast<int32_t *>(sbt);
+  const int32_t *src = reinterpret_cast<const int32_t *>(btab_g);
+  for (int i = threadIdx.x; i < kBTabEntries * 30; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+}
+
+// Per-signature hand-off from the prep to the main kernel: k, s, A.x, A.y, ok
+// (37 words padded to 10 x int4), stored [chunk q][slot] for coalescing.
+constexpr int kPrepInt4 = 10;
+
+__device__ __forceinline__ void prep_store(int4 *prep, uint32_t stride, uint32_t slot, const uint32_t k[8],
+                                           const uint32_t s[8], const ge_p3 &A, bool ok) {
+  int32_t w[40];
+#pragma unroll
+  for (int i = 0; i < 8; i++) { w[i] = (int32_t)k[i]; w[8 + i] = (int32_t)s[i]; }
+#pragma unroll
+  for (int i = 0; i < 10; i++) { w[16 + i] = A.X.v[i]; w[26 + i] = A.Y.v[i]; }
+  w[36] = ok ? 1 : 0;
+  w[37] = w[38] = w[39] = 0;
+#pragma unroll
+  for (int q = 0; q < kPrepInt4; q++)
+    prep[(size_t)q * stride + slot] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
+__device__ __forceinline__ bool prep_load(const int4 *prep, uint32_t stride, uint32_t slot, uint32_t k[8],
+                                          uint32_t s[8], ge_p3 &A) {
+  int32_t w[40];
+#pragma unroll
+  for (int q = 0; q < kPrepInt4; q++) {
+    const int4 v = prep[(size_t)q * stride + slot];
+    w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) { k[i] = (uint32_t)w[i]; s[i] = (uint32_t)w[8 + i]; }
+#pragma unroll
+  for (int i = 0; i < 10; i++) { A.X.v[i] = w[16 + i]; A.Y.v[i] = w[26 + i]; }
+  fe_1(A.Z);
+  fe_mul(A.T, A.X, A.Y);
+  return w[36] != 0;
+}
+
 __device__ __forceinline__ void load_row_words(uint32_t *w, const uint8_t *p, int nwords16) {
   const uint4 *q = reinterpret_cast<const uint4 *>(p);
 #pragma unroll
@@ -66,41 +110,47 @@ __device__ __forceinline__ void load_row_words(uint32_t *w, const uint8_t *p, in
   }
 }
 
-__global__ __launch_bounds__(kThreadsPerBlock) void verify_kernel(
+// Phase 1: SHA-512(R||A||M) mod L, S < L, A = Point.SetBytes(pub)  (one lane per signature
+// of the chunk [base, base + count)).
+__global__ __launch_bounds__(kThreadsPerBlock) void verify_prep_kernel(
     const uint8_t *__restrict__ pub, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msgs,
-    const uint32_t *__restrict__ off, uint32_t n, uint8_t *__restrict__ out, int4 *__restrict__ slab,
-    uint32_t slab_stride, const ge_niels *__restrict__ btab_g) {
-  __shared__ ge_niels sbt[9];
-  {
-    int32_t *dst = reinterpret_cast<int32_t *>(sbt);
-    const int32_t *src = reinterpret_cast<const int32_t *>(btab_g);
-    for (int i = threadIdx.x; i < 9 * 30; i += blockDim.x) dst[i] = src[i];
-  }
-  __syncthreads();
-  const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
-  const SlabTab tab{slab, slab_stride, gtid};
+    const uint32_t *__restrict__ off, uint32_t base, uint32_t count, int4 *__restrict__ prep, uint32_t stride) {
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= count) return;
+  const uint32_t i = base + slot;
+  uint32_t pw[8], sw[16], k[8], s[8];
+  load_row_words(pw, pub + 32 * (size_t)i, 2);
+  load_row_words(sw, sig + 64 * (size_t)i, 4);
+  const uint32_t o0 = off[i], o1 = off[i + 1];
+  ge_p3 A;
+  const bool ok = verify_prep(pw, sw, msgs + o0, o1 - o0, k, s, A);
+  prep_store(prep, stride, slot, k, s, A, ok);
+}
+
+// Phase 2: table of -A, Straus [k](-A) + [s]B, encode, compare with R.
+__global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_kernel(
+    const uint8_t *__restrict__ sig, uint32_t base, uint32_t count, const int4 *__restrict__ prep,
+    uint32_t stride, int4 *__restrict__ slab, const ge_niels *__restrict__ btab_g, uint8_t *__restrict__ out) {
+  __shared__ ge_niels sbt[kBTabEntries];
+  stage_btab(sbt, btab_g);
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= count) return;
+  const uint32_t i = base + slot;
+  uint32_t k[8], s[8], Rw[8];
+  ge_p3 A;
+  const bool ok = prep_load(prep, stride, slot, k, s, A);
+  load_row_words(Rw, sig + 64 * (size_t)i, 2);
+  SlabTab tab{slab, stride, slot};
   const LdsBTab bt{sbt};
-  for (uint32_t i = gtid; i < n; i += gridDim.x * blockDim.x) {
-    uint32_t pw[8], sw[16];
-    load_row_words(pw, pub + 32 * (size_t)i, 2);
-    load_row_words(sw, sig + 64 * (size_t)i, 4);
-    const uint32_t o0 = off[i], o1 = off[i + 1];
-    SlabTab t = tab;
-    out[i] = verify_one(pw, sw, msgs + o0, o1 - o0, t, bt) ? 1 : 0;
-  }
+  out[i] = (verify_main(k, s, A, Rw, tab, bt) && ok) ? 1 : 0;
 }
 
 __global__ __launch_bounds__(kThreadsPerBlock) void sign_kernel(
     const uint8_t *__restrict__ seeds, const uint8_t *__restrict__ msgs, const uint32_t *__restrict__ off,
     uint32_t n, uint8_t *__restrict__ sig_out, uint8_t *__restrict__ pub_out, int4 *__restrict__ slab,
     uint32_t slab_stride, const ge_niels *__restrict__ btab_g) {
-  __shared__ ge_niels sbt[9];
-  {
-    int32_t *dst = reinterpret_cast<int32_t *>(sbt);
-    const int32_t *src = reinterpret_cast<const int32_t *>(btab_g);
-    for (int i = threadIdx.x; i < 9 * 30; i += blockDim.x) dst[i] = src[i];
-  }
-  __syncthreads();
+  __shared__ ge_niels sbt[kBTabEntries];
+  stage_btab(sbt, btab_g);
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
   const LdsBTab bt{sbt};
   for (uint32_t i = gtid; i < n; i += gridDim.x * blockDim.x) {
@@ -127,11 +177,20 @@ uint32_t grid_for(size_t n, uint32_t max_blocks) {
 
 hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                          uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
-                         hipStream_t stream) {
-  const uint32_t grid = grid_for(n, slab_stride / kThreadsPerBlock);
-  hipLaunchKernelGGL(verify_kernel, dim3(grid), dim3(kThreadsPerBlock), 0, stream, pub, sig, msgs, off, n, out,
-                     slab, slab_stride, btab);
-  return hipGetLastError();
+                         int4 *prep, hipStream_t stream) {
+  // Chunks of slab_stride signatures: the per-lane tables (slab) and the prep
+  // hand-off are sized for one chunk.
+  for (uint32_t base = 0; base < n; base += slab_stride) {
+    const uint32_t count = (n - base) < slab_stride ? (n - base) : slab_stride;
+    const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
+    hipLaunchKernelGGL(verify_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, pub, sig, msgs, off,
+                       base, count, prep, slab_stride);
+    hipLaunchKernelGGL(verify_main_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base, count, prep,
+                       slab_stride, slab, btab, out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t *off, uint32_t n, uint8_t *sig_out,
@@ -143,7 +202,7 @@ hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t
   return hipGetLastError();
 }
 
-void host_build_btab(ge_niels out[9]) { build_btab_niels(out); }
+void host_build_btab(ge_niels out[129]) { build_btab_niels(out); }
 
 // ============================================================ fixed-base combs
 
@@ -227,20 +286,46 @@ struct GlobalComb {
   }
 };
 
-__global__ __launch_bounds__(kThreadsPerBlock) void verify_keyset_kernel(
+__global__ __launch_bounds__(kThreadsPerBlock) void verify_keyset_prep_kernel(
     const uint32_t *__restrict__ val_idx, const uint8_t *__restrict__ key_pub, const uint8_t *__restrict__ key_ok,
-    const int4 *__restrict__ acomb, const int4 *__restrict__ bcomb, const uint8_t *__restrict__ sig,
-    const uint8_t *__restrict__ msgs, const uint32_t *__restrict__ off, uint32_t n, uint8_t *__restrict__ out) {
-  const GlobalComb bc{bcomb};
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t v = val_idx[i];
-    uint32_t pw[8], sw[16];
-    load_row_words(pw, key_pub + 32 * (size_t)v, 2);
-    load_row_words(sw, sig + 64 * (size_t)i, 4);
-    const uint32_t o0 = off[i], o1 = off[i + 1];
-    const GlobalComb ac{acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4};
-    out[i] = verify_one_comb(pw, key_ok[v] != 0, sw, msgs + o0, o1 - o0, ac, bc) ? 1 : 0;
+    const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msgs, const uint32_t *__restrict__ off,
+    uint32_t base, uint32_t count, int4 *__restrict__ prep, uint32_t stride) {
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= count) return;
+  const uint32_t i = base + slot;
+  const uint32_t v = val_idx[i];
+  uint32_t pw[8], sw[16], k[8], s[8];
+  load_row_words(pw, key_pub + 32 * (size_t)v, 2);
+  load_row_words(sw, sig + 64 * (size_t)i, 4);
+  const uint32_t o0 = off[i], o1 = off[i + 1];
+  const bool ok = verify_prep_comb(pw, key_ok[v] != 0, sw, msgs + o0, o1 - o0, k, s);
+  ge_p3 dummy;
+  ge_p3_0(dummy);
+  prep_store(prep, stride, slot, k, s, dummy, ok);
+}
+
+__global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_keyset_main_kernel(
+    const uint32_t *__restrict__ val_idx, const int4 *__restrict__ acomb, const int4 *__restrict__ bcomb,
+    const uint8_t *__restrict__ sig, uint32_t base, uint32_t count, const int4 *__restrict__ prep, uint32_t stride,
+    uint8_t *__restrict__ out) {
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= count) return;
+  const uint32_t i = base + slot;
+  const uint32_t v = val_idx[i];
+  uint32_t k[8], s[8], Rw[8];
+  int32_t w[40];
+#pragma unroll
+  for (int q = 0; q < 5; q++) {  // k, s, (A unused), ok at word 36
+    const int4 x = prep[(size_t)q * stride + slot];
+    w[4 * q] = x.x; w[4 * q + 1] = x.y; w[4 * q + 2] = x.z; w[4 * q + 3] = x.w;
   }
+  const bool ok = prep[(size_t)9 * stride + slot].x != 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) { k[j] = (uint32_t)w[j]; s[j] = (uint32_t)w[8 + j]; }
+  load_row_words(Rw, sig + 64 * (size_t)i, 2);
+  const GlobalComb ac{acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4};
+  const GlobalComb bc{bcomb};
+  out[i] = (verify_main_comb(k, s, Rw, ac, bc) && ok) ? 1 : 0;
 }
 
 hipError_t launch_comb_bases(const uint8_t *pubs, uint32_t n, int negate, uint8_t *ok, int32_t *bases,
@@ -258,11 +343,19 @@ hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStr
 
 hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
                                 const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
-                                const uint32_t *off, uint32_t n, uint8_t *out, hipStream_t stream) {
-  const uint32_t grid = grid_for(n, 4096);
-  hipLaunchKernelGGL(verify_keyset_kernel, dim3(grid), dim3(kThreadsPerBlock), 0, stream, val_idx, key_pub, key_ok,
-                     acomb, bcomb, sig, msgs, off, n, out);
-  return hipGetLastError();
+                                const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
+                                hipStream_t stream) {
+  for (uint32_t base = 0; base < n; base += stride) {
+    const uint32_t count = (n - base) < stride ? (n - base) : stride;
+    const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
+    hipLaunchKernelGGL(verify_keyset_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx, key_pub,
+                       key_ok, sig, msgs, off, base, count, prep, stride);
+    hipLaunchKernelGGL(verify_keyset_main_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx, acomb,
+                       bcomb, sig, base, count, prep, stride, out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace tmed

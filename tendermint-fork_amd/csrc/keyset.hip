@@ -83,7 +83,7 @@ int tmed_verify_batch_keyset_device(tmed_ctx *c, uint64_t handle, const uint32_t
   (void)hipSetDevice(c->device);
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   return map_err(launch_verify_keyset(d_val_idx, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb, d_sigs, d_msgs, d_msg_off,
-                                      (uint32_t)n, d_out, s));
+                                      (uint32_t)n, d_out, c->d_prep, c->slab_slots, s));
 }
 
 int tmed_verify_batch_keyset(tmed_ctx *c, uint64_t handle, const uint32_t *val_idx, const uint8_t *sigs,
@@ -127,7 +127,7 @@ int tmed_verify_batch_keyset(tmed_ctx *c, uint64_t handle, const uint32_t *val_i
   if (e == hipSuccess)
     e = launch_verify_keyset((const uint32_t *)c->d_a.p, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb,
                              (const uint8_t *)c->d_b.p, (const uint8_t *)c->d_msg.p, (const uint32_t *)c->d_off.p,
-                             (uint32_t)n, (uint8_t *)c->d_out.p, s);
+                             (uint32_t)n, (uint8_t *)c->d_out.p, c->d_prep, c->slab_slots, s);
   if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
   if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, n, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);

@@ -53,14 +53,16 @@ int tmed_init(int device, tmed_ctx **out) {
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
-  ge_niels bt[9];
-  host_build_btab(bt);
+  static ge_niels bt[kBTabSize];
+  static std::once_flag bt_once;
+  std::call_once(bt_once, [] { host_build_btab(bt); });
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_btab, sizeof(bt));
   if (e == hipSuccess) e = hipMemcpy(c->d_btab, bt, sizeof(bt), hipMemcpyHostToDevice);
   // Lane slots for the per-lane tables: 4x the resident lanes of 256 CUs at
   // 8 waves/CU is plenty for the grid-stride loop (~377 MB of HBM).
   c->slab_slots = 1024 * kThreadsPerBlock;
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_slab, (size_t)c->slab_slots * kSlabSlotBytes);
+  if (e == hipSuccess) e = hipMalloc((void **)&c->d_prep, (size_t)c->slab_slots * kPrepSlotBytes);
   // Shared signed radix-256 comb of +B (528 KB, L2-resident) for the key-cached path.
   uint8_t *d_bpub = nullptr, *d_bok = nullptr;
   const uint8_t benc[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
@@ -92,6 +94,7 @@ void tmed_destroy(tmed_ctx *c) {
   c->keysets.clear();
   if (c->d_bcomb) hipFree(c->d_bcomb);
   if (c->d_slab) hipFree(c->d_slab);
+  if (c->d_prep) hipFree(c->d_prep);
   if (c->d_btab) hipFree(c->d_btab);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
@@ -109,7 +112,7 @@ int tmed_verify_batch_device(tmed_ctx *c, const uint8_t *d_pub, const uint8_t *d
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   hipSetDevice(c->device);
   hipError_t e = launch_verify(d_pub, d_sig, d_msgs, d_off, (uint32_t)n, d_out, c->d_slab, c->slab_slots,
-                               c->d_btab, s);
+                               c->d_btab, c->d_prep, s);
   return map_err(e);
 }
 
@@ -165,7 +168,7 @@ int tmed_verify_batch(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, const
   if (e == hipSuccess)
     e = launch_verify((const uint8_t *)c->d_a.p, (const uint8_t *)c->d_b.p, (const uint8_t *)c->d_msg.p,
                       (const uint32_t *)c->d_off.p, (uint32_t)n, (uint8_t *)c->d_out.p, c->d_slab, c->slab_slots,
-                      c->d_btab, s);
+                      c->d_btab, c->d_prep, s);
   if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
   if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, n, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);

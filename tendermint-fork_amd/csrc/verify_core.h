@@ -22,6 +22,27 @@
 
 namespace tmed {
 
+// Signed radix-256 recoding: r = k + 0x8080...80; digit w = byte_w(r) - 128 (k < 2^255).
+TMED_HD void sc_recode256(uint32_t r[8], const uint32_t k[8]) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t t = (uint64_t)k[i] + 0x80808080u + c;
+    r[i] = (uint32_t)t;
+    c = t >> 32;
+  }
+}
+
+// e <- sign(d) * entry(|d|): -(y+x, y-x, 2dxy) = (y-x, y+x, -2dxy)
+TMED_HD void niels_apply_sign(ge_niels &e, bool neg) {
+  fe t;
+  fe_copy(t, e.YpX);
+  fe_select(e.YpX, e.YpX, e.YmX, neg);
+  fe_select(e.YmX, e.YmX, t, neg);
+  fe_neg(t, e.XY2d);
+  fe_select(e.XY2d, e.XY2d, t, neg);
+}
+
 // Per-lane variable-base table access.  T must provide
 //   void store(int j, const ge_cached&)  and  void load(int j, ge_cached&)
 // for j in [0, 8] (j = 0 is the identity).  The device implementation lives in a
@@ -47,45 +68,50 @@ TMED_HD void build_table_negA(T &tab, const ge_p3 &A) {
   }
 }
 
-// out = [k](-A) + [S]B  using the per-lane table of (-A) multiples and the
-// shared niels table of B multiples.
+// out = [k](-A) + [S]B  (Straus, most-significant first).
+// k: signed radix-16 digits (64 windows) from the per-lane table of j*(-A), j=0..8;
+// S: signed radix-256 digits (32 windows) from the shared table of j*B, j=0..128
+// (BT::load(j, niels)), added once per 8 doublings — half the B additions of a
+// radix-16 B window, for a 15.5 KB LDS table.
 template <class T, class BT>
 TMED_HD void double_scalarmult(ge_p2 &out, const uint32_t k[8], const uint32_t s[8], T &tab, const BT &btab) {
   uint32_t kr[8], sr[8];
   sc_recode16(kr, k);
-  sc_recode16(sr, s);
+  sc_recode256(sr, s);
   ge_p2 q;
   ge_p2_0(q);
   ge_p1p1 t;
   ge_p3 r;
+  ge_cached ca;
+  ge_niels nb;
 #pragma unroll 1
-  for (int j = 0; j < 8; j++) {
+  for (int j = 0; j < 8; j++) {  // 32-bit word of the scalars, most significant first
     uint32_t kc = kr[7], sc = sr[7];
 #pragma unroll
     for (int m = 7; m > 0; m--) { kr[m] = kr[m - 1]; sr[m] = sr[m - 1]; }
 #pragma unroll 1
-    for (int i = 0; i < 8; i++) {
-      const int da = (int)(kc >> 28) - 8;
-      const int db = (int)(sc >> 28) - 8;
-      kc <<= 4;
-      sc <<= 4;
-      // q = 16 * q
+    for (int i = 0; i < 4; i++) {  // byte of the word: two radix-16 A windows, one radix-256 B window
+      const int db = (int)(sc >> 24) - 128;
+      sc <<= 8;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int da = (int)(kc >> 28) - 8;
+        kc <<= 4;
 #pragma unroll 1
-      for (int d = 0; d < 3; d++) {
+        for (int d = 0; d < 3; d++) {
+          ge_p2_dbl(t, q);
+          ge_p1p1_to_p2(q, t);
+        }
         ge_p2_dbl(t, q);
-        ge_p1p1_to_p2(q, t);
+        ge_p1p1_to_p3(r, t);
+        tab.load(da < 0 ? -da : da, ca);
+        ge_add_cached(t, r, ca, da < 0);
+        if (h == 0) ge_p1p1_to_p2(q, t);
       }
-      ge_p2_dbl(t, q);
       ge_p1p1_to_p3(r, t);
-      // + da * (-A)
-      ge_cached ca;
-      tab.load(da < 0 ? -da : da, ca);
-      ge_add_cached(t, r, ca, da < 0);
-      ge_p1p1_to_p3(r, t);
-      // + db * B
-      ge_niels nb;
       btab.load(db < 0 ? -db : db, nb);
-      ge_madd_niels(t, r, nb, db < 0);
+      niels_apply_sign(nb, db < 0);
+      ge_madd_niels(t, r, nb, false);
       ge_p1p1_to_p2(q, t);
     }
   }
@@ -100,21 +126,27 @@ TMED_HD void load_words8(uint32_t w[8], const uint8_t *p) {
            ((uint32_t)p[4 * i + 3] << 24);
 }
 
-// One verification.  pubw: 8 words of A; sigw: 16 words (R = 0..7, S = 8..15).
-template <class T, class BT>
-TMED_HD bool verify_one(const uint32_t pubw[8], const uint32_t sigw[16], const uint8_t *msg, uint32_t mlen,
-                        T &tab, const BT &btab) {
+// Verification phase 1 (hash / scalar checks / decompression — the register-hungry
+// part): returns ok and writes k = SHA-512(R||A||M) mod L, s (S, or 0 if rejected)
+// and the decoded A (identity if rejected).
+TMED_HD bool verify_prep(const uint32_t pubw[8], const uint32_t sigw[16], const uint8_t *msg, uint32_t mlen,
+                         uint32_t k[8], uint32_t s[8], ge_p3 &A) {
   bool ok = (sigw[15] & 0xE0000000u) == 0;        // sig[63] & 0xE0
   const uint32_t *S = sigw + 8;
   ok = ok && sc_is_canonical(S);                  // Scalar.SetCanonicalBytes
-  ge_p3 A;
   ok = ge_frombytes_go(A, pubw) && ok;            // Point.SetBytes (identity on failure)
-  uint32_t h[16], k[8];
+  uint32_t h[16];
   sha512_stream(h, sigw, pubw, 64, msg, mlen);     // SHA-512(R || A || M)
   sc_reduce512(k, h);                              // Scalar.SetUniformBytes
-  uint32_t s[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) s[i] = ok ? S[i] : 0u;  // keep S < 2^255 for the recoding
+  return ok;
+}
+
+// Verification phase 2 (point arithmetic): enc([k](-A) + [s]B) == R ?
+template <class T, class BT>
+TMED_HD bool verify_main(const uint32_t k[8], const uint32_t s[8], const ge_p3 &A, const uint32_t Rw[8], T &tab,
+                         const BT &btab) {
   build_table_negA(tab, A);
   ge_p2 R;
   double_scalarmult(R, k, s, tab, btab);
@@ -122,8 +154,18 @@ TMED_HD bool verify_one(const uint32_t pubw[8], const uint32_t sigw[16], const u
   ge_tobytes(enc, R.X, R.Y, R.Z);
   uint32_t diff = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) diff |= enc[i] ^ sigw[i];
-  return ok && diff == 0;
+  for (int i = 0; i < 8; i++) diff |= enc[i] ^ Rw[i];
+  return diff == 0;
+}
+
+// One verification.  pubw: 8 words of A; sigw: 16 words (R = 0..7, S = 8..15).
+template <class T, class BT>
+TMED_HD bool verify_one(const uint32_t pubw[8], const uint32_t sigw[16], const uint8_t *msg, uint32_t mlen,
+                        T &tab, const BT &btab) {
+  uint32_t k[8], s[8];
+  ge_p3 A;
+  const bool ok = verify_prep(pubw, sigw, msg, mlen, k, s, A);
+  return verify_main(k, s, A, sigw, tab, btab) && ok;
 }
 
 // [s]B for s < 2^255 via the same window schedule (k = 0 uses the identity
@@ -219,39 +261,27 @@ TMED_HD void comb_entry(ge_niels &out, const ge_p3 &base, uint32_t j) {
   fe_mul(out.XY2d, xy, d2);
 }
 
-// Signed radix-256 recoding: r = k + 0x8080...80; digit w = byte_w(r) - 128 (k < 2^255).
-TMED_HD void sc_recode256(uint32_t r[8], const uint32_t k[8]) {
-  uint64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint64_t t = (uint64_t)k[i] + 0x80808080u + c;
-    r[i] = (uint32_t)t;
-    c = t >> 32;
-  }
-}
-
-// e <- sign(d) * entry(|d|): -(y+x, y-x, 2dxy) = (y-x, y+x, -2dxy)
-TMED_HD void niels_apply_sign(ge_niels &e, bool neg) {
-  fe t;
-  fe_copy(t, e.YpX);
-  fe_select(e.YpX, e.YpX, e.YmX, neg);
-  fe_select(e.YmX, e.YmX, t, neg);
-  fe_neg(t, e.XY2d);
-  fe_select(e.XY2d, e.XY2d, t, neg);
-}
-
-// Key-cached verification: [k](-A) from the key's comb, [S]B from the shared comb.
-// AC/BC provide  void load(int window, int j, ge_niels&) const  for j in 0..128.
-template <class AC, class BC>
-TMED_HD bool verify_one_comb(const uint32_t pubw[8], bool key_ok, const uint32_t sigw[16], const uint8_t *msg,
-                             uint32_t mlen, const AC &acomb, const BC &bcomb) {
+// Key-cached verification, phase 1: k = SHA-512(R||A||M) mod L and the S checks (A is
+// already decoded in the key set; key_ok carries Point.SetBytes' verdict).
+TMED_HD bool verify_prep_comb(const uint32_t pubw[8], bool key_ok, const uint32_t sigw[16], const uint8_t *msg,
+                              uint32_t mlen, uint32_t k[8], uint32_t s[8]) {
   bool ok = key_ok && (sigw[15] & 0xE0000000u) == 0;
   ok = ok && sc_is_canonical(sigw + 8);
-  uint32_t h[16], k[8], s[8], kr[8], sr[8];
+  uint32_t h[16];
   sha512_stream(h, sigw, pubw, 64, msg, mlen);
   sc_reduce512(k, h);
 #pragma unroll
   for (int w = 0; w < 8; w++) s[w] = ok ? sigw[8 + w] : 0u;
+  return ok;
+}
+
+// Key-cached verification, phase 2: [k](-A) from the key's comb, [s]B from the shared
+// comb: 32 + 32 mixed additions, then encode and compare with R.
+// AC/BC provide  void load(int window, int j, ge_niels&) const  for j in 0..128.
+template <class AC, class BC>
+TMED_HD bool verify_main_comb(const uint32_t k[8], const uint32_t s[8], const uint32_t Rw[8], const AC &acomb,
+                              const BC &bcomb) {
+  uint32_t kr[8], sr[8];
   sc_recode256(kr, k);
   sc_recode256(sr, s);
   ge_p3 acc;
@@ -284,13 +314,20 @@ TMED_HD bool verify_one_comb(const uint32_t pubw[8], bool key_ok, const uint32_t
   ge_tobytes(enc, acc.X, acc.Y, acc.Z);
   uint32_t diff = 0;
 #pragma unroll
-  for (int w = 0; w < 8; w++) diff |= enc[w] ^ sigw[w];
-  return ok && diff == 0;
+  for (int w = 0; w < 8; w++) diff |= enc[w] ^ Rw[w];
+  return diff == 0;
 }
 
-// Host-side construction of the shared B table (j*B, j = 0..8, niels form),
-// using the same field code.  Run once per context.
-TMED_HD void build_btab_niels(ge_niels out[9]) {
+template <class AC, class BC>
+TMED_HD bool verify_one_comb(const uint32_t pubw[8], bool key_ok, const uint32_t sigw[16], const uint8_t *msg,
+                             uint32_t mlen, const AC &acomb, const BC &bcomb) {
+  uint32_t k[8], s[8];
+  const bool ok = verify_prep_comb(pubw, key_ok, sigw, msg, mlen, k, s);
+  return verify_main_comb(k, s, sigw, acomb, bcomb) && ok;
+}
+
+// Construction of the shared B table: out[j] = j*B (niels, affine), j = 0..128.
+TMED_HD void build_btab_niels(ge_niels out[129]) {
   // B = (x, 4/5), x even
   uint32_t byw[8];
   const uint8_t by[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
@@ -300,26 +337,7 @@ TMED_HD void build_btab_niels(ge_niels out[9]) {
   ge_p3 B;
   ge_frombytes_go(B, byw);
   ge_niels_0(out[0]);
-  ge_p3 cur = B;
-  ge_cached cb;
-  ge_p3_to_cached(cb, B);
-  ge_p1p1 t;
-  fe d2;
-  fe_const_d2(d2);
-  for (int j = 1; j <= 8; j++) {
-    if (j > 1) {
-      ge_add_cached(t, cur, cb, false);
-      ge_p1p1_to_p3(cur, t);
-    }
-    fe zi, x, y, xy;
-    fe_invert(zi, cur.Z);
-    fe_mul(x, cur.X, zi);
-    fe_mul(y, cur.Y, zi);
-    fe_add(out[j].YpX, y, x); fe_carry(out[j].YpX, out[j].YpX);
-    fe_sub(out[j].YmX, y, x); fe_carry(out[j].YmX, out[j].YmX);
-    fe_mul(xy, x, y);
-    fe_mul(out[j].XY2d, xy, d2);
-  }
+  for (uint32_t j = 1; j <= 128; j++) comb_entry(out[j], B, j);
 }
 
 }  // namespace tmed

@@ -19,7 +19,7 @@ struct HostTab {
   void load(int j, ge_cached &c) const { c = e[j]; }
 };
 struct HostBTab {
-  ge_niels e[9];
+  ge_niels e[129];
   void load(int j, ge_niels &n) const { n = e[j]; }
 };
 HostBTab &btab() {
