@@ -82,6 +82,8 @@ struct tmed_ctx {
   int4 *d_slab = nullptr;
   int4 *d_prep = nullptr;
   uint32_t slab_slots = 0;
+  uint32_t chunk = 0;     // signatures per prep/main launch pair (0 = slab_slots); env TMED_CHUNK
+  int main_waves = 2;     // register budget variant of the main kernel; env TMED_MAIN_WAVES
   tmed::DevBuf d_a, d_b, d_msg, d_off, d_out, d_c;
   tmed::HostBuf h_a, h_b, h_msg, h_off, h_out, h_c;
   std::unordered_map<uint64_t, tmed::Keyset> keysets;

@@ -32,28 +32,11 @@ namespace tmed {
 
 struct fe { int32_t v[10]; };
 
-// x*19 and x*38 as two full-rate v_lshl_add_u32 (LLVM would otherwise fold the
-// shift-adds back into v_mul_lo_u32, a multi-pass op on CDNA).
-TMED_HD int32_t mul19(int32_t x) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t t, r;
-  asm("v_lshl_add_u32 %0, %1, 4, %1" : "=v"(t) : "v"(x));      // 17x
-  asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(r) : "v"(x), "v"(t));  // 19x
-  return (int32_t)r;
-#else
-  return (int32_t)(19u * (uint32_t)x);
-#endif
-}
-TMED_HD int32_t mul38(int32_t x) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t t, r;
-  asm("v_lshl_add_u32 %0, %1, 4, %1" : "=v"(t) : "v"(x));      // 17x
-  asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(r) : "v"(x), "v"(t));  // 19x
-  return (int32_t)(r << 1);
-#else
-  return (int32_t)(38u * (uint32_t)x);
-#endif
-}
+// x*19, x*38: one v_mul_lo_u32 each.  (Measured on gfx950, tools/probe_valu.py:
+// v_mul_lo_u32 issues at the same rate as one v_lshl_add_u32, so the two-shift-add
+// form would cost twice as much.)
+TMED_HD int32_t mul19(int32_t x) { return (int32_t)(19u * (uint32_t)x); }
+TMED_HD int32_t mul38(int32_t x) { return (int32_t)(38u * (uint32_t)x); }
 
 TMED_HD void fe_0(fe &h) {
 #pragma unroll

@@ -15,7 +15,7 @@ constexpr uint32_t kSlabSlotBytes = 9 * 160;
 
 hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                          uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
-                         int4 *prep, hipStream_t stream);
+                         int4 *prep, hipStream_t stream, uint32_t chunk = 0, int main_waves = 2);
 
 hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t *off, uint32_t n, uint8_t *sig_out,
                        uint8_t *pub_out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,

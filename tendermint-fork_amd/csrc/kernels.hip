@@ -128,7 +128,9 @@ __global__ __launch_bounds__(kThreadsPerBlock) void verify_prep_kernel(
 }
 
 // Phase 2: table of -A, Straus [k](-A) + [s]B, encode, compare with R.
-__global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_kernel(
+// WAVES = minimum waves per SIMD the register allocation must allow.
+template <int WAVES>
+__global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_main_kernel(
     const uint8_t *__restrict__ sig, uint32_t base, uint32_t count, const int4 *__restrict__ prep,
     uint32_t stride, int4 *__restrict__ slab, const ge_niels *__restrict__ btab_g, uint8_t *__restrict__ out) {
   __shared__ ge_niels sbt[kBTabEntries];
@@ -177,16 +179,21 @@ uint32_t grid_for(size_t n, uint32_t max_blocks) {
 
 hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                          uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
-                         int4 *prep, hipStream_t stream) {
-  // Chunks of slab_stride signatures: the per-lane tables (slab) and the prep
-  // hand-off are sized for one chunk.
-  for (uint32_t base = 0; base < n; base += slab_stride) {
-    const uint32_t count = (n - base) < slab_stride ? (n - base) : slab_stride;
+                         int4 *prep, hipStream_t stream, uint32_t chunk, int main_waves) {
+  // Chunks of at most slab_stride signatures: the per-lane tables (slab) and the
+  // prep hand-off are sized for one chunk.
+  if (chunk == 0 || chunk > slab_stride) chunk = slab_stride;
+  for (uint32_t base = 0; base < n; base += chunk) {
+    const uint32_t count = (n - base) < chunk ? (n - base) : chunk;
     const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
     hipLaunchKernelGGL(verify_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, pub, sig, msgs, off,
                        base, count, prep, slab_stride);
-    hipLaunchKernelGGL(verify_main_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base, count, prep,
-                       slab_stride, slab, btab, out);
+    if (main_waves >= 3)
+      hipLaunchKernelGGL(verify_main_kernel<3>, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base, count,
+                         prep, slab_stride, slab, btab, out);
+    else
+      hipLaunchKernelGGL(verify_main_kernel<2>, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base, count,
+                         prep, slab_stride, slab, btab, out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

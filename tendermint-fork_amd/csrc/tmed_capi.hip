@@ -7,6 +7,7 @@
 // different goroutines; ValidatorSet itself is not goroutine-safe,
 // types/validator_set.go:49, so no shared mutable state crosses the seam).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -61,6 +62,8 @@ int tmed_init(int device, tmed_ctx **out) {
   // Lane slots for the per-lane tables: 4x the resident lanes of 256 CUs at
   // 8 waves/CU is plenty for the grid-stride loop (~377 MB of HBM).
   c->slab_slots = 1024 * kThreadsPerBlock;
+  if (const char *v = getenv("TMED_CHUNK")) c->chunk = (uint32_t)strtoul(v, nullptr, 10);
+  if (const char *v = getenv("TMED_MAIN_WAVES")) c->main_waves = atoi(v);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_slab, (size_t)c->slab_slots * kSlabSlotBytes);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_prep, (size_t)c->slab_slots * kPrepSlotBytes);
   // Shared signed radix-256 comb of +B (528 KB, L2-resident) for the key-cached path.
@@ -112,7 +115,7 @@ int tmed_verify_batch_device(tmed_ctx *c, const uint8_t *d_pub, const uint8_t *d
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   hipSetDevice(c->device);
   hipError_t e = launch_verify(d_pub, d_sig, d_msgs, d_off, (uint32_t)n, d_out, c->d_slab, c->slab_slots,
-                               c->d_btab, c->d_prep, s);
+                               c->d_btab, c->d_prep, s, c->chunk, c->main_waves);
   return map_err(e);
 }
 
@@ -168,7 +171,7 @@ int tmed_verify_batch(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, const
   if (e == hipSuccess)
     e = launch_verify((const uint8_t *)c->d_a.p, (const uint8_t *)c->d_b.p, (const uint8_t *)c->d_msg.p,
                       (const uint32_t *)c->d_off.p, (uint32_t)n, (uint8_t *)c->d_out.p, c->d_slab, c->slab_slots,
-                      c->d_btab, c->d_prep, s);
+                      c->d_btab, c->d_prep, s, c->chunk, c->main_waves);
   if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
   if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, n, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);

@@ -23,6 +23,13 @@ for s in $STEPS; do
       cd /tmp && export TMPDIR=/tmp
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1; rc=$?
       cd $GRAFT_REPO_ROOT; echo "prof rc=$rc" | tee -a $OUT/prof.log ;;
+    variants)
+      rc=0
+      for cfg in "TMED_MAIN_WAVES=2" "TMED_MAIN_WAVES=3" "TMED_MAIN_WAVES=3 TMED_CHUNK=131072" "TMED_MAIN_WAVES=2 TMED_CHUNK=131072" "TMED_MAIN_WAVES=3" "TMED_MAIN_WAVES=2"; do
+        env $cfg timeout -k 10 300 python bench.py --no-cpu-baseline --no-peak --steps 5 > $OUT/variant.log 2>&1; rc=$?
+        echo "$cfg rc=$rc $(tail -1 $OUT/variant.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])' 2>/dev/null)" | tee -a $OUT/variants.txt
+        if fatal $rc; then break; fi
+      done ;;
     probe)
       timeout -k 10 300 python tools/probe_valu.py > $OUT/probe_valu.json 2>$OUT/probe_valu.err; rc=$?
       echo "probe rc=$rc"; cat $OUT/probe_valu.json ;;
