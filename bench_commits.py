@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""bench_commits.py — commit-level workloads of BASELINE.json through the drop-in seam.
+
+  --config c1   VerifyCommit p50 latency @175 validators (BASELINE metric, second half):
+                end-to-end through tmed_verify_commits (sign-bytes + staging + device + replay),
+                generic and key-cached paths, next to the CPU path (the port verifying the
+                same 175 tuples sequentially, 1 thread: the reference's loop).
+  --config c3   light client: H headers x 175 validators, the set changing by one key per
+                height; each (h, h+2) pair = VerifyCommitLightTrusting(1/3) + VerifyCommitLight,
+                all pairs in one seam call (light/verifier.go:32-79).
+  --config c4   blocksync replay: B blocks x V validators, VerifyCommitLight per block
+                (blockchain/v0/reactor.go:366-367), key-cached; with N ranks the blocks are
+                sharded and the per-rank int64 tallies all-reduced (RCCL; gloo on CPU).
+Synthetic data (seeded keys, GPU RFC 8032 signer); prints one JSON line per config.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tendermint-fork_amd"))
+
+T2023 = 1672531200
+
+
+def block_id(tag: bytes):
+    from tmed.types import BlockID
+    return BlockID(hashlib.sha256(tag).digest(), 123, hashlib.sha256(tag + b"/psh").digest())
+
+
+def c1(eng, reps: int, cpu: bool):
+    import tmed.types as T
+    from tmed.workload import make_valset, pubkeys_of, seeds_from_tag, sign_commits
+    n = 175
+    seeds = seeds_from_tag(b"tmed-bench-key", 0, n)
+    pubs = pubkeys_of(eng, seeds)
+    vals, order = make_valset(pubs, [10] * n)
+    addrs = np.array([np.frombuffer(v.address, np.uint8) for v in vals.validators])
+    bid = block_id(b"tmed-c1")
+    commit = sign_commits(eng, "test_chain_id", [(seeds[order], addrs, 3, 0, bid, T2023, None)])[0]
+    out = {}
+    for path in ("generic", "keyset"):
+        if path == "keyset":
+            vals.keyset = eng.keyset_load(np.array([np.frombuffer(v.pub_key, np.uint8) for v in vals.validators]))
+        pb = T.PreparedBatch([(T.MODE_COMMIT, vals, "test_chain_id", bid, 3, commit, 0, 0)])
+        for _ in range(20):
+            pb.run(eng)
+        assert pb.codes()[0] == 0 and pb.verified()[0] == n
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            pb.run(eng)
+            ts.append(time.perf_counter() - t0)
+        ts = np.array(ts) * 1e3
+        out[path] = {"p50_ms": round(float(np.median(ts)), 4), "p90_ms": round(float(np.percentile(ts, 90)), 4),
+                     "min_ms": round(float(ts.min()), 4)}
+    eng.keyset_free(vals.keyset)
+    res = {"metric": "VerifyCommit p50 latency @175 validators", "unit": "ms", "higher_is_better": False,
+           "value": out["keyset"]["p50_ms"], "paths": out, "reps": reps,
+           "config": {"workload": "C1: 175-validator commit, equal power 10, test_chain_id, height 3, round 0",
+                      "seam": "tmed_verify_commits (C++ plan/sign-bytes/replay + gfx950 batch)"}}
+    if cpu:
+        sys.path.insert(0, ROOT)
+        from oracle import port  # cpu_baseline leg only
+        from tmed.signbytes import make_template, vote_sign_bytes_batch
+        t = make_template("test_chain_id", 3, 0, bid.hash, bid.psh_total, bid.psh_hash)
+        msgs, offs = vote_sign_bytes_batch(t, commit.ts_seconds, commit.ts_nanos, commit.flags)
+        vp = np.array([np.frombuffer(v.pub_key, np.uint8) for v in vals.validators])
+        ts = []
+        for _ in range(max(50, reps // 10)):
+            t0 = time.perf_counter()
+            ok = port.verify_batch(vp, commit.sigs, msgs, offs.astype(np.uint64), 1)
+            ts.append(time.perf_counter() - t0)
+        assert ok.all()
+        p50 = float(np.median(ts)) * 1e3
+        res["cpu_baseline"] = {"value": round(p50, 4), "unit": "ms (p50)", "cores": 1, "kind": "port",
+                               "sample": "the 175 VerifySignature calls of the same commit, sequential, 1 thread"}
+        res["speedup_vs_cpu"] = round(p50 / out["keyset"]["p50_ms"], 2)
+    return res
+
+
+def c3(eng, headers: int, gap: int, use_keyset: bool):
+    import tmed.types as T
+    from tmed.workload import make_valset, pubkeys_of, seeds_from_tag, sign_commits
+    nv = 175
+    pool_seeds = seeds_from_tag(b"tmed-c3-key", 0, headers + gap + nv)
+    pool_pubs = pubkeys_of(eng, pool_seeds)
+    ks = eng.keyset_load(pool_pubs) if use_keyset else 0
+    sets, specs = [], []
+    for h in range(headers + gap):
+        vals, order = make_valset(pool_pubs[h:h + nv], [10] * nv)
+        vals.keyset = ks
+        vals.keyset_index = (order + h).astype(np.uint32)
+        sets.append(vals)
+        addrs = np.array([np.frombuffer(v.address, np.uint8) for v in vals.validators])
+        specs.append((pool_seeds[h:h + nv][order], addrs, h + 1, 0, block_id(b"c3-%d" % (h + 1)), T2023 + h, None))
+    t_sign = time.perf_counter()
+    commits = sign_commits(eng, "test_chain_id", specs)
+    t_sign = time.perf_counter() - t_sign
+    reqs = []
+    for h in range(headers):
+        u = h + gap
+        reqs.append((T.MODE_LIGHT_TRUSTING, sets[h], "test_chain_id", None, 0, commits[u], 1, 3))
+        reqs.append((T.MODE_LIGHT, sets[u], "test_chain_id", commits[u].block_id, u + 1, commits[u], 0, 0))
+    pb = T.PreparedBatch(reqs)
+    pb.run(eng)  # warm
+    t0 = time.perf_counter()
+    pb.run(eng)
+    dt = time.perf_counter() - t0
+    codes = pb.codes()
+    ver = int(pb.verified().sum())
+    if ks:
+        eng.keyset_free(ks)
+    return {"metric": "light-client headers/s (VerifyCommitLightTrusting + VerifyCommitLight per header)",
+            "value": round(headers / dt, 1), "unit": "headers/s", "verifies_per_s": round(ver / dt, 1),
+            "verifies": ver, "all_ok": bool((codes == 0).all()), "seconds": round(dt, 4),
+            "config": {"workload": "C3: %d headers x 175 validators, trust 1/3, gap %d, set changes 1 key/height"
+                       % (headers, gap), "key_cache": bool(ks), "sign_s": round(t_sign, 2)}}
+
+
+def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev):
+    import torch
+    import torch.distributed as dist
+    import tmed.types as T
+    from tmed.workload import make_valset, pubkeys_of, seeds_from_tag, sign_commits
+    seeds = seeds_from_tag(b"tmed-c4-key", 0, nvals)
+    pubs = pubkeys_of(eng, seeds)
+    vals, order = make_valset(pubs, [10] * nvals)
+    t_ks = time.perf_counter()
+    vals.keyset = eng.keyset_load(np.array([np.frombuffer(v.pub_key, np.uint8) for v in vals.validators]))
+    t_ks = time.perf_counter() - t_ks
+    addrs = np.array([np.frombuffer(v.address, np.uint8) for v in vals.validators])
+    mine = list(range(rank, blocks, world))  # shard blocks across ranks
+    specs = [(seeds[order], addrs, b + 1, 0, block_id(b"c4-%d" % (b + 1)), T2023 + b, None) for b in mine]
+    t_sign = time.perf_counter()
+    commits = sign_commits(eng, "test_chain_id", specs) if specs else []
+    t_sign = time.perf_counter() - t_sign
+    reqs = [(T.MODE_LIGHT, vals, "test_chain_id", c.block_id, c.height, c, 0, 0) for c in commits]
+    pb = T.PreparedBatch(reqs)
+    if reqs:
+        pb.run(eng)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    if reqs:
+        pb.run(eng)
+    dt = time.perf_counter() - t0
+    ok = int((pb.codes() == 0).sum()) if reqs else 0
+    ver = int(pb.verified().sum()) if reqs else 0
+    tally = torch.tensor([ok, len(reqs), ver], dtype=torch.int64, device=dev)
+    tm = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tally)                      # int64 tallies
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+    ok, nb, ver = (int(x) for x in tally.tolist())
+    dt = float(tm.item())
+    eng.keyset_free(vals.keyset)
+    full = 100_000 * (nvals * 2 // 3 + 1)
+    return {"metric": "blocksync replay verifies/s (VerifyCommitLight per block)", "value": round(ver / dt, 1),
+            "unit": "verifies/s", "blocks_per_s": round(nb / dt, 1), "blocks": nb, "all_ok": ok == nb,
+            "verifies": ver, "seconds": round(dt, 4), "n_gpus": world,
+            "extrapolated_100k_blocks_s": round(full / (ver / dt), 2),
+            "config": {"workload": "C4 subset: %d blocks x %d validators (of 100k), key-cached, blocks sharded over %d GPU(s)"
+                       % (blocks, nvals, world), "keyset_build_s": round(t_ks, 3), "sign_s": round(t_sign, 2)}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c1,c3,c4")
+    ap.add_argument("--reps", type=int, default=1000)
+    ap.add_argument("--headers", type=int, default=10_000)
+    ap.add_argument("--gap", type=int, default=2)
+    ap.add_argument("--blocks", type=int, default=100)
+    ap.add_argument("--validators", type=int, default=10_000)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-keyset", action="store_true")
+    args = ap.parse_args()
+    import torch
+    import torch.distributed as dist
+    from tmed import Engine
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+    eng = Engine(local)
+    for cfg in args.config.split(","):
+        if cfg == "c1" and rank == 0:
+            r = c1(eng, args.reps, not args.no_cpu)
+        elif cfg == "c3" and rank == 0:
+            r = c3(eng, args.headers, args.gap, not args.no_keyset)
+        elif cfg == "c4":
+            r = c4(eng, args.blocks, args.validators, rank, world, dev)
+        else:
+            continue
+        if rank == 0:
+            print(json.dumps(r), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -169,7 +169,9 @@ typedef struct {
   const int64_t *powers;    /* n voting powers */
   const uint8_t *addresses; /* n x 20, PubKey.Address(); needed by LightTrusting only (may be NULL otherwise) */
   int64_t total_power;      /* vals.TotalVotingPower() (its panics stay in Go, :298-321) */
-  uint64_t keyset;          /* 0, or a tmed_keyset_load handle of exactly these pubkeys (key-cached path) */
+  uint64_t keyset;          /* 0, or a tmed_keyset_load handle holding these pubkeys (key-cached path) */
+  const uint32_t *keyset_index; /* NULL: validator i is key i of the key set; else its index there
+                                   (one key set can then serve many validator sets, e.g. the light client) */
 } tmed_valset;
 
 /* Commit + CommitSigs (types/block.go:575-634, 737-752). */

@@ -217,7 +217,7 @@ static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_resul
       const uint32_t sl = c.sig_lens ? c.sig_lens[i] : 64;
       memcpy(&sigs[k * 64], c.sigs + 64 * i, sl < 64 ? sl : 64);
       lens[k] = sl;
-      cb.val_idx[k] = (uint32_t)cd.val_idx;
+      cb.val_idx[k] = r.vals->keyset_index ? r.vals->keyset_index[cd.val_idx] : (uint32_t)cd.val_idx;
       cb.keyset[k] = r.vals->keyset;
     }
     int rc = verify(cb, valid.data());

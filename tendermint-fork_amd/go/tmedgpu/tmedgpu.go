@@ -74,10 +74,12 @@ const (
 // ValSet / CommitData are flat copies of types.ValidatorSet / types.Commit
 // (filled by the caller in package types, which owns those types).
 type ValSet struct {
-	PubKeys    []byte  // n x 32
-	Powers     []int64 // n
-	Addresses  []byte  // n x 20
-	TotalPower int64
+	PubKeys     []byte  // n x 32
+	Powers      []int64 // n
+	Addresses   []byte  // n x 20
+	TotalPower  int64
+	Keyset      uint64   // 0 or a LoadKeyset handle (cache key: ValidatorSet.Hash())
+	KeysetIndex []uint32 // nil, or validator i -> index in the key set
 }
 
 type BlockID struct {
@@ -175,6 +177,20 @@ func (a *arena) blockID(b *BlockID) C.tmed_block_id {
 		psh_hash: a.bytes(b.PSHHash), psh_hash_len: C.uint32_t(len(b.PSHHash))}
 }
 
+// LoadKeyset decodes a validator set's keys once and builds their comb tables in HBM.
+func (e *Engine) LoadKeyset(pubKeys []byte) (uint64, error) {
+	var a arena
+	defer a.free()
+	var h C.uint64_t
+	if rc := C.tmed_keyset_load(e.ctx, a.bytes(pubKeys), C.size_t(len(pubKeys)/32), &h); rc != 0 {
+		return 0, errors.New(C.GoString(C.tmed_strerror(rc)))
+	}
+	return uint64(h), nil
+}
+
+// FreeKeyset releases a key set.
+func (e *Engine) FreeKeyset(h uint64) { C.tmed_keyset_free(e.ctx, C.uint64_t(h)) }
+
 // VerifyCommits verifies many commits with ONE device batch.
 func (e *Engine) VerifyCommits(reqs []Request) ([]Result, error) {
 	n := len(reqs)
@@ -190,7 +206,8 @@ func (e *Engine) VerifyCommits(reqs []Request) ([]Result, error) {
 	for i := range reqs {
 		r := &reqs[i]
 		vs[i] = C.tmed_valset{n: C.size_t(len(r.Vals.Powers)), pubkeys: a.bytes(r.Vals.PubKeys),
-			powers: a.i64(r.Vals.Powers), addresses: a.bytes(r.Vals.Addresses), total_power: C.int64_t(r.Vals.TotalPower)}
+			powers: a.i64(r.Vals.Powers), addresses: a.bytes(r.Vals.Addresses), total_power: C.int64_t(r.Vals.TotalPower),
+			keyset: C.uint64_t(r.Vals.Keyset), keyset_index: a.u32(r.Vals.KeysetIndex)}
 		c := r.Commit
 		cs[i] = C.tmed_commit{height: C.int64_t(c.Height), round: C.int32_t(c.Round), block_id: a.blockID(&c.BlockID),
 			n_sigs: C.size_t(len(c.Flags)), flags: a.bytes(c.Flags), addresses: a.bytes(c.Addresses),

@@ -69,6 +69,37 @@ class Commit:
 
 
 @dataclass
+class PackedCommit:
+    """A Commit held as arrays (bulk workloads: blocksync replay, light-client batches)."""
+    height: int
+    round: int
+    block_id: BlockID
+    flags: np.ndarray        # u8[n]  BlockIDFlag
+    addresses: np.ndarray    # u8[n,20]
+    ts_seconds: np.ndarray   # i64[n]
+    ts_nanos: np.ndarray     # i32[n]
+    sigs: np.ndarray         # u8[n,64]
+    sig_lens: np.ndarray     # u32[n]
+
+    @property
+    def signatures(self):
+        return _PackedSigs(self)
+
+
+class _PackedSigs:
+    def __init__(self, pc):
+        self.pc = pc
+
+    def __len__(self):
+        return self.pc.flags.shape[0]
+
+    def __getitem__(self, i):
+        pc = self.pc
+        return CommitSig(int(pc.flags[i]), pc.addresses[i].tobytes(), (int(pc.ts_seconds[i]), int(pc.ts_nanos[i])),
+                         pc.sigs[i, :int(pc.sig_lens[i])].tobytes())
+
+
+@dataclass
 class Validator:
     pub_key: bytes
     voting_power: int
@@ -89,6 +120,8 @@ class ValidatorSet:
     validators: List[Validator]
     _total: int = field(default=0, repr=False)
     _packed: Optional[tuple] = field(default=None, repr=False)
+    keyset: int = field(default=0, repr=False)                       # tmed_keyset_load handle (0 = none)
+    keyset_index: Optional[np.ndarray] = field(default=None, repr=False)  # validator -> key-set index (u32)
 
     def size(self) -> int:
         return len(self.validators)
@@ -172,7 +205,8 @@ class _BlockIDC(ctypes.Structure):
 
 class _ValsetC(ctypes.Structure):
     _fields_ = [("n", ctypes.c_size_t), ("pubkeys", ctypes.c_void_p), ("powers", ctypes.c_void_p),
-                ("addresses", ctypes.c_void_p), ("total_power", ctypes.c_int64)]
+                ("addresses", ctypes.c_void_p), ("total_power", ctypes.c_int64), ("keyset", ctypes.c_uint64),
+                ("keyset_index", ctypes.c_void_p)]
 
 
 class _CommitC(ctypes.Structure):
@@ -222,7 +256,13 @@ def _block_id_c(b: BlockID, keep):
                      ctypes.cast(ctypes.c_char_p(ph), ctypes.c_void_p), len(ph))
 
 
-def _commit_c(c: Commit, keep):
+def _commit_c(c, keep):
+    if isinstance(c, PackedCommit):
+        arrs = [np.ascontiguousarray(c.flags, np.uint8), np.ascontiguousarray(c.addresses, np.uint8),
+                np.ascontiguousarray(c.ts_seconds, np.int64), np.ascontiguousarray(c.ts_nanos, np.int32),
+                np.ascontiguousarray(c.sigs, np.uint8), np.ascontiguousarray(c.sig_lens, np.uint32)]
+        keep.extend(arrs)
+        return _CommitC(c.height, c.round, _block_id_c(c.block_id, keep), arrs[0].shape[0], *[_ptr(a) for a in arrs])
     n = len(c.signatures)
     m = max(n, 1)
     flags = np.zeros(m, np.uint8)
@@ -267,6 +307,49 @@ def _to_error(code, r: _ResultC, vals: ValidatorSet, block_id, commit: Commit):
     raise RuntimeError("tmed: unknown commit outcome %d" % code)
 
 
+class PreparedBatch:
+    """Requests packed into C structs once, for repeated timing of the seam itself
+    (host sign-bytes + staging + device + replay), without Python packing in the loop."""
+
+    def __init__(self, requests: Sequence[tuple]):
+        self.requests = list(requests)
+        self.keep = []
+        n = len(self.requests)
+        self.n = n
+        self.reqs = (_RequestC * max(n, 1))()
+        for q, (mode, vals, chain_id, block_id, height, commit, num, den) in enumerate(self.requests):
+            pubs, powers, addrs = vals.packed()
+            kidx = getattr(vals, "keyset_index", None)
+            vs = _ValsetC(len(vals.validators), _ptr(pubs), _ptr(powers), _ptr(addrs), vals.total_voting_power(),
+                          getattr(vals, "keyset", 0) or 0, None if kidx is None else _ptr(kidx))
+            cc = _commit_c(commit, self.keep)
+            cid = chain_id.encode()
+            bid = _block_id_c(block_id, self.keep) if block_id is not None else None
+            self.keep.extend([vs, cc, cid, bid, kidx, pubs, powers, addrs])
+            self.reqs[q] = _RequestC(mode, cid, len(cid), ctypes.pointer(vs),
+                                     ctypes.pointer(bid) if bid is not None else None, height, ctypes.pointer(cc),
+                                     num, den)
+        self.res = (_ResultC * max(n, 1))()
+
+    def run(self, engine):
+        rc = _bind().tmed_verify_commits(engine._h, self.reqs, self.n, self.res)
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_verify_commits")
+        return self.res
+
+    def codes(self):
+        return np.array([self.res[q].code for q in range(self.n)], np.int32)
+
+    def verified(self):
+        return np.array([self.res[q].verified for q in range(self.n)], np.int64)
+
+    def errors(self):
+        out = []
+        for q, (mode, vals, chain_id, block_id, height, commit, num, den) in enumerate(self.requests):
+            out.append(_to_error(self.res[q].code, self.res[q], vals, block_id, commit))
+        return out
+
+
 def verify_commits(engine, requests: Sequence[tuple], verifier=None, stats: Optional[list] = None):
     """Verify many commits with one device batch.
 
@@ -281,7 +364,10 @@ def verify_commits(engine, requests: Sequence[tuple], verifier=None, stats: Opti
     reqs = (_RequestC * max(n, 1))()
     for q, (mode, vals, chain_id, block_id, height, commit, num, den) in enumerate(requests):
         pubs, powers, addrs = vals.packed()
-        vs = _ValsetC(len(vals.validators), _ptr(pubs), _ptr(powers), _ptr(addrs), vals.total_voting_power())
+        kidx = getattr(vals, "keyset_index", None)
+        vs = _ValsetC(len(vals.validators), _ptr(pubs), _ptr(powers), _ptr(addrs), vals.total_voting_power(),
+                      getattr(vals, "keyset", 0) or 0, None if kidx is None else _ptr(kidx))
+        keep.append(kidx)
         cc = _commit_c(commit, keep)
         cid = chain_id.encode()
         bid = _block_id_c(block_id, keep) if block_id is not None else None

@@ -47,3 +47,66 @@ def c2_messages(start: int, n: int, chain_id: str = "test_chain_id"):
         base += int(off[-1])
         i = j_end
     return np.concatenate(parts), np.concatenate(offs).astype(np.uint32)
+
+
+# ----------------------------------------------------------------------------- commits (C1, C3, C4)
+
+def seeds_from_tag(tag: bytes, start: int, n: int) -> np.ndarray:
+    out = np.empty((n, 32), np.uint8)
+    for j in range(n):
+        out[j] = np.frombuffer(hashlib.sha256(tag + (start + j).to_bytes(8, "little")).digest(), np.uint8)
+    return out
+
+
+def pubkeys_of(engine, seeds: np.ndarray) -> np.ndarray:
+    """ed25519 public keys of seeds (GPU RFC 8032 key derivation)."""
+    n = seeds.shape[0]
+    _, pubs = engine.sign_arrays(seeds, np.zeros(16, np.uint8), np.zeros(n + 1, np.uint32))
+    return pubs
+
+
+def make_valset(pubs: np.ndarray, powers):
+    """ValidatorSet sorted like types.ValidatorsByVotingPower (power desc, address asc,
+    types/validator_set.go:906-911); returns (vals, order) with order[i] = input index of validator i."""
+    from .types import Validator, ValidatorSet, address_of
+    items = [(int(powers[i]), address_of(pubs[i].tobytes()), i) for i in range(pubs.shape[0])]
+    items.sort(key=lambda t: (-t[0], t[1]))
+    vals = ValidatorSet([Validator(pubs[i].tobytes(), p, 0, a) for p, a, i in items])
+    return vals, np.array([i for _, _, i in items], np.int64)
+
+
+def sign_commits(engine, chain_id: str, specs):
+    """specs: list of (seeds_in_validator_order u8[n,32], addresses u8[n,20], height, round, BlockID,
+    ts_base_seconds, flags or None).  All votes of all commits are signed in ONE GPU call.
+    Returns a list of PackedCommit (timestamps: base + i ms for validator i)."""
+    from .types import PackedCommit
+    flats, offs, seeds_all, metas = [], [], [], []
+    base = 0
+    for seeds, addrs, height, round_, bid, ts0, flags in specs:
+        n = seeds.shape[0]
+        t = make_template(chain_id, height, round_, bid.hash, bid.psh_total, bid.psh_hash)
+        sec = np.full(n, ts0, np.int64) + (np.arange(n) // 1000)
+        nan = ((np.arange(n) % 1000) * 1_000_000).astype(np.int32)
+        fl = np.full(n, 2, np.uint8) if flags is None else np.asarray(flags, np.uint8)
+        f, o = vote_sign_bytes_batch(t, sec, nan, fl)
+        flats.append(f)
+        offs.append(o[:-1].astype(np.int64) + base)
+        base += int(o[-1])
+        seeds_all.append(seeds)
+        metas.append((height, round_, bid, addrs, sec, nan, fl))
+    flat = np.concatenate(flats) if flats else np.zeros(0, np.uint8)
+    off = np.concatenate(offs + [np.array([base], np.int64)]).astype(np.uint32)
+    sigs, _ = engine.sign_arrays(np.concatenate(seeds_all), np.concatenate([flat, np.zeros(16, np.uint8)]), off)
+    out, k = [], 0
+    for (height, round_, bid, addrs, sec, nan, fl) in metas:
+        n = sec.shape[0]
+        s = sigs[k:k + n].copy()
+        lens = np.full(n, 64, np.uint32)
+        absent = fl == 1
+        s[absent] = 0
+        lens[absent] = 0
+        a = addrs.copy()
+        a[absent] = 0
+        out.append(PackedCommit(height, round_, bid, fl, a, sec, nan, s, lens))
+        k += n
+    return out

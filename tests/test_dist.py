@@ -1,0 +1,72 @@
+"""N>1 path on CPU: two gloo ranks shard a batch of commits, verify their shards through the
+C++ seam (oracle as the batch verifier — no GPU here), all-reduce the int64 tallies and
+all-gather the decisions; the result must equal the single-process result."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _requests():
+    from commit_cases import pbid, scenarios
+    reqs, exp = [], []
+    from commit_cases import oracle_result
+    for mode, vs, pv, chain, bid, h, cm, pc, num, den in scenarios(seed=9, count=24):
+        reqs.append((mode, pv, chain, pbid(bid), h, pc, num, den))
+        exp.append(oracle_result(mode, vs, chain, bid, h, cm, num, den))
+    return reqs, exp
+
+
+def _verifier(pubs, sigs, lens, msgs, offs):
+    from oracle import port
+    out = port.verify_batch(pubs, sigs, msgs, offs.astype(np.uint64), 2)
+    out[lens != 64] = 0
+    return out
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "tendermint-fork_amd"), os.path.join(ROOT, "tests")]
+    import torch.distributed as dist
+    from tmed.dist import verify_sharded
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    reqs, exp = _requests()
+    r = verify_sharded(None, reqs, rank, world, verifier=_verifier)
+    q.put((rank, r["ok"], r["commits"], r["verified"], r["codes"].tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_tallies_match_single_process(world):
+    import torch.distributed as dist  # noqa: F401
+    from tmed.dist import shard
+    reqs, exp = _requests()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp_ok = sum(e is None for e in exp)
+    exp_codes = [0 if e is None else 1 for e in exp]
+    for rank, ok, n, verified, codes in res:
+        assert ok == exp_ok and n == len(reqs)
+        assert codes == exp_codes
+    assert sorted(sum((shard(len(reqs), r, world) for r in range(world)), [])) == list(range(len(reqs)))

@@ -34,3 +34,46 @@ def test_reference_cases_gpu(engine):
     resign(cm2, 2, seeds[2], "CentaurusA")
     pv, pc2 = to_product(vs, cm2)
     assert pv.verify_commit_light_trusting(engine, "test_chain_id", pc2, 1, 3) is None
+
+
+def test_keyset_seam_and_packed_commits(engine):
+    """Key-cached seam (global key set + per-valset index) and PackedCommit == reference loops."""
+    import numpy as np
+    from oracle import commit as C
+    from oracle.fixtures import make_block_id, make_commit, make_valset, resign, seed_of
+    from commit_cases import to_product
+    vs, seeds = make_valset([seed_of("ks", i) for i in range(12)], [10] * 11 + [30])
+    bid = make_block_id("ks")
+    cms = []
+    for h in range(6):
+        cm = make_commit(vs, seeds, "kc", 100 + h, 0, bid)
+        if h % 2:
+            resign(cm, h, seeds[h], "bad")
+        cms.append(cm)
+    pv, _ = to_product(vs, cms[0])
+    pubs = np.array([np.frombuffer(v.pub_key, np.uint8) for v in pv.validators])
+    # key set holds the keys in reverse order: exercise keyset_index
+    ks = engine.keyset_load(pubs[::-1].copy())
+    pv.keyset = ks
+    pv.keyset_index = np.arange(len(pubs) - 1, -1, -1).astype(np.uint32)
+    try:
+        reqs, exp = [], []
+        for cm in cms:
+            _, pc = to_product(vs, cm)
+            packed = T.PackedCommit(pc.height, pc.round, pc.block_id,
+                                    np.array([s.flag for s in pc.signatures], np.uint8),
+                                    np.array([np.frombuffer(s.address, np.uint8) for s in pc.signatures]),
+                                    np.array([s.timestamp[0] for s in pc.signatures], np.int64),
+                                    np.array([s.timestamp[1] for s in pc.signatures], np.int32),
+                                    np.array([np.frombuffer(s.signature, np.uint8) for s in pc.signatures]),
+                                    np.full(len(pc.signatures), 64, np.uint32))
+            for mode in (T.MODE_COMMIT, T.MODE_LIGHT, T.MODE_LIGHT_TRUSTING):
+                reqs.append((mode, pv, "kc", pbid(bid), cm.height, packed, 1, 3))
+                exp.append(oracle_result(mode, vs, "kc", bid, cm.height, cm, 1, 3))
+        got = T.verify_commits(engine, reqs)
+        pb = T.PreparedBatch(reqs)
+        pb.run(engine)
+        for g, g2, e in zip(got, pb.errors(), exp):
+            assert same(g, e) and same(g2, e), (g, g2, e)
+    finally:
+        engine.keyset_free(ks)

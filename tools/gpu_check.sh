@@ -30,6 +30,9 @@ for s in $STEPS; do
         echo "$cfg rc=$rc $(tail -1 $OUT/variant.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])' 2>/dev/null)" | tee -a $OUT/variants.txt
         if fatal $rc; then break; fi
       done ;;
+    commits)
+      timeout -k 10 900 python bench_commits.py --config c1,c3,c4 > $OUT/bench_commits.log 2>&1; rc=$?
+      echo "commits rc=$rc"; grep '^{' $OUT/bench_commits.log ;;
     probe)
       timeout -k 10 300 python tools/probe_valu.py > $OUT/probe_valu.json 2>$OUT/probe_valu.err; rc=$?
       echo "probe rc=$rc"; cat $OUT/probe_valu.json ;;
