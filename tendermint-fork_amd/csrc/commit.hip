@@ -17,11 +17,14 @@
 #include <string.h>
 
 #include <functional>
+#include <memory>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <vector>
 
 #include "../../include/tmed25519.h"
+#include "ctx.h"
 #include "signbytes.h"
 
 namespace {
@@ -67,11 +70,13 @@ AddrKey addr_key(const uint8_t *p) {
   return k;
 }
 
+using AddrIndex = std::unordered_map<AddrKey, int32_t, AddrHash>;  // address -> first validator idx
+
 struct Plan {
   bool decided = false;
   int64_t needed = 0;
   std::vector<int32_t> bit_of_sig;  // sig idx -> candidate slot (-1 = not sent)
-  std::unordered_map<AddrKey, int32_t, AddrHash> addr_index;  // Trusting: address -> first validator idx
+  const AddrIndex *addr_index = nullptr;  // Trusting only (shared by requests on the same valset)
 };
 
 int check_request(const tmed_commit_request &r) {
@@ -91,16 +96,98 @@ int check_request(const tmed_commit_request &r) {
 // Flattened candidates of one seam call.
 struct CandBatch {
   size_t m = 0;
-  std::vector<uint8_t> pubs, sigs, msgs;
-  std::vector<uint32_t> lens, offs, val_idx;
+  std::vector<uint8_t> pubs, sigs, flags;
+  std::vector<uint32_t> lens, val_idx, tmpl;
+  std::vector<int64_t> ts_sec;
+  std::vector<int32_t> ts_nanos;
   std::vector<uint64_t> keyset;
+  std::vector<tmed::VoteEncoder> enc;  // per request
+  // host-assembled sign-bytes (built on demand: callback verifiers, oversize templates)
+  std::vector<uint8_t> msgs;
+  std::vector<uint32_t> offs;
+  int build_host_msgs() {
+    if (!offs.empty()) return TMED_OK;
+    offs.resize(m + 1);
+    size_t total = 0;
+    for (size_t k = 0; k < m; k++) {
+      offs[k] = (uint32_t)total;
+      total += enc[tmpl[k]].size(flags[k], ts_sec[k], ts_nanos[k]);
+      if (total > 0xffffffffu) return TMED_EINVAL;
+    }
+    offs[m] = (uint32_t)total;
+    msgs.resize(total + 16);
+    for (size_t k = 0; k < m; k++) enc[tmpl[k]].write(msgs.data() + offs[k], flags[k], ts_sec[k], ts_nanos[k]);
+    return TMED_OK;
+  }
 };
-using BatchVerifier = std::function<int(const CandBatch &, uint8_t *valid)>;
+using BatchVerifier =
+    std::function<int(const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands, uint8_t *valid)>;
+
+// Per-request CanonicalVote encoders for the requests that have candidates.
+static int init_encoders(const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands,
+                         std::vector<tmed::VoteEncoder> &enc, std::vector<uint8_t> &used) {
+  enc.assign(n, tmed::VoteEncoder());
+  used.assign(n, 0);
+  for (const Cand &cd : cands) used[cd.req] = 1;
+  for (size_t q = 0; q < n; q++) {
+    if (!used[q]) continue;
+    const tmed_commit &c = *reqs[q].commit;
+    tmed_vote_template t;
+    t.chain_id = reqs[q].chain_id;
+    t.chain_id_len = reqs[q].chain_id_len;
+    t.height = c.height;
+    t.round = c.round;
+    t.block_hash = c.block_id.hash;
+    t.block_hash_len = c.block_id.hash_len;
+    t.psh_total = c.block_id.psh_total;
+    t.psh_hash = c.block_id.psh_hash;
+    t.psh_hash_len = c.block_id.psh_hash_len;
+    if (enc[q].init(&t) != TMED_OK) return TMED_EINVAL;
+  }
+  return TMED_OK;
+}
+
+// Flatten candidates with host-assembled sign-bytes (callback verifiers; oversize templates).
+static int build_cand_batch(const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands,
+                            CandBatch &cb) {
+  std::vector<uint8_t> used;
+  int rc = init_encoders(reqs, n, cands, cb.enc, used);
+  if (rc != TMED_OK) return rc;
+  const size_t m = cands.size();
+  cb.m = m;
+  cb.pubs.resize(m * 32);
+  cb.sigs.assign(m * 64, 0);
+  cb.lens.resize(m);
+  cb.val_idx.resize(m);
+  cb.keyset.resize(m);
+  cb.tmpl.resize(m);
+  cb.flags.resize(m);
+  cb.ts_sec.resize(m);
+  cb.ts_nanos.resize(m);
+  for (size_t k = 0; k < m; k++) {
+    const Cand &cd = cands[k];
+    const tmed_commit_request &r = reqs[cd.req];
+    const tmed_commit &c = *r.commit;
+    const size_t i = (size_t)cd.sig_idx;
+    memcpy(&cb.pubs[k * 32], r.vals->pubkeys + 32 * (size_t)cd.val_idx, 32);
+    const uint32_t sl = c.sig_lens ? c.sig_lens[i] : 64;
+    memcpy(&cb.sigs[k * 64], c.sigs + 64 * i, sl < 64 ? sl : 64);
+    cb.lens[k] = sl;
+    cb.val_idx[k] = r.vals->keyset_index ? r.vals->keyset_index[cd.val_idx] : (uint32_t)cd.val_idx;
+    cb.keyset[k] = r.vals->keyset;
+    cb.tmpl[k] = (uint32_t)cd.req;
+    cb.flags[k] = c.flags[i];
+    cb.ts_sec[k] = c.ts_seconds[i];
+    cb.ts_nanos[k] = c.ts_nanos[i];
+  }
+  return cb.build_host_msgs();
+}
 
 static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, const BatchVerifier &verify) {
   if (n && (!reqs || !out)) return TMED_EINVAL;
   std::vector<Plan> plans(n);
   std::vector<Cand> cands;
+  std::unordered_map<const tmed_valset *, std::unique_ptr<AddrIndex>> addr_cache;
   for (size_t q = 0; q < n; q++) {
     const tmed_commit_request &r = reqs[q];
     tmed_commit_result &o = out[q];
@@ -147,14 +234,19 @@ static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_resul
       int64_t prod;
       if (safe_mul(vs.total_power, r.trust_num, &prod)) { o.code = TMED_COMMIT_OVERFLOW; pl.decided = true; continue; }
       pl.needed = prod / r.trust_den;  // Go int64 division truncates toward zero, as C++ does
-      pl.addr_index.reserve(vs.n * 2);
-      for (size_t v = 0; v < vs.n; v++) pl.addr_index.emplace(addr_key(vs.addresses + 20 * v), (int32_t)v);  // first match wins
+      auto &slot = addr_cache[r.vals];
+      if (!slot) {
+        slot.reset(new AddrIndex());
+        slot->reserve(vs.n * 2);
+        for (size_t v = 0; v < vs.n; v++) slot->emplace(addr_key(vs.addresses + 20 * v), (int32_t)v);  // first match wins
+      }
+      pl.addr_index = slot.get();
       std::vector<int32_t> seen(vs.n, -1);
       int64_t tally = 0;
       for (size_t i = 0; i < c.n_sigs; i++) {
         if (c.flags[i] != kCommit) continue;
-        auto it = pl.addr_index.find(addr_key(c.addresses + 20 * i));
-        if (it == pl.addr_index.end()) continue;
+        auto it = pl.addr_index->find(addr_key(c.addresses + 20 * i));
+        if (it == pl.addr_index->end()) continue;
         const int32_t v = it->second;
         if (seen[v] >= 0) break;  // the loop returns the double-vote error here
         seen[v] = (int32_t)i;
@@ -170,57 +262,7 @@ static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_resul
   const size_t m = cands.size();
   std::vector<uint8_t> valid(m, 0);
   if (m) {
-    CandBatch cb;
-    cb.m = m;
-    cb.pubs.resize(m * 32);
-    cb.sigs.resize(m * 64);
-    cb.lens.resize(m);
-    cb.offs.resize(m + 1);
-    cb.val_idx.resize(m);
-    cb.keyset.resize(m);
-    std::vector<uint8_t> &pubs = cb.pubs, &sigs = cb.sigs;
-    std::vector<uint32_t> &lens = cb.lens, &offs = cb.offs;
-    std::vector<tmed::VoteEncoder> enc(n);
-    for (size_t q = 0; q < n; q++) {
-      if (plans[q].decided) continue;
-      const tmed_commit &c = *reqs[q].commit;
-      tmed_vote_template t;
-      t.chain_id = reqs[q].chain_id;
-      t.chain_id_len = reqs[q].chain_id_len;
-      t.height = c.height;
-      t.round = c.round;
-      t.block_hash = c.block_id.hash;
-      t.block_hash_len = c.block_id.hash_len;
-      t.psh_total = c.block_id.psh_total;
-      t.psh_hash = c.block_id.psh_hash;
-      t.psh_hash_len = c.block_id.psh_hash_len;
-      if (enc[q].init(&t) != TMED_OK) return TMED_EINVAL;
-    }
-    size_t total = 0;
-    for (size_t k = 0; k < m; k++) {
-      const Cand &cd = cands[k];
-      const tmed_commit &c = *reqs[cd.req].commit;
-      offs[k] = (uint32_t)total;
-      total += enc[cd.req].size(c.flags[cd.sig_idx], c.ts_seconds[cd.sig_idx], c.ts_nanos[cd.sig_idx]);
-      if (total > 0xffffffffu) return TMED_EINVAL;
-    }
-    offs[m] = (uint32_t)total;
-    cb.msgs.resize(total + 16);
-    std::vector<uint8_t> &msgs = cb.msgs;
-    for (size_t k = 0; k < m; k++) {
-      const Cand &cd = cands[k];
-      const tmed_commit_request &r = reqs[cd.req];
-      const tmed_commit &c = *r.commit;
-      const size_t i = (size_t)cd.sig_idx;
-      enc[cd.req].write(msgs.data() + offs[k], c.flags[i], c.ts_seconds[i], c.ts_nanos[i]);
-      memcpy(&pubs[k * 32], r.vals->pubkeys + 32 * (size_t)cd.val_idx, 32);
-      const uint32_t sl = c.sig_lens ? c.sig_lens[i] : 64;
-      memcpy(&sigs[k * 64], c.sigs + 64 * i, sl < 64 ? sl : 64);
-      lens[k] = sl;
-      cb.val_idx[k] = r.vals->keyset_index ? r.vals->keyset_index[cd.val_idx] : (uint32_t)cd.val_idx;
-      cb.keyset[k] = r.vals->keyset;
-    }
-    int rc = verify(cb, valid.data());
+    int rc = verify(reqs, n, cands, valid.data());
     if (rc != TMED_OK) return rc;
   }
 
@@ -263,8 +305,8 @@ static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_resul
       std::vector<int32_t> seen(vs.n, -1);
       for (size_t i = 0; i < c.n_sigs && o.code < 0; i++) {
         if (c.flags[i] != kCommit) continue;
-        auto it = pl.addr_index.find(addr_key(c.addresses + 20 * i));
-        if (it == pl.addr_index.end()) continue;
+        auto it = pl.addr_index->find(addr_key(c.addresses + 20 * i));
+        if (it == pl.addr_index->end()) continue;
         const int32_t v = it->second;
         if (seen[v] >= 0) {
           o.code = TMED_COMMIT_DOUBLE_VOTE; o.val_idx = v; o.idx_first = seen[v]; o.idx = (int32_t)i;
@@ -285,19 +327,24 @@ static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_resul
 extern "C" int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out,
                                         tmed_batch_verify_fn verify, void *user) {
   if (!verify) return TMED_EINVAL;
-  return run_seam(reqs, n, out, [&](const CandBatch &cb, uint8_t *valid) {
-    return verify(user, cb.pubs.data(), cb.sigs.data(), cb.lens.data(), cb.msgs.data(), cb.offs.data(), cb.m, valid);
-  });
+  return run_seam(reqs, n, out,
+                  [&](const tmed_commit_request *rq, size_t nr, const std::vector<Cand> &cands, uint8_t *valid) {
+                    CandBatch cb;
+                    int rc = build_cand_batch(rq, nr, cands, cb);
+                    if (rc != TMED_OK) return rc;
+                    return verify(user, cb.pubs.data(), cb.sigs.data(), cb.lens.data(), cb.msgs.data(),
+                                  cb.offs.data(), cb.m, valid);
+                  });
 }
 
-// GPU verifier: candidates of validator sets with a key-set handle go through the
-// key-cached kernel (one launch per distinct key set), the rest through the generic one.
-static int ctx_verify(tmed_ctx *ctx, const CandBatch &cb, uint8_t *valid) {
+// Host fallback of the GPU verifier for templates the device assembler cannot hold.
+static int ctx_verify_host_msgs(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
+                                const std::vector<Cand> &cands, uint8_t *valid) {
+  CandBatch cb;
+  int rc = build_cand_batch(reqs, n, cands, cb);
+  if (rc != TMED_OK) return rc;
   std::unordered_map<uint64_t, std::vector<uint32_t>> groups;
   for (size_t k = 0; k < cb.m; k++) groups[cb.keyset[k]].push_back((uint32_t)k);
-  if (groups.size() == 1 && groups.begin()->first == 0)
-    return tmed_verify_batch(ctx, cb.pubs.data(), cb.sigs.data(), cb.lens.data(), cb.msgs.data(), cb.offs.data(),
-                             cb.m, valid);
   for (auto &g : groups) {
     const std::vector<uint32_t> &ix = g.second;
     const size_t m = ix.size();
@@ -319,12 +366,89 @@ static int ctx_verify(tmed_ctx *ctx, const CandBatch &cb, uint8_t *valid) {
       total += len;
     }
     offs[m] = (uint32_t)total;
-    int rc = g.first == 0
-                 ? tmed_verify_batch(ctx, pubs.data(), sigs.data(), lens.data(), msgs.data(), offs.data(), m, out.data())
-                 : tmed_verify_batch_keyset(ctx, g.first, vidx.data(), sigs.data(), lens.data(), msgs.data(),
-                                            offs.data(), m, out.data());
+    rc = g.first == 0 ? tmed_verify_batch(ctx, pubs.data(), sigs.data(), lens.data(), msgs.data(), offs.data(), m,
+                                          out.data())
+                      : tmed_verify_batch_keyset(ctx, g.first, vidx.data(), sigs.data(), lens.data(), msgs.data(),
+                                                 offs.data(), m, out.data());
     if (rc != TMED_OK) return rc;
     for (size_t j = 0; j < m; j++) valid[ix[j]] = out[j];
+  }
+  return TMED_OK;
+}
+
+// GPU verifier: sign-bytes are assembled on the device from per-commit templates
+// (SURVEY.md §8f f1), so only key references, signatures, flags and timestamps cross
+// PCIe; they are written straight from the request arrays into the pinned staging area
+// (multi-threaded for large batches).  Candidates of validator sets with a key-set handle
+// go through the key-cached kernels, one launch sequence per distinct key set.
+static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands,
+                      uint8_t *valid) {
+  std::vector<tmed::VoteEncoder> enc;
+  std::vector<uint8_t> used;
+  int rc = init_encoders(reqs, n, cands, enc, used);
+  if (rc != TMED_OK) return rc;
+  std::vector<uint8_t> tmpl(n * tmed::kVoteTmplBytes);
+  for (size_t q = 0; q < n; q++)
+    if (used[q] && !enc[q].device_template(&tmpl[q * tmed::kVoteTmplBytes], tmed::kVoteTmplBytes))
+      return ctx_verify_host_msgs(ctx, reqs, n, cands, valid);
+  // group by key set (usually a single group)
+  std::vector<uint64_t> gkeys;
+  std::vector<std::vector<uint32_t>> gidx;
+  for (size_t k = 0; k < cands.size(); k++) {
+    const uint64_t ks = reqs[cands[k].req].vals->keyset;
+    size_t g = 0;
+    while (g < gkeys.size() && gkeys[g] != ks) g++;
+    if (g == gkeys.size()) { gkeys.push_back(ks); gidx.emplace_back(); }
+    gidx[g].push_back((uint32_t)k);
+  }
+  for (size_t g = 0; g < gkeys.size(); g++) {
+    const std::vector<uint32_t> &ix = gidx[g];
+    const uint32_t m = (uint32_t)ix.size();
+    const bool keyed = gkeys[g] != 0;
+    tmed::VoteStage st;
+    rc = tmed::votes_stage(ctx, gkeys[g], m, n, st);
+    if (rc != TMED_OK) return rc;
+    memcpy(st.tmpl, tmpl.data(), tmpl.size());
+    auto fill = [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t j = lo; j < hi; j++) {
+        const Cand &cd = cands[ix[j]];
+        const tmed_commit_request &r = reqs[cd.req];
+        const tmed_commit &c = *r.commit;
+        const size_t i = (size_t)cd.sig_idx;
+        if (keyed) {
+          const uint32_t v = r.vals->keyset_index ? r.vals->keyset_index[cd.val_idx] : (uint32_t)cd.val_idx;
+          memcpy(st.key + (size_t)j * 4, &v, 4);
+        } else {
+          memcpy(st.key + (size_t)j * 32, r.vals->pubkeys + 32 * (size_t)cd.val_idx, 32);
+        }
+        const uint32_t sl = c.sig_lens ? c.sig_lens[i] : 64;
+        uint8_t *sd = st.sig + (size_t)j * 64;
+        if (sl >= 64) memcpy(sd, c.sigs + 64 * i, 64);
+        else { memset(sd, 0, 64); memcpy(sd, c.sigs + 64 * i, sl); }
+        st.tidx[j] = (uint32_t)cd.req;
+        st.flag[j] = c.flags[i];
+        st.sec[j] = c.ts_seconds[i];
+        st.nan[j] = c.ts_nanos[i];
+      }
+    };
+    const uint32_t nthreads = m >= 65536 ? std::min<uint32_t>(16, std::max(1u, std::thread::hardware_concurrency())) : 1;
+    if (nthreads > 1) {
+      std::vector<std::thread> th;
+      for (uint32_t t = 0; t < nthreads; t++)
+        th.emplace_back(fill, (uint32_t)((uint64_t)m * t / nthreads), (uint32_t)((uint64_t)m * (t + 1) / nthreads));
+      for (auto &x : th) x.join();
+    } else {
+      fill(0, m);
+    }
+    std::vector<uint8_t> out(m);
+    rc = tmed::votes_launch(ctx, st, out.data());
+    if (rc != TMED_OK) return rc;
+    for (uint32_t j = 0; j < m; j++) {
+      const Cand &cd = cands[ix[j]];
+      const tmed_commit &c = *reqs[cd.req].commit;
+      const uint32_t sl = c.sig_lens ? c.sig_lens[cd.sig_idx] : 64;
+      valid[ix[j]] = sl == 64 ? out[j] : 0;  // crypto/ed25519/ed25519.go:150-152
+    }
   }
   return TMED_OK;
 }
@@ -332,5 +456,8 @@ static int ctx_verify(tmed_ctx *ctx, const CandBatch &cb, uint8_t *valid) {
 extern "C" int tmed_verify_commits(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
                                    tmed_commit_result *out) {
   if (!ctx) return TMED_EINVAL;
-  return run_seam(reqs, n, out, [&](const CandBatch &cb, uint8_t *valid) { return ctx_verify(ctx, cb, valid); });
+  return run_seam(reqs, n, out,
+                  [&](const tmed_commit_request *rq, size_t nr, const std::vector<Cand> &cands, uint8_t *valid) {
+                    return ctx_verify(ctx, rq, nr, cands, valid);
+                  });
 }

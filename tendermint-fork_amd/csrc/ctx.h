@@ -67,6 +67,30 @@ struct Keyset {
 };
 
 int build_comb(tmed_ctx *c, const uint8_t *d_pubs, size_t n, int negate, uint8_t *d_ok, int4 *d_comb);
+
+// Commit-seam device path (f1): stage votes (key refs, signatures, per-commit templates,
+// template index / flag / timestamp per vote), assemble sign-bytes on the device, verify
+// (generic when keyset == 0, key-cached otherwise), return one byte per vote.
+int verify_votes_device(tmed_ctx *c, uint64_t keyset, const uint8_t *keys, const uint8_t *sigs,
+                        const uint8_t *tmpl, size_t n_tmpl, const uint32_t *tmpl_idx, const uint8_t *flags,
+                        const int64_t *ts_sec, const int32_t *ts_nanos, uint32_t m, uint8_t *out);
+
+// Zero-copy form of the same: votes_stage() locks the context and returns pointers into
+// the pinned staging area; the caller fills them; votes_launch() copies, runs and
+// unlocks.  (The seam fills the staging area straight from the request arrays.)
+struct VoteStage {
+  std::unique_lock<std::mutex> lock;
+  const Keyset *ks = nullptr;
+  uint32_t m = 0;
+  size_t n_tmpl = 0, total = 0;
+  size_t o_key = 0, o_sig = 0, o_tmpl = 0, o_tidx = 0, o_flag = 0, o_sec = 0, o_nan = 0;
+  uint8_t *key = nullptr, *sig = nullptr, *tmpl = nullptr, *flag = nullptr;
+  uint32_t *tidx = nullptr;
+  int64_t *sec = nullptr;
+  int32_t *nan = nullptr;
+};
+int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st);
+int votes_launch(tmed_ctx *c, VoteStage &st, uint8_t *out);
 void free_keyset(Keyset &k);
 
 }  // namespace tmed
@@ -84,8 +108,8 @@ struct tmed_ctx {
   uint32_t slab_slots = 0;
   uint32_t chunk = 0;     // signatures per prep/main launch pair (0 = slab_slots); env TMED_CHUNK
   int main_waves = 2;     // register budget variant of the main kernel; env TMED_MAIN_WAVES
-  tmed::DevBuf d_a, d_b, d_msg, d_off, d_out, d_c;
-  tmed::HostBuf h_a, h_b, h_msg, h_off, h_out, h_c;
+  tmed::DevBuf d_a, d_b, d_msg, d_off, d_out, d_c, d_votes, d_vmsg;
+  tmed::HostBuf h_a, h_b, h_msg, h_off, h_out, h_c, h_votes;
   std::unordered_map<uint64_t, tmed::Keyset> keysets;
   uint64_t next_keyset = 1;
 };

@@ -15,7 +15,8 @@ constexpr uint32_t kSlabSlotBytes = 9 * 160;
 
 hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                          uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
-                         int4 *prep, hipStream_t stream, uint32_t chunk = 0, int main_waves = 2);
+                         int4 *prep, hipStream_t stream, uint32_t chunk = 0, int main_waves = 2,
+                         bool msg_slots = false);
 
 hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t *off, uint32_t n, uint8_t *sig_out,
                        uint8_t *pub_out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
@@ -46,6 +47,16 @@ hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStr
 hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
                                 const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                 const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
-                                hipStream_t stream);
+                                hipStream_t stream, bool msg_slots = false);
+
+// f1: on-device CanonicalVote assembly.  Templates are kVoteTmplBytes records
+// ([pre_len, bid_len, cid_len, 0] + bytes); message i is written to out + i * kVoteSlot
+// and its length to out_len[i].  With msg_slots = true the verify launchers read
+// messages that way (off = lengths).
+constexpr uint32_t kVoteTmplBytes = 256;
+constexpr uint32_t kVoteSlot = 256;
+hipError_t launch_assemble_votes(const uint8_t *tmpl, const uint32_t *tmpl_idx, const uint8_t *flags,
+                                 const int64_t *ts_sec, const int32_t *ts_nanos, uint32_t n, uint8_t *out,
+                                 uint32_t *out_len, hipStream_t stream);
 
 }  // namespace tmed

@@ -17,10 +17,18 @@
 
 namespace tmed {
 
-struct SlabTab {
+// LANE_MAJOR = false: [entry][chunk][slot] (lanes with equal digits read contiguous 16-B
+// pieces); true: [slot][entry][chunk] (each lane's 160-B entry is contiguous, so a
+// divergent lookup reads whole lines instead of one 16-B piece per line).
+template <bool LANE_MAJOR>
+struct SlabTabT {
   int4 *base;
   uint32_t stride;  // lane slots in the slab
   uint32_t slot;
+
+  __device__ __forceinline__ size_t idx(int j, int q) const {
+    return LANE_MAJOR ? ((size_t)slot * 9 + j) * 10 + q : (size_t)(j * 10 + q) * stride + slot;
+  }
 
   __device__ __forceinline__ void store(int j, const ge_cached &c) const {
     const fe *fs[4] = {&c.YpX, &c.YmX, &c.Z, &c.T2d};
@@ -32,14 +40,14 @@ struct SlabTab {
         const int f = 4 * q + e;
         w[e] = fs[f / 10]->v[f % 10];
       }
-      base[(size_t)(j * 10 + q) * stride + slot] = make_int4(w[0], w[1], w[2], w[3]);
+      base[idx(j, q)] = make_int4(w[0], w[1], w[2], w[3]);
     }
   }
   __device__ __forceinline__ void load(int j, ge_cached &c) const {
     fe *fs[4] = {&c.YpX, &c.YmX, &c.Z, &c.T2d};
 #pragma unroll
     for (int q = 0; q < 10; q++) {
-      const int4 v = base[(size_t)(j * 10 + q) * stride + slot];
+      const int4 v = base[idx(j, q)];
       const int32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int e = 0; e < 4; e++) {
@@ -49,6 +57,8 @@ struct SlabTab {
     }
   }
 };
+
+using SlabTab = SlabTabT<false>;
 
 struct LdsBTab {
   const ge_niels *t;
@@ -110,26 +120,91 @@ __device__ __forceinline__ void load_row_words(uint32_t *w, const uint8_t *p, in
   }
 }
 
+// Where message i lives: packed (off[i] .. off[i+1]) or fixed-stride slots written by
+// the on-device vote assembler (msgs + i * kVoteSlot, length len[i]).
+struct MsgSrc {
+  const uint8_t *msgs;
+  const uint32_t *off;  // packed mode (len == nullptr): n + 1 offsets; slot mode: lengths
+  bool slots;
+  __device__ __forceinline__ void get(uint32_t i, const uint8_t *&p, uint32_t &len) const {
+    if (slots) {
+      p = msgs + (size_t)i * kVoteSlot;
+      len = off[i];
+    } else {
+      const uint32_t o0 = off[i], o1 = off[i + 1];
+      p = msgs + o0;
+      len = o1 - o0;
+    }
+  }
+};
+
 // Phase 1: SHA-512(R||A||M) mod L, S < L, A = Point.SetBytes(pub)  (one lane per signature
 // of the chunk [base, base + count)).
 __global__ __launch_bounds__(kThreadsPerBlock) void verify_prep_kernel(
-    const uint8_t *__restrict__ pub, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msgs,
-    const uint32_t *__restrict__ off, uint32_t base, uint32_t count, int4 *__restrict__ prep, uint32_t stride) {
+    const uint8_t *__restrict__ pub, const uint8_t *__restrict__ sig, MsgSrc ms, uint32_t base, uint32_t count,
+    int4 *__restrict__ prep, uint32_t stride) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   if (slot >= count) return;
   const uint32_t i = base + slot;
   uint32_t pw[8], sw[16], k[8], s[8];
   load_row_words(pw, pub + 32 * (size_t)i, 2);
   load_row_words(sw, sig + 64 * (size_t)i, 4);
-  const uint32_t o0 = off[i], o1 = off[i + 1];
+  const uint8_t *m;
+  uint32_t mlen;
+  ms.get(i, m, mlen);
   ge_p3 A;
-  const bool ok = verify_prep(pw, sw, msgs + o0, o1 - o0, k, s, A);
+  const bool ok = verify_prep(pw, sw, m, mlen, k, s, A);
   prep_store(prep, stride, slot, k, s, A, ok);
+}
+
+// ---- f1: CanonicalVote sign-bytes assembled on the device ----------
+// Per commit a template (signbytes.hip VoteEncoder): [pre_len, bid_len, cid_len, 0] then the
+// pre bytes (type/height/round), the complete BlockID field (tag 0x22 + len + body) and the
+// complete chain-id field (tag 0x32 + len + bytes).  Per vote only the flag and the
+// timestamp vary (types/block.go:784-810): the message is
+//   uvarint(body) || pre || [BlockID field if flag == Commit] || 0x2a len {0x08 sec}{0x10 nanos} || chain
+__device__ __forceinline__ int uvarint_len_dev(uint64_t v) {
+  int n = 1;
+  while (v >= 0x80) { v >>= 7; n++; }
+  return n;
+}
+__device__ __forceinline__ uint32_t put_uvarint_dev(uint8_t *p, uint32_t pos, uint64_t v) {
+  while (v >= 0x80) { p[pos++] = (uint8_t)(v | 0x80); v >>= 7; }
+  p[pos++] = (uint8_t)v;
+  return pos;
+}
+
+__global__ __launch_bounds__(kThreadsPerBlock) void assemble_votes_kernel(
+    const uint8_t *__restrict__ tmpl, const uint32_t *__restrict__ tmpl_idx, const uint8_t *__restrict__ flags,
+    const int64_t *__restrict__ ts_sec, const int32_t *__restrict__ ts_nanos, uint32_t n, uint8_t *__restrict__ out,
+    uint32_t *__restrict__ out_len) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t *t = tmpl + (size_t)tmpl_idx[i] * kVoteTmplBytes;
+  const uint32_t pre_len = t[0], bid_len = t[1], cid_len = t[2];
+  const bool with_bid = flags[i] == 2;
+  const uint64_t s = (uint64_t)ts_sec[i], ns = (uint64_t)(int64_t)ts_nanos[i];
+  const uint32_t ts_body = (s ? 1 + uvarint_len_dev(s) : 0) + (ns ? 1 + uvarint_len_dev(ns) : 0);
+  const uint32_t body = pre_len + (with_bid ? bid_len : 0) + 1 + uvarint_len_dev(ts_body) + ts_body + cid_len;
+  uint8_t *o = out + (size_t)i * kVoteSlot;
+  uint32_t p = put_uvarint_dev(o, 0, body);
+  const uint8_t *src = t + 4;
+  for (uint32_t j = 0; j < pre_len; j++) o[p++] = src[j];
+  src += pre_len;
+  if (with_bid)
+    for (uint32_t j = 0; j < bid_len; j++) o[p++] = src[j];
+  src += bid_len;
+  o[p++] = 0x2a;
+  p = put_uvarint_dev(o, p, ts_body);
+  if (s) { o[p++] = 0x08; p = put_uvarint_dev(o, p, s); }
+  if (ns) { o[p++] = 0x10; p = put_uvarint_dev(o, p, ns); }
+  for (uint32_t j = 0; j < cid_len; j++) o[p++] = src[j];
+  out_len[i] = p;
 }
 
 // Phase 2: table of -A, Straus [k](-A) + [s]B, encode, compare with R.
 // WAVES = minimum waves per SIMD the register allocation must allow.
-template <int WAVES>
+template <int WAVES, bool LANE_MAJOR>
 __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_main_kernel(
     const uint8_t *__restrict__ sig, uint32_t base, uint32_t count, const int4 *__restrict__ prep,
     uint32_t stride, int4 *__restrict__ slab, const ge_niels *__restrict__ btab_g, uint8_t *__restrict__ out) {
@@ -142,7 +217,7 @@ __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_main_kernel(
   ge_p3 A;
   const bool ok = prep_load(prep, stride, slot, k, s, A);
   load_row_words(Rw, sig + 64 * (size_t)i, 2);
-  SlabTab tab{slab, stride, slot};
+  SlabTabT<LANE_MAJOR> tab{slab, stride, slot};
   const LdsBTab bt{sbt};
   out[i] = (verify_main(k, s, A, Rw, tab, bt) && ok) ? 1 : 0;
 }
@@ -179,21 +254,25 @@ uint32_t grid_for(size_t n, uint32_t max_blocks) {
 
 hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                          uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
-                         int4 *prep, hipStream_t stream, uint32_t chunk, int main_waves) {
+                         int4 *prep, hipStream_t stream, uint32_t chunk, int main_waves, bool msg_slots) {
+  const MsgSrc ms{msgs, off, msg_slots};
   // Chunks of at most slab_stride signatures: the per-lane tables (slab) and the
   // prep hand-off are sized for one chunk.
   if (chunk == 0 || chunk > slab_stride) chunk = slab_stride;
   for (uint32_t base = 0; base < n; base += chunk) {
     const uint32_t count = (n - base) < chunk ? (n - base) : chunk;
     const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
-    hipLaunchKernelGGL(verify_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, pub, sig, msgs, off,
-                       base, count, prep, slab_stride);
+    hipLaunchKernelGGL(verify_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, pub, sig, ms, base,
+                       count, prep, slab_stride);
     if (main_waves >= 3)
-      hipLaunchKernelGGL(verify_main_kernel<3>, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base, count,
-                         prep, slab_stride, slab, btab, out);
+      hipLaunchKernelGGL((verify_main_kernel<3, false>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base,
+                         count, prep, slab_stride, slab, btab, out);
+    else if (main_waves < 0)  // lane-major slab layout (A/B variant)
+      hipLaunchKernelGGL((verify_main_kernel<2, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base,
+                         count, prep, slab_stride, slab, btab, out);
     else
-      hipLaunchKernelGGL(verify_main_kernel<2>, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base, count,
-                         prep, slab_stride, slab, btab, out);
+      hipLaunchKernelGGL((verify_main_kernel<2, false>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base,
+                         count, prep, slab_stride, slab, btab, out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -295,8 +374,8 @@ struct GlobalComb {
 
 __global__ __launch_bounds__(kThreadsPerBlock) void verify_keyset_prep_kernel(
     const uint32_t *__restrict__ val_idx, const uint8_t *__restrict__ key_pub, const uint8_t *__restrict__ key_ok,
-    const uint8_t *__restrict__ sig, const uint8_t *__restrict__ msgs, const uint32_t *__restrict__ off,
-    uint32_t base, uint32_t count, int4 *__restrict__ prep, uint32_t stride) {
+    const uint8_t *__restrict__ sig, MsgSrc ms, uint32_t base, uint32_t count, int4 *__restrict__ prep,
+    uint32_t stride) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   if (slot >= count) return;
   const uint32_t i = base + slot;
@@ -304,8 +383,10 @@ __global__ __launch_bounds__(kThreadsPerBlock) void verify_keyset_prep_kernel(
   uint32_t pw[8], sw[16], k[8], s[8];
   load_row_words(pw, key_pub + 32 * (size_t)v, 2);
   load_row_words(sw, sig + 64 * (size_t)i, 4);
-  const uint32_t o0 = off[i], o1 = off[i + 1];
-  const bool ok = verify_prep_comb(pw, key_ok[v] != 0, sw, msgs + o0, o1 - o0, k, s);
+  const uint8_t *m;
+  uint32_t mlen;
+  ms.get(i, m, mlen);
+  const bool ok = verify_prep_comb(pw, key_ok[v] != 0, sw, m, mlen, k, s);
   ge_p3 dummy;
   ge_p3_0(dummy);
   prep_store(prep, stride, slot, k, s, dummy, ok);
@@ -351,18 +432,32 @@ hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStr
 hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
                                 const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                 const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
-                                hipStream_t stream) {
+                                hipStream_t stream, bool msg_slots) {
+  const MsgSrc ms{msgs, off, msg_slots};
   for (uint32_t base = 0; base < n; base += stride) {
     const uint32_t count = (n - base) < stride ? (n - base) : stride;
     const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
     hipLaunchKernelGGL(verify_keyset_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx, key_pub,
-                       key_ok, sig, msgs, off, base, count, prep, stride);
+                       key_ok, sig, ms, base, count, prep, stride);
     hipLaunchKernelGGL(verify_keyset_main_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx, acomb,
                        bcomb, sig, base, count, prep, stride, out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+}  // namespace tmed
+
+namespace tmed {
+
+hipError_t launch_assemble_votes(const uint8_t *tmpl, const uint32_t *tmpl_idx, const uint8_t *flags,
+                                 const int64_t *ts_sec, const int32_t *ts_nanos, uint32_t n, uint8_t *out,
+                                 uint32_t *out_len, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(assemble_votes_kernel, dim3((n + kThreadsPerBlock - 1) / kThreadsPerBlock),
+                     dim3(kThreadsPerBlock), 0, stream, tmpl, tmpl_idx, flags, ts_sec, ts_nanos, n, out, out_len);
+  return hipGetLastError();
 }
 
 }  // namespace tmed

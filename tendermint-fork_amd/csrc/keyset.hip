@@ -32,6 +32,95 @@ void free_keyset(Keyset &k) {
   k = Keyset();
 }
 
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st) {
+  st.lock = std::unique_lock<std::mutex>(c->mu);
+  st.m = m;
+  st.n_tmpl = n_tmpl;
+  st.ks = nullptr;
+  if (keyset) {
+    auto it = c->keysets.find(keyset);
+    if (it == c->keysets.end()) return TMED_ENOKEYSET;
+    st.ks = &it->second;
+  }
+  (void)hipSetDevice(c->device);
+  const size_t key_bytes = keyset ? (size_t)m * 4 : (size_t)m * 32;
+  st.o_key = 0;
+  st.o_sig = align256(st.o_key + key_bytes);
+  st.o_tmpl = align256(st.o_sig + (size_t)m * 64);
+  st.o_tidx = align256(st.o_tmpl + n_tmpl * kVoteTmplBytes);
+  st.o_flag = align256(st.o_tidx + (size_t)m * 4);
+  st.o_sec = align256(st.o_flag + m);
+  st.o_nan = align256(st.o_sec + (size_t)m * 8);
+  st.total = align256(st.o_nan + (size_t)m * 4);
+  hipError_t e = c->d_votes.ensure(st.total);
+  if (e == hipSuccess) e = c->h_votes.ensure(st.total);
+  if (e == hipSuccess) e = c->d_vmsg.ensure((size_t)m * kVoteSlot);
+  if (e == hipSuccess) e = c->d_off.ensure((size_t)m * 4);
+  if (e == hipSuccess) e = c->d_out.ensure(m);
+  if (e == hipSuccess) e = c->h_out.ensure(m);
+  if (e != hipSuccess) return map_err(e);
+  uint8_t *h = (uint8_t *)c->h_votes.p;
+  st.key = h + st.o_key;
+  st.sig = h + st.o_sig;
+  st.tmpl = h + st.o_tmpl;
+  st.tidx = (uint32_t *)(h + st.o_tidx);
+  st.flag = h + st.o_flag;
+  st.sec = (int64_t *)(h + st.o_sec);
+  st.nan = (int32_t *)(h + st.o_nan);
+  return TMED_OK;
+}
+
+int votes_launch(tmed_ctx *c, VoteStage &st, uint8_t *out) {
+  const uint32_t m = st.m;
+  if (st.ks)
+    for (uint32_t j = 0; j < m; j++)
+      if (((const uint32_t *)st.key)[j] >= st.ks->n) return TMED_EINVAL;
+  uint8_t *d = (uint8_t *)c->d_votes.p;
+  hipStream_t s = c->stream;
+  hipError_t e = hipMemcpyAsync(d, c->h_votes.p, st.total, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipEventRecord(c->ev0, s);
+  if (e == hipSuccess)
+    e = launch_assemble_votes(d + st.o_tmpl, (const uint32_t *)(d + st.o_tidx), d + st.o_flag,
+                              (const int64_t *)(d + st.o_sec), (const int32_t *)(d + st.o_nan), m,
+                              (uint8_t *)c->d_vmsg.p, (uint32_t *)c->d_off.p, s);
+  if (e == hipSuccess) {
+    if (st.ks)
+      e = launch_verify_keyset((const uint32_t *)(d + st.o_key), st.ks->d_pub, st.ks->d_ok, st.ks->d_comb, c->d_bcomb,
+                               d + st.o_sig, (const uint8_t *)c->d_vmsg.p, (const uint32_t *)c->d_off.p, m,
+                               (uint8_t *)c->d_out.p, c->d_prep, c->slab_slots, s, /*msg_slots=*/true);
+    else
+      e = launch_verify(d + st.o_key, d + st.o_sig, (const uint8_t *)c->d_vmsg.p, (const uint32_t *)c->d_off.p, m,
+                        (uint8_t *)c->d_out.p, c->d_slab, c->slab_slots, c->d_btab, c->d_prep, s, c->chunk,
+                        c->main_waves, /*msg_slots=*/true);
+  }
+  if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, m, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return map_err(e);
+  (void)hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
+  memcpy(out, c->h_out.p, m);
+  return TMED_OK;
+}
+
+int verify_votes_device(tmed_ctx *c, uint64_t keyset, const uint8_t *keys, const uint8_t *sigs, const uint8_t *tmpl,
+                        size_t n_tmpl, const uint32_t *tmpl_idx, const uint8_t *flags, const int64_t *ts_sec,
+                        const int32_t *ts_nanos, uint32_t m, uint8_t *out) {
+  if (m == 0) return TMED_OK;
+  VoteStage st;
+  int rc = votes_stage(c, keyset, m, n_tmpl, st);
+  if (rc != TMED_OK) return rc;
+  memcpy(st.key, keys, keyset ? (size_t)m * 4 : (size_t)m * 32);
+  memcpy(st.sig, sigs, (size_t)m * 64);
+  memcpy(st.tmpl, tmpl, n_tmpl * kVoteTmplBytes);
+  memcpy(st.tidx, tmpl_idx, (size_t)m * 4);
+  memcpy(st.flag, flags, m);
+  memcpy(st.sec, ts_sec, (size_t)m * 8);
+  memcpy(st.nan, ts_nanos, (size_t)m * 4);
+  return votes_launch(c, st, out);
+}
+
 }  // namespace tmed
 
 extern "C" {

@@ -20,6 +20,10 @@ struct VoteEncoder {
   int init(const tmed_vote_template *t);
   size_t size(int flag, int64_t sec, int32_t nanos) const;
   uint8_t *write(uint8_t *out, int flag, int64_t sec, int32_t nanos) const;
+  // Device template record for the on-device assembler (kernels.h kVoteTmplBytes):
+  // [pre_len, bid_field_len, cid_field_len, 0] + pre + BlockID field + chain-id field.
+  // Returns false if it does not fit in `cap` bytes (very long chain IDs: host path).
+  bool device_template(uint8_t *out, size_t cap) const;
 };
 
 }  // namespace tmed

@@ -92,6 +92,20 @@ uint8_t *VoteEncoder::write(uint8_t *w, int flag, int64_t sec, int32_t nanos) co
   return w;
 }
 
+bool VoteEncoder::device_template(uint8_t *out, size_t cap) const {
+  const size_t need = 4 + (size_t)pre_len + (size_t)bid_field + (size_t)cid_field;
+  if (need > cap || bid_field > 255 || cid_field > 255) return false;
+  out[0] = (uint8_t)pre_len;
+  out[1] = (uint8_t)bid_field;
+  out[2] = (uint8_t)cid_field;
+  out[3] = 0;
+  uint8_t *w = out + 4;
+  memcpy(w, pre, pre_len); w += pre_len;
+  if (bid_body) { *w++ = 0x22; w = put_uvarint(w, (uint64_t)bid_body); memcpy(w, bid, bid_body); w += bid_body; }
+  if (cid_len) { *w++ = 0x32; w = put_uvarint(w, cid_len); memcpy(w, cid, cid_len); w += cid_len; }
+  return true;
+}
+
 }  // namespace tmed
 
 extern "C" int tmed_vote_sign_bytes(const tmed_vote_template *t, size_t n, const uint8_t *flags,

@@ -62,6 +62,7 @@ int tmed_init(int device, tmed_ctx **out) {
   // Lane slots for the per-lane tables: 4x the resident lanes of 256 CUs at
   // 8 waves/CU is plenty for the grid-stride loop (~377 MB of HBM).
   c->slab_slots = 1024 * kThreadsPerBlock;
+  c->chunk = 512 * kThreadsPerBlock;  // 131,072 signatures per prep/main pair (measured best, profiles/r01/variants.txt)
   if (const char *v = getenv("TMED_CHUNK")) c->chunk = (uint32_t)strtoul(v, nullptr, 10);
   if (const char *v = getenv("TMED_MAIN_WAVES")) c->main_waves = atoi(v);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_slab, (size_t)c->slab_slots * kSlabSlotBytes);
@@ -91,8 +92,8 @@ void tmed_destroy(tmed_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
-  for (DevBuf *b : {&c->d_a, &c->d_b, &c->d_msg, &c->d_off, &c->d_out, &c->d_c}) b->release();
-  for (HostBuf *b : {&c->h_a, &c->h_b, &c->h_msg, &c->h_off, &c->h_out, &c->h_c}) b->release();
+  for (DevBuf *b : {&c->d_a, &c->d_b, &c->d_msg, &c->d_off, &c->d_out, &c->d_c, &c->d_votes, &c->d_vmsg}) b->release();
+  for (HostBuf *b : {&c->h_a, &c->h_b, &c->h_msg, &c->h_off, &c->h_out, &c->h_c, &c->h_votes}) b->release();
   for (auto &kv : c->keysets) free_keyset(kv.second);
   c->keysets.clear();
   if (c->d_bcomb) hipFree(c->d_bcomb);
