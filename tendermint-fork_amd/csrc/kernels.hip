@@ -264,14 +264,16 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
     const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
     hipLaunchKernelGGL(verify_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, pub, sig, ms, base,
                        count, prep, slab_stride);
+    // default: 2 waves/SIMD, lane-major per-lane tables (+3.7 % over the slot-interleaved
+    // layout, profiles/r01/variants.txt); the others are kept as measured A/B variants.
     if (main_waves >= 3)
-      hipLaunchKernelGGL((verify_main_kernel<3, false>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base,
+      hipLaunchKernelGGL((verify_main_kernel<3, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base,
                          count, prep, slab_stride, slab, btab, out);
-    else if (main_waves < 0)  // lane-major slab layout (A/B variant)
-      hipLaunchKernelGGL((verify_main_kernel<2, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base,
+    else if (main_waves == -2)  // slot-interleaved slab layout
+      hipLaunchKernelGGL((verify_main_kernel<2, false>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base,
                          count, prep, slab_stride, slab, btab, out);
     else
-      hipLaunchKernelGGL((verify_main_kernel<2, false>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base,
+      hipLaunchKernelGGL((verify_main_kernel<2, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base,
                          count, prep, slab_stride, slab, btab, out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
