@@ -91,6 +91,15 @@ int tmed_sign_batch_device(tmed_ctx *ctx, const uint8_t *d_seeds, const uint8_t 
 /* Device time (ms) of the last verify/sign launch on this context (HIP events). */
 float tmed_last_kernel_ms(tmed_ctx *ctx);
 
+/*
+ * Per-kernel timing of tmed_verify_batch_device (diagnostics, bench roofline): when on,
+ * HIP events are recorded on the launch stream around each prep and main kernel of a
+ * call; tmed_kernel_times returns their sums (ms) for the last call and the number of
+ * prep/main launch pairs.
+ */
+int tmed_set_kernel_timing(tmed_ctx *ctx, int on);
+int tmed_kernel_times(tmed_ctx *ctx, float *prep_ms, float *main_ms, int *launches);
+
 
 /* ------------------------------------------------------- key-set cache */
 

@@ -108,6 +108,8 @@ struct tmed_ctx {
   uint32_t slab_slots = 0;
   uint32_t chunk = 0;     // signatures per prep/main launch pair (0 = slab_slots); env TMED_CHUNK
   int main_waves = 2;     // register budget variant of the main kernel; env TMED_MAIN_WAVES
+  bool timing = false;    // tmed_set_kernel_timing
+  tmed::KernelTimer timer;
   tmed::DevBuf d_a, d_b, d_msg, d_off, d_out, d_c, d_votes, d_vmsg;
   tmed::HostBuf h_a, h_b, h_msg, h_off, h_out, h_c, h_votes;
   std::unordered_map<uint64_t, tmed::Keyset> keysets;

@@ -8,6 +8,16 @@
 
 namespace tmed {
 
+// Optional per-launch HIP-event timing of the verify pipeline (diagnostics / bench roofline):
+// events are recorded on the launch stream before prep, between prep and main, after main.
+struct KernelTimer {
+  hipEvent_t ev[96];
+  int n = 0;
+  void mark(hipStream_t s) {
+    if (n < 96) (void)hipEventRecord(ev[n++], s);
+  }
+};
+
 constexpr uint32_t kThreadsPerBlock = 256;
 // Variable-base table slab: lane slots (grid-stride loop bounds the grid to
 // slab_slots / kThreadsPerBlock blocks).  9 entries x 160 B per slot.
@@ -16,7 +26,7 @@ constexpr uint32_t kSlabSlotBytes = 9 * 160;
 hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                          uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
                          int4 *prep, hipStream_t stream, uint32_t chunk = 0, int main_waves = 2,
-                         bool msg_slots = false);
+                         bool msg_slots = false, KernelTimer *timer = nullptr);
 
 hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t *off, uint32_t n, uint8_t *sig_out,
                        uint8_t *pub_out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,

@@ -254,7 +254,8 @@ uint32_t grid_for(size_t n, uint32_t max_blocks) {
 
 hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                          uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
-                         int4 *prep, hipStream_t stream, uint32_t chunk, int main_waves, bool msg_slots) {
+                         int4 *prep, hipStream_t stream, uint32_t chunk, int main_waves, bool msg_slots,
+                         KernelTimer *timer) {
   const MsgSrc ms{msgs, off, msg_slots};
   // Chunks of at most slab_stride signatures: the per-lane tables (slab) and the
   // prep hand-off are sized for one chunk.
@@ -262,8 +263,10 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
   for (uint32_t base = 0; base < n; base += chunk) {
     const uint32_t count = (n - base) < chunk ? (n - base) : chunk;
     const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
+    if (timer) timer->mark(stream);
     hipLaunchKernelGGL(verify_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, pub, sig, ms, base,
                        count, prep, slab_stride);
+    if (timer) timer->mark(stream);
     // default: 2 waves/SIMD, lane-major per-lane tables (+3.7 % over the slot-interleaved
     // layout, profiles/r01/variants.txt); the others are kept as measured A/B variants.
     if (main_waves >= 3)
@@ -275,6 +278,7 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
     else
       hipLaunchKernelGGL((verify_main_kernel<2, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base,
                          count, prep, slab_stride, slab, btab, out);
+    if (timer) timer->mark(stream);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

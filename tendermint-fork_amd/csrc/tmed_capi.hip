@@ -108,6 +108,35 @@ void tmed_destroy(tmed_ctx *c) {
 
 float tmed_last_kernel_ms(tmed_ctx *c) { return c ? c->last_ms : 0.f; }
 
+int tmed_set_kernel_timing(tmed_ctx *c, int on) {
+  if (!c) return TMED_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  (void)hipSetDevice(c->device);
+  if (on && !c->timing)
+    for (auto &e : c->timer.ev)
+      if (hipEventCreate(&e) != hipSuccess) return TMED_EHIP;
+  if (!on && c->timing)
+    for (auto &e : c->timer.ev) (void)hipEventDestroy(e);
+  c->timing = on != 0;
+  c->timer.n = 0;
+  return TMED_OK;
+}
+
+int tmed_kernel_times(tmed_ctx *c, float *prep_ms, float *main_ms, int *launches) {
+  if (!c || !prep_ms || !main_ms || !launches || !c->timing) return TMED_EINVAL;
+  *prep_ms = *main_ms = 0.f;
+  *launches = c->timer.n / 3;
+  for (int i = 0; i + 2 < c->timer.n; i += 3) {
+    float a = 0.f, b = 0.f;
+    if (hipEventSynchronize(c->timer.ev[i + 2]) != hipSuccess) return TMED_EHIP;
+    (void)hipEventElapsedTime(&a, c->timer.ev[i], c->timer.ev[i + 1]);
+    (void)hipEventElapsedTime(&b, c->timer.ev[i + 1], c->timer.ev[i + 2]);
+    *prep_ms += a;
+    *main_ms += b;
+  }
+  return TMED_OK;
+}
+
 int tmed_verify_batch_device(tmed_ctx *c, const uint8_t *d_pub, const uint8_t *d_sig, const uint8_t *d_msgs,
                              const uint32_t *d_off, size_t n, uint8_t *d_out, void *stream) {
   if (!c) return TMED_EINVAL;
@@ -115,8 +144,10 @@ int tmed_verify_batch_device(tmed_ctx *c, const uint8_t *d_pub, const uint8_t *d
   if (!d_pub || !d_sig || !d_msgs || !d_off || !d_out || n > 0xffffffffu) return TMED_EINVAL;
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   hipSetDevice(c->device);
+  if (c->timing) c->timer.n = 0;
   hipError_t e = launch_verify(d_pub, d_sig, d_msgs, d_off, (uint32_t)n, d_out, c->d_slab, c->slab_slots,
-                               c->d_btab, c->d_prep, s, c->chunk, c->main_waves);
+                               c->d_btab, c->d_prep, s, c->chunk, c->main_waves, false,
+                               c->timing ? &c->timer : nullptr);
   return map_err(e);
 }
 

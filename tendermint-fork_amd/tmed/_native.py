@@ -69,6 +69,11 @@ def lib() -> ctypes.CDLL:
     l.tmed_verify_batch_keyset.argtypes = [P, ctypes.c_uint64, P, P, P, P, P, SZ, P]
     l.tmed_verify_batch_keyset_device.restype = I
     l.tmed_verify_batch_keyset_device.argtypes = [P, ctypes.c_uint64, P, P, P, P, SZ, P, P]
+    l.tmed_set_kernel_timing.restype = I
+    l.tmed_set_kernel_timing.argtypes = [P, I]
+    l.tmed_kernel_times.restype = I
+    l.tmed_kernel_times.argtypes = [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
+                                    ctypes.POINTER(ctypes.c_int)]
     l.tmed_last_kernel_ms.restype = ctypes.c_float
     l.tmed_last_kernel_ms.argtypes = [P]
     _lib = l
@@ -82,4 +87,5 @@ EXPORTED_SYMBOLS = [
     "tmed_sign_batch", "tmed_sign_batch_device", "tmed_last_kernel_ms",
     "tmed_vote_sign_bytes", "tmed_valu_peak", "tmed_verify_commits", "tmed_verify_commits_with",
     "tmed_keyset_load", "tmed_keyset_free", "tmed_verify_batch_keyset", "tmed_verify_batch_keyset_device",
+    "tmed_set_kernel_timing", "tmed_kernel_times",
 ]

@@ -155,5 +155,18 @@ class Engine:
         if rc != TMED_OK:
             raise TmedError(rc, "tmed_verify_batch_keyset_device")
 
+    def set_kernel_timing(self, on: bool) -> None:
+        rc = lib().tmed_set_kernel_timing(self._h, 1 if on else 0)
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_set_kernel_timing")
+
+    def kernel_times(self):
+        """(prep_ms, main_ms, launch pairs) of the last verify_device call (timing on)."""
+        a, b, n = ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
+        rc = lib().tmed_kernel_times(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n))
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_kernel_times")
+        return a.value, b.value, n.value
+
     def last_kernel_ms(self) -> float:
         return float(lib().tmed_last_kernel_ms(self._h))
