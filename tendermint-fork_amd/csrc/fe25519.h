@@ -65,31 +65,43 @@ TMED_HD void fe_select(fe &h, const fe &f, const fe &g, bool b) {
   for (int i = 0; i < 10; i++) h.v[i] = b ? g.v[i] : f.v[i];
 }
 
-// Carry pass over 64-bit column sums -> carried limbs.  Two interleaved chains
-// (0..4 and 4..9) give the scheduler independent work.
-TMED_HD void fe_carry64(fe &out, int64_t h[10]) {
+// Column biases: the accumulators start at B_k = 2^25 (even k) / 2^24 (odd k), so the
+// rounding carry c = (h + B) >> s needs no separate bias add.  Carried columns are kept
+// biased (L_k = (h_k + B_k) mod 2^s, 32-bit) until the end, where limb_k = L_k - B_k in
+// [-2^25, 2^25) / [-2^24, 2^24): the same centered result as the unbiased chain, with
+// one 64-bit shift, one 32-bit and, one 64-bit add per carry (+ one 32-bit sub per limb).
+TMED_HD int64_t fe_bias(int k) { return (k & 1) ? ((int64_t)1 << 24) : ((int64_t)1 << 25); }
+
+// Carry pass over BIASED 64-bit column sums H_k = h_k + B_k -> carried limbs.  Two
+// interleaved chains (0..4 and 4..9) give the scheduler independent work.
+TMED_HD void fe_carry64(fe &out, int64_t H[10]) {
+  uint32_t L[10];
   int64_t c;
-  c = (h[0] + (int64_t)(1 << 25)) >> 26; h[1] += c; h[0] -= c * ((int64_t)1 << 26);
-  c = (h[4] + (int64_t)(1 << 25)) >> 26; h[5] += c; h[4] -= c * ((int64_t)1 << 26);
-  c = (h[1] + (int64_t)(1 << 24)) >> 25; h[2] += c; h[1] -= c * ((int64_t)1 << 25);
-  c = (h[5] + (int64_t)(1 << 24)) >> 25; h[6] += c; h[5] -= c * ((int64_t)1 << 25);
-  c = (h[2] + (int64_t)(1 << 25)) >> 26; h[3] += c; h[2] -= c * ((int64_t)1 << 26);
-  c = (h[6] + (int64_t)(1 << 25)) >> 26; h[7] += c; h[6] -= c * ((int64_t)1 << 26);
-  c = (h[3] + (int64_t)(1 << 24)) >> 25; h[4] += c; h[3] -= c * ((int64_t)1 << 25);
-  c = (h[7] + (int64_t)(1 << 24)) >> 25; h[8] += c; h[7] -= c * ((int64_t)1 << 25);
-  c = (h[4] + (int64_t)(1 << 25)) >> 26; h[5] += c; h[4] -= c * ((int64_t)1 << 26);
-  c = (h[8] + (int64_t)(1 << 25)) >> 26; h[9] += c; h[8] -= c * ((int64_t)1 << 26);
-  c = (h[9] + (int64_t)(1 << 24)) >> 25; h[0] += c * 19; h[9] -= c * ((int64_t)1 << 25);
-  c = (h[0] + (int64_t)(1 << 25)) >> 26; h[1] += c; h[0] -= c * ((int64_t)1 << 26);
+#define TMED_CARRY(k, s)              \
+  c = H[k] >> (s);                    \
+  L[k] = (uint32_t)H[k] & ((1u << (s)) - 1u);
+  TMED_CARRY(0, 26); H[1] += c;
+  TMED_CARRY(4, 26); H[5] += c;
+  TMED_CARRY(1, 25); H[2] += c;
+  TMED_CARRY(5, 25); H[6] += c;
+  TMED_CARRY(2, 26); H[3] += c;
+  TMED_CARRY(6, 26); H[7] += c;
+  TMED_CARRY(3, 25); H[4] = (int64_t)L[4] + c;   // column 4 again (biased L4 + carry)
+  TMED_CARRY(7, 25); H[8] += c;
+  TMED_CARRY(4, 26); L[5] += (uint32_t)c;           // column 5 already carried
+  TMED_CARRY(8, 26); H[9] += c;
+  TMED_CARRY(9, 25); H[0] = (int64_t)L[0] + c * 19;  // 2^255 = 19 (mod p)
+  TMED_CARRY(0, 26); L[1] += (uint32_t)c;           // column 1 already carried
+#undef TMED_CARRY
 #pragma unroll
-  for (int i = 0; i < 10; i++) out.v[i] = (int32_t)h[i];
+  for (int i = 0; i < 10; i++) out.v[i] = (int32_t)(L[i] - (uint32_t)fe_bias(i));
 }
 
 // Re-carry a 32-bit-limb value (e.g. a 2- or 3-sum) into carried form.
 TMED_HD void fe_carry(fe &h, const fe &f) {
   int64_t t[10];
 #pragma unroll
-  for (int i = 0; i < 10; i++) t[i] = f.v[i];
+  for (int i = 0; i < 10; i++) t[i] = (int64_t)f.v[i] + fe_bias(i);
   fe_carry64(h, t);
 }
 
@@ -102,7 +114,7 @@ TMED_HD void fe_mul(fe &h, const fe &f, const fe &g) {
   for (int i = 0; i < 10; i++) f2[i] = (int32_t)(2u * (uint32_t)f.v[i]);
   int64_t acc[10];
 #pragma unroll
-  for (int k = 0; k < 10; k++) acc[k] = 0;
+  for (int k = 0; k < 10; k++) acc[k] = fe_bias(k);
 #pragma unroll
   for (int i = 0; i < 10; i++) {
 #pragma unroll
@@ -120,7 +132,7 @@ TMED_HD void fe_mul(fe &h, const fe &f, const fe &g) {
 // (i<j ? 2 : 1) * (i,j odd ? 2 : 1) * (i+j>=10 ? 19 : 1); the factor 19 (and
 // its companion 2 for odd-odd pairs) is put on the odd-index operand where
 // there is one, so every pre-multiplied operand stays inside int32.
-TMED_HD void fe_sq_acc(int64_t acc[10], const fe &f) {
+TMED_HD void fe_sq_acc(int64_t acc[10], const fe &f, bool biased) {
   int32_t x2[10], x19[10], x38[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) {
@@ -128,7 +140,7 @@ TMED_HD void fe_sq_acc(int64_t acc[10], const fe &f) {
     x2[i] = (int32_t)(2u * u); x19[i] = mul19(f.v[i]); x38[i] = mul38(f.v[i]);
   }
 #pragma unroll
-  for (int k = 0; k < 10; k++) acc[k] = 0;
+  for (int k = 0; k < 10; k++) acc[k] = biased ? fe_bias(k) : 0;
 #pragma unroll
   for (int i = 0; i < 10; i++) {
 #pragma unroll
@@ -158,16 +170,16 @@ TMED_HD void fe_sq_acc(int64_t acc[10], const fe &f) {
 
 TMED_HD void fe_sq(fe &h, const fe &f) {
   int64_t acc[10];
-  fe_sq_acc(acc, f);
+  fe_sq_acc(acc, f, true);
   fe_carry64(h, acc);
 }
 
 // h = 2 f^2
 TMED_HD void fe_sq2(fe &h, const fe &f) {
   int64_t acc[10];
-  fe_sq_acc(acc, f);
+  fe_sq_acc(acc, f, false);
 #pragma unroll
-  for (int k = 0; k < 10; k++) acc[k] += acc[k];
+  for (int k = 0; k < 10; k++) acc[k] = 2 * acc[k] + fe_bias(k);
   fe_carry64(h, acc);
 }
 
@@ -218,7 +230,7 @@ TMED_HD void fe_from_words(fe &h, const uint32_t w[8]) {
     const uint64_t hi = (q + 1 < 8) ? (uint64_t)w[q + 1] : 0;
     const uint64_t x = ((hi << 32) | lo) >> r;
     const uint32_t mask = (i & 1) ? 0x1ffffffu : 0x3ffffffu;
-    t[i] = (int64_t)(uint32_t)(x & mask);
+    t[i] = (int64_t)(uint32_t)(x & mask) + fe_bias(i);
   }
   fe_carry64(h, t);
 }
