@@ -93,12 +93,13 @@ float tmed_last_kernel_ms(tmed_ctx *ctx);
 
 /*
  * Per-kernel timing of tmed_verify_batch_device (diagnostics, bench roofline): when on,
- * HIP events are recorded on the launch stream around each prep and main kernel of a
- * call; tmed_kernel_times returns their sums (ms) for the last call and the number of
- * prep/main launch pairs.
+ * HIP events are recorded on the launch stream around each kernel of a call;
+ * tmed_kernel_times returns, for the last call, the summed device time (ms) and the
+ * launch count of each kernel kind: [0] prep (SHA-512, scalar checks, decompression),
+ * [1] main (table + Straus), [2] finish (batched inversion + encode + compare).
  */
 int tmed_set_kernel_timing(tmed_ctx *ctx, int on);
-int tmed_kernel_times(tmed_ctx *ctx, float *prep_ms, float *main_ms, int *launches);
+int tmed_kernel_times(tmed_ctx *ctx, float ms[3], int launches[3]);
 
 
 /* ------------------------------------------------------- key-set cache */

@@ -105,6 +105,8 @@ struct tmed_ctx {
   int4 *d_bcomb = nullptr;  // signed radix-256 comb of +B (shared)
   int4 *d_slab = nullptr;
   int4 *d_prep = nullptr;
+  int4 *d_fin = nullptr;      // batched-finish hand-off (kFinBytes)
+  int4 *d_fin_pre = nullptr;  // batched-finish prefix products (kFinPreBytes)
   uint32_t slab_slots = 0;
   uint32_t chunk = 0;     // signatures per prep/main launch pair (0 = slab_slots); env TMED_CHUNK
   int main_waves = 2;     // register budget variant of the main kernel; env TMED_MAIN_WAVES

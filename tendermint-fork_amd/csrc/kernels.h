@@ -10,11 +10,15 @@ namespace tmed {
 
 // Optional per-launch HIP-event timing of the verify pipeline (diagnostics / bench roofline):
 // events are recorded on the launch stream before prep, between prep and main, after main.
+// mark(s, kind) records an event that ENDS a kernel of that kind (0 prep, 1 main, 2 finish;
+// -1 = start mark); interval i (ev[i-1] -> ev[i]) is charged to kind[i].
 struct KernelTimer {
-  hipEvent_t ev[96];
+  static constexpr int kMax = 160;
+  hipEvent_t ev[kMax];
+  int kind[kMax];
   int n = 0;
-  void mark(hipStream_t s) {
-    if (n < 96) (void)hipEventRecord(ev[n++], s);
+  void mark(hipStream_t s, int k) {
+    if (n < kMax) { kind[n] = k; (void)hipEventRecord(ev[n++], s); }
   }
 };
 
@@ -23,10 +27,21 @@ constexpr uint32_t kThreadsPerBlock = 256;
 // slab_slots / kThreadsPerBlock blocks).  9 entries x 160 B per slot.
 constexpr uint32_t kSlabSlotBytes = 9 * 160;
 
+// Batched finish (verify_core.h finish_group): the main kernels hand projective R' over in
+// fin ([q][slot], kFinInt4 int4 per signature, kFinCap slots); the finish kernel runs once per
+// block of <= kFinCap signatures, with up to kFinGroupMax signatures per inversion.  fin_pre
+// holds the prefix products ([3][kFinPreStride] int4).
+constexpr uint32_t kFinCap = 1u << 20;
+constexpr int kFinInt4 = 8;
+constexpr uint32_t kFinGroupMax = 16;
+constexpr uint32_t kFinPreStride = kFinCap + 64;
+constexpr size_t kFinBytes = (size_t)kFinCap * kFinInt4 * 16;
+constexpr size_t kFinPreBytes = (size_t)kFinPreStride * 3 * 16;
+
 hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                          uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
-                         int4 *prep, hipStream_t stream, uint32_t chunk = 0, int main_waves = 2,
-                         bool msg_slots = false, KernelTimer *timer = nullptr);
+                         int4 *prep, int4 *fin, int4 *fin_pre, hipStream_t stream, uint32_t chunk = 0,
+                         int main_waves = 2, bool msg_slots = false, KernelTimer *timer = nullptr);
 
 hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t *off, uint32_t n, uint8_t *sig_out,
                        uint8_t *pub_out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
@@ -57,7 +72,7 @@ hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStr
 hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
                                 const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                 const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
-                                hipStream_t stream, bool msg_slots = false);
+                                int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots = false);
 
 // f1: on-device CanonicalVote assembly.  Templates are kVoteTmplBytes records
 // ([pre_len, bid_len, cid_len, 0] + bytes); message i is written to out + i * kVoteSlot

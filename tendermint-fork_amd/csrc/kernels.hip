@@ -202,24 +202,114 @@ __global__ __launch_bounds__(kThreadsPerBlock) void assemble_votes_kernel(
   out_len[i] = p;
 }
 
-// Phase 2: table of -A, Straus [k](-A) + [s]B, encode, compare with R.
+// Projective R' of signature slot (X, Y, Z: 30 limbs + 2 pad = 8 int4), stored [q][slot].
+__device__ __forceinline__ void fin_store(int4 *fin, uint32_t stride, uint32_t slot, const fe &X, const fe &Y,
+                                          const fe &Z) {
+  int32_t w[32];
+#pragma unroll
+  for (int i = 0; i < 10; i++) { w[i] = X.v[i]; w[10 + i] = Y.v[i]; w[20 + i] = Z.v[i]; }
+  w[30] = w[31] = 0;
+#pragma unroll
+  for (int q = 0; q < kFinInt4; q++)
+    fin[(size_t)q * stride + slot] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
+// Phase 2: table of -A, Straus [k](-A) + [s]B -> projective R' (hand-off to the finish).
 // WAVES = minimum waves per SIMD the register allocation must allow.
 template <int WAVES, bool LANE_MAJOR>
 __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_main_kernel(
-    const uint8_t *__restrict__ sig, uint32_t base, uint32_t count, const int4 *__restrict__ prep,
-    uint32_t stride, int4 *__restrict__ slab, const ge_niels *__restrict__ btab_g, uint8_t *__restrict__ out) {
+    uint32_t base, uint32_t count, const int4 *__restrict__ prep, uint32_t stride, int4 *__restrict__ slab,
+    const ge_niels *__restrict__ btab_g, int4 *__restrict__ fin, uint32_t fin_base, uint8_t *__restrict__ out) {
   __shared__ ge_niels sbt[kBTabEntries];
   stage_btab(sbt, btab_g);
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   if (slot >= count) return;
   const uint32_t i = base + slot;
-  uint32_t k[8], s[8], Rw[8];
+  uint32_t k[8], s[8];
   ge_p3 A;
   const bool ok = prep_load(prep, stride, slot, k, s, A);
-  load_row_words(Rw, sig + 64 * (size_t)i, 2);
   SlabTabT<LANE_MAJOR> tab{slab, stride, slot};
   const LdsBTab bt{sbt};
-  out[i] = (verify_main(k, s, A, Rw, tab, bt) && ok) ? 1 : 0;
+  ge_p2 R;
+  verify_main_point(R, k, s, A, tab, bt);
+  fin_store(fin, kFinCap, i - fin_base, R.X, R.Y, R.Z);
+  out[i] = ok ? 1 : 0;
+}
+
+// Phase 3: batched finish.  Lane l owns slots l, l + L, l + 2L, ... (< m) of the block of m
+// signatures starting at fin_base (coalesced [q][slot] loads); finish_group inverts their
+// Z with one inversion and compares each canonical encoding with R.
+struct FinDev {
+  const int4 *fin;
+  int4 *pre;
+  const uint8_t *sig;
+  uint8_t *out;
+  uint32_t fin_base, lane, L, m;
+  __device__ __forceinline__ int count() const { return lane < m ? (int)((m - lane + L - 1) / L) : 0; }
+  __device__ __forceinline__ uint32_t slot(int j) const { return lane + (uint32_t)j * L; }
+  __device__ __forceinline__ void load_z(int j, fe &z) const {
+    int32_t w[12];  // words 20..31
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      const int4 v = fin[(size_t)(5 + q) * kFinCap + slot(j)];
+      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 10; i++) z.v[i] = w[i];
+  }
+  __device__ __forceinline__ void load_xy(int j, fe &X, fe &Y) const {
+    int32_t w[20];  // words 0..19
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+      const int4 v = fin[(size_t)q * kFinCap + slot(j)];
+      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 10; i++) { X.v[i] = w[i]; Y.v[i] = w[10 + i]; }
+  }
+  __device__ __forceinline__ void store_pre(int j, const fe &p) const {
+    const size_t idx = (size_t)j * L + lane;
+    pre[idx] = make_int4(p.v[0], p.v[1], p.v[2], p.v[3]);
+    pre[kFinPreStride + idx] = make_int4(p.v[4], p.v[5], p.v[6], p.v[7]);
+    pre[2 * (size_t)kFinPreStride + idx] = make_int4(p.v[8], p.v[9], 0, 0);
+  }
+  __device__ __forceinline__ void load_pre(int j, fe &p) const {
+    const size_t idx = (size_t)j * L + lane;
+    const int4 a = pre[idx], b = pre[kFinPreStride + idx], c = pre[2 * (size_t)kFinPreStride + idx];
+    p.v[0] = a.x; p.v[1] = a.y; p.v[2] = a.z; p.v[3] = a.w;
+    p.v[4] = b.x; p.v[5] = b.y; p.v[6] = b.z; p.v[7] = b.w;
+    p.v[8] = c.x; p.v[9] = c.y;
+  }
+  __device__ __forceinline__ void load_r(int j, uint32_t Rw[8]) const {
+    load_row_words(Rw, sig + 64 * (size_t)(fin_base + slot(j)), 2);
+  }
+  __device__ __forceinline__ void result(int j, bool ok) const {
+    uint8_t *o = out + fin_base + slot(j);
+    *o = (*o && ok) ? 1 : 0;
+  }
+};
+
+__global__ __launch_bounds__(kThreadsPerBlock) void verify_finish_kernel(
+    const int4 *__restrict__ fin, int4 *__restrict__ pre, const uint8_t *__restrict__ sig, uint8_t *__restrict__ out,
+    uint32_t fin_base, uint32_t L, uint32_t m) {
+  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= L) return;
+  FinDev a{fin, pre, sig, out, fin_base, lane, L, m};
+  finish_group(a);
+}
+
+// Finish launch for the m signatures at fin_base: group size G = m / 65536 clamped to
+// [1, 16] (65,536 lanes keep every SIMD busy; each lane pays one inversion per group).
+hipError_t launch_finish(const int4 *fin, int4 *pre, const uint8_t *sig, uint8_t *out, uint32_t fin_base, uint32_t m,
+                         hipStream_t stream) {
+  if (m == 0) return hipSuccess;
+  uint32_t G = m / 65536;
+  if (G < 1) G = 1;
+  if (G > kFinGroupMax) G = kFinGroupMax;
+  const uint32_t L = (m + G - 1) / G;
+  hipLaunchKernelGGL(verify_finish_kernel, dim3((L + kThreadsPerBlock - 1) / kThreadsPerBlock),
+                     dim3(kThreadsPerBlock), 0, stream, fin, pre, sig, out, fin_base, L, m);
+  return hipGetLastError();
 }
 
 __global__ __launch_bounds__(kThreadsPerBlock) void sign_kernel(
@@ -254,32 +344,38 @@ uint32_t grid_for(size_t n, uint32_t max_blocks) {
 
 hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                          uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
-                         int4 *prep, hipStream_t stream, uint32_t chunk, int main_waves, bool msg_slots,
-                         KernelTimer *timer) {
+                         int4 *prep, int4 *fin, int4 *fin_pre, hipStream_t stream, uint32_t chunk, int main_waves,
+                         bool msg_slots, KernelTimer *timer) {
   const MsgSrc ms{msgs, off, msg_slots};
   // Chunks of at most slab_stride signatures: the per-lane tables (slab) and the
-  // prep hand-off are sized for one chunk.
+  // prep hand-off are sized for one chunk.  The finish runs once per kFinCap block.
   if (chunk == 0 || chunk > slab_stride) chunk = slab_stride;
-  for (uint32_t base = 0; base < n; base += chunk) {
-    const uint32_t count = (n - base) < chunk ? (n - base) : chunk;
-    const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
-    if (timer) timer->mark(stream);
-    hipLaunchKernelGGL(verify_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, pub, sig, ms, base,
-                       count, prep, slab_stride);
-    if (timer) timer->mark(stream);
-    // default: 2 waves/SIMD, lane-major per-lane tables (+3.7 % over the slot-interleaved
-    // layout, profiles/r01/variants.txt); the others are kept as measured A/B variants.
-    if (main_waves >= 3)
-      hipLaunchKernelGGL((verify_main_kernel<3, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base,
-                         count, prep, slab_stride, slab, btab, out);
-    else if (main_waves == -2)  // slot-interleaved slab layout
-      hipLaunchKernelGGL((verify_main_kernel<2, false>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base,
-                         count, prep, slab_stride, slab, btab, out);
-    else
-      hipLaunchKernelGGL((verify_main_kernel<2, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base,
-                         count, prep, slab_stride, slab, btab, out);
-    if (timer) timer->mark(stream);
-    hipError_t e = hipGetLastError();
+  if (timer) timer->mark(stream, -1);
+  for (uint32_t fbase = 0; fbase < n; fbase += kFinCap) {
+    const uint32_t m = (n - fbase) < kFinCap ? (n - fbase) : kFinCap;
+    for (uint32_t base = fbase; base < fbase + m; base += chunk) {
+      const uint32_t count = (fbase + m - base) < chunk ? (fbase + m - base) : chunk;
+      const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
+      hipLaunchKernelGGL(verify_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, pub, sig, ms, base,
+                         count, prep, slab_stride);
+      if (timer) timer->mark(stream, 0);
+      // default: 2 waves/SIMD, lane-major per-lane tables (+3.7 % over the slot-interleaved
+      // layout, profiles/r01/variants.txt); the others are kept as measured A/B variants.
+      if (main_waves >= 3)
+        hipLaunchKernelGGL((verify_main_kernel<3, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base,
+                           count, prep, slab_stride, slab, btab, fin, fbase, out);
+      else if (main_waves == -2)  // slot-interleaved slab layout
+        hipLaunchKernelGGL((verify_main_kernel<2, false>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base,
+                           count, prep, slab_stride, slab, btab, fin, fbase, out);
+      else
+        hipLaunchKernelGGL((verify_main_kernel<2, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base,
+                           count, prep, slab_stride, slab, btab, fin, fbase, out);
+      if (timer) timer->mark(stream, 1);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    hipError_t e = launch_finish(fin, fin_pre, sig, out, fbase, m, stream);
+    if (timer) timer->mark(stream, 2);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -400,13 +496,13 @@ __global__ __launch_bounds__(kThreadsPerBlock) void verify_keyset_prep_kernel(
 
 __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_keyset_main_kernel(
     const uint32_t *__restrict__ val_idx, const int4 *__restrict__ acomb, const int4 *__restrict__ bcomb,
-    const uint8_t *__restrict__ sig, uint32_t base, uint32_t count, const int4 *__restrict__ prep, uint32_t stride,
-    uint8_t *__restrict__ out) {
+    uint32_t base, uint32_t count, const int4 *__restrict__ prep, uint32_t stride, int4 *__restrict__ fin,
+    uint32_t fin_base, uint8_t *__restrict__ out) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   if (slot >= count) return;
   const uint32_t i = base + slot;
   const uint32_t v = val_idx[i];
-  uint32_t k[8], s[8], Rw[8];
+  uint32_t k[8], s[8];
   int32_t w[40];
 #pragma unroll
   for (int q = 0; q < 5; q++) {  // k, s, (A unused), ok at word 36
@@ -416,10 +512,12 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_keyset_main_kernel
   const bool ok = prep[(size_t)9 * stride + slot].x != 0;
 #pragma unroll
   for (int j = 0; j < 8; j++) { k[j] = (uint32_t)w[j]; s[j] = (uint32_t)w[8 + j]; }
-  load_row_words(Rw, sig + 64 * (size_t)i, 2);
   const GlobalComb ac{acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4};
   const GlobalComb bc{bcomb};
-  out[i] = (verify_main_comb(k, s, Rw, ac, bc) && ok) ? 1 : 0;
+  ge_p3 R;
+  verify_main_comb_point(R, k, s, ac, bc);
+  fin_store(fin, kFinCap, i - fin_base, R.X, R.Y, R.Z);
+  out[i] = ok ? 1 : 0;
 }
 
 hipError_t launch_comb_bases(const uint8_t *pubs, uint32_t n, int negate, uint8_t *ok, int32_t *bases,
@@ -438,16 +536,22 @@ hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStr
 hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
                                 const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                 const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
-                                hipStream_t stream, bool msg_slots) {
+                                int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots) {
   const MsgSrc ms{msgs, off, msg_slots};
-  for (uint32_t base = 0; base < n; base += stride) {
-    const uint32_t count = (n - base) < stride ? (n - base) : stride;
-    const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
-    hipLaunchKernelGGL(verify_keyset_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx, key_pub,
-                       key_ok, sig, ms, base, count, prep, stride);
-    hipLaunchKernelGGL(verify_keyset_main_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx, acomb,
-                       bcomb, sig, base, count, prep, stride, out);
-    hipError_t e = hipGetLastError();
+  if (stride > kFinCap) stride = kFinCap;
+  for (uint32_t fbase = 0; fbase < n; fbase += kFinCap) {
+    const uint32_t m = (n - fbase) < kFinCap ? (n - fbase) : kFinCap;
+    for (uint32_t base = fbase; base < fbase + m; base += stride) {
+      const uint32_t count = (fbase + m - base) < stride ? (fbase + m - base) : stride;
+      const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
+      hipLaunchKernelGGL(verify_keyset_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx,
+                         key_pub, key_ok, sig, ms, base, count, prep, stride);
+      hipLaunchKernelGGL(verify_keyset_main_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx, acomb,
+                         bcomb, base, count, prep, stride, fin, fbase, out);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    hipError_t e = launch_finish(fin, fin_pre, sig, out, fbase, m, stream);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;

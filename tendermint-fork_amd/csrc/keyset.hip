@@ -89,10 +89,12 @@ int votes_launch(tmed_ctx *c, VoteStage &st, uint8_t *out) {
     if (st.ks)
       e = launch_verify_keyset((const uint32_t *)(d + st.o_key), st.ks->d_pub, st.ks->d_ok, st.ks->d_comb, c->d_bcomb,
                                d + st.o_sig, (const uint8_t *)c->d_vmsg.p, (const uint32_t *)c->d_off.p, m,
-                               (uint8_t *)c->d_out.p, c->d_prep, c->slab_slots, s, /*msg_slots=*/true);
+                               (uint8_t *)c->d_out.p, c->d_prep, c->slab_slots, c->d_fin, c->d_fin_pre, s,
+                               /*msg_slots=*/true);
     else
       e = launch_verify(d + st.o_key, d + st.o_sig, (const uint8_t *)c->d_vmsg.p, (const uint32_t *)c->d_off.p, m,
-                        (uint8_t *)c->d_out.p, c->d_slab, c->slab_slots, c->d_btab, c->d_prep, s, c->chunk,
+                        (uint8_t *)c->d_out.p, c->d_slab, c->slab_slots, c->d_btab, c->d_prep, c->d_fin,
+                        c->d_fin_pre, s, c->chunk,
                         c->main_waves, /*msg_slots=*/true);
   }
   if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
@@ -172,7 +174,8 @@ int tmed_verify_batch_keyset_device(tmed_ctx *c, uint64_t handle, const uint32_t
   (void)hipSetDevice(c->device);
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   return map_err(launch_verify_keyset(d_val_idx, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb, d_sigs, d_msgs, d_msg_off,
-                                      (uint32_t)n, d_out, c->d_prep, c->slab_slots, s));
+                                      (uint32_t)n, d_out, c->d_prep, c->slab_slots, c->d_fin,
+                                      c->d_fin_pre, s));
 }
 
 int tmed_verify_batch_keyset(tmed_ctx *c, uint64_t handle, const uint32_t *val_idx, const uint8_t *sigs,
@@ -216,7 +219,8 @@ int tmed_verify_batch_keyset(tmed_ctx *c, uint64_t handle, const uint32_t *val_i
   if (e == hipSuccess)
     e = launch_verify_keyset((const uint32_t *)c->d_a.p, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb,
                              (const uint8_t *)c->d_b.p, (const uint8_t *)c->d_msg.p, (const uint32_t *)c->d_off.p,
-                             (uint32_t)n, (uint8_t *)c->d_out.p, c->d_prep, c->slab_slots, s);
+                             (uint32_t)n, (uint8_t *)c->d_out.p, c->d_prep, c->slab_slots, c->d_fin,
+                             c->d_fin_pre, s);
   if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
   if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, n, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);

@@ -67,6 +67,8 @@ int tmed_init(int device, tmed_ctx **out) {
   if (const char *v = getenv("TMED_MAIN_WAVES")) c->main_waves = atoi(v);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_slab, (size_t)c->slab_slots * kSlabSlotBytes);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_prep, (size_t)c->slab_slots * kPrepSlotBytes);
+  if (e == hipSuccess) e = hipMalloc((void **)&c->d_fin, kFinBytes);          // 128 MB: projective R'
+  if (e == hipSuccess) e = hipMalloc((void **)&c->d_fin_pre, kFinPreBytes);   // 48 MB: prefix products
   // Shared signed radix-256 comb of +B (528 KB, L2-resident) for the key-cached path.
   uint8_t *d_bpub = nullptr, *d_bok = nullptr;
   const uint8_t benc[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
@@ -99,6 +101,8 @@ void tmed_destroy(tmed_ctx *c) {
   if (c->d_bcomb) hipFree(c->d_bcomb);
   if (c->d_slab) hipFree(c->d_slab);
   if (c->d_prep) hipFree(c->d_prep);
+  if (c->d_fin) hipFree(c->d_fin);
+  if (c->d_fin_pre) hipFree(c->d_fin_pre);
   if (c->d_btab) hipFree(c->d_btab);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
@@ -122,17 +126,17 @@ int tmed_set_kernel_timing(tmed_ctx *c, int on) {
   return TMED_OK;
 }
 
-int tmed_kernel_times(tmed_ctx *c, float *prep_ms, float *main_ms, int *launches) {
-  if (!c || !prep_ms || !main_ms || !launches || !c->timing) return TMED_EINVAL;
-  *prep_ms = *main_ms = 0.f;
-  *launches = c->timer.n / 3;
-  for (int i = 0; i + 2 < c->timer.n; i += 3) {
-    float a = 0.f, b = 0.f;
-    if (hipEventSynchronize(c->timer.ev[i + 2]) != hipSuccess) return TMED_EHIP;
-    (void)hipEventElapsedTime(&a, c->timer.ev[i], c->timer.ev[i + 1]);
-    (void)hipEventElapsedTime(&b, c->timer.ev[i + 1], c->timer.ev[i + 2]);
-    *prep_ms += a;
-    *main_ms += b;
+int tmed_kernel_times(tmed_ctx *c, float ms[3], int launches[3]) {
+  if (!c || !ms || !launches || !c->timing) return TMED_EINVAL;
+  for (int k = 0; k < 3; k++) { ms[k] = 0.f; launches[k] = 0; }
+  if (c->timer.n > 0 && hipEventSynchronize(c->timer.ev[c->timer.n - 1]) != hipSuccess) return TMED_EHIP;
+  for (int i = 1; i < c->timer.n; i++) {
+    const int k = c->timer.kind[i];
+    if (k < 0 || k > 2) continue;
+    float t = 0.f;
+    (void)hipEventElapsedTime(&t, c->timer.ev[i - 1], c->timer.ev[i]);
+    ms[k] += t;
+    launches[k] += 1;
   }
   return TMED_OK;
 }
@@ -146,7 +150,7 @@ int tmed_verify_batch_device(tmed_ctx *c, const uint8_t *d_pub, const uint8_t *d
   hipSetDevice(c->device);
   if (c->timing) c->timer.n = 0;
   hipError_t e = launch_verify(d_pub, d_sig, d_msgs, d_off, (uint32_t)n, d_out, c->d_slab, c->slab_slots,
-                               c->d_btab, c->d_prep, s, c->chunk, c->main_waves, false,
+                               c->d_btab, c->d_prep, c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves, false,
                                c->timing ? &c->timer : nullptr);
   return map_err(e);
 }
@@ -203,7 +207,7 @@ int tmed_verify_batch(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, const
   if (e == hipSuccess)
     e = launch_verify((const uint8_t *)c->d_a.p, (const uint8_t *)c->d_b.p, (const uint8_t *)c->d_msg.p,
                       (const uint32_t *)c->d_off.p, (uint32_t)n, (uint8_t *)c->d_out.p, c->d_slab, c->slab_slots,
-                      c->d_btab, c->d_prep, s, c->chunk, c->main_waves);
+                      c->d_btab, c->d_prep, c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves);
   if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
   if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, n, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);

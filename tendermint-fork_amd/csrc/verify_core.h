@@ -143,19 +143,81 @@ TMED_HD bool verify_prep(const uint32_t pubw[8], const uint32_t sigw[16], const 
   return ok;
 }
 
-// Verification phase 2 (point arithmetic): enc([k](-A) + [s]B) == R ?
+// Verification phase 2 (point arithmetic): R' = [k](-A) + [s]B in projective form.  The
+// canonical encoding of R' (one inversion) is left to the batched finish below.
 template <class T, class BT>
-TMED_HD bool verify_main(const uint32_t k[8], const uint32_t s[8], const ge_p3 &A, const uint32_t Rw[8], T &tab,
-                         const BT &btab) {
+TMED_HD void verify_main_point(ge_p2 &R, const uint32_t k[8], const uint32_t s[8], const ge_p3 &A, T &tab,
+                               const BT &btab) {
   build_table_negA(tab, A);
-  ge_p2 R;
   double_scalarmult(R, k, s, tab, btab);
+}
+
+// enc(X/Z, Y/Z) == R bytes, given zi = 1/Z.
+TMED_HD bool encoding_matches(const fe &X, const fe &Y, const fe &zi, const uint32_t Rw[8]) {
+  fe x, y;
+  fe_mul(x, X, zi);
+  fe_mul(y, Y, zi);
   uint32_t enc[8];
-  ge_tobytes(enc, R.X, R.Y, R.Z);
+  fe_to_words(enc, y);
+  enc[7] |= (uint32_t)fe_isnegative(x) << 31;
   uint32_t diff = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) diff |= enc[i] ^ Rw[i];
   return diff == 0;
+}
+
+// Unbatched phase 2 + compare (one inversion per signature).
+template <class T, class BT>
+TMED_HD bool verify_main(const uint32_t k[8], const uint32_t s[8], const ge_p3 &A, const uint32_t Rw[8], T &tab,
+                         const BT &btab) {
+  ge_p2 R;
+  verify_main_point(R, k, s, A, tab, btab);
+  fe zi;
+  fe_invert(zi, R.Z);
+  return encoding_matches(R.X, R.Y, zi, Rw);
+}
+
+// Batched finish (Montgomery's simultaneous inversion): one lane owns the G' <= G
+// signatures j = 0..count-1 of its group; with prefix products P_j = Z_0 ... Z_j,
+// 1/Z_j = P_{j-1} / P_j, so the group costs one inversion + 3 multiplications per
+// signature instead of one inversion per signature (the inversion is ~254 squarings).
+// Acc provides: count(); load_z(j, fe&); load_xy(j, fe&, fe&); load_r(j, uint32_t[8]);
+// store_pre(j, const fe&); load_pre(j, fe&); result(j, bool).
+// Z = 0 cannot come out of the complete formulas for points on the curve; it is still
+// guarded (replaced by 1 and the signature rejected) so one bad value cannot poison the
+// inversion of its whole group.
+template <class Acc>
+TMED_HD void finish_group(Acc &a) {
+  const int cnt = a.count();
+  if (cnt <= 0) return;
+  fe acc, z;
+  uint32_t bad = 0;
+#pragma unroll 1
+  for (int j = 0; j < cnt; j++) {
+    a.load_z(j, z);
+    if (fe_iszero(z)) { fe_1(z); bad |= 1u << j; }
+    if (j == 0) fe_copy(acc, z); else fe_mul(acc, acc, z);
+    a.store_pre(j, acc);
+  }
+  fe inv;
+  fe_invert(inv, acc);  // 1 / (Z_0 ... Z_{cnt-1})
+#pragma unroll 1
+  for (int j = cnt - 1; j >= 0; j--) {
+    fe zi, X, Y;
+    if (j > 0) {
+      a.load_pre(j - 1, zi);
+      fe_mul(zi, zi, inv);  // 1 / Z_j
+      a.load_z(j, z);
+      if ((bad >> j) & 1u) fe_1(z);
+      fe_mul(inv, inv, z);  // 1 / (Z_0 ... Z_{j-1})
+    } else {
+      fe_copy(zi, inv);
+    }
+    a.load_xy(j, X, Y);
+    uint32_t Rw[8];
+    a.load_r(j, Rw);
+    a.result(j, encoding_matches(X, Y, zi, Rw) && !((bad >> j) & 1u));
+  }
 }
 
 // One verification.  pubw: 8 words of A; sigw: 16 words (R = 0..7, S = 8..15).
@@ -276,15 +338,14 @@ TMED_HD bool verify_prep_comb(const uint32_t pubw[8], bool key_ok, const uint32_
 }
 
 // Key-cached verification, phase 2: [k](-A) from the key's comb, [s]B from the shared
-// comb: 32 + 32 mixed additions, then encode and compare with R.
+// comb: 32 + 32 mixed additions (projective result; encoding by the batched finish).
 // AC/BC provide  void load(int window, int j, ge_niels&) const  for j in 0..128.
 template <class AC, class BC>
-TMED_HD bool verify_main_comb(const uint32_t k[8], const uint32_t s[8], const uint32_t Rw[8], const AC &acomb,
-                              const BC &bcomb) {
+TMED_HD void verify_main_comb_point(ge_p3 &acc, const uint32_t k[8], const uint32_t s[8], const AC &acomb,
+                                    const BC &bcomb) {
   uint32_t kr[8], sr[8];
   sc_recode256(kr, k);
   sc_recode256(sr, s);
-  ge_p3 acc;
   ge_p3_0(acc);
   ge_p1p1 t;
   ge_niels e;
@@ -310,12 +371,16 @@ TMED_HD bool verify_main_comb(const uint32_t k[8], const uint32_t s[8], const ui
       ge_p1p1_to_p3(acc, t);
     }
   }
-  uint32_t enc[8];
-  ge_tobytes(enc, acc.X, acc.Y, acc.Z);
-  uint32_t diff = 0;
-#pragma unroll
-  for (int w = 0; w < 8; w++) diff |= enc[w] ^ Rw[w];
-  return diff == 0;
+}
+
+template <class AC, class BC>
+TMED_HD bool verify_main_comb(const uint32_t k[8], const uint32_t s[8], const uint32_t Rw[8], const AC &acomb,
+                              const BC &bcomb) {
+  ge_p3 acc;
+  verify_main_comb_point(acc, k, s, acomb, bcomb);
+  fe zi;
+  fe_invert(zi, acc.Z);
+  return encoding_matches(acc.X, acc.Y, zi, Rw);
 }
 
 template <class AC, class BC>

@@ -72,8 +72,7 @@ def lib() -> ctypes.CDLL:
     l.tmed_set_kernel_timing.restype = I
     l.tmed_set_kernel_timing.argtypes = [P, I]
     l.tmed_kernel_times.restype = I
-    l.tmed_kernel_times.argtypes = [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
-                                    ctypes.POINTER(ctypes.c_int)]
+    l.tmed_kernel_times.argtypes = [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
     l.tmed_last_kernel_ms.restype = ctypes.c_float
     l.tmed_last_kernel_ms.argtypes = [P]
     _lib = l

@@ -161,12 +161,13 @@ class Engine:
             raise TmedError(rc, "tmed_set_kernel_timing")
 
     def kernel_times(self):
-        """(prep_ms, main_ms, launch pairs) of the last verify_device call (timing on)."""
-        a, b, n = ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
-        rc = lib().tmed_kernel_times(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n))
+        """Per kernel kind (prep, main, finish) of the last verify_device call (timing on):
+        ([ms...], [launches...])."""
+        ms, n = (ctypes.c_float * 3)(), (ctypes.c_int * 3)()
+        rc = lib().tmed_kernel_times(self._h, ms, n)
         if rc != TMED_OK:
             raise TmedError(rc, "tmed_kernel_times")
-        return a.value, b.value, n.value
+        return list(ms), list(n)
 
     def last_kernel_ms(self) -> float:
         return float(lib().tmed_last_kernel_ms(self._h))

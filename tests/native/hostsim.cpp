@@ -28,13 +28,45 @@ HostBTab &btab() {
   if (!init) { build_btab_niels(t.e); init = true; }
   return t;
 }
+// The device finish's accessor, on host arrays: lane l owns slots l, l + L, ... < m.
+struct HostFin {
+  const std::vector<ge_p2> *pts;
+  std::vector<fe> *pre;
+  const uint8_t *sig;
+  uint8_t *out;
+  uint32_t lane, L, m;
+  int count() const { return lane < m ? (int)((m - lane + L - 1) / L) : 0; }
+  uint32_t slot(int j) const { return lane + (uint32_t)j * L; }
+  void load_z(int j, fe &z) const { z = (*pts)[slot(j)].Z; }
+  void load_xy(int j, fe &X, fe &Y) const { X = (*pts)[slot(j)].X; Y = (*pts)[slot(j)].Y; }
+  void store_pre(int j, const fe &p) const { (*pre)[(size_t)j * L + lane] = p; }
+  void load_pre(int j, fe &p) const { p = (*pre)[(size_t)j * L + lane]; }
+  void load_r(int j, uint32_t Rw[8]) const { load_words8(Rw, sig + 64 * (size_t)slot(j)); }
+  void result(int j, bool ok) const { uint8_t &o = out[slot(j)]; o = (o && ok) ? 1 : 0; }
+};
+
+// Host twin of launch_finish: same group-size rule, but G is a parameter so tests can
+// cover partial groups.
+void host_finish(const std::vector<ge_p2> &pts, const uint8_t *sig, uint8_t *out, uint32_t m, uint32_t G) {
+  if (m == 0) return;
+  const uint32_t L = (m + G - 1) / G;
+  std::vector<fe> pre((size_t)G * L);
+#pragma omp parallel for schedule(dynamic, 8)
+  for (long l = 0; l < (long)L; l++) {
+    HostFin a{&pts, &pre, sig, out, (uint32_t)l, L, m};
+    finish_group(a);
+  }
+}
 }  // namespace
 
 extern "C" {
 
-void hostsim_verify_batch(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
-                          size_t n, uint8_t *out) {
+// group = 0: per-signature encoding (verify_one); group >= 1: prep + main point per
+// signature, then the batched finish with that group size (the device path).
+void hostsim_verify_batch_g(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
+                            size_t n, uint8_t *out, int group) {
   HostBTab &bt = btab();
+  std::vector<ge_p2> pts(group > 0 ? n : 0);
 #pragma omp parallel for schedule(dynamic, 16)
   for (long i = 0; i < (long)n; i++) {
     HostTab tab;
@@ -42,8 +74,22 @@ void hostsim_verify_batch(const uint8_t *pub, const uint8_t *sig, const uint8_t 
     load_words8(pw, pub + 32 * i);
     load_words8(sw, sig + 64 * i);
     load_words8(sw + 8, sig + 64 * i + 32);
-    out[i] = verify_one(pw, sw, msgs + off[i], off[i + 1] - off[i], tab, bt) ? 1 : 0;
+    if (group <= 0) {
+      out[i] = verify_one(pw, sw, msgs + off[i], off[i + 1] - off[i], tab, bt) ? 1 : 0;
+    } else {
+      uint32_t k[8], s[8];
+      ge_p3 A;
+      const bool ok = verify_prep(pw, sw, msgs + off[i], off[i + 1] - off[i], k, s, A);
+      verify_main_point(pts[i], k, s, A, tab, bt);
+      out[i] = ok ? 1 : 0;
+    }
   }
+  if (group > 0) host_finish(pts, sig, out, (uint32_t)n, (uint32_t)group);
+}
+
+void hostsim_verify_batch(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
+                          size_t n, uint8_t *out) {
+  hostsim_verify_batch_g(pub, sig, msgs, off, n, out, 16);
 }
 
 void hostsim_sign_batch(const uint8_t *seeds, const uint8_t *msgs, const uint32_t *off, size_t n,
@@ -103,15 +149,21 @@ void hostsim_verify_comb_batch(const uint8_t *keys, size_t nkeys, const uint32_t
     build_host_comb(ac[k], pw, true, &ok);
     kok[k] = ok;
   }
+  std::vector<ge_p2> pts(n);
 #pragma omp parallel for schedule(dynamic, 8)
   for (long i = 0; i < (long)n; i++) {
-    uint32_t pw[8], sw[16];
+    uint32_t pw[8], sw[16], k[8], s[8];
     const uint32_t v = key_idx[i];
     load_words8(pw, keys + 32 * v);
     load_words8(sw, sig + 64 * i);
     load_words8(sw + 8, sig + 64 * i + 32);
-    out[i] = verify_one_comb(pw, kok[v] != 0, sw, msgs + off[i], off[i + 1] - off[i], ac[v], bcomb) ? 1 : 0;
+    const bool ok = verify_prep_comb(pw, kok[v] != 0, sw, msgs + off[i], off[i + 1] - off[i], k, s);
+    ge_p3 R;
+    verify_main_comb_point(R, k, s, ac[v], bcomb);
+    pts[i].X = R.X; pts[i].Y = R.Y; pts[i].Z = R.Z;
+    out[i] = ok ? 1 : 0;
   }
+  host_finish(pts, sig, out, (uint32_t)n, 3);
 }
 
 // Field-level probes: inputs/outputs are 32-byte LE encodings.

@@ -6,6 +6,7 @@ import hashlib
 import random
 
 import numpy as np
+import pytest
 
 from oracle import ed25519_go as E
 from oracle import port
@@ -68,14 +69,18 @@ def test_decode_matches_go_rule(hostsim):
             assert o.raw == E.encode(pt)
 
 
-def _verify(l, pubs, sigs, msgs, offs):
+def _verify(l, pubs, sigs, msgs, offs, group=16):
     n = len(pubs)
     out = np.zeros(n, np.uint8)
-    l.hostsim_verify_batch(_p(pubs), _p(sigs), _p(msgs), _p(offs), ctypes.c_size_t(n), _p(out))
+    l.hostsim_verify_batch_g(_p(pubs), _p(sigs), _p(msgs), _p(offs), ctypes.c_size_t(n), _p(out),
+                             ctypes.c_int(group))
     return out
 
 
-def test_golden_vectors_hostsim(hostsim, golden):
+@pytest.mark.parametrize("group", [0, 1, 5, 16])
+def test_golden_vectors_hostsim(hostsim, golden, group):
+    """Every golden tuple, with per-signature encoding (group 0) and through the batched
+    finish (Montgomery inversion over groups of 1, 5 and 16 signatures, partial last group)."""
     vs = [v for v in golden if len(v["sig"]) == 128]
     pubs = np.array([np.frombuffer(bytes.fromhex(v["pub"]), np.uint8) for v in vs])
     sigs = np.array([np.frombuffer(bytes.fromhex(v["sig"]), np.uint8) for v in vs])
@@ -83,7 +88,7 @@ def test_golden_vectors_hostsim(hostsim, golden):
     offs = np.zeros(len(vs) + 1, np.uint32)
     offs[1:] = np.cumsum([len(m) for m in ms])
     msgs = np.frombuffer(b"".join(ms) + b"\0", np.uint8)
-    out = _verify(hostsim, pubs, sigs, msgs, offs)
+    out = _verify(hostsim, pubs, sigs, msgs, offs, group)
     exp = np.array([v["valid"] for v in vs], np.uint8)
     bad = [vs[i]["class"] for i in np.nonzero(out != exp)[0]]
     assert not bad, bad
