@@ -24,8 +24,10 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define TMED_HD __host__ __device__ __forceinline__
+#define TMED_HDM __host__ __device__ __forceinline__  // member functions
 #else
 #define TMED_HD static inline
+#define TMED_HDM inline
 #endif
 
 namespace tmed {
@@ -72,6 +74,18 @@ TMED_HD void fe_select(fe &h, const fe &f, const fe &g, bool b) {
 // one 64-bit shift, one 32-bit and, one 64-bit add per carry (+ one 32-bit sub per limb).
 TMED_HD int64_t fe_bias(int k) { return (k & 1) ? ((int64_t)1 << 24) : ((int64_t)1 << 25); }
 
+// The same constant hidden from constant folding: as a known constant LLVM re-associates
+// the bias to the END of the column sum (one extra 64-bit add per column, 10 per mul);
+// opaque, it stays the addend of the column's first v_mad_i64_i32.  (The empty asm is
+// not volatile, so it is CSE'd and hoisted: two SGPR pairs for the whole kernel.)
+TMED_HD int64_t fe_bias_acc(int k) {
+  int64_t b = fe_bias(k);
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+s"(b));
+#endif
+  return b;
+}
+
 // Carry pass over BIASED 64-bit column sums H_k = h_k + B_k -> carried limbs.  Two
 // interleaved chains (0..4 and 4..9) give the scheduler independent work.
 TMED_HD void fe_carry64(fe &out, int64_t H[10]) {
@@ -114,7 +128,7 @@ TMED_HD void fe_mul(fe &h, const fe &f, const fe &g) {
   for (int i = 0; i < 10; i++) f2[i] = (int32_t)(2u * (uint32_t)f.v[i]);
   int64_t acc[10];
 #pragma unroll
-  for (int k = 0; k < 10; k++) acc[k] = fe_bias(k);
+  for (int k = 0; k < 10; k++) acc[k] = fe_bias_acc(k);
 #pragma unroll
   for (int i = 0; i < 10; i++) {
 #pragma unroll
@@ -140,7 +154,7 @@ TMED_HD void fe_sq_acc(int64_t acc[10], const fe &f, bool biased) {
     x2[i] = (int32_t)(2u * u); x19[i] = mul19(f.v[i]); x38[i] = mul38(f.v[i]);
   }
 #pragma unroll
-  for (int k = 0; k < 10; k++) acc[k] = biased ? fe_bias(k) : 0;
+  for (int k = 0; k < 10; k++) acc[k] = biased ? fe_bias_acc(k) : 0;
 #pragma unroll
   for (int i = 0; i < 10; i++) {
 #pragma unroll

@@ -140,7 +140,7 @@ struct MsgSrc {
 
 // Phase 1: SHA-512(R||A||M) mod L, S < L, A = Point.SetBytes(pub)  (one lane per signature
 // of the chunk [base, base + count)).
-__global__ __launch_bounds__(kThreadsPerBlock) void verify_prep_kernel(
+__global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_prep_kernel(
     const uint8_t *__restrict__ pub, const uint8_t *__restrict__ sig, MsgSrc ms, uint32_t base, uint32_t count,
     int4 *__restrict__ prep, uint32_t stride) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;

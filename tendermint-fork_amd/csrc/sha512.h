@@ -19,8 +19,8 @@ namespace tmed {
 #define TMED_ROTR64(x, n) (((x) >> (n)) | ((x) << (64 - (n))))
 #endif
 
-TMED_HD uint64_t sha512_k(int i) {
-  const uint64_t K[80] = {
+#if defined(__HIPCC__)
+__constant__ static const uint64_t kSha512K[80] = {
       0x428a2f98d728ae22ull, 0x7137449123ef65cdull, 0xb5c0fbcfec4d3b2full, 0xe9b5dba58189dbbcull,
       0x3956c25bf348b538ull, 0x59f111f1b605d019ull, 0x923f82a4af194f9bull, 0xab1c5ed5da6d8118ull,
       0xd807aa98a3030242ull, 0x12835b0145706fbeull, 0x243185be4ee4b28cull, 0x550c7dc3d5ffb4e2ull,
@@ -41,7 +41,36 @@ TMED_HD uint64_t sha512_k(int i) {
       0x06f067aa72176fbaull, 0x0a637dc5a2c898a6ull, 0x113f9804bef90daeull, 0x1b710b35131c471bull,
       0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull, 0x431d67c49c100d4cull,
       0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull};
-  return K[i];
+#else
+static const uint64_t kSha512K[80] = {
+      0x428a2f98d728ae22ull, 0x7137449123ef65cdull, 0xb5c0fbcfec4d3b2full, 0xe9b5dba58189dbbcull,
+      0x3956c25bf348b538ull, 0x59f111f1b605d019ull, 0x923f82a4af194f9bull, 0xab1c5ed5da6d8118ull,
+      0xd807aa98a3030242ull, 0x12835b0145706fbeull, 0x243185be4ee4b28cull, 0x550c7dc3d5ffb4e2ull,
+      0x72be5d74f27b896full, 0x80deb1fe3b1696b1ull, 0x9bdc06a725c71235ull, 0xc19bf174cf692694ull,
+      0xe49b69c19ef14ad2ull, 0xefbe4786384f25e3ull, 0x0fc19dc68b8cd5b5ull, 0x240ca1cc77ac9c65ull,
+      0x2de92c6f592b0275ull, 0x4a7484aa6ea6e483ull, 0x5cb0a9dcbd41fbd4ull, 0x76f988da831153b5ull,
+      0x983e5152ee66dfabull, 0xa831c66d2db43210ull, 0xb00327c898fb213full, 0xbf597fc7beef0ee4ull,
+      0xc6e00bf33da88fc2ull, 0xd5a79147930aa725ull, 0x06ca6351e003826full, 0x142929670a0e6e70ull,
+      0x27b70a8546d22ffcull, 0x2e1b21385c26c926ull, 0x4d2c6dfc5ac42aedull, 0x53380d139d95b3dfull,
+      0x650a73548baf63deull, 0x766a0abb3c77b2a8ull, 0x81c2c92e47edaee6ull, 0x92722c851482353bull,
+      0xa2bfe8a14cf10364ull, 0xa81a664bbc423001ull, 0xc24b8b70d0f89791ull, 0xc76c51a30654be30ull,
+      0xd192e819d6ef5218ull, 0xd69906245565a910ull, 0xf40e35855771202aull, 0x106aa07032bbd1b8ull,
+      0x19a4c116b8d2d0c8ull, 0x1e376c085141ab53ull, 0x2748774cdf8eeb99ull, 0x34b0bcb5e19b48a8ull,
+      0x391c0cb3c5c95a63ull, 0x4ed8aa4ae3418acbull, 0x5b9cca4f7763e373ull, 0x682e6ff3d6b2b8a3ull,
+      0x748f82ee5defb2fcull, 0x78a5636f43172f60ull, 0x84c87814a1f0ab72ull, 0x8cc702081a6439ecull,
+      0x90befffa23631e28ull, 0xa4506cebde82bde9ull, 0xbef9a3f7b2c67915ull, 0xc67178f2e372532bull,
+      0xca273eceea26619cull, 0xd186b8c721c0c207ull, 0xeada7dd6cde0eb1eull, 0xf57d4f7fee6ed178ull,
+      0x06f067aa72176fbaull, 0x0a637dc5a2c898a6ull, 0x113f9804bef90daeull, 0x1b710b35131c471bull,
+      0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull, 0x431d67c49c100d4cull,
+      0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull};
+#endif
+
+TMED_HD uint64_t sha512_k(int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return kSha512K[i];  // i is wave-uniform: scalar load
+#else
+  return kSha512K[i];
+#endif
 }
 
 TMED_HD void sha512_init(uint64_t st[8]) {
@@ -51,22 +80,28 @@ TMED_HD void sha512_init(uint64_t st[8]) {
   st[6] = 0x1f83d9abfb41bd6bull; st[7] = 0x5be0cd19137e2179ull;
 }
 
+// 80 rounds as 5 x 16 (the message-schedule window w[i & 15] stays register-indexed);
+// the round constants come from a uniform table (scalar loads on the device), so the
+// rolled outer loop keeps the live set at state + window (~50 VGPRs).
 TMED_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
   uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll 1
+  for (int r = 0; r < 80; r += 16) {
 #pragma unroll
-  for (int i = 0; i < 80; i++) {
-    if (i >= 16) {
-      const uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      const uint64_t s0 = TMED_ROTR64(w15, 1) ^ TMED_ROTR64(w15, 8) ^ (w15 >> 7);
-      const uint64_t s1 = TMED_ROTR64(w2, 19) ^ TMED_ROTR64(w2, 61) ^ (w2 >> 6);
-      w[i & 15] += s0 + w[(i - 7) & 15] + s1;
+    for (int j = 0; j < 16; j++) {
+      if (r > 0) {
+        const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+        const uint64_t s0 = TMED_ROTR64(w15, 1) ^ TMED_ROTR64(w15, 8) ^ (w15 >> 7);
+        const uint64_t s1 = TMED_ROTR64(w2, 19) ^ TMED_ROTR64(w2, 61) ^ (w2 >> 6);
+        w[j] += s0 + w[(j + 9) & 15] + s1;
+      }
+      const uint64_t S1 = TMED_ROTR64(e, 14) ^ TMED_ROTR64(e, 18) ^ TMED_ROTR64(e, 41);
+      const uint64_t ch = (e & f) ^ (~e & g);
+      const uint64_t t1 = h + S1 + ch + sha512_k(r + j) + w[j];
+      const uint64_t S0 = TMED_ROTR64(a, 28) ^ TMED_ROTR64(a, 34) ^ TMED_ROTR64(a, 39);
+      const uint64_t mj = (a & b) ^ (c & (a ^ b));
+      h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
     }
-    const uint64_t S1 = TMED_ROTR64(e, 14) ^ TMED_ROTR64(e, 18) ^ TMED_ROTR64(e, 41);
-    const uint64_t ch = (e & f) ^ (~e & g);
-    const uint64_t t1 = h + S1 + ch + sha512_k(i) + w[i & 15];
-    const uint64_t S0 = TMED_ROTR64(a, 28) ^ TMED_ROTR64(a, 34) ^ TMED_ROTR64(a, 39);
-    const uint64_t mj = (a & b) ^ (c & (a ^ b));
-    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
   }
   st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
@@ -75,13 +110,45 @@ TMED_HD uint32_t bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
 }
 
+// Message reader: big-endian 32-bit groups of M (any byte alignment) from aligned dword
+// loads.  On the device one v_perm_b32 per group realigns and byte-swaps (the selector
+// depends only on the lane's misalignment r); dwords past the last one that overlaps M
+// are never read.
+struct MsgReader {
+  const uint32_t *base;  // M rounded down to a dword boundary
+  uint32_t ndw;          // aligned dwords overlapping M
+  uint32_t r;            // misalignment of M in bytes
+  const uint8_t *m;
+  uint32_t mlen;
+  TMED_HDM MsgReader(const uint8_t *m_, uint32_t mlen_) : m(m_), mlen(mlen_) {
+    const uintptr_t a = (uintptr_t)m_;
+    r = (uint32_t)(a & 3u);
+    base = (const uint32_t *)(a - r);
+    ndw = (r + mlen_ + 3u) >> 2;
+  }
+  // bytes M[o .. o+3] (o % 4 == 0) as a big-endian word; bytes past M are unspecified
+  // (the caller masks them).
+  TMED_HDM uint32_t be32(uint32_t o) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t q = o >> 2;
+    const uint32_t lo = q < ndw ? base[q] : 0u;
+    const uint32_t hi = (q + 1) < ndw ? base[q + 1] : 0u;
+    const uint32_t sel = (r << 24) | ((r + 1) << 16) | ((r + 2) << 8) | (r + 3);
+    return __builtin_amdgcn_perm(hi, lo, sel);
+#else
+    uint32_t v = 0;
+    for (uint32_t i = 0; i < 4; i++) v = (v << 8) | (o + i < mlen ? m[o + i] : 0u);
+    return v;
+#endif
+  }
+};
+
 // Big-endian 64-bit word of the padded virtual stream  P0 || P1 || M || 0x80 || 0* || len128
 // at byte position pos (multiple of 8).  npre = 0, 32 or 64 bytes of register prefix
-// (p0 then p1, LE words).  mlen = |M|, total = npre + mlen, nblocks*128 = padded length.
-TMED_HD uint64_t sha512_stream_word(const uint32_t p0[8], const uint32_t p1[8], int npre,
-                                    const uint8_t *m, uint32_t mlen, uint32_t pos,
-                                    uint32_t padded_len) {
-  const uint32_t total = (uint32_t)npre + mlen;
+// (p0 then p1, LE words).  total = npre + |M|, padded = 128 * nblocks.
+TMED_HD uint64_t sha512_stream_word(const uint32_t p0[8], const uint32_t p1[8], int npre, const MsgReader &rd,
+                                    uint32_t pos, uint32_t padded_len) {
+  const uint32_t total = (uint32_t)npre + rd.mlen;
   if (pos + 8 <= (uint32_t)npre) {
     const uint32_t q = pos >> 2;  // word index into the 64-byte prefix
     const uint32_t lo = q < 8 ? p0[q] : p1[q - 8];
@@ -89,21 +156,13 @@ TMED_HD uint64_t sha512_stream_word(const uint32_t p0[8], const uint32_t p1[8], 
     return ((uint64_t)bswap32(lo) << 32) | bswap32(hi);
   }
   if (pos + 8 == padded_len) return (uint64_t)total * 8u;  // length (low 64 bits of len128)
+  const uint32_t mo = pos - (uint32_t)npre;                // npre and pos are multiples of 8
+  const int32_t nv = (int32_t)rd.mlen - (int32_t)mo;       // message bytes in this word
   uint64_t v = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint32_t p = pos + i;
-    uint32_t byte;
-    if (p < (uint32_t)npre) {
-      const uint32_t q = p >> 2;
-      const uint32_t word = q < 8 ? p0[q] : p1[q - 8];
-      byte = (word >> (8 * (p & 3))) & 0xffu;
-    } else if (p < total) {
-      byte = m[p - npre];
-    } else {
-      byte = (p == total) ? 0x80u : 0u;
-    }
-    v = (v << 8) | byte;
+  if (nv > 0) v = ((uint64_t)rd.be32(mo) << 32) | rd.be32(mo + 4);
+  if (nv < 8) {
+    if (nv > 0) v &= ~(~0ull >> (8 * nv));
+    if (nv >= 0) v |= 0x80ull << (56 - 8 * nv);
   }
   return v;
 }
@@ -115,13 +174,14 @@ TMED_HD void sha512_stream(uint32_t out[16], const uint32_t p0[8], const uint32_
   const uint32_t total = (uint32_t)npre + mlen;
   const uint32_t nblocks = (total + 17 + 127) >> 7;
   const uint32_t padded = nblocks << 7;
+  const MsgReader rd(m, mlen);
   uint64_t st[8];
   sha512_init(st);
 #pragma unroll 1
   for (uint32_t b = 0; b < nblocks; b++) {
     uint64_t w[16];
 #pragma unroll
-    for (int t = 0; t < 16; t++) w[t] = sha512_stream_word(p0, p1, npre, m, mlen, b * 128 + 8 * t, padded);
+    for (int t = 0; t < 16; t++) w[t] = sha512_stream_word(p0, p1, npre, rd, b * 128 + 8 * t, padded);
     sha512_compress(st, w);
   }
 #pragma unroll

@@ -97,13 +97,17 @@ TMED_HD void double_scalarmult(ge_p2 &out, const uint32_t k[8], const uint32_t s
       for (int h = 0; h < 2; h++) {
         const int da = (int)(kc >> 28) - 8;
         kc <<= 4;
+        if (h == 0 && j == 0 && i == 0) {
+          ge_p3_0(r);  // the first four doublings would double the identity: skipped
+        } else {
 #pragma unroll 1
-        for (int d = 0; d < 3; d++) {
+          for (int d = 0; d < 3; d++) {
+            ge_p2_dbl(t, q);
+            ge_p1p1_to_p2(q, t);
+          }
           ge_p2_dbl(t, q);
-          ge_p1p1_to_p2(q, t);
+          ge_p1p1_to_p3(r, t);
         }
-        ge_p2_dbl(t, q);
-        ge_p1p1_to_p3(r, t);
         tab.load(da < 0 ? -da : da, ca);
         ge_add_cached(t, r, ca, da < 0);
         if (h == 0) ge_p1p1_to_p2(q, t);

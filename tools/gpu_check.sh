@@ -41,9 +41,11 @@ for s in $STEPS; do
     pmc)
       cd /tmp && export TMPDIR=/tmp
       rc=0
-      for ctr in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE" "SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES"; do
+      PMC_SETS=${PMC_SETS:-"FETCH_SIZE|WRITE_SIZE|SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE|SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES"}
+      IFS='|' read -ra SETS <<< "$PMC_SETS"
+      for ctr in "${SETS[@]}"; do
         tag=$(echo $ctr | tr ' ' '_')
-        timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$OUT/pmc_$tag -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-peak > $GRAFT_REPO_ROOT/$OUT/pmc_$tag.log 2>&1; rc=$?
+        timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$OUT/pmc_$tag -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-peak > $GRAFT_REPO_ROOT/$OUT/pmc_$tag.log 2>&1; rc=$?
         echo "pmc $ctr rc=$rc" | tee -a $GRAFT_REPO_ROOT/$OUT/pmc.log
         if fatal $rc; then break; fi
       done
