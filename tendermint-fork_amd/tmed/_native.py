@@ -9,7 +9,8 @@ import ctypes
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libtmed25519_hip.so")
+# TMED_LIB overrides the library path (A/B runs of two builds of the same sources).
+LIB_PATH = os.environ.get("TMED_LIB") or os.path.join(PKG_ROOT, "lib", "libtmed25519_hip.so")
 
 TMED_OK = 0
 TMED_EINVAL = -1

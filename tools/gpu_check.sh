@@ -25,7 +25,8 @@ for s in $STEPS; do
       cd $GRAFT_REPO_ROOT; echo "prof rc=$rc" | tee -a $OUT/prof.log ;;
     variants)
       rc=0
-      for cfg in ${VARIANTS:-"TMED_MAIN_WAVES=2" "TMED_MAIN_WAVES=-1" "TMED_MAIN_WAVES=3" "TMED_MAIN_WAVES=2" "TMED_MAIN_WAVES=-1" "TMED_MAIN_WAVES=2 TMED_CHUNK=262144"}; do
+      IFS='|' read -ra VLIST <<< "${VARIANTS:-TMED_MAIN_WAVES=2|TMED_MAIN_WAVES=-2|TMED_MAIN_WAVES=3}"
+      for cfg in "${VLIST[@]}"; do
         env $cfg timeout -k 10 300 python bench.py --no-cpu-baseline --no-peak --steps 5 > $OUT/variant.log 2>&1; rc=$?
         echo "$cfg rc=$rc $(tail -1 $OUT/variant.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])' 2>/dev/null)" | tee -a $OUT/variants.txt
         if fatal $rc; then break; fi
