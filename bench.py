@@ -156,11 +156,13 @@ def main():
             (prep_ms, main_ms, fin_ms), (launches, _, fin_launches) = eng.kernel_times()
             eng.set_kernel_timing(False)
             achieved = n * MADS_MAIN / (main_ms * 1e-3) / 1e12
+            traffic, traffic_src = pmc_traffic(n / max(1, launches))
             roof = {"bound": "valu", "kernel": "verify_main_kernel", "achieved": round(achieved, 3),
                     "peak": round(peak, 3) if peak else None,
                     "unit": "Tmad/s (v_mad_i64_i32 lane-ops; peak = measured sustained rate)",
                     "frac": round(achieved / peak, 4) if peak else None,
-                    "traffic": None,
+                    "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                    "traffic_source": traffic_src,
                     "mads_per_verify_main": MADS_MAIN, "mads_per_verify_total": MADS_PER_VERIFY_GENERIC,
                     "kernel_avg_ms": round(main_ms / max(1, launches), 4), "launches_per_step": launches,
                     "prep_kernel_avg_ms": round(prep_ms / max(1, launches), 4),
@@ -196,6 +198,22 @@ def main():
         dist.destroy_process_group()
     eng.close()
     return result
+
+
+def pmc_traffic(sigs_per_launch):
+    """HBM bytes per main-kernel launch from the committed rocprofv3 --pmc summary
+    (tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE per signature, gfx950-corrected),
+    scaled to this run's launch size; (None, None) when no summary is present."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as fh:
+            pmc = json.load(fh)
+    except (OSError, ValueError):
+        return None, None
+    for k, d in pmc.items():
+        if k.startswith("verify_main_kernel") and "hbm_bytes_per_sig" in d:
+            return round(d["hbm_bytes_per_sig"] * sigs_per_launch), "profiles/pmc_summary.json[%s]" % k
+    return None, None
 
 
 def cpu_baseline(eng, d_pub, d_sig, msgs, offs, m):

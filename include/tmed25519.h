@@ -258,6 +258,37 @@ typedef int (*tmed_batch_verify_fn)(void *user, const uint8_t *pubkeys, const ui
 int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out,
                              tmed_batch_verify_fn verify, void *user);
 
+/* ------------------------------------------------- blocksync replay (f4) */
+
+/*
+ * A window of blocks for the blocksync reactor: for each block h of the
+ * window, the reactor's check  state.Validators.VerifyCommitLight(chainID, firstID,
+ * first.Height, second.LastCommit)  (blockchain/v0/reactor.go:366-367, with first/second
+ * from pool.PeekTwoBlocks, pool.go:193-205).  All blocks of a window are verified against
+ * the same validator set (the state's set, predicted for the window; the reactor confirms
+ * ValidatorsHash as it applies each block and re-verifies from there if the set changed).
+ */
+typedef struct {
+  const char *chain_id;
+  uint32_t chain_id_len;
+  const tmed_valset *vals;          /* use a key-set handle for the key-cached kernels */
+  size_t n_blocks;
+  const tmed_block_id *block_ids;   /* firstID of each block */
+  const int64_t *heights;           /* first.Height */
+  const tmed_commit *commits;       /* second.LastCommit */
+} tmed_blocksync_window;
+
+/*
+ * out[h] = the VerifyCommitLight outcome for block h — identical to tmed_verify_commits
+ * over TMED_MODE_LIGHT requests — computed speculatively for the whole window, so the
+ * caller applies blocks in order and stops at the first non-OK one (the reactor then
+ * redoes that request, reactor.go:368-388).  The window is processed in device batches
+ * of batch_blocks blocks (0 = 256) through a two-slot pipeline: while the device verifies
+ * batch b, the host plans and stages batch b+1 and replays batch b-1.
+ */
+int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t batch_blocks,
+                          tmed_commit_result *out);
+
 #ifdef __cplusplus
 }
 #endif

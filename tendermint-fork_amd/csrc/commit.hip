@@ -16,6 +16,7 @@
 //      exit, Got/Needed and error kinds come out identical by construction.
 #include <string.h>
 
+#include <algorithm>
 #include <functional>
 #include <memory>
 #include <thread>
@@ -183,145 +184,234 @@ static int build_cand_batch(const tmed_commit_request *reqs, size_t n, const std
   return cb.build_host_msgs();
 }
 
-static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, const BatchVerifier &verify) {
-  if (n && (!reqs || !out)) return TMED_EINVAL;
-  std::vector<Plan> plans(n);
-  std::vector<Cand> cands;
-  std::unordered_map<const tmed_valset *, std::unique_ptr<AddrIndex>> addr_cache;
+// ---- planning: prechecks + candidate selection, parallel over requests ----------------
+
+// Address indexes for every LightTrusting valset of the call (built once, read-only after).
+using AddrCache = std::unordered_map<const tmed_valset *, std::unique_ptr<AddrIndex>>;
+
+static void build_addr_cache(const tmed_commit_request *reqs, size_t n, AddrCache &cache) {
   for (size_t q = 0; q < n; q++) {
     const tmed_commit_request &r = reqs[q];
-    tmed_commit_result &o = out[q];
-    memset(&o, 0, sizeof o);
-    int rc = check_request(r);
-    if (rc != TMED_OK) return rc;
+    if (r.mode != TMED_MODE_LIGHT_TRUSTING || !r.vals) continue;
+    auto &slot = cache[r.vals];
+    if (slot) continue;
     const tmed_valset &vs = *r.vals;
-    const tmed_commit &c = *r.commit;
-    Plan &pl = plans[q];
-    pl.bit_of_sig.assign(c.n_sigs, -1);
-    if (r.mode != TMED_MODE_LIGHT_TRUSTING) {
-      if (vs.n != c.n_sigs) {
-        o.code = TMED_COMMIT_WRONG_SET_SIZE; o.expected = (int64_t)vs.n; o.actual = (int64_t)c.n_sigs;
-        pl.decided = true; continue;
-      }
-      if (r.height != c.height) {
-        o.code = TMED_COMMIT_WRONG_HEIGHT; o.expected = r.height; o.actual = c.height;
-        pl.decided = true; continue;
-      }
-      if (!block_id_equal(*r.block_id, c.block_id)) {
-        o.code = TMED_COMMIT_WRONG_BLOCK_ID; pl.decided = true; continue;
-      }
-      pl.needed = vs.total_power * 2 / 3;
-      if (r.mode == TMED_MODE_COMMIT) {
-        for (size_t i = 0; i < c.n_sigs; i++) {
-          const uint8_t f = c.flags[i];
-          if (f == kAbsent) continue;
-          if (f != kCommit && f != kNil) return TMED_EINVAL;  // CommitSig.BlockID panics (types/block.go:663)
-          pl.bit_of_sig[i] = (int32_t)cands.size();
-          cands.push_back({q, (int32_t)i, (int32_t)i});
-        }
-      } else {
-        int64_t tally = 0;
-        for (size_t i = 0; i < c.n_sigs; i++) {
-          if (c.flags[i] != kCommit) continue;
-          pl.bit_of_sig[i] = (int32_t)cands.size();
-          cands.push_back({q, (int32_t)i, (int32_t)i});
-          tally += vs.powers[i];
-          if (tally > pl.needed) break;
-        }
+    slot.reset(new AddrIndex());
+    slot->reserve(vs.n * 2);
+    for (size_t v = 0; v < vs.n; v++) slot->emplace(addr_key(vs.addresses + 20 * v), (int32_t)v);  // first wins
+  }
+}
+
+// Plan one request; candidates are appended to `cands` and bit_of_sig holds their index there.
+static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_result &o, Plan &pl,
+                        std::vector<Cand> &cands, const AddrCache &cache) {
+  const tmed_commit_request &r = reqs[q];
+  memset(&o, 0, sizeof o);
+  int rc = check_request(r);
+  if (rc != TMED_OK) return rc;
+  const tmed_valset &vs = *r.vals;
+  const tmed_commit &c = *r.commit;
+  pl.bit_of_sig.assign(c.n_sigs, -1);
+  if (r.mode != TMED_MODE_LIGHT_TRUSTING) {
+    if (vs.n != c.n_sigs) {
+      o.code = TMED_COMMIT_WRONG_SET_SIZE; o.expected = (int64_t)vs.n; o.actual = (int64_t)c.n_sigs;
+      pl.decided = true; return TMED_OK;
+    }
+    if (r.height != c.height) {
+      o.code = TMED_COMMIT_WRONG_HEIGHT; o.expected = r.height; o.actual = c.height;
+      pl.decided = true; return TMED_OK;
+    }
+    if (!block_id_equal(*r.block_id, c.block_id)) {
+      o.code = TMED_COMMIT_WRONG_BLOCK_ID; pl.decided = true; return TMED_OK;
+    }
+    pl.needed = vs.total_power * 2 / 3;
+    if (r.mode == TMED_MODE_COMMIT) {
+      for (size_t i = 0; i < c.n_sigs; i++) {
+        const uint8_t f = c.flags[i];
+        if (f == kAbsent) continue;
+        if (f != kCommit && f != kNil) return TMED_EINVAL;  // CommitSig.BlockID panics (types/block.go:663)
+        pl.bit_of_sig[i] = (int32_t)cands.size();
+        cands.push_back({q, (int32_t)i, (int32_t)i});
       }
     } else {
-      if (r.trust_den == 0) { o.code = TMED_COMMIT_ZERO_DENOMINATOR; pl.decided = true; continue; }
-      int64_t prod;
-      if (safe_mul(vs.total_power, r.trust_num, &prod)) { o.code = TMED_COMMIT_OVERFLOW; pl.decided = true; continue; }
-      pl.needed = prod / r.trust_den;  // Go int64 division truncates toward zero, as C++ does
-      auto &slot = addr_cache[r.vals];
-      if (!slot) {
-        slot.reset(new AddrIndex());
-        slot->reserve(vs.n * 2);
-        for (size_t v = 0; v < vs.n; v++) slot->emplace(addr_key(vs.addresses + 20 * v), (int32_t)v);  // first match wins
-      }
-      pl.addr_index = slot.get();
-      std::vector<int32_t> seen(vs.n, -1);
       int64_t tally = 0;
       for (size_t i = 0; i < c.n_sigs; i++) {
         if (c.flags[i] != kCommit) continue;
-        auto it = pl.addr_index->find(addr_key(c.addresses + 20 * i));
-        if (it == pl.addr_index->end()) continue;
-        const int32_t v = it->second;
-        if (seen[v] >= 0) break;  // the loop returns the double-vote error here
-        seen[v] = (int32_t)i;
         pl.bit_of_sig[i] = (int32_t)cands.size();
-        cands.push_back({q, (int32_t)i, v});
-        tally += vs.powers[v];
+        cands.push_back({q, (int32_t)i, (int32_t)i});
+        tally += vs.powers[i];
         if (tally > pl.needed) break;
       }
     }
+  } else {
+    if (r.trust_den == 0) { o.code = TMED_COMMIT_ZERO_DENOMINATOR; pl.decided = true; return TMED_OK; }
+    int64_t prod;
+    if (safe_mul(vs.total_power, r.trust_num, &prod)) { o.code = TMED_COMMIT_OVERFLOW; pl.decided = true; return TMED_OK; }
+    pl.needed = prod / r.trust_den;  // Go int64 division truncates toward zero, as C++ does
+    pl.addr_index = cache.at(r.vals).get();
+    std::vector<int32_t> seen(vs.n, -1);
+    int64_t tally = 0;
+    for (size_t i = 0; i < c.n_sigs; i++) {
+      if (c.flags[i] != kCommit) continue;
+      auto it = pl.addr_index->find(addr_key(c.addresses + 20 * i));
+      if (it == pl.addr_index->end()) continue;
+      const int32_t v = it->second;
+      if (seen[v] >= 0) break;  // the loop returns the double-vote error here
+      seen[v] = (int32_t)i;
+      pl.bit_of_sig[i] = (int32_t)cands.size();
+      cands.push_back({q, (int32_t)i, v});
+      tally += vs.powers[v];
+      if (tally > pl.needed) break;
+    }
   }
+  return TMED_OK;
+}
 
+// Worker count for host loops over `items` units of work (requests x signatures).
+static unsigned host_threads(size_t items) {
+  if (items < (1u << 16)) return 1;
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  return std::min(16u, hw);
+}
+
+template <class F>
+static void parallel_ranges(size_t n, unsigned nt, F &&f) {
+  if (nt <= 1 || n < 2) { f(0, n, 0u); return; }
+  if (nt > n) nt = (unsigned)n;
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; t++) th.emplace_back(f, n * t / nt, n * (t + 1) / nt, t);
+  for (auto &x : th) x.join();
+}
+
+static size_t total_sigs(const tmed_commit_request *reqs, size_t n) {
+  size_t s = 0;
+  for (size_t q = 0; q < n; q++) s += reqs[q].commit ? reqs[q].commit->n_sigs : 0;
+  return s;
+}
+
+// Candidates of requests [0, n) in request order (identical to a serial plan).
+static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, std::vector<Plan> &plans,
+                     std::vector<Cand> &cands, AddrCache &cache) {
+  plans.assign(n, Plan());
+  cands.clear();
+  for (size_t q = 0; q < n; q++)
+    if (check_request(reqs[q]) != TMED_OK) return TMED_EINVAL;
+  build_addr_cache(reqs, n, cache);
+  const unsigned nt = host_threads(total_sigs(reqs, n));
+  if (nt <= 1) {
+    for (size_t q = 0; q < n; q++) {
+      int rc = plan_request(reqs, q, out[q], plans[q], cands, cache);
+      if (rc != TMED_OK) return rc;
+    }
+    return TMED_OK;
+  }
+  std::vector<std::vector<Cand>> part(nt);
+  std::vector<size_t> lo_of(nt, 0), hi_of(nt, 0);
+  std::vector<int> rcs(nt, TMED_OK);
+  parallel_ranges(n, nt, [&](size_t lo, size_t hi, unsigned t) {
+    lo_of[t] = lo; hi_of[t] = hi;
+    for (size_t q = lo; q < hi && rcs[t] == TMED_OK; q++) rcs[t] = plan_request(reqs, q, out[q], plans[q], part[t], cache);
+  });
+  for (int rc : rcs)
+    if (rc != TMED_OK) return rc;
+  std::vector<size_t> base(nt + 1, 0);
+  for (unsigned t = 0; t < nt; t++) base[t + 1] = base[t] + part[t].size();
+  cands.resize(base[nt]);
+  parallel_ranges(nt, nt, [&](size_t lo, size_t hi, unsigned) {
+    for (size_t t = lo; t < hi; t++) {
+      std::copy(part[t].begin(), part[t].end(), cands.begin() + base[t]);
+      if (base[t])
+        for (size_t q = lo_of[t]; q < hi_of[t]; q++)
+          for (int32_t &k : plans[q].bit_of_sig)
+            if (k >= 0) k += (int32_t)base[t];
+    }
+  });
+  return TMED_OK;
+}
+
+// ---- replay of every reference loop over the validity bits (parallel over requests) ----
+
+static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, const Plan &pl, const uint8_t *valid) {
+  const tmed_valset &vs = *r.vals;
+  const tmed_commit &c = *r.commit;
+  auto bit = [&](size_t i, bool *ok) -> bool {
+    const int32_t k = pl.bit_of_sig[i];
+    if (k < 0) { *ok = false; return false; }
+    o.verified++;
+    return valid[(size_t)k] != 0;
+  };
+  bool ok = true;
+  int64_t tally = 0;
+  o.code = -1;
+  if (r.mode == TMED_MODE_COMMIT) {
+    for (size_t i = 0; i < c.n_sigs && o.code < 0; i++) {
+      if (c.flags[i] == kAbsent) continue;
+      if (!bit(i, &ok)) { if (ok) { o.code = TMED_COMMIT_WRONG_SIGNATURE; o.idx = (int32_t)i; } break; }
+      if (c.flags[i] == kCommit) tally += vs.powers[i];
+    }
+    if (o.code < 0 && ok) {
+      if (tally <= pl.needed) { o.code = TMED_COMMIT_NOT_ENOUGH_POWER; o.got = tally; o.needed = pl.needed; }
+      else o.code = TMED_COMMIT_OK;
+    }
+  } else if (r.mode == TMED_MODE_LIGHT) {
+    for (size_t i = 0; i < c.n_sigs && o.code < 0; i++) {
+      if (c.flags[i] != kCommit) continue;
+      if (!bit(i, &ok)) { if (ok) { o.code = TMED_COMMIT_WRONG_SIGNATURE; o.idx = (int32_t)i; } break; }
+      tally += vs.powers[i];
+      if (tally > pl.needed) o.code = TMED_COMMIT_OK;
+    }
+    if (o.code < 0 && ok) { o.code = TMED_COMMIT_NOT_ENOUGH_POWER; o.got = tally; o.needed = pl.needed; }
+  } else {
+    std::vector<int32_t> seen(vs.n, -1);
+    for (size_t i = 0; i < c.n_sigs && o.code < 0; i++) {
+      if (c.flags[i] != kCommit) continue;
+      auto it = pl.addr_index->find(addr_key(c.addresses + 20 * i));
+      if (it == pl.addr_index->end()) continue;
+      const int32_t v = it->second;
+      if (seen[v] >= 0) {
+        o.code = TMED_COMMIT_DOUBLE_VOTE; o.val_idx = v; o.idx_first = seen[v]; o.idx = (int32_t)i;
+        break;
+      }
+      seen[v] = (int32_t)i;
+      if (!bit(i, &ok)) { if (ok) { o.code = TMED_COMMIT_WRONG_SIGNATURE; o.idx = (int32_t)i; } break; }
+      tally += vs.powers[v];
+      if (tally > pl.needed) o.code = TMED_COMMIT_OK;
+    }
+    if (o.code < 0 && ok) { o.code = TMED_COMMIT_NOT_ENOUGH_POWER; o.got = tally; o.needed = pl.needed; }
+  }
+  return ok ? TMED_OK : TMED_EINVAL;  // replay reached a signature the plan did not send (cannot happen)
+}
+
+static int seam_replay(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out,
+                       const std::vector<Plan> &plans, const uint8_t *valid) {
+  const unsigned nt = host_threads(total_sigs(reqs, n));
+  std::vector<int> rcs(std::max(1u, nt), TMED_OK);
+  parallel_ranges(n, nt, [&](size_t lo, size_t hi, unsigned t) {
+    for (size_t q = lo; q < hi; q++) {
+      if (plans[q].decided) continue;
+      if (replay_request(reqs[q], out[q], plans[q], valid) != TMED_OK) rcs[t] = TMED_EINVAL;
+    }
+  });
+  for (int rc : rcs)
+    if (rc != TMED_OK) return rc;
+  return TMED_OK;
+}
+
+static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, const BatchVerifier &verify) {
+  if (n && (!reqs || !out)) return TMED_EINVAL;
+  std::vector<Plan> plans;
+  std::vector<Cand> cands;
+  AddrCache cache;
+  int rc = seam_plan(reqs, n, out, plans, cands, cache);
+  if (rc != TMED_OK) return rc;
   // ---- one device batch for every candidate of every request
   const size_t m = cands.size();
   std::vector<uint8_t> valid(m, 0);
   if (m) {
-    int rc = verify(reqs, n, cands, valid.data());
+    rc = verify(reqs, n, cands, valid.data());
     if (rc != TMED_OK) return rc;
   }
-
-  // ---- replay every reference loop over the bits
-  for (size_t q = 0; q < n; q++) {
-    Plan &pl = plans[q];
-    if (pl.decided) continue;
-    const tmed_commit_request &r = reqs[q];
-    const tmed_valset &vs = *r.vals;
-    const tmed_commit &c = *r.commit;
-    tmed_commit_result &o = out[q];
-    auto bit = [&](size_t i, bool *ok) -> bool {
-      const int32_t k = pl.bit_of_sig[i];
-      if (k < 0) { *ok = false; return false; }
-      o.verified++;
-      return valid[(size_t)k] != 0;
-    };
-    bool ok = true;
-    int64_t tally = 0;
-    o.code = -1;
-    if (r.mode == TMED_MODE_COMMIT) {
-      for (size_t i = 0; i < c.n_sigs && o.code < 0; i++) {
-        if (c.flags[i] == kAbsent) continue;
-        if (!bit(i, &ok)) { if (ok) { o.code = TMED_COMMIT_WRONG_SIGNATURE; o.idx = (int32_t)i; } break; }
-        if (c.flags[i] == kCommit) tally += vs.powers[i];
-      }
-      if (o.code < 0 && ok) {
-        if (tally <= pl.needed) { o.code = TMED_COMMIT_NOT_ENOUGH_POWER; o.got = tally; o.needed = pl.needed; }
-        else o.code = TMED_COMMIT_OK;
-      }
-    } else if (r.mode == TMED_MODE_LIGHT) {
-      for (size_t i = 0; i < c.n_sigs && o.code < 0; i++) {
-        if (c.flags[i] != kCommit) continue;
-        if (!bit(i, &ok)) { if (ok) { o.code = TMED_COMMIT_WRONG_SIGNATURE; o.idx = (int32_t)i; } break; }
-        tally += vs.powers[i];
-        if (tally > pl.needed) o.code = TMED_COMMIT_OK;
-      }
-      if (o.code < 0 && ok) { o.code = TMED_COMMIT_NOT_ENOUGH_POWER; o.got = tally; o.needed = pl.needed; }
-    } else {
-      std::vector<int32_t> seen(vs.n, -1);
-      for (size_t i = 0; i < c.n_sigs && o.code < 0; i++) {
-        if (c.flags[i] != kCommit) continue;
-        auto it = pl.addr_index->find(addr_key(c.addresses + 20 * i));
-        if (it == pl.addr_index->end()) continue;
-        const int32_t v = it->second;
-        if (seen[v] >= 0) {
-          o.code = TMED_COMMIT_DOUBLE_VOTE; o.val_idx = v; o.idx_first = seen[v]; o.idx = (int32_t)i;
-          break;
-        }
-        seen[v] = (int32_t)i;
-        if (!bit(i, &ok)) { if (ok) { o.code = TMED_COMMIT_WRONG_SIGNATURE; o.idx = (int32_t)i; } break; }
-        tally += vs.powers[v];
-        if (tally > pl.needed) o.code = TMED_COMMIT_OK;
-      }
-      if (o.code < 0 && ok) { o.code = TMED_COMMIT_NOT_ENOUGH_POWER; o.got = tally; o.needed = pl.needed; }
-    }
-    if (!ok) return TMED_EINVAL;  // replay reached a signature the plan did not send (cannot happen)
-  }
-  return TMED_OK;
+  return seam_replay(reqs, n, out, plans, valid.data());
 }
 
 extern "C" int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out,
@@ -376,21 +466,79 @@ static int ctx_verify_host_msgs(tmed_ctx *ctx, const tmed_commit_request *reqs, 
   return TMED_OK;
 }
 
-// GPU verifier: sign-bytes are assembled on the device from per-commit templates
-// (SURVEY.md §8f f1), so only key references, signatures, flags and timestamps cross
-// PCIe; they are written straight from the request arrays into the pinned staging area
-// (multi-threaded for large batches).  Candidates of validator sets with a key-set handle
-// go through the key-cached kernels, one launch sequence per distinct key set.
-static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands,
-                      uint8_t *valid) {
+// Device staging of the candidates ix[...] (all of one key set) into vote slot `slot`:
+// sign-bytes are assembled on the device from per-commit templates, so
+// only key references, signatures, flags and timestamps cross PCIe; they are written
+// straight from the request arrays into the pinned staging area (multi-threaded for
+// large batches).  The caller holds ctx->mu.
+static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands,
+                       const uint32_t *ix, uint32_t m, uint64_t keyset, const uint8_t *tmpl, int slot,
+                       tmed::VoteStage &st) {
+  const bool keyed = keyset != 0;
+  int rc = tmed::votes_stage(ctx, keyset, m, n, st, slot);
+  if (rc != TMED_OK) return rc;
+  memcpy(st.tmpl, tmpl, n * tmed::kVoteTmplBytes);
+  auto fill = [&](size_t lo, size_t hi, unsigned) {
+    for (size_t j = lo; j < hi; j++) {
+      const Cand &cd = cands[ix ? ix[j] : j];
+      const tmed_commit_request &r = reqs[cd.req];
+      const tmed_commit &c = *r.commit;
+      const size_t i = (size_t)cd.sig_idx;
+      if (keyed) {
+        const uint32_t v = r.vals->keyset_index ? r.vals->keyset_index[cd.val_idx] : (uint32_t)cd.val_idx;
+        memcpy(st.key + j * 4, &v, 4);
+      } else {
+        memcpy(st.key + j * 32, r.vals->pubkeys + 32 * (size_t)cd.val_idx, 32);
+      }
+      const uint32_t sl = c.sig_lens ? c.sig_lens[i] : 64;
+      uint8_t *sd = st.sig + j * 64;
+      if (sl >= 64) memcpy(sd, c.sigs + 64 * i, 64);
+      else { memset(sd, 0, 64); memcpy(sd, c.sigs + 64 * i, sl); }
+      st.tidx[j] = (uint32_t)cd.req;
+      st.flag[j] = c.flags[i];
+      st.sec[j] = c.ts_seconds[i];
+      st.nan[j] = c.ts_nanos[i];
+    }
+  };
+  parallel_ranges(m, host_threads(m), fill);
+  return TMED_OK;
+}
+
+// Collected bits -> valid[] (signatures of length != 64 are false: ed25519.go:150-152).
+static void scatter_bits(const tmed_commit_request *reqs, const std::vector<Cand> &cands, const uint32_t *ix,
+                         uint32_t m, const uint8_t *bits, uint8_t *valid) {
+  for (uint32_t j = 0; j < m; j++) {
+    const uint32_t k = ix ? ix[j] : j;
+    const Cand &cd = cands[k];
+    const tmed_commit &c = *reqs[cd.req].commit;
+    const uint32_t sl = c.sig_lens ? c.sig_lens[cd.sig_idx] : 64;
+    valid[k] = sl == 64 ? bits[j] : 0;
+  }
+}
+
+// Device templates of the requests that have candidates; false if one does not fit.
+static int device_templates(const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands,
+                            std::vector<uint8_t> &tmpl, bool *fits) {
   std::vector<tmed::VoteEncoder> enc;
   std::vector<uint8_t> used;
   int rc = init_encoders(reqs, n, cands, enc, used);
   if (rc != TMED_OK) return rc;
-  std::vector<uint8_t> tmpl(n * tmed::kVoteTmplBytes);
+  tmpl.assign(n * tmed::kVoteTmplBytes, 0);
+  *fits = true;
   for (size_t q = 0; q < n; q++)
-    if (used[q] && !enc[q].device_template(&tmpl[q * tmed::kVoteTmplBytes], tmed::kVoteTmplBytes))
-      return ctx_verify_host_msgs(ctx, reqs, n, cands, valid);
+    if (used[q] && !enc[q].device_template(&tmpl[q * tmed::kVoteTmplBytes], tmed::kVoteTmplBytes)) *fits = false;
+  return TMED_OK;
+}
+
+// GPU verifier of one seam call: candidates of validator sets with a key-set handle go
+// through the key-cached kernels, one launch sequence per distinct key set.
+static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands,
+                      uint8_t *valid) {
+  std::vector<uint8_t> tmpl;
+  bool fits = true;
+  int rc = device_templates(reqs, n, cands, tmpl, &fits);
+  if (rc != TMED_OK) return rc;
+  if (!fits) return ctx_verify_host_msgs(ctx, reqs, n, cands, valid);
   // group by key set (usually a single group)
   std::vector<uint64_t> gkeys;
   std::vector<std::vector<uint32_t>> gidx;
@@ -401,54 +549,16 @@ static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, 
     if (g == gkeys.size()) { gkeys.push_back(ks); gidx.emplace_back(); }
     gidx[g].push_back((uint32_t)k);
   }
+  std::lock_guard<std::mutex> lk(ctx->mu);
   for (size_t g = 0; g < gkeys.size(); g++) {
     const std::vector<uint32_t> &ix = gidx[g];
     const uint32_t m = (uint32_t)ix.size();
-    const bool keyed = gkeys[g] != 0;
     tmed::VoteStage st;
-    rc = tmed::votes_stage(ctx, gkeys[g], m, n, st);
-    if (rc != TMED_OK) return rc;
-    memcpy(st.tmpl, tmpl.data(), tmpl.size());
-    auto fill = [&](uint32_t lo, uint32_t hi) {
-      for (uint32_t j = lo; j < hi; j++) {
-        const Cand &cd = cands[ix[j]];
-        const tmed_commit_request &r = reqs[cd.req];
-        const tmed_commit &c = *r.commit;
-        const size_t i = (size_t)cd.sig_idx;
-        if (keyed) {
-          const uint32_t v = r.vals->keyset_index ? r.vals->keyset_index[cd.val_idx] : (uint32_t)cd.val_idx;
-          memcpy(st.key + (size_t)j * 4, &v, 4);
-        } else {
-          memcpy(st.key + (size_t)j * 32, r.vals->pubkeys + 32 * (size_t)cd.val_idx, 32);
-        }
-        const uint32_t sl = c.sig_lens ? c.sig_lens[i] : 64;
-        uint8_t *sd = st.sig + (size_t)j * 64;
-        if (sl >= 64) memcpy(sd, c.sigs + 64 * i, 64);
-        else { memset(sd, 0, 64); memcpy(sd, c.sigs + 64 * i, sl); }
-        st.tidx[j] = (uint32_t)cd.req;
-        st.flag[j] = c.flags[i];
-        st.sec[j] = c.ts_seconds[i];
-        st.nan[j] = c.ts_nanos[i];
-      }
-    };
-    const uint32_t nthreads = m >= 65536 ? std::min<uint32_t>(16, std::max(1u, std::thread::hardware_concurrency())) : 1;
-    if (nthreads > 1) {
-      std::vector<std::thread> th;
-      for (uint32_t t = 0; t < nthreads; t++)
-        th.emplace_back(fill, (uint32_t)((uint64_t)m * t / nthreads), (uint32_t)((uint64_t)m * (t + 1) / nthreads));
-      for (auto &x : th) x.join();
-    } else {
-      fill(0, m);
-    }
+    rc = stage_group(ctx, reqs, n, cands, ix.data(), m, gkeys[g], tmpl.data(), 0, st);
     std::vector<uint8_t> out(m);
-    rc = tmed::votes_launch(ctx, st, out.data());
+    if (rc == TMED_OK) rc = tmed::votes_launch(ctx, st, out.data());
     if (rc != TMED_OK) return rc;
-    for (uint32_t j = 0; j < m; j++) {
-      const Cand &cd = cands[ix[j]];
-      const tmed_commit &c = *reqs[cd.req].commit;
-      const uint32_t sl = c.sig_lens ? c.sig_lens[cd.sig_idx] : 64;
-      valid[ix[j]] = sl == 64 ? out[j] : 0;  // crypto/ed25519/ed25519.go:150-152
-    }
+    scatter_bits(reqs, cands, ix.data(), m, out.data(), valid);
   }
   return TMED_OK;
 }
@@ -460,4 +570,86 @@ extern "C" int tmed_verify_commits(tmed_ctx *ctx, const tmed_commit_request *req
                   [&](const tmed_commit_request *rq, size_t nr, const std::vector<Cand> &cands, uint8_t *valid) {
                     return ctx_verify(ctx, rq, nr, cands, valid);
                   });
+}
+
+// ---- blocksync replay window (f4): pipelined LIGHT batches --------------------------------
+namespace {
+struct BsBatch {
+  size_t lo = 0, n = 0;
+  std::vector<Plan> plans;
+  std::vector<Cand> cands;
+  AddrCache cache;
+  std::vector<uint8_t> tmpl, bits, valid;
+  tmed::VoteStage st;
+  bool device = false;  // queued on a vote slot (else verified synchronously / nothing to verify)
+};
+}  // namespace
+
+extern "C" int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t batch_blocks,
+                                     tmed_commit_result *out) {
+  if (!ctx || !w || (w->n_blocks && (!w->vals || !w->block_ids || !w->heights || !w->commits || !out)))
+    return TMED_EINVAL;
+  const size_t nb = w->n_blocks;
+  if (nb == 0) return TMED_OK;
+  const size_t bsz = batch_blocks ? batch_blocks : 256;
+  std::vector<tmed_commit_request> reqs(nb);
+  for (size_t h = 0; h < nb; h++) {
+    tmed_commit_request &r = reqs[h];
+    memset(&r, 0, sizeof r);
+    r.mode = TMED_MODE_LIGHT;
+    r.chain_id = w->chain_id;
+    r.chain_id_len = w->chain_id_len;
+    r.vals = w->vals;
+    r.block_id = &w->block_ids[h];
+    r.height = w->heights[h];
+    r.commit = &w->commits[h];
+  }
+  const uint64_t keyset = w->vals->keyset;
+  BsBatch slots[2];
+  int rc = TMED_OK;
+  auto finish = [&](BsBatch &b) -> int {
+    if (b.n == 0) return TMED_OK;
+    const size_t m = b.cands.size();
+    if (b.device) {
+      b.bits.resize(m);
+      int r = tmed::votes_collect(ctx, b.st, b.bits.data());
+      if (r != TMED_OK) return r;
+      scatter_bits(reqs.data() + b.lo, b.cands, nullptr, (uint32_t)m, b.bits.data(), b.valid.data());
+    }
+    int r = seam_replay(reqs.data() + b.lo, b.n, out + b.lo, b.plans, b.valid.data());
+    b.n = 0;
+    b.device = false;
+    return r;
+  };
+  std::unique_lock<std::mutex> lk(ctx->mu);
+  size_t idx = 0;
+  for (size_t lo = 0; lo < nb && rc == TMED_OK; lo += bsz, idx++) {
+    BsBatch &b = slots[idx & 1];
+    BsBatch &prev = slots[(idx + 1) & 1];
+    b.lo = lo;
+    b.n = std::min(bsz, nb - lo);
+    const tmed_commit_request *rq = reqs.data() + lo;
+    rc = seam_plan(rq, b.n, out + lo, b.plans, b.cands, b.cache);
+    const size_t m = b.cands.size();
+    b.valid.assign(m, 0);
+    bool fits = true;
+    if (rc == TMED_OK && m) rc = device_templates(rq, b.n, b.cands, b.tmpl, &fits);
+    if (rc == TMED_OK && m) {
+      if (fits && m <= 0xffffffffu) {
+        rc = stage_group(ctx, rq, b.n, b.cands, nullptr, (uint32_t)m, keyset, b.tmpl.data(), (int)(idx & 1), b.st);
+        if (rc == TMED_OK) rc = tmed::votes_enqueue(ctx, b.st);
+        b.device = rc == TMED_OK;
+      } else {  // oversize template: host-assembled messages, synchronous (drain the pipeline first)
+        rc = finish(prev);
+        lk.unlock();
+        if (rc == TMED_OK) rc = ctx_verify_host_msgs(ctx, rq, b.n, b.cands, b.valid.data());
+        lk.lock();
+      }
+    }
+    if (rc == TMED_OK) rc = finish(prev);  // overlaps the device work of batch b
+  }
+  for (BsBatch &b : slots)
+    if (rc == TMED_OK) rc = finish(b);
+  if (rc != TMED_OK) (void)hipStreamSynchronize(ctx->stream);
+  return rc;
 }

@@ -75,11 +75,14 @@ int verify_votes_device(tmed_ctx *c, uint64_t keyset, const uint8_t *keys, const
                         const uint8_t *tmpl, size_t n_tmpl, const uint32_t *tmpl_idx, const uint8_t *flags,
                         const int64_t *ts_sec, const int32_t *ts_nanos, uint32_t m, uint8_t *out);
 
-// Zero-copy form of the same: votes_stage() locks the context and returns pointers into
-// the pinned staging area; the caller fills them; votes_launch() copies, runs and
-// unlocks.  (The seam fills the staging area straight from the request arrays.)
+// Zero-copy form of the same: votes_stage() returns pointers into the pinned staging area
+// of one of the context's two vote slots; the caller fills them; votes_enqueue() queues
+// copy-in, assembly, verification and copy-out on the context stream; votes_collect()
+// waits for that slot and returns the bits.  votes_launch() = enqueue + collect.  Two
+// slots let a pipelined caller (tmed_blocksync_verify) stage batch b+1 on the host while
+// the device runs batch b.  The caller holds ctx->mu across stage..collect.
 struct VoteStage {
-  std::unique_lock<std::mutex> lock;
+  int slot = 0;
   const Keyset *ks = nullptr;
   uint32_t m = 0;
   size_t n_tmpl = 0, total = 0;
@@ -89,10 +92,21 @@ struct VoteStage {
   int64_t *sec = nullptr;
   int32_t *nan = nullptr;
 };
-int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st);
+int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st, int slot = 0);
+int votes_enqueue(tmed_ctx *c, VoteStage &st);
+int votes_collect(tmed_ctx *c, const VoteStage &st, uint8_t *out);
 int votes_launch(tmed_ctx *c, VoteStage &st, uint8_t *out);
 void free_keyset(Keyset &k);
 
+}  // namespace tmed
+
+namespace tmed {
+struct VoteSlot {
+  DevBuf d_votes, d_vmsg, d_off, d_out;
+  HostBuf h_votes, h_out;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the device work of the slot's last batch
+  hipEvent_t done = nullptr;                // after its copy-out
+};
 }  // namespace tmed
 
 struct tmed_ctx {
@@ -112,8 +126,9 @@ struct tmed_ctx {
   int main_waves = 2;     // register budget variant of the main kernel; env TMED_MAIN_WAVES
   bool timing = false;    // tmed_set_kernel_timing
   tmed::KernelTimer timer;
-  tmed::DevBuf d_a, d_b, d_msg, d_off, d_out, d_c, d_votes, d_vmsg;
-  tmed::HostBuf h_a, h_b, h_msg, h_off, h_out, h_c, h_votes;
+  tmed::DevBuf d_a, d_b, d_msg, d_off, d_out, d_c;
+  tmed::HostBuf h_a, h_b, h_msg, h_off, h_out, h_c;
+  tmed::VoteSlot vslot[2];
   std::unordered_map<uint64_t, tmed::Keyset> keysets;
   uint64_t next_keyset = 1;
 };

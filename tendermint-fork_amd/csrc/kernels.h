@@ -43,9 +43,9 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
                          int4 *prep, int4 *fin, int4 *fin_pre, hipStream_t stream, uint32_t chunk = 0,
                          int main_waves = 2, bool msg_slots = false, KernelTimer *timer = nullptr);
 
+// RFC 8032 signer (synthetic commits) on the shared comb of B.
 hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t *off, uint32_t n, uint8_t *sig_out,
-                       uint8_t *pub_out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
-                       hipStream_t stream);
+                       uint8_t *pub_out, const int4 *bcomb, hipStream_t stream);
 
 // Shared fixed-base table j*B, j = 0..128 (niels), staged in LDS by the kernels.
 constexpr int kBTabSize = 129;

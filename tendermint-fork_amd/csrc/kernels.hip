@@ -312,20 +312,20 @@ hipError_t launch_finish(const int4 *fin, int4 *pre, const uint8_t *sig, uint8_t
   return hipGetLastError();
 }
 
+struct GlobalComb;  // defined with the key-set kernels below
+__device__ void comb_sign_one(uint32_t sg[16], uint32_t pb[8], const uint32_t seed[8], const uint8_t *m,
+                              uint32_t mlen, const int4 *bcomb);
+
+// RFC 8032 signer for synthetic commits: [a]B and [r]B from the shared comb of B.
 __global__ __launch_bounds__(kThreadsPerBlock) void sign_kernel(
     const uint8_t *__restrict__ seeds, const uint8_t *__restrict__ msgs, const uint32_t *__restrict__ off,
-    uint32_t n, uint8_t *__restrict__ sig_out, uint8_t *__restrict__ pub_out, int4 *__restrict__ slab,
-    uint32_t slab_stride, const ge_niels *__restrict__ btab_g) {
-  __shared__ ge_niels sbt[kBTabEntries];
-  stage_btab(sbt, btab_g);
+    uint32_t n, uint8_t *__restrict__ sig_out, uint8_t *__restrict__ pub_out, const int4 *__restrict__ bcomb) {
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
-  const LdsBTab bt{sbt};
   for (uint32_t i = gtid; i < n; i += gridDim.x * blockDim.x) {
     uint32_t seed[8], sg[16], pb[8];
     load_row_words(seed, seeds + 32 * (size_t)i, 2);
     const uint32_t o0 = off[i], o1 = off[i + 1];
-    SlabTab t{slab, slab_stride, gtid};
-    sign_one(sg, pb, seed, msgs + o0, o1 - o0, t, bt);
+    comb_sign_one(sg, pb, seed, msgs + o0, o1 - o0, bcomb);
     uint4 *so = reinterpret_cast<uint4 *>(sig_out + 64 * (size_t)i);
 #pragma unroll
     for (int q = 0; q < 4; q++) so[q] = make_uint4(sg[4 * q], sg[4 * q + 1], sg[4 * q + 2], sg[4 * q + 3]);
@@ -382,11 +382,10 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
 }
 
 hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t *off, uint32_t n, uint8_t *sig_out,
-                       uint8_t *pub_out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
-                       hipStream_t stream) {
-  const uint32_t grid = grid_for(n, slab_stride / kThreadsPerBlock);
+                       uint8_t *pub_out, const int4 *bcomb, hipStream_t stream) {
+  const uint32_t grid = grid_for(n, 4096);
   hipLaunchKernelGGL(sign_kernel, dim3(grid), dim3(kThreadsPerBlock), 0, stream, seeds, msgs, off, n, sig_out,
-                     pub_out, slab, slab_stride, btab);
+                     pub_out, bcomb);
   return hipGetLastError();
 }
 
@@ -473,6 +472,12 @@ struct GlobalComb {
     niels_load(e, base + ((size_t)w * kCombEntries + j) * kCombEntryInt4);
   }
 };
+
+__device__ void comb_sign_one(uint32_t sg[16], uint32_t pb[8], const uint32_t seed[8], const uint8_t *m,
+                              uint32_t mlen, const int4 *bcomb) {
+  const GlobalComb bc{bcomb};
+  sign_one_bm(sg, pb, seed, m, mlen, [&](uint32_t enc[8], const uint32_t s[8]) { comb_base_mult(enc, s, bc); });
+}
 
 __global__ __launch_bounds__(kThreadsPerBlock) void verify_keyset_prep_kernel(
     const uint32_t *__restrict__ val_idx, const uint8_t *__restrict__ key_pub, const uint8_t *__restrict__ key_ok,

@@ -34,8 +34,8 @@ void free_keyset(Keyset &k) {
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st) {
-  st.lock = std::unique_lock<std::mutex>(c->mu);
+int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st, int slot) {
+  st.slot = slot;
   st.m = m;
   st.n_tmpl = n_tmpl;
   st.ks = nullptr;
@@ -45,6 +45,7 @@ int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteSta
     st.ks = &it->second;
   }
   (void)hipSetDevice(c->device);
+  VoteSlot &vs = c->vslot[slot];
   const size_t key_bytes = keyset ? (size_t)m * 4 : (size_t)m * 32;
   st.o_key = 0;
   st.o_sig = align256(st.o_key + key_bytes);
@@ -54,14 +55,17 @@ int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteSta
   st.o_sec = align256(st.o_flag + m);
   st.o_nan = align256(st.o_sec + (size_t)m * 8);
   st.total = align256(st.o_nan + (size_t)m * 4);
-  hipError_t e = c->d_votes.ensure(st.total);
-  if (e == hipSuccess) e = c->h_votes.ensure(st.total);
-  if (e == hipSuccess) e = c->d_vmsg.ensure((size_t)m * kVoteSlot);
-  if (e == hipSuccess) e = c->d_off.ensure((size_t)m * 4);
-  if (e == hipSuccess) e = c->d_out.ensure(m);
-  if (e == hipSuccess) e = c->h_out.ensure(m);
+  hipError_t e = vs.d_votes.ensure(st.total);
+  if (e == hipSuccess) e = vs.h_votes.ensure(st.total);
+  if (e == hipSuccess) e = vs.d_vmsg.ensure((size_t)m * kVoteSlot);
+  if (e == hipSuccess) e = vs.d_off.ensure((size_t)m * 4);
+  if (e == hipSuccess) e = vs.d_out.ensure(m);
+  if (e == hipSuccess) e = vs.h_out.ensure(m);
+  if (e == hipSuccess && !vs.ev0) e = hipEventCreate(&vs.ev0);
+  if (e == hipSuccess && !vs.ev1) e = hipEventCreate(&vs.ev1);
+  if (e == hipSuccess && !vs.done) e = hipEventCreateWithFlags(&vs.done, hipEventDisableTiming);
   if (e != hipSuccess) return map_err(e);
-  uint8_t *h = (uint8_t *)c->h_votes.p;
+  uint8_t *h = (uint8_t *)vs.h_votes.p;
   st.key = h + st.o_key;
   st.sig = h + st.o_sig;
   st.tmpl = h + st.o_tmpl;
@@ -72,44 +76,57 @@ int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteSta
   return TMED_OK;
 }
 
-int votes_launch(tmed_ctx *c, VoteStage &st, uint8_t *out) {
+int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   const uint32_t m = st.m;
   if (st.ks)
     for (uint32_t j = 0; j < m; j++)
       if (((const uint32_t *)st.key)[j] >= st.ks->n) return TMED_EINVAL;
-  uint8_t *d = (uint8_t *)c->d_votes.p;
+  VoteSlot &vs = c->vslot[st.slot];
+  uint8_t *d = (uint8_t *)vs.d_votes.p;
   hipStream_t s = c->stream;
-  hipError_t e = hipMemcpyAsync(d, c->h_votes.p, st.total, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipEventRecord(c->ev0, s);
+  hipError_t e = hipMemcpyAsync(d, vs.h_votes.p, st.total, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipEventRecord(vs.ev0, s);
   if (e == hipSuccess)
     e = launch_assemble_votes(d + st.o_tmpl, (const uint32_t *)(d + st.o_tidx), d + st.o_flag,
                               (const int64_t *)(d + st.o_sec), (const int32_t *)(d + st.o_nan), m,
-                              (uint8_t *)c->d_vmsg.p, (uint32_t *)c->d_off.p, s);
+                              (uint8_t *)vs.d_vmsg.p, (uint32_t *)vs.d_off.p, s);
   if (e == hipSuccess) {
     if (st.ks)
       e = launch_verify_keyset((const uint32_t *)(d + st.o_key), st.ks->d_pub, st.ks->d_ok, st.ks->d_comb, c->d_bcomb,
-                               d + st.o_sig, (const uint8_t *)c->d_vmsg.p, (const uint32_t *)c->d_off.p, m,
-                               (uint8_t *)c->d_out.p, c->d_prep, c->slab_slots, c->d_fin, c->d_fin_pre, s,
+                               d + st.o_sig, (const uint8_t *)vs.d_vmsg.p, (const uint32_t *)vs.d_off.p, m,
+                               (uint8_t *)vs.d_out.p, c->d_prep, c->slab_slots, c->d_fin, c->d_fin_pre, s,
                                /*msg_slots=*/true);
     else
-      e = launch_verify(d + st.o_key, d + st.o_sig, (const uint8_t *)c->d_vmsg.p, (const uint32_t *)c->d_off.p, m,
-                        (uint8_t *)c->d_out.p, c->d_slab, c->slab_slots, c->d_btab, c->d_prep, c->d_fin,
-                        c->d_fin_pre, s, c->chunk,
-                        c->main_waves, /*msg_slots=*/true);
+      e = launch_verify(d + st.o_key, d + st.o_sig, (const uint8_t *)vs.d_vmsg.p, (const uint32_t *)vs.d_off.p, m,
+                        (uint8_t *)vs.d_out.p, c->d_slab, c->slab_slots, c->d_btab, c->d_prep, c->d_fin,
+                        c->d_fin_pre, s, c->chunk, c->main_waves, /*msg_slots=*/true);
   }
-  if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, m, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = hipEventRecord(vs.ev1, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(vs.h_out.p, vs.d_out.p, m, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipEventRecord(vs.done, s);
+  return map_err(e);
+}
+
+int votes_collect(tmed_ctx *c, const VoteStage &st, uint8_t *out) {
+  VoteSlot &vs = c->vslot[st.slot];
+  hipError_t e = hipEventSynchronize(vs.done);  // this slot only: a later batch may be queued behind it
   if (e != hipSuccess) return map_err(e);
-  (void)hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
-  memcpy(out, c->h_out.p, m);
+  (void)hipEventElapsedTime(&c->last_ms, vs.ev0, vs.ev1);
+  memcpy(out, vs.h_out.p, st.m);
   return TMED_OK;
+}
+
+int votes_launch(tmed_ctx *c, VoteStage &st, uint8_t *out) {
+  int rc = votes_enqueue(c, st);
+  if (rc == TMED_OK) rc = votes_collect(c, st, out);
+  return rc;
 }
 
 int verify_votes_device(tmed_ctx *c, uint64_t keyset, const uint8_t *keys, const uint8_t *sigs, const uint8_t *tmpl,
                         size_t n_tmpl, const uint32_t *tmpl_idx, const uint8_t *flags, const int64_t *ts_sec,
                         const int32_t *ts_nanos, uint32_t m, uint8_t *out) {
   if (m == 0) return TMED_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
   VoteStage st;
   int rc = votes_stage(c, keyset, m, n_tmpl, st);
   if (rc != TMED_OK) return rc;

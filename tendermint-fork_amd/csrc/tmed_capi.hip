@@ -94,8 +94,15 @@ void tmed_destroy(tmed_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
-  for (DevBuf *b : {&c->d_a, &c->d_b, &c->d_msg, &c->d_off, &c->d_out, &c->d_c, &c->d_votes, &c->d_vmsg}) b->release();
-  for (HostBuf *b : {&c->h_a, &c->h_b, &c->h_msg, &c->h_off, &c->h_out, &c->h_c, &c->h_votes}) b->release();
+  for (DevBuf *b : {&c->d_a, &c->d_b, &c->d_msg, &c->d_off, &c->d_out, &c->d_c}) b->release();
+  for (HostBuf *b : {&c->h_a, &c->h_b, &c->h_msg, &c->h_off, &c->h_out, &c->h_c}) b->release();
+  for (VoteSlot &v : c->vslot) {
+    for (DevBuf *b : {&v.d_votes, &v.d_vmsg, &v.d_off, &v.d_out}) b->release();
+    for (HostBuf *b : {&v.h_votes, &v.h_out}) b->release();
+    if (v.ev0) hipEventDestroy(v.ev0);
+    if (v.ev1) hipEventDestroy(v.ev1);
+    if (v.done) hipEventDestroy(v.done);
+  }
   for (auto &kv : c->keysets) free_keyset(kv.second);
   c->keysets.clear();
   if (c->d_bcomb) hipFree(c->d_bcomb);
@@ -162,8 +169,7 @@ int tmed_sign_batch_device(tmed_ctx *c, const uint8_t *d_seeds, const uint8_t *d
   if (!d_seeds || !d_msgs || !d_off || !d_sig_out || !d_pub_out || n > 0xffffffffu) return TMED_EINVAL;
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   hipSetDevice(c->device);
-  return map_err(launch_sign(d_seeds, d_msgs, d_off, (uint32_t)n, d_sig_out, d_pub_out, c->d_slab,
-                             c->slab_slots, c->d_btab, s));
+  return map_err(launch_sign(d_seeds, d_msgs, d_off, (uint32_t)n, d_sig_out, d_pub_out, c->d_bcomb, s));
 }
 
 static int check_offsets(const uint32_t *off, size_t n) {
@@ -244,7 +250,7 @@ int tmed_sign_batch(tmed_ctx *c, const uint8_t *seeds, const uint8_t *msgs, cons
   if (e == hipSuccess) e = hipEventRecord(c->ev0, s);
   if (e == hipSuccess)
     e = launch_sign((const uint8_t *)c->d_a.p, (const uint8_t *)c->d_msg.p, (const uint32_t *)c->d_off.p,
-                    (uint32_t)n, (uint8_t *)c->d_b.p, (uint8_t *)c->d_c.p, c->d_slab, c->slab_slots, c->d_btab, s);
+                    (uint32_t)n, (uint8_t *)c->d_b.p, (uint8_t *)c->d_c.p, c->d_bcomb, s);
   if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
   if (e == hipSuccess) e = hipMemcpyAsync(sigs_out, c->d_b.p, n * 64, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipMemcpyAsync(pubs_out, c->d_c.p, n * 32, hipMemcpyDeviceToHost, s);

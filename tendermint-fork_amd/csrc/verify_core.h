@@ -252,9 +252,10 @@ TMED_HD void scalarmult_base(uint32_t enc[8], const uint32_t s[8], T &tab, const
 // RFC 8032 signing (crypto/ed25519/ed25519.go:57-60 -> Go ed25519.Sign):
 //   h = SHA-512(seed); a = clamp(h[0:32]) mod L; A = [a]B;
 //   r = SHA-512(h[32:64] || M) mod L; R = [r]B; k = SHA-512(R || A || M) mod L; S = r + k a.
-template <class T, class BT>
-TMED_HD void sign_one(uint32_t sig[16], uint32_t pub[8], const uint32_t seed[8], const uint8_t *msg,
-                      uint32_t mlen, T &tab, const BT &btab) {
+// bm(enc, s) must write the canonical encoding of [s]B (s < L).
+template <class BM>
+TMED_HD void sign_one_bm(uint32_t sig[16], uint32_t pub[8], const uint32_t seed[8], const uint8_t *msg,
+                         uint32_t mlen, const BM &bm) {
   uint32_t h[16], zero[8], a[8], x[16], r[8], k[8], s[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) zero[i] = 0;
@@ -265,18 +266,27 @@ TMED_HD void sign_one(uint32_t sig[16], uint32_t pub[8], const uint32_t seed[8],
 #pragma unroll
   for (int i = 0; i < 16; i++) x[i] = i < 8 ? h[i] : 0u;
   sc_reduce512(a, x);
-  scalarmult_base(pub, a, tab, btab);
+  bm(pub, a);
   uint32_t prefix[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) prefix[i] = h[8 + i];
   sha512_stream(x, prefix, zero, 32, msg, mlen);
   sc_reduce512(r, x);
-  scalarmult_base(sig, r, tab, btab);
+  bm(sig, r);
   sha512_stream(x, sig, pub, 64, msg, mlen);
   sc_reduce512(k, x);
   sc_muladd(s, k, a, r);
 #pragma unroll
   for (int i = 0; i < 8; i++) sig[8 + i] = s[i];
+}
+
+// Signing with [s]B by the Straus schedule (k = 0) — the host test build's signer.
+template <class T, class BT>
+TMED_HD void sign_one(uint32_t sig[16], uint32_t pub[8], const uint32_t seed[8], const uint8_t *msg,
+                      uint32_t mlen, T &tab, const BT &btab) {
+  sign_one_bm(sig, pub, seed, msg, mlen, [&](uint32_t enc[8], const uint32_t s[8]) {
+    scalarmult_base(enc, s, tab, btab);
+  });
 }
 
 // ------------------------------------------------------------------ combs
@@ -375,6 +385,27 @@ TMED_HD void verify_main_comb_point(ge_p3 &acc, const uint32_t k[8], const uint3
       ge_p1p1_to_p3(acc, t);
     }
   }
+}
+
+// enc([s]B) from the shared signed radix-256 comb of B (32 mixed additions; the device
+// signer, which generates the synthetic commits of the benches).
+template <class BC>
+TMED_HD void comb_base_mult(uint32_t enc[8], const uint32_t s[8], const BC &bcomb) {
+  uint32_t sr[8];
+  sc_recode256(sr, s);
+  ge_p3 acc;
+  ge_p3_0(acc);
+  ge_p1p1 t;
+  ge_niels e;
+#pragma unroll 1
+  for (int w = 0; w < 32; w++) {
+    const int d = (int)((sr[w >> 2] >> (8 * (w & 3))) & 0xffu) - 128;
+    bcomb.load(w, d < 0 ? -d : d, e);
+    niels_apply_sign(e, d < 0);
+    ge_madd_niels(t, acc, e, false);
+    ge_p1p1_to_p3(acc, t);
+  }
+  ge_tobytes(enc, acc.X, acc.Y, acc.Z);
 }
 
 template <class AC, class BC>

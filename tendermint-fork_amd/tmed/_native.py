@@ -87,5 +87,5 @@ EXPORTED_SYMBOLS = [
     "tmed_sign_batch", "tmed_sign_batch_device", "tmed_last_kernel_ms",
     "tmed_vote_sign_bytes", "tmed_valu_peak", "tmed_verify_commits", "tmed_verify_commits_with",
     "tmed_keyset_load", "tmed_keyset_free", "tmed_verify_batch_keyset", "tmed_verify_batch_keyset_device",
-    "tmed_set_kernel_timing", "tmed_kernel_times",
+    "tmed_set_kernel_timing", "tmed_kernel_times", "tmed_blocksync_verify",
 ]

@@ -229,6 +229,12 @@ class _ResultC(ctypes.Structure):
                 ("idx_first", ctypes.c_int32), ("val_idx", ctypes.c_int32), ("verified", ctypes.c_uint32)]
 
 
+class _BlocksyncWindowC(ctypes.Structure):
+    _fields_ = [("chain_id", ctypes.c_char_p), ("chain_id_len", ctypes.c_uint32), ("vals", ctypes.POINTER(_ValsetC)),
+                ("n_blocks", ctypes.c_size_t), ("block_ids", ctypes.POINTER(_BlockIDC)),
+                ("heights", ctypes.c_void_p), ("commits", ctypes.POINTER(_CommitC))]
+
+
 VERIFY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
 
@@ -239,6 +245,9 @@ def _bind():
         l.tmed_verify_commits.restype = ctypes.c_int
         l.tmed_verify_commits.argtypes = [ctypes.c_void_p, ctypes.POINTER(_RequestC), ctypes.c_size_t,
                                           ctypes.POINTER(_ResultC)]
+        l.tmed_blocksync_verify.restype = ctypes.c_int
+        l.tmed_blocksync_verify.argtypes = [ctypes.c_void_p, ctypes.POINTER(_BlocksyncWindowC), ctypes.c_uint32,
+                                            ctypes.POINTER(_ResultC)]
         l.tmed_verify_commits_with.restype = ctypes.c_int
         l.tmed_verify_commits_with.argtypes = [ctypes.POINTER(_RequestC), ctypes.c_size_t,
                                                ctypes.POINTER(_ResultC), VERIFY_FN, ctypes.c_void_p]
@@ -401,3 +410,47 @@ def verify_commits(engine, requests: Sequence[tuple], verifier=None, stats: Opti
         if stats is not None:
             stats.append(int(res[q].verified))
     return out
+
+
+class BlocksyncWindow:
+    """A window of blocks for the blocksync reactor (f4; blockchain/v0/reactor.go:349-418):
+    block h is checked with vals.VerifyCommitLight(chain_id, block_ids[h], heights[h], commits[h]).
+    Packed into C structs once; run() verifies the whole window speculatively through the
+    pipelined device path (tmed_blocksync_verify) and returns the C results."""
+
+    def __init__(self, vals: "ValidatorSet", chain_id: str, block_ids: Sequence[BlockID], heights: Sequence[int],
+                 commits: Sequence):
+        n = len(commits)
+        self.n, self.vals, self.block_ids, self.commits = n, vals, list(block_ids), list(commits)
+        self.keep = []
+        pubs, powers, addrs = vals.packed()
+        kidx = getattr(vals, "keyset_index", None)
+        self.vs = _ValsetC(len(vals.validators), _ptr(pubs), _ptr(powers), _ptr(addrs), vals.total_voting_power(),
+                           getattr(vals, "keyset", 0) or 0, None if kidx is None else _ptr(kidx))
+        self.keep.extend([pubs, powers, addrs, kidx])
+        self.bids = (_BlockIDC * max(n, 1))()
+        self.ccs = (_CommitC * max(n, 1))()
+        for h in range(n):
+            self.bids[h] = _block_id_c(self.block_ids[h], self.keep)
+            self.ccs[h] = _commit_c(self.commits[h], self.keep)
+        self.heights = np.ascontiguousarray(np.asarray(heights, np.int64).reshape(max(n, 0)))
+        self.cid = chain_id.encode()
+        self.win = _BlocksyncWindowC(self.cid, len(self.cid), ctypes.pointer(self.vs), n, self.bids,
+                                     _ptr(self.heights), self.ccs)
+        self.res = (_ResultC * max(n, 1))()
+
+    def run(self, engine, batch_blocks: int = 0):
+        rc = _bind().tmed_blocksync_verify(engine._h, ctypes.byref(self.win), batch_blocks, self.res)
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_blocksync_verify")
+        return self.res
+
+    def codes(self):
+        return np.array([self.res[h].code for h in range(self.n)], np.int32)
+
+    def verified(self):
+        return np.array([self.res[h].verified for h in range(self.n)], np.int64)
+
+    def errors(self):
+        return [_to_error(self.res[h].code, self.res[h], self.vals, self.block_ids[h], self.commits[h])
+                for h in range(self.n)]

@@ -75,10 +75,13 @@ def make_valset(pubs: np.ndarray, powers):
     return vals, np.array([i for _, _, i in items], np.int64)
 
 
-def sign_commits(engine, chain_id: str, specs):
+def sign_commits(engine, chain_id: str, specs, sign_upto: int | None = None):
     """specs: list of (seeds_in_validator_order u8[n,32], addresses u8[n,20], height, round, BlockID,
     ts_base_seconds, flags or None).  All votes of all commits are signed in ONE GPU call.
-    Returns a list of PackedCommit (timestamps: base + i ms for validator i)."""
+    Returns a list of PackedCommit (timestamps: base + i ms for validator i).
+    sign_upto: only validators [0, sign_upto) sign; the others' signatures are filled with
+    seeded random bytes (present, flag Commit, invalid) — for workloads whose loop provably
+    stops before them (VerifyCommitLight at equal powers stops after 2n/3+1 signatures)."""
     from .types import PackedCommit
     flats, offs, seeds_all, metas = [], [], [], []
     base = 0
@@ -88,19 +91,24 @@ def sign_commits(engine, chain_id: str, specs):
         sec = np.full(n, ts0, np.int64) + (np.arange(n) // 1000)
         nan = ((np.arange(n) % 1000) * 1_000_000).astype(np.int32)
         fl = np.full(n, 2, np.uint8) if flags is None else np.asarray(flags, np.uint8)
-        f, o = vote_sign_bytes_batch(t, sec, nan, fl)
+        ns = n if sign_upto is None else min(n, sign_upto)
+        f, o = vote_sign_bytes_batch(t, sec[:ns], nan[:ns], fl[:ns])
         flats.append(f)
         offs.append(o[:-1].astype(np.int64) + base)
         base += int(o[-1])
-        seeds_all.append(seeds)
-        metas.append((height, round_, bid, addrs, sec, nan, fl))
+        seeds_all.append(seeds[:ns])
+        metas.append((height, round_, bid, addrs, sec, nan, fl, ns))
     flat = np.concatenate(flats) if flats else np.zeros(0, np.uint8)
     off = np.concatenate(offs + [np.array([base], np.int64)]).astype(np.uint32)
     sigs, _ = engine.sign_arrays(np.concatenate(seeds_all), np.concatenate([flat, np.zeros(16, np.uint8)]), off)
     out, k = [], 0
-    for (height, round_, bid, addrs, sec, nan, fl) in metas:
+    rng = np.random.default_rng(0x5EED)
+    for (height, round_, bid, addrs, sec, nan, fl, ns) in metas:
         n = sec.shape[0]
-        s = sigs[k:k + n].copy()
+        s = np.empty((n, 64), np.uint8)
+        s[:ns] = sigs[k:k + ns]
+        if ns < n:
+            s[ns:] = rng.integers(0, 256, (n - ns, 64), dtype=np.uint8)
         lens = np.full(n, 64, np.uint32)
         absent = fl == 1
         s[absent] = 0
@@ -108,5 +116,5 @@ def sign_commits(engine, chain_id: str, specs):
         a = addrs.copy()
         a[absent] = 0
         out.append(PackedCommit(height, round_, bid, fl, a, sec, nan, s, lens))
-        k += n
+        k += ns
     return out

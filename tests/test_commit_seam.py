@@ -44,3 +44,38 @@ def test_light_verifies_only_the_prefix():
                             verifier=oracle_verifier, stats=stats)
     assert errs == [None, None, None]
     assert stats == [21, 30, 11]  # > 2/3 of 300 after 21 sigs; all 30; > 1/3 after 11
+
+
+def test_parallel_plan_and_replay_equal_serial():
+    """Batches above 65,536 signatures are planned and replayed on host threads; the result
+    of every request must equal its result as a single (serial) call.  The verifier is a
+    deterministic stand-in (bit = low bit of sig[1]) so the test needs no signing."""
+    rng = np.random.default_rng(3)
+    n_vals, n_req = 150, 480
+    pubs = rng.integers(0, 256, (n_vals, 32), dtype=np.uint8)
+    vals = T.ValidatorSet([T.Validator(bytes(p), int(w), 0) for p, w in zip(pubs, rng.integers(1, 50, n_vals))])
+    addrs = np.array([np.frombuffer(v.address, np.uint8) for v in vals.validators])
+    reqs = []
+    for q in range(n_req):
+        flags = rng.choice(np.array([1, 2, 2, 2, 2, 3], np.uint8), n_vals)
+        sigs = rng.integers(0, 256, (n_vals, 64), dtype=np.uint8)
+        sigs[:, 1] |= (rng.random(n_vals) < 0.97).astype(np.uint8)  # ~3% invalid
+        bid = T.BlockID(bytes(rng.integers(0, 256, 32, dtype=np.uint8)), 3,
+                        bytes(rng.integers(0, 256, 32, dtype=np.uint8)))
+        ad = addrs.copy()
+        if q % 5 == 4:
+            ad[7] = ad[3]                                        # double vote for Trusting
+        pc = T.PackedCommit(10 + q, 0, bid, flags, ad, np.full(n_vals, 1700000000 + q, np.int64),
+                            np.zeros(n_vals, np.int32), sigs, np.full(n_vals, 64, np.uint32))
+        mode = q % 3
+        reqs.append((mode, vals, "par", bid if mode != 2 else None, 10 + q, pc, 1, 3))
+
+    def bitfn(pubs_, sigs_, lens, msgs, offs):
+        return (sigs_[:, 1] & 1).astype(np.uint8)
+
+    got = T.verify_commits(None, reqs, verifier=bitfn)
+    assert sum(int(reqs[q][5].flags.shape[0]) for q in range(n_req)) >= 65536
+    for q in range(0, n_req, 3):
+        one = T.verify_commits(None, [reqs[q]], verifier=bitfn)[0]
+        assert same(got[q], one), (q, got[q], one)
+    assert len({type(e).__name__ for e in got}) >= 2

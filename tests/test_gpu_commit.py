@@ -77,3 +77,53 @@ def test_keyset_seam_and_packed_commits(engine):
             assert same(g, e) and same(g2, e), (g, g2, e)
     finally:
         engine.keyset_free(ks)
+
+
+@pytest.mark.parametrize("batch", [1, 3, 256])
+@pytest.mark.parametrize("keyed", [False, True])
+def test_blocksync_window_matches_light_loops(engine, batch, keyed):
+    """tmed_blocksync_verify (f4: pipelined LIGHT batches over one validator set) gives the
+    reference VerifyCommitLight outcome for every block: valid commits, a bad signature
+    before and after the 2/3 crossing, wrong height, wrong BlockID, not enough power."""
+    import numpy as np
+    from oracle.fixtures import make_block_id, make_commit, make_valset, resign, seed_of
+    from commit_cases import to_product
+    vs, seeds = make_valset([seed_of("bs", i) for i in range(7)], [10] * 7)
+    blocks, exp, bids, heights = [], [], [], []
+    for h in range(11):
+        bid = make_block_id("bs%d" % h)
+        cm = make_commit(vs, seeds, "bs-chain", 50 + h, 0, bid)
+        want_h, want_bid = 50 + h, bid
+        if h == 2:
+            resign(cm, 0, seeds[0], "bad")          # before the crossing -> wrong signature (#0)
+        elif h == 3:
+            resign(cm, 6, seeds[6], "bad")          # after the crossing -> never verified, OK
+        elif h == 4:
+            want_h = 49                             # wrong height
+        elif h == 5:
+            want_bid = make_block_id("other")       # wrong block ID
+        elif h == 6:
+            for i in range(3, 7):                   # absent -> not enough power
+                cm.signatures[i].flag = 1
+                cm.signatures[i].signature = b""
+        exp.append(oracle_result(T.MODE_LIGHT, vs, "bs-chain", want_bid, want_h, cm, 0, 0))
+        _, pc = to_product(vs, cm)
+        blocks.append(pc)
+        bids.append(pbid(want_bid))
+        heights.append(want_h)
+    pv = to_product(vs, make_commit(vs, seeds, "bs-chain", 1, 0, make_block_id("x")))[0]
+    ks = 0
+    if keyed:
+        ks = engine.keyset_load(np.array([np.frombuffer(v.pub_key, np.uint8) for v in pv.validators]))
+        pv.keyset = ks
+    try:
+        w = T.BlocksyncWindow(pv, "bs-chain", bids, heights, blocks)
+        w.run(engine, batch)
+        for h, (g, e) in enumerate(zip(w.errors(), exp)):
+            assert same(g, e), (h, g, e)
+        ref = T.verify_commits(engine, [(T.MODE_LIGHT, pv, "bs-chain", b, hh, c, 0, 0)
+                                        for b, hh, c in zip(bids, heights, blocks)])
+        assert all(same(a, b) for a, b in zip(ref, w.errors()))
+    finally:
+        if ks:
+            engine.keyset_free(ks)

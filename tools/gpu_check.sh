@@ -31,8 +31,11 @@ for s in $STEPS; do
         echo "$cfg rc=$rc $(tail -1 $OUT/variant.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])' 2>/dev/null)" | tee -a $OUT/variants.txt
         if fatal $rc; then break; fi
       done ;;
+    keyset)
+      timeout -k 10 300 python bench_keyset.py > $OUT/bench_keyset.log 2>&1; rc=$?
+      echo "keyset rc=$rc"; grep '^{' $OUT/bench_keyset.log ;;
     commits)
-      timeout -k 10 900 python bench_commits.py --config c1,c3,c4 > $OUT/bench_commits.log 2>&1; rc=$?
+      timeout -k 10 900 python bench_commits.py --config ${COMMITS_CFG:-c1,c3,c4} ${COMMITS_ARGS:-} > $OUT/bench_commits.log 2>&1; rc=$?
       echo "commits rc=$rc"; grep '^{' $OUT/bench_commits.log ;;
     probe)
       timeout -k 10 300 python tools/probe_valu.py > $OUT/probe_valu.json 2>$OUT/probe_valu.err; rc=$?

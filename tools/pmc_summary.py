@@ -1,12 +1,21 @@
 #!/usr/bin/env python3
-"""Per-kernel average of every PMC counter in rocprofv3 counter-collection CSVs.
-Usage: pmc_summary.py DIR_OR_CSV... -> JSON {kernel: {counter: mean per dispatch, "dispatches": n}}"""
+"""Per-kernel summary of rocprofv3 --pmc counter-collection CSVs (one pass per counter set).
+
+Usage: pmc_summary.py OUT.json DIR_OR_CSV...
+For every kernel of interest: mean of each counter per dispatch, the mean grid size
+(= signatures per dispatch: one lane per signature), and HBM traffic per dispatch and per
+signature, corrected as /opt/skills/guides/MI355X_MICROARCH.md §HBM prescribes for gfx950:
+FETCH_SIZE (KB) reports half the bytes of wide coalesced reads -> x2; WRITE_SIZE (KB) is exact
+for 16-B stores.  bench.py reads the result (profiles/pmc_summary.json) for roofline.traffic."""
 import collections
 import csv
 import glob
 import json
 import os
 import sys
+
+KERNELS = ("verify_main_kernel", "verify_prep_kernel", "verify_finish_kernel", "verify_keyset_main_kernel",
+           "verify_keyset_prep_kernel", "sign_kernel", "merkle", "sha256")
 
 
 def files(args):
@@ -18,26 +27,44 @@ def files(args):
 
 
 def short(name):
-    for k in ("verify_main_kernel", "verify_prep_kernel", "verify_finish_kernel", "verify_keyset_main_kernel",
-              "verify_keyset_prep_kernel", "sign_kernel", "sha256", "merkle"):
+    for k in KERNELS:
         if k in name:
-            return k + (name[name.index("<"):name.index(">") + 1] if "<" in name and k == "verify_main_kernel" else "")
+            if k == "verify_main_kernel" and "<" in name:
+                return k + name[name.index("<"):name.index(">") + 1]
+            return k
     return None
 
 
 def main():
+    out_path, srcs = sys.argv[1], sys.argv[2:]
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
-    for f in files(sys.argv[1:]):
+    grid = collections.defaultdict(list)
+    for f in files(srcs):
         for r in csv.DictReader(open(f)):
             k = short(r["Kernel_Name"])
-            if k:
-                acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    out = {}
+            if not k:
+                continue
+            acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            grid[k].append(int(r["Grid_Size"]))
+    res = {}
     for k, cs in acc.items():
-        out[k] = {c: sum(v) / len(v) for c, v in cs.items()}
-        out[k]["dispatches"] = max(len(v) for v in cs.values())
-    json.dump(out, sys.stdout, indent=1)
-    print()
+        d = {c: sum(v) / len(v) for c, v in cs.items()}
+        d["dispatches"] = max(len(v) for v in cs.values())
+        d["grid_mean"] = sum(grid[k]) / len(grid[k])
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            fb = d["FETCH_SIZE"] * 1024 * 2   # gfx950: FETCH_SIZE counts half of wide reads
+            wb = d["WRITE_SIZE"] * 1024
+            d["hbm_bytes_per_dispatch"] = fb + wb
+            d["hbm_read_bytes_per_sig"] = fb / d["grid_mean"]
+            d["hbm_write_bytes_per_sig"] = wb / d["grid_mean"]
+            d["hbm_bytes_per_sig"] = (fb + wb) / d["grid_mean"]
+        if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d:
+            d["valu_insts_per_wave"] = d["SQ_INSTS_VALU"] / d["SQ_WAVES"]
+        res[k] = d
+    with open(out_path, "w") as fh:
+        json.dump(res, fh, indent=1, sort_keys=True)
+    for k, d in res.items():
+        print(k, {x: round(d[x], 1) for x in ("hbm_bytes_per_sig", "valu_insts_per_wave", "grid_mean") if x in d})
 
 
 if __name__ == "__main__":
