@@ -258,6 +258,58 @@ typedef int (*tmed_batch_verify_fn)(void *user, const uint8_t *pubkeys, const ui
 int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out,
                              tmed_batch_verify_fn verify, void *user);
 
+/* ------------------------------------------------ Merkle hashing (f3) */
+
+/*
+ * crypto/merkle.HashFromByteSlices (crypto/merkle/tree.go:9-22; RFC-6962 leaf 0x00 /
+ * inner 0x01 prefixes, crypto/merkle/hash.go:19-27) for n_trees trees at once: tree t's
+ * leaves are leaf indices [tree_off[t], tree_off[t+1]); leaf i is
+ * leaves[leaf_off[i] .. leaf_off[i+1]).  roots: n_trees x 32 bytes.  An empty tree's root is
+ * SHA-256("") as in the reference.  SHA-256 runs on the device (one lane per leaf, then one
+ * launch per tree level across all trees).
+ */
+int tmed_merkle_roots(tmed_ctx *ctx, const uint8_t *leaves, const uint64_t *leaf_off, const uint32_t *tree_off,
+                      size_t n_trees, uint8_t *roots);
+
+/*
+ * ValidatorSet.Hash (types/validator_set.go:347-353) for n_sets ed25519 validator sets:
+ * set s = validators [set_off[s], set_off[s+1]) in set order; leaves are
+ * Validator.Bytes() = SimpleValidator{PubKey ed25519, VotingPower} (types/validator.go:117-133),
+ * encoded on the device.  out: n_sets x 32 bytes.
+ */
+int tmed_valset_hashes(tmed_ctx *ctx, const uint8_t *pubkeys, const int64_t *powers, const uint32_t *set_off,
+                       size_t n_sets, uint8_t *out);
+
+/* Header fields hashed by Header.Hash (types/block.go:440-475), in struct order. */
+typedef struct {
+  uint64_t version_block, version_app;  /* tmversion.Consensus */
+  const char *chain_id;
+  uint32_t chain_id_len;
+  int64_t height;
+  int64_t time_seconds;                 /* Time.Unix() */
+  int32_t time_nanos;                   /* Time.Nanosecond() */
+  tmed_block_id last_block_id;
+  /* LastCommitHash, DataHash, ValidatorsHash, NextValidatorsHash, ConsensusHash, AppHash,
+     LastResultsHash, EvidenceHash, ProposerAddress */
+  const uint8_t *hashes[9];
+  uint32_t hash_lens[9];
+} tmed_header;
+
+/*
+ * Header.Hash for n headers: out[i] (32 bytes) with ok[i] = 1, or ok[i] = 0 where the
+ * reference returns nil (empty ValidatorsHash, :441-443).  Leaves are encoded on the host
+ * (gogoproto wrappers as cdcEncode, types/encoding_helper.go), hashed on the device.
+ */
+int tmed_header_hashes(tmed_ctx *ctx, const tmed_header *headers, size_t n, uint8_t *out, uint8_t *ok);
+
+/*
+ * PartSet root hash of n_blocks byte strings (NewPartSetFromData, types/part_set.go:166-194):
+ * block b = data[data_off[b] .. data_off[b+1]) split into part_size chunks
+ * (types.BlockPartSizeBytes = 65536 in the reference); roots: n_blocks x 32 bytes.
+ */
+int tmed_partset_roots(tmed_ctx *ctx, const uint8_t *data, const uint64_t *data_off, size_t n_blocks,
+                       uint32_t part_size, uint8_t *roots);
+
 /* ------------------------------------------------- blocksync replay (f4) */
 
 /*

@@ -71,7 +71,36 @@ AddrKey addr_key(const uint8_t *p) {
   return k;
 }
 
-using AddrIndex = std::unordered_map<AddrKey, int32_t, AddrHash>;  // address -> first validator idx
+// address -> first validator index with that address (GetByAddress, types/validator_set.go:270-278
+// returns the first match).  Flat open-addressing table: a light-client batch builds one per
+// trusted set (10k sets x 175 validators in C3), so construction cost matters.
+struct AddrIndex {
+  std::vector<AddrKey> keys;
+  std::vector<int32_t> vals;  // -1 = empty
+  size_t mask = 0;
+  void build(const uint8_t *addresses, size_t n) {
+    size_t cap = 16;
+    while (cap < 2 * n + 1) cap <<= 1;
+    mask = cap - 1;
+    keys.assign(cap, AddrKey{0, 0, 0});
+    vals.assign(cap, -1);
+    for (size_t v = 0; v < n; v++) {
+      const AddrKey k = addr_key(addresses + 20 * v);
+      size_t h = AddrHash()(k) & mask;
+      while (vals[h] >= 0 && !(keys[h] == k)) h = (h + 1) & mask;
+      if (vals[h] < 0) { keys[h] = k; vals[h] = (int32_t)v; }  // keep the first match
+    }
+  }
+  int32_t find(const uint8_t *addr) const {
+    const AddrKey k = addr_key(addr);
+    size_t h = AddrHash()(k) & mask;
+    while (vals[h] >= 0) {
+      if (keys[h] == k) return vals[h];
+      h = (h + 1) & mask;
+    }
+    return -1;
+  }
+};
 
 struct Plan {
   bool decided = false;
@@ -189,17 +218,25 @@ static int build_cand_batch(const tmed_commit_request *reqs, size_t n, const std
 // Address indexes for every LightTrusting valset of the call (built once, read-only after).
 using AddrCache = std::unordered_map<const tmed_valset *, std::unique_ptr<AddrIndex>>;
 
+static unsigned host_threads(size_t items);
+template <class F>
+static void parallel_ranges(size_t n, unsigned nt, F &&f);
+
 static void build_addr_cache(const tmed_commit_request *reqs, size_t n, AddrCache &cache) {
+  std::vector<std::pair<const tmed_valset *, AddrIndex *>> todo;
+  size_t work = 0;
   for (size_t q = 0; q < n; q++) {
     const tmed_commit_request &r = reqs[q];
     if (r.mode != TMED_MODE_LIGHT_TRUSTING || !r.vals) continue;
     auto &slot = cache[r.vals];
     if (slot) continue;
-    const tmed_valset &vs = *r.vals;
     slot.reset(new AddrIndex());
-    slot->reserve(vs.n * 2);
-    for (size_t v = 0; v < vs.n; v++) slot->emplace(addr_key(vs.addresses + 20 * v), (int32_t)v);  // first wins
+    todo.emplace_back(r.vals, slot.get());
+    work += r.vals->n;
   }
+  parallel_ranges(todo.size(), host_threads(work), [&](size_t lo, size_t hi, unsigned) {
+    for (size_t t = lo; t < hi; t++) todo[t].second->build(todo[t].first->addresses, todo[t].first->n);
+  });
 }
 
 // Plan one request; candidates are appended to `cands` and bit_of_sig holds their index there.
@@ -253,9 +290,8 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
     int64_t tally = 0;
     for (size_t i = 0; i < c.n_sigs; i++) {
       if (c.flags[i] != kCommit) continue;
-      auto it = pl.addr_index->find(addr_key(c.addresses + 20 * i));
-      if (it == pl.addr_index->end()) continue;
-      const int32_t v = it->second;
+      const int32_t v = pl.addr_index->find(c.addresses + 20 * i);
+      if (v < 0) continue;
       if (seen[v] >= 0) break;  // the loop returns the double-vote error here
       seen[v] = (int32_t)i;
       pl.bit_of_sig[i] = (int32_t)cands.size();
@@ -365,9 +401,8 @@ static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, c
     std::vector<int32_t> seen(vs.n, -1);
     for (size_t i = 0; i < c.n_sigs && o.code < 0; i++) {
       if (c.flags[i] != kCommit) continue;
-      auto it = pl.addr_index->find(addr_key(c.addresses + 20 * i));
-      if (it == pl.addr_index->end()) continue;
-      const int32_t v = it->second;
+      const int32_t v = pl.addr_index->find(c.addresses + 20 * i);
+      if (v < 0) continue;
       if (seen[v] >= 0) {
         o.code = TMED_COMMIT_DOUBLE_VOTE; o.val_idx = v; o.idx_first = seen[v]; o.idx = (int32_t)i;
         break;

@@ -129,6 +129,7 @@ struct tmed_ctx {
   tmed::DevBuf d_a, d_b, d_msg, d_off, d_out, d_c;
   tmed::HostBuf h_a, h_b, h_msg, h_off, h_out, h_c;
   tmed::VoteSlot vslot[2];
+  tmed::DevBuf d_merkle_a, d_merkle_b, d_merkle_idx;  // Merkle level digests (ping-pong) + level indexes
   std::unordered_map<uint64_t, tmed::Keyset> keysets;
   uint64_t next_keyset = 1;
 };

@@ -115,7 +115,7 @@ TMED_HD uint32_t bswap32(uint32_t x) {
 // depends only on the lane's misalignment r); dwords past the last one that overlaps M
 // are never read.
 struct MsgReader {
-  const uint32_t *base;  // M rounded down to a dword boundary
+  const uint32_t *base;  // M rounded down to a dword boundary (never read past ndw dwords)
   uint32_t ndw;          // aligned dwords overlapping M
   uint32_t r;            // misalignment of M in bytes
   const uint8_t *m;

@@ -96,6 +96,7 @@ void tmed_destroy(tmed_ctx *c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   for (DevBuf *b : {&c->d_a, &c->d_b, &c->d_msg, &c->d_off, &c->d_out, &c->d_c}) b->release();
   for (HostBuf *b : {&c->h_a, &c->h_b, &c->h_msg, &c->h_off, &c->h_out, &c->h_c}) b->release();
+  for (DevBuf *b : {&c->d_merkle_a, &c->d_merkle_b, &c->d_merkle_idx}) b->release();
   for (VoteSlot &v : c->vslot) {
     for (DevBuf *b : {&v.d_votes, &v.d_vmsg, &v.d_off, &v.d_out}) b->release();
     for (HostBuf *b : {&v.h_votes, &v.h_out}) b->release();

@@ -9,6 +9,7 @@
 
 #include <vector>
 #include "verify_core.h"
+#include "sha256.h"
 
 using namespace tmed;
 
@@ -214,3 +215,21 @@ void hostsim_sc_reduce(const uint8_t *h64, uint8_t *out) {
 }
 
 }  // extern "C"
+
+// SHA-256 paths of the Merkle kernels (csrc/sha256.h), on the host.
+extern "C" void hostsim_sha256(int npre, uint8_t prefix, const uint8_t *m, uint32_t mlen, uint8_t *out) {
+  uint32_t st[8];
+  sha256_prefixed(st, npre, prefix, m, mlen);
+  for (int k = 0; k < 8; k++)
+    for (int b = 0; b < 4; b++) out[4 * k + b] = (uint8_t)(st[k] >> (24 - 8 * b));
+}
+extern "C" void hostsim_sha256_inner(const uint8_t *l, const uint8_t *r, uint8_t *out) {
+  uint32_t lw[8], rw[8], st[8];
+  for (int k = 0; k < 8; k++) {
+    lw[k] = ((uint32_t)l[4 * k] << 24) | ((uint32_t)l[4 * k + 1] << 16) | ((uint32_t)l[4 * k + 2] << 8) | l[4 * k + 3];
+    rw[k] = ((uint32_t)r[4 * k] << 24) | ((uint32_t)r[4 * k + 1] << 16) | ((uint32_t)r[4 * k + 2] << 8) | r[4 * k + 3];
+  }
+  sha256_inner(st, lw, rw);
+  for (int k = 0; k < 8; k++)
+    for (int b = 0; b < 4; b++) out[4 * k + b] = (uint8_t)(st[k] >> (24 - 8 * b));
+}

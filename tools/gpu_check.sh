@@ -31,6 +31,9 @@ for s in $STEPS; do
         echo "$cfg rc=$rc $(tail -1 $OUT/variant.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])' 2>/dev/null)" | tee -a $OUT/variants.txt
         if fatal $rc; then break; fi
       done ;;
+    merkle)
+      timeout -k 10 300 python bench_merkle.py > $OUT/bench_merkle.log 2>&1; rc=$?
+      echo "merkle rc=$rc"; grep '^{' $OUT/bench_merkle.log ;;
     keyset)
       timeout -k 10 300 python bench_keyset.py > $OUT/bench_keyset.log 2>&1; rc=$?
       echo "keyset rc=$rc"; grep '^{' $OUT/bench_keyset.log ;;
