@@ -50,3 +50,57 @@ def verify_sharded(engine, requests: Sequence[tuple], rank: int, world: int, dev
         full = torch.stack(gathered).max(dim=0).values  # each slot owned by exactly one rank
     ok, n, verified = (int(x) for x in tally.tolist())
     return {"ok": ok, "commits": n, "verified": verified, "codes": full.cpu().numpy()}
+
+
+def slice_bounds(m: int, rank: int, world: int) -> tuple:
+    """Contiguous candidate slice [lo, hi) of `rank` (sizes differ by at most one)."""
+    return m * rank // world, m * (rank + 1) // world
+
+
+def verify_commit_sliced(engine, request: tuple, rank: int, world: int, device=None, verifier=None):
+    """Latency mode for ONE large commit: the validator index range is split
+    over the ranks instead of whole commits.
+
+    Every rank runs the seam on the whole commit — prechecks, candidate selection and
+    sign-bytes are host work and identical everywhere — but verifies only its contiguous
+    slice of the candidates.  The ranks then agree on f, the first failing candidate, with
+    ONE int64 all-reduce MIN, and every rank replays the reference loop with bits "valid
+    before f, invalid at f".  The loop never looks past f: VerifyCommit errors at f
+    (types/validator_set.go:695-698), and Light/Trusting either crossed 2/3 before f or error
+    at f (:751-761, :812-822), so the error, its index and Got/Needed equal the
+    single-process result.  (The power tally needs no collective: every rank holds the
+    commit.)  Returns the Go-style error (None = ok) and the number of candidates."""
+    import torch
+    import torch.distributed as dist
+    from .types import verify_commits
+
+    dev = device if device is not None else torch.device("cpu")
+    seen = []
+
+    def sliced(pubs, sigs, lens, msgs, offs):
+        m = pubs.shape[0]
+        lo, hi = slice_bounds(m, rank, world)
+        first = m
+        if hi > lo:
+            o = offs[lo:hi + 1].astype(np.int64)
+            sub_msgs = msgs[o[0]:o[-1]]
+            sub_offs = (o - o[0]).astype(np.uint32)
+            if verifier is None:
+                bits = engine.verify_arrays(pubs[lo:hi], sigs[lo:hi], sub_msgs, sub_offs, lens[lo:hi])
+            else:
+                bits = np.asarray(verifier(pubs[lo:hi], sigs[lo:hi], lens[lo:hi], sub_msgs, sub_offs), np.uint8)
+            bad = np.flatnonzero(bits == 0)
+            if bad.size:
+                first = lo + int(bad[0])
+        f = torch.tensor([first], dtype=torch.int64, device=dev)
+        if world > 1:
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        f = int(f.item())
+        out = np.ones(m, np.uint8)
+        if f < m:
+            out[f] = 0
+        seen.append(m)
+        return out
+
+    err = verify_commits(engine, [request], verifier=sliced)[0]
+    return err, (seen[0] if seen else 0)

@@ -70,3 +70,50 @@ def test_sharded_tallies_match_single_process(world):
         assert ok == exp_ok and n == len(reqs)
         assert codes == exp_codes
     assert sorted(sum((shard(len(reqs), r, world) for r in range(world)), [])) == list(range(len(reqs)))
+
+
+def _sliced_worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "tendermint-fork_amd"), os.path.join(ROOT, "tests")]
+    import torch.distributed as dist
+    from commit_cases import pbid, scenarios
+    from tmed.dist import verify_commit_sliced
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    out = []
+    for mode, vs, pv, chain, bid, h, cm, pc, num, den in scenarios(seed=17, count=30):
+        err, m = verify_commit_sliced(None, (mode, pv, chain, pbid(bid), h, pc, num, den), rank, world,
+                                      verifier=_verifier_slice)
+        out.append((None if err is None else (type(err).__name__, str(err)), m))
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _verifier_slice(pubs, sigs, lens, msgs, offs):
+    return _verifier(pubs, sigs, lens, msgs, offs)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_index_sliced_commit_matches_reference_loop(world):
+    """§8e latency mode: one commit's candidates split over the ranks, one all-reduce MIN of
+    the first failing index; every rank must return the reference loop's exact error."""
+    from commit_cases import oracle_result, scenarios
+    exp = [oracle_result(mode, vs, chain, bid, h, cm, num, den)
+           for mode, vs, pv, chain, bid, h, cm, pc, num, den in scenarios(seed=17, count=30)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sliced_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    kinds = set()
+    for rank, out in res:
+        for (got, m), e in zip(out, exp):
+            want = None if e is None else (type(e).__name__, str(e))
+            assert got == want, (rank, got, want)
+            kinds.add("ok" if e is None else type(e).__name__)
+    assert len(kinds) >= 3, kinds  # ok, wrong-signature and not-enough-power cases all crossed slices

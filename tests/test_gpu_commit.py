@@ -19,6 +19,16 @@ def test_seam_matches_reference_loops_gpu(engine):
         assert same(T.verify_commits(engine, [reqs[q]])[0], exp[q])
 
 
+def test_index_sliced_commit_gpu(engine):
+    """§8e latency mode on one rank: the slice verifier runs on the GPU (tmed_verify_batch) and
+    the first-failure replay must give the reference loop's exact error."""
+    from tmed.dist import verify_commit_sliced
+    for mode, vs, pv, chain, bid, h, cm, pc, num, den in scenarios(seed=5, count=40):
+        e = oracle_result(mode, vs, chain, bid, h, cm, num, den)
+        got, _ = verify_commit_sliced(engine, (mode, pv, chain, pbid(bid), h, pc, num, den), 0, 1)
+        assert same(got, e), (str(got), str(e))
+
+
 def test_reference_cases_gpu(engine):
     """types/validator_set_test.go:746-815 through the GPU seam."""
     from oracle.fixtures import make_block_id, make_commit, make_valset, resign, seed_of
