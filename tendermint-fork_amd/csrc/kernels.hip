@@ -56,6 +56,51 @@ struct SlabTabT {
       }
     }
   }
+  int pf = 0;
+  __device__ __forceinline__ void prefetch(int j) { pf = j; }
+  __device__ __forceinline__ void take(ge_cached &c) const { load(pf, c); }
+};
+
+typedef __attribute__((address_space(1))) void global_void;
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void unpack_cached(ge_cached &c, const int4 v[10]) {
+  fe *fs[4] = {&c.YpX, &c.YmX, &c.Z, &c.T2d};
+#pragma unroll
+  for (int q = 0; q < 10; q++) {
+    const int32_t w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int f = 4 * q + e;
+      fs[f / 10]->v[f % 10] = w[e];
+    }
+  }
+}
+
+// Lane-major slab whose next entry is fetched asynchronously into LDS
+// (global_load_lds_dwordx4, gfx950): the fetch is issued right after an A addition and
+// consumed by the next one, four doublings later, so the entry's HBM/MALL latency is
+// hidden without holding 40 VGPRs across the doublings (the kernel has none to spare at
+// 2 waves/SIMD).  buf is this wave's [10][64] int4 region: lane l's 16-B piece q lands at
+// buf[q * 64 + l] (M0 = buf + q * 1 KB, LDS address = M0 + 16 * lane).  Single-buffered:
+// the next prefetch is issued only after take()'s values have been consumed.
+struct SlabTabPf {
+  SlabTabT<true> s;
+  int4 *buf;
+  uint32_t lane;
+  __device__ __forceinline__ void store(int j, const ge_cached &c) const { s.store(j, c); }
+  __device__ __forceinline__ void prefetch(int j) const {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the previous take's LDS reads are done
+#pragma unroll
+    for (int q = 0; q < 10; q++)
+      __builtin_amdgcn_global_load_lds((global_void *)(s.base + s.idx(j, q)), (lds_void *)(buf + q * 64), 16, 0, 0);
+  }
+  __device__ __forceinline__ void take(ge_cached &c) const {
+    int4 v[10];
+#pragma unroll
+    for (int q = 0; q < 10; q++) v[q] = buf[q * 64 + lane];
+    unpack_cached(c, v);
+  }
 };
 
 using SlabTab = SlabTabT<false>;
@@ -216,11 +261,14 @@ __device__ __forceinline__ void fin_store(int4 *fin, uint32_t stride, uint32_t s
 
 // Phase 2: table of -A, Straus [k](-A) + [s]B -> projective R' (hand-off to the finish).
 // WAVES = minimum waves per SIMD the register allocation must allow.
-template <int WAVES, bool LANE_MAJOR>
+// PF: the per-lane A table is lane-major and its next entry is prefetched into LDS
+// (SlabTabPf, 40 KB per 256-lane block on top of the 15.5 KB B table).
+template <int WAVES, bool LANE_MAJOR, bool PF = false>
 __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_main_kernel(
     uint32_t base, uint32_t count, const int4 *__restrict__ prep, uint32_t stride, int4 *__restrict__ slab,
     const ge_niels *__restrict__ btab_g, int4 *__restrict__ fin, uint32_t fin_base, uint8_t *__restrict__ out) {
   __shared__ ge_niels sbt[kBTabEntries];
+  __shared__ int4 spf[PF ? kThreadsPerBlock / 64 : 1][PF ? 10 * 64 : 1];
   stage_btab(sbt, btab_g);
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   if (slot >= count) return;
@@ -228,10 +276,15 @@ __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_main_kernel(
   uint32_t k[8], s[8];
   ge_p3 A;
   const bool ok = prep_load(prep, stride, slot, k, s, A);
-  SlabTabT<LANE_MAJOR> tab{slab, stride, slot};
   const LdsBTab bt{sbt};
   ge_p2 R;
-  verify_main_point(R, k, s, A, tab, bt);
+  if constexpr (PF) {
+    SlabTabPf tab{SlabTabT<true>{slab, stride, slot}, spf[threadIdx.x >> 6], threadIdx.x & 63u};
+    verify_main_point(R, k, s, A, tab, bt);
+  } else {
+    SlabTabT<LANE_MAJOR> tab{slab, stride, slot};
+    verify_main_point(R, k, s, A, tab, bt);
+  }
   fin_store(fin, kFinCap, i - fin_base, R.X, R.Y, R.Z);
   out[i] = ok ? 1 : 0;
 }
@@ -361,7 +414,10 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
       if (timer) timer->mark(stream, 0);
       // default: 2 waves/SIMD, lane-major per-lane tables (+3.7 % over the slot-interleaved
       // layout, profiles/r01/variants.txt); the others are kept as measured A/B variants.
-      if (main_waves >= 3)
+      if (main_waves == 4)  // lane-major + LDS prefetch of the next A entry
+        hipLaunchKernelGGL((verify_main_kernel<2, true, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream,
+                           base, count, prep, slab_stride, slab, btab, fin, fbase, out);
+      else if (main_waves >= 3)
         hipLaunchKernelGGL((verify_main_kernel<3, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base,
                            count, prep, slab_stride, slab, btab, fin, fbase, out);
       else if (main_waves == -2)  // slot-interleaved slab layout

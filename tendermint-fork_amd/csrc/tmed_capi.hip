@@ -59,12 +59,15 @@ int tmed_init(int device, tmed_ctx **out) {
   std::call_once(bt_once, [] { host_build_btab(bt); });
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_btab, sizeof(bt));
   if (e == hipSuccess) e = hipMemcpy(c->d_btab, bt, sizeof(bt), hipMemcpyHostToDevice);
-  // Lane slots for the per-lane tables: 4x the resident lanes of 256 CUs at
-  // 8 waves/CU is plenty for the grid-stride loop (~377 MB of HBM).
-  c->slab_slots = 1024 * kThreadsPerBlock;
-  c->chunk = 512 * kThreadsPerBlock;  // 131,072 signatures per prep/main pair (measured best, profiles/r01/variants.txt)
+  // Lane slots for the per-lane tables and the prep hand-off: 2^20 signatures per
+  // prep/main pair (1.5 GB slab + 168 MB hand-off of the 288 GB HBM), so a BASELINE C2
+  // batch is one prep, one main and one finish launch: +2.6 % over 131,072-signature
+  // chunks, which paid a drain/ramp bubble per launch (profiles/r01/session2/variants_chunk.txt).
+  c->slab_slots = 4096 * kThreadsPerBlock;
+  c->chunk = c->slab_slots;
   if (const char *v = getenv("TMED_CHUNK")) c->chunk = (uint32_t)strtoul(v, nullptr, 10);
   if (const char *v = getenv("TMED_MAIN_WAVES")) c->main_waves = atoi(v);
+  if (const char *v = getenv("TMED_SLAB_SLOTS")) c->slab_slots = (uint32_t)strtoul(v, nullptr, 10);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_slab, (size_t)c->slab_slots * kSlabSlotBytes);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_prep, (size_t)c->slab_slots * kPrepSlotBytes);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_fin, kFinBytes);          // 128 MB: projective R'

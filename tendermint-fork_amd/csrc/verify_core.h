@@ -44,8 +44,9 @@ TMED_HD void niels_apply_sign(ge_niels &e, bool neg) {
 }
 
 // Per-lane variable-base table access.  T must provide
-//   void store(int j, const ge_cached&)  and  void load(int j, ge_cached&)
-// for j in [0, 8] (j = 0 is the identity).  The device implementation lives in a
+//   void store(int j, const ge_cached&), void prefetch(int j)  and  void take(ge_cached&)
+// for j in [0, 8] (j = 0 is the identity): prefetch names the entry the next take
+// returns, so a device table can start the fetch one window (four doublings) ahead.  The device implementation lives in a
 // global-memory slab (per-lane tables are 1.4 KB: too large for LDS at useful
 // occupancy); the host test build uses a local array.
 template <class T>
@@ -84,6 +85,10 @@ TMED_HD void double_scalarmult(ge_p2 &out, const uint32_t k[8], const uint32_t s
   ge_p3 r;
   ge_cached ca;
   ge_niels nb;
+  {
+    const int da0 = (int)(kr[7] >> 28) - 8;
+    tab.prefetch(da0 < 0 ? -da0 : da0);
+  }
 #pragma unroll 1
   for (int j = 0; j < 8; j++) {  // 32-bit word of the scalars, most significant first
     uint32_t kc = kr[7], sc = sr[7];
@@ -97,6 +102,9 @@ TMED_HD void double_scalarmult(ge_p2 &out, const uint32_t k[8], const uint32_t s
       for (int h = 0; h < 2; h++) {
         const int da = (int)(kc >> 28) - 8;
         kc <<= 4;
+        // the window after this one (the next word's first digit after the last nibble;
+        // past the final window any in-range index will do)
+        const int dn = (int)(((h == 1 && i == 3) ? kr[7] : kc) >> 28) - 8;
         if (h == 0 && j == 0 && i == 0) {
           ge_p3_0(r);  // the first four doublings would double the identity: skipped
         } else {
@@ -108,8 +116,9 @@ TMED_HD void double_scalarmult(ge_p2 &out, const uint32_t k[8], const uint32_t s
           ge_p2_dbl(t, q);
           ge_p1p1_to_p3(r, t);
         }
-        tab.load(da < 0 ? -da : da, ca);
+        tab.take(ca);
         ge_add_cached(t, r, ca, da < 0);
+        tab.prefetch(dn < 0 ? -dn : dn);
         if (h == 0) ge_p1p1_to_p2(q, t);
       }
       ge_p1p1_to_p3(r, t);

@@ -18,6 +18,9 @@ struct HostTab {
   ge_cached e[9];
   void store(int j, const ge_cached &c) { e[j] = c; }
   void load(int j, ge_cached &c) const { c = e[j]; }
+  int pf = 0;
+  void prefetch(int j) { pf = j; }
+  void take(ge_cached &c) const { c = e[pf]; }
 };
 struct HostBTab {
   ge_niels e[129];
