@@ -234,3 +234,106 @@ func (e *Engine) VerifyCommits(reqs []Request) ([]Result, error) {
 	}
 	return out, nil
 }
+
+func toResults(res []C.tmed_commit_result) []Result {
+	out := make([]Result, len(res))
+	for i := range res {
+		out[i] = Result{Code: int(res[i].code), Got: int64(res[i].got), Needed: int64(res[i].needed),
+			Expected: int64(res[i].expected), Actual: int64(res[i].actual), Idx: int32(res[i].idx),
+			IdxFirst: int32(res[i].idx_first), ValIdx: int32(res[i].val_idx)}
+	}
+	return out
+}
+
+// BlocksyncWindow is a run of buffered blocks checked against one (predicted) validator
+// set: block h is vals.VerifyCommitLight(ChainID, BlockIDs[h], Heights[h], Commits[h])
+// (blockchain/v0/reactor.go:366-367).
+type BlocksyncWindow struct {
+	ChainID  string
+	Vals     *ValSet
+	BlockIDs []BlockID
+	Heights  []int64
+	Commits  []*CommitData
+}
+
+// BlocksyncVerify returns the VerifyCommitLight outcome of every block of the window,
+// computed speculatively through the pipelined device path (tmed_blocksync_verify).
+// The reactor applies blocks in order and stops at the first non-OK result.
+func (e *Engine) BlocksyncVerify(w *BlocksyncWindow, batchBlocks int) ([]Result, error) {
+	n := len(w.Commits)
+	if n == 0 {
+		return nil, nil
+	}
+	var a arena
+	defer a.free()
+	vs := (*C.tmed_valset)(a.alloc(unsafe.Sizeof(C.tmed_valset{})))
+	*vs = C.tmed_valset{n: C.size_t(len(w.Vals.Powers)), pubkeys: a.bytes(w.Vals.PubKeys),
+		powers: a.i64(w.Vals.Powers), addresses: a.bytes(w.Vals.Addresses), total_power: C.int64_t(w.Vals.TotalPower),
+		keyset: C.uint64_t(w.Vals.Keyset), keyset_index: a.u32(w.Vals.KeysetIndex)}
+	cs := (*[1 << 26]C.tmed_commit)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_commit{})))[:n:n]
+	bids := (*[1 << 26]C.tmed_block_id)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_block_id{})))[:n:n]
+	for i, c := range w.Commits {
+		cs[i] = C.tmed_commit{height: C.int64_t(c.Height), round: C.int32_t(c.Round), block_id: a.blockID(&c.BlockID),
+			n_sigs: C.size_t(len(c.Flags)), flags: a.bytes(c.Flags), addresses: a.bytes(c.Addresses),
+			ts_seconds: a.i64(c.TsSeconds), ts_nanos: a.i32(c.TsNanos), sigs: a.bytes(c.Sigs), sig_lens: a.u32(c.SigLens)}
+		bids[i] = a.blockID(&w.BlockIDs[i])
+	}
+	cid := C.CString(w.ChainID)
+	a.ptrs = append(a.ptrs, unsafe.Pointer(cid))
+	win := (*C.tmed_blocksync_window)(a.alloc(unsafe.Sizeof(C.tmed_blocksync_window{})))
+	*win = C.tmed_blocksync_window{chain_id: cid, chain_id_len: C.uint32_t(len(w.ChainID)), vals: vs,
+		n_blocks: C.size_t(n), block_ids: &bids[0], heights: a.i64(w.Heights), commits: &cs[0]}
+	res := make([]C.tmed_commit_result, n)
+	if rc := C.tmed_blocksync_verify(e.ctx, win, C.uint32_t(batchBlocks), &res[0]); rc != 0 {
+		return nil, errors.New(C.GoString(C.tmed_strerror(rc)))
+	}
+	return toResults(res), nil
+}
+
+// ValsetHashes returns ValidatorSet.Hash() of every set: set s is validators
+// [setOff[s], setOff[s+1]) of (pubKeys n x 32, powers n) in set order (tmed_valset_hashes).
+func (e *Engine) ValsetHashes(pubKeys []byte, powers []int64, setOff []uint32) ([][32]byte, error) {
+	ns := len(setOff) - 1
+	if ns <= 0 {
+		return nil, nil
+	}
+	var a arena
+	defer a.free()
+	out := (*[1 << 26][32]byte)(a.alloc(uintptr(ns) * 32))[:ns:ns]
+	if rc := C.tmed_valset_hashes(e.ctx, a.bytes(pubKeys), a.i64(powers), a.u32(setOff), C.size_t(ns),
+		(*C.uint8_t)(unsafe.Pointer(&out[0]))); rc != 0 {
+		return nil, errors.New(C.GoString(C.tmed_strerror(rc)))
+	}
+	return append([][32]byte(nil), out...), nil
+}
+
+// MerkleRoots returns merkle.HashFromByteSlices of every tree (tmed_merkle_roots).
+func (e *Engine) MerkleRoots(trees [][][]byte) ([][32]byte, error) {
+	nt := len(trees)
+	if nt == 0 {
+		return nil, nil
+	}
+	var flat []byte
+	leafOff := []uint64{0}
+	treeOff := []uint32{0}
+	for _, t := range trees {
+		for _, l := range t {
+			flat = append(flat, l...)
+			leafOff = append(leafOff, uint64(len(flat)))
+		}
+		treeOff = append(treeOff, uint32(len(leafOff)-1))
+	}
+	flat = append(flat, make([]byte, 8)...) // the device reader may touch the last dword
+	var a arena
+	defer a.free()
+	lo := (*[1 << 26]C.uint64_t)(a.alloc(uintptr(len(leafOff)) * 8))[:len(leafOff):len(leafOff)]
+	for i, v := range leafOff {
+		lo[i] = C.uint64_t(v)
+	}
+	out := (*[1 << 26][32]byte)(a.alloc(uintptr(nt) * 32))[:nt:nt]
+	if rc := C.tmed_merkle_roots(e.ctx, a.bytes(flat), &lo[0], a.u32(treeOff), C.size_t(nt),
+		(*C.uint8_t)(unsafe.Pointer(&out[0]))); rc != 0 {
+		return nil, errors.New(C.GoString(C.tmed_strerror(rc)))
+	}
+	return append([][32]byte(nil), out...), nil
+}
