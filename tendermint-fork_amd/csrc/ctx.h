@@ -124,6 +124,8 @@ struct tmed_ctx {
   uint32_t slab_slots = 0;
   uint32_t chunk = 0;     // signatures per prep/main launch pair (0 = slab_slots); env TMED_CHUNK
   int main_waves = 2;     // register budget variant of the main kernel; env TMED_MAIN_WAVES
+  uint32_t lat_max = 24576;  // key-cached batches up to this size take the latency kernels (crossover ~32k,
+                             // profiles/r01/session3/lat_sweep.jsonl); env TMED_LAT_MAX
   bool timing = false;    // tmed_set_kernel_timing
   tmed::KernelTimer timer;
   tmed::DevBuf d_a, d_b, d_msg, d_off, d_out, d_c;

@@ -74,6 +74,15 @@ hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub,
                                 const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
                                 int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots = false);
 
+// Latency mode for small key-cached batches (n <= kLatMax): 8 lanes per signature for the
+// comb sum, strict decode of R on other lanes instead of the inversion; two launches.
+// fin as above; dec: kLatDecInt4 x n int4 (fits the fin_pre buffer for n <= kLatMax).
+constexpr uint32_t kLatMax = 1u << 16;
+hipError_t launch_verify_keyset_lat(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
+                                    const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
+                                    const uint32_t *off, uint32_t n, uint8_t *out, int4 *fin, int4 *dec,
+                                    hipStream_t stream, bool msg_slots = false);
+
 // f1: on-device CanonicalVote assembly.  Templates are kVoteTmplBytes records
 // ([pre_len, bid_len, cid_len, 0] + bytes); message i is written to out + i * kVoteSlot
 // and its length to out_len[i].  With msg_slots = true the verify launchers read

@@ -594,6 +594,112 @@ hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStr
   return hipGetLastError();
 }
 
+// ---- latency mode (verify_core.h): small key-cached batches ------------------------------
+// One launch, two roles by block (64-lane blocks; the R blocks come first so the longest
+// chain is dispatched first):
+//  * blocks [0, nR): lane i strictly decodes R of signature i -> (x_R, y_R, ok) in dec;
+//  * blocks [nR, nR + nC): 8 lanes per signature; every lane of the group hashes (the same
+//    SHA-512, so no divergence), lane r sums its 8 comb entries, three __shfl_down steps
+//    add the partial sums, lane 0 writes R' (fin) and the prep verdict (out).
+// verify_lat_finish_kernel then compares projectively.  dec layout: [q][i], q < 6 int4.
+constexpr int kLatDecInt4 = 6;
+
+__device__ __forceinline__ void shfl_down_fe(fe &o, const fe &f, int L) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) o.v[i] = __shfl_down(f.v[i], (unsigned)L, kLatLanes);
+}
+
+__global__ __launch_bounds__(64) void verify_keyset_lat_kernel(
+    const uint32_t *__restrict__ val_idx, const uint8_t *__restrict__ key_pub, const uint8_t *__restrict__ key_ok,
+    const int4 *__restrict__ acomb, const int4 *__restrict__ bcomb, const uint8_t *__restrict__ sig, MsgSrc ms,
+    uint32_t m, uint32_t nR, int4 *__restrict__ fin, int4 *__restrict__ dec, uint8_t *__restrict__ out) {
+  if (blockIdx.x < nR) {
+    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= m) return;
+    uint32_t Rw[8];
+    load_row_words(Rw, sig + 64 * (size_t)i, 2);
+    fe x, y;
+    const bool ok = r_decode_strict(x, y, Rw);
+    int32_t w[24];
+#pragma unroll
+    for (int j = 0; j < 10; j++) { w[j] = x.v[j]; w[10 + j] = y.v[j]; }
+    w[20] = ok ? 1 : 0;
+    w[21] = w[22] = w[23] = 0;
+#pragma unroll
+    for (int q = 0; q < kLatDecInt4; q++) dec[(size_t)q * m + i] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    return;
+  }
+  const uint32_t g = (blockIdx.x - nR) * (64 / kLatLanes) + (threadIdx.x / kLatLanes);
+  const int r = (int)(threadIdx.x % kLatLanes);
+  if (g >= m) return;  // whole 8-lane groups leave together: the shuffles stay inside live groups
+  const uint32_t v = val_idx[g];
+  uint32_t pw[8], sw[16], k[8], s[8], kr[8], sr[8];
+  load_row_words(pw, key_pub + 32 * (size_t)v, 2);
+  load_row_words(sw, sig + 64 * (size_t)g, 4);
+  const uint8_t *msg;
+  uint32_t mlen;
+  ms.get(g, msg, mlen);
+  const bool ok = verify_prep_comb(pw, key_ok[v] != 0, sw, msg, mlen, k, s);
+  sc_recode256(kr, k);
+  sc_recode256(sr, s);
+  const GlobalComb ac{acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4};
+  const GlobalComb bc{bcomb};
+  ge_p3 acc, o;
+  comb_partial(acc, kr, sr, r, ac, bc);
+#pragma unroll 1
+  for (int L = 1; L < kLatLanes; L <<= 1) {
+    shfl_down_fe(o.X, acc.X, L);
+    shfl_down_fe(o.Y, acc.Y, L);
+    shfl_down_fe(o.Z, acc.Z, L);
+    shfl_down_fe(o.T, acc.T, L);
+    ge_p3_add(acc, o);
+  }
+  if (r == 0) {
+    fin_store(fin, kFinCap, g, acc.X, acc.Y, acc.Z);
+    out[g] = ok ? 1 : 0;
+  }
+}
+
+__global__ __launch_bounds__(kThreadsPerBlock) void verify_lat_finish_kernel(const int4 *__restrict__ fin,
+                                                                            const int4 *__restrict__ dec, uint32_t m,
+                                                                            uint8_t *__restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  int32_t w[32];
+#pragma unroll
+  for (int q = 0; q < kFinInt4; q++) {
+    const int4 t = fin[(size_t)q * kFinCap + i];
+    w[4 * q] = t.x; w[4 * q + 1] = t.y; w[4 * q + 2] = t.z; w[4 * q + 3] = t.w;
+  }
+  fe X, Y, Z, x, y;
+#pragma unroll
+  for (int j = 0; j < 10; j++) { X.v[j] = w[j]; Y.v[j] = w[10 + j]; Z.v[j] = w[20 + j]; }
+#pragma unroll
+  for (int q = 0; q < kLatDecInt4; q++) {
+    const int4 t = dec[(size_t)q * m + i];
+    w[4 * q] = t.x; w[4 * q + 1] = t.y; w[4 * q + 2] = t.z; w[4 * q + 3] = t.w;
+  }
+#pragma unroll
+  for (int j = 0; j < 10; j++) { x.v[j] = w[j]; y.v[j] = w[10 + j]; }
+  const bool ok = out[i] && w[20] && projective_matches(X, Y, Z, x, y);
+  out[i] = ok ? 1 : 0;
+}
+
+hipError_t launch_verify_keyset_lat(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
+                                    const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
+                                    const uint32_t *off, uint32_t n, uint8_t *out, int4 *fin, int4 *dec,
+                                    hipStream_t stream, bool msg_slots) {
+  if (n == 0) return hipSuccess;
+  if (n > kLatMax) return hipErrorInvalidValue;  // fin / dec are sized for kLatMax signatures
+  const MsgSrc ms{msgs, off, msg_slots};
+  const uint32_t nR = (n + 63) / 64, nC = (n + 64 / kLatLanes - 1) / (64 / kLatLanes);
+  hipLaunchKernelGGL(verify_keyset_lat_kernel, dim3(nR + nC), dim3(64), 0, stream, val_idx, key_pub, key_ok, acomb,
+                     bcomb, sig, ms, n, nR, fin, dec, out);
+  hipLaunchKernelGGL(verify_lat_finish_kernel, dim3((n + kThreadsPerBlock - 1) / kThreadsPerBlock),
+                     dim3(kThreadsPerBlock), 0, stream, fin, dec, n, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
                                 const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                 const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,

@@ -34,6 +34,18 @@ void free_keyset(Keyset &k) {
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Key-cached batch on the context's stream: latency kernels for small batches (C1: one
+// commit), the throughput kernels (prep / comb main / batched finish) above c->lat_max.
+static hipError_t keyset_verify(tmed_ctx *c, const Keyset &k, const uint32_t *d_idx, const uint8_t *d_sig,
+                                const uint8_t *d_msgs, const uint32_t *d_off, uint32_t n, uint8_t *d_out,
+                                hipStream_t s, bool msg_slots) {
+  if (n <= c->lat_max)
+    return launch_verify_keyset_lat(d_idx, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb, d_sig, d_msgs, d_off, n, d_out,
+                                    c->d_fin, c->d_fin_pre, s, msg_slots);
+  return launch_verify_keyset(d_idx, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb, d_sig, d_msgs, d_off, n, d_out, c->d_prep,
+                              c->slab_slots, c->d_fin, c->d_fin_pre, s, msg_slots);
+}
+
 int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st, int slot) {
   st.slot = slot;
   st.m = m;
@@ -92,10 +104,8 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
                               (uint8_t *)vs.d_vmsg.p, (uint32_t *)vs.d_off.p, s);
   if (e == hipSuccess) {
     if (st.ks)
-      e = launch_verify_keyset((const uint32_t *)(d + st.o_key), st.ks->d_pub, st.ks->d_ok, st.ks->d_comb, c->d_bcomb,
-                               d + st.o_sig, (const uint8_t *)vs.d_vmsg.p, (const uint32_t *)vs.d_off.p, m,
-                               (uint8_t *)vs.d_out.p, c->d_prep, c->slab_slots, c->d_fin, c->d_fin_pre, s,
-                               /*msg_slots=*/true);
+      e = keyset_verify(c, *st.ks, (const uint32_t *)(d + st.o_key), d + st.o_sig, (const uint8_t *)vs.d_vmsg.p,
+                        (const uint32_t *)vs.d_off.p, m, (uint8_t *)vs.d_out.p, s, /*msg_slots=*/true);
     else
       e = launch_verify(d + st.o_key, d + st.o_sig, (const uint8_t *)vs.d_vmsg.p, (const uint32_t *)vs.d_off.p, m,
                         (uint8_t *)vs.d_out.p, c->d_slab, c->slab_slots, c->d_btab, c->d_prep, c->d_fin,
@@ -190,9 +200,7 @@ int tmed_verify_batch_keyset_device(tmed_ctx *c, uint64_t handle, const uint32_t
   const Keyset &k = it->second;
   (void)hipSetDevice(c->device);
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  return map_err(launch_verify_keyset(d_val_idx, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb, d_sigs, d_msgs, d_msg_off,
-                                      (uint32_t)n, d_out, c->d_prep, c->slab_slots, c->d_fin,
-                                      c->d_fin_pre, s));
+  return map_err(keyset_verify(c, k, d_val_idx, d_sigs, d_msgs, d_msg_off, (uint32_t)n, d_out, s, false));
 }
 
 int tmed_verify_batch_keyset(tmed_ctx *c, uint64_t handle, const uint32_t *val_idx, const uint8_t *sigs,
@@ -234,10 +242,8 @@ int tmed_verify_batch_keyset(tmed_ctx *c, uint64_t handle, const uint32_t *val_i
   if (e == hipSuccess) e = hipMemcpyAsync(c->d_off.p, c->h_off.p, moff, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipEventRecord(c->ev0, s);
   if (e == hipSuccess)
-    e = launch_verify_keyset((const uint32_t *)c->d_a.p, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb,
-                             (const uint8_t *)c->d_b.p, (const uint8_t *)c->d_msg.p, (const uint32_t *)c->d_off.p,
-                             (uint32_t)n, (uint8_t *)c->d_out.p, c->d_prep, c->slab_slots, c->d_fin,
-                             c->d_fin_pre, s);
+    e = keyset_verify(c, k, (const uint32_t *)c->d_a.p, (const uint8_t *)c->d_b.p, (const uint8_t *)c->d_msg.p,
+                      (const uint32_t *)c->d_off.p, (uint32_t)n, (uint8_t *)c->d_out.p, s, false);
   if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
   if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, n, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);

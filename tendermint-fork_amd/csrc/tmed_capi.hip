@@ -68,6 +68,8 @@ int tmed_init(int device, tmed_ctx **out) {
   if (const char *v = getenv("TMED_CHUNK")) c->chunk = (uint32_t)strtoul(v, nullptr, 10);
   if (const char *v = getenv("TMED_MAIN_WAVES")) c->main_waves = atoi(v);
   if (const char *v = getenv("TMED_SLAB_SLOTS")) c->slab_slots = (uint32_t)strtoul(v, nullptr, 10);
+  if (const char *v = getenv("TMED_LAT_MAX")) c->lat_max = (uint32_t)strtoul(v, nullptr, 10);
+  if (c->lat_max > kLatMax) c->lat_max = kLatMax;
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_slab, (size_t)c->slab_slots * kSlabSlotBytes);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_prep, (size_t)c->slab_slots * kPrepSlotBytes);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_fin, kFinBytes);          // 128 MB: projective R'

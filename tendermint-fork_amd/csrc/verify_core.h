@@ -396,6 +396,78 @@ TMED_HD void verify_main_comb_point(ge_p3 &acc, const uint32_t k[8], const uint3
   }
 }
 
+// ------------------------------------------------------------------ latency mode
+// A small batch (C1: one 175-validator commit) is bound by ONE lane's serial work — 64
+// dependent comb additions, then one inversion — not by throughput.  Latency mode:
+//  * splits a signature's 64 additions over kLatLanes = 8 lanes: lane r sums windows
+//    r, r+8, r+16, r+24 of both combs (comb_partial), and three cross-lane additions
+//    (level L = 1, 2, 4: lane r += lane r+L) combine the partial sums;
+//  * replaces the inversion by a strict decode of R, run concurrently by other lanes:
+//    encode(R') == R_bytes  iff  R_bytes is the canonical encoding of a curve point P_R
+//    (y < p, x^2 = (y^2-1)/(dy^2+1) solvable, not x = 0 with the sign bit set) and
+//    R' == P_R projectively (X' = x_R Z', Y' = y_R Z').  Both are exact.
+constexpr int kLatLanes = 8;
+
+// Partial comb sum of lane rr (0..7) of a signature: windows rr + 8t, t = 0..3.
+template <class AC, class BC>
+TMED_HD void comb_partial(ge_p3 &acc, const uint32_t kr[8], const uint32_t sr[8], int rr, const AC &acomb,
+                          const BC &bcomb) {
+  ge_p3_0(acc);
+  ge_p1p1 t;
+  ge_niels e;
+  const int sh = 8 * (rr & 3);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int w = rr + 8 * q;  // byte w of the recoded scalars: word 2q + (rr >> 2)
+    const uint32_t kw = (rr & 4) ? kr[2 * q + 1] : kr[2 * q];
+    const uint32_t sw = (rr & 4) ? sr[2 * q + 1] : sr[2 * q];
+    const int da = (int)((kw >> sh) & 0xffu) - 128;
+    const int db = (int)((sw >> sh) & 0xffu) - 128;
+    acomb.load(w, da < 0 ? -da : da, e);
+    niels_apply_sign(e, da < 0);
+    ge_madd_niels(t, acc, e, false);
+    ge_p1p1_to_p3(acc, t);
+    bcomb.load(w, db < 0 ? -db : db, e);
+    niels_apply_sign(e, db < 0);
+    ge_madd_niels(t, acc, e, false);
+    ge_p1p1_to_p3(acc, t);
+  }
+}
+
+// acc += o (both extended): one reduction step of the cross-lane tree.
+TMED_HD void ge_p3_add(ge_p3 &acc, const ge_p3 &o) {
+  ge_cached c;
+  ge_p1p1 t;
+  ge_p3_to_cached(c, o);
+  ge_add_cached(t, acc, c, false);
+  ge_p1p1_to_p3(acc, t);
+}
+
+// Strict decode of R (the set of byte strings Point.Bytes can produce): false unless R is
+// a canonical encoding of a curve point; then (x, y) is that point.
+TMED_HD bool r_decode_strict(fe &x, fe &y, const uint32_t Rw[8]) {
+  bool ones = (Rw[7] & 0x7fffffffu) == 0x7fffffffu;
+#pragma unroll
+  for (int i = 1; i < 7; i++) ones = ones && Rw[i] == 0xffffffffu;
+  const bool canonical = !(ones && Rw[0] >= 0xffffffedu);  // y < p = 2^255 - 19
+  ge_p3 P;
+  bool ok = ge_frombytes_go(P, Rw);
+  ok = ok && canonical && !(fe_iszero(P.X) && (Rw[7] >> 31) != 0);
+  fe_copy(x, P.X);
+  fe_copy(y, P.Y);
+  return ok;
+}
+
+// (X : Y : Z) == (x, y)
+TMED_HD bool projective_matches(const fe &X, const fe &Y, const fe &Z, const fe &x, const fe &y) {
+  fe t;
+  fe_mul(t, x, Z);
+  const bool a = fe_equal(t, X);
+  fe_mul(t, y, Z);
+  const bool b = fe_equal(t, Y);
+  return a && b && !fe_iszero(Z);
+}
+
 // enc([s]B) from the shared signed radix-256 comb of B (32 mixed additions; the device
 // signer, which generates the synthetic commits of the benches).
 template <class BC>

@@ -130,8 +130,7 @@ static void build_host_comb(HostComb &c, const uint32_t pw[8], bool negate, bool
   }
 }
 
-void hostsim_verify_comb_batch(const uint8_t *keys, size_t nkeys, const uint32_t *key_idx, const uint8_t *sig,
-                               const uint8_t *msgs, const uint32_t *off, size_t n, uint8_t *out) {
+static const HostComb &host_bcomb() {
   static HostComb bcomb;
   static bool binit = false;
   if (!binit) {
@@ -144,8 +143,12 @@ void hostsim_verify_comb_batch(const uint8_t *keys, size_t nkeys, const uint32_t
     build_host_comb(bcomb, bw, false, &ok);
     binit = true;
   }
-  std::vector<HostComb> ac(nkeys);
-  std::vector<uint8_t> kok(nkeys);
+  return bcomb;
+}
+
+static void build_key_combs(const uint8_t *keys, size_t nkeys, std::vector<HostComb> &ac, std::vector<uint8_t> &kok) {
+  ac.resize(nkeys);
+  kok.resize(nkeys);
   for (size_t k = 0; k < nkeys; k++) {
     uint32_t pw[8];
     load_words8(pw, keys + 32 * k);
@@ -153,6 +156,42 @@ void hostsim_verify_comb_batch(const uint8_t *keys, size_t nkeys, const uint32_t
     build_host_comb(ac[k], pw, true, &ok);
     kok[k] = ok;
   }
+}
+
+// Latency mode (verify_core.h): 8 partial comb sums, the device's cross-lane tree order,
+// strict decode of R and the projective compare — no inversion.
+void hostsim_verify_comb_lat(const uint8_t *keys, size_t nkeys, const uint32_t *key_idx, const uint8_t *sig,
+                             const uint8_t *msgs, const uint32_t *off, size_t n, uint8_t *out) {
+  const HostComb &bcomb = host_bcomb();
+  std::vector<HostComb> ac;
+  std::vector<uint8_t> kok;
+  build_key_combs(keys, nkeys, ac, kok);
+#pragma omp parallel for schedule(dynamic, 8)
+  for (long i = 0; i < (long)n; i++) {
+    uint32_t pw[8], sw[16], k[8], s[8], kr[8], sr[8];
+    const uint32_t v = key_idx[i];
+    load_words8(pw, keys + 32 * v);
+    load_words8(sw, sig + 64 * i);
+    load_words8(sw + 8, sig + 64 * i + 32);
+    const bool ok = verify_prep_comb(pw, kok[v] != 0, sw, msgs + off[i], off[i + 1] - off[i], k, s);
+    sc_recode256(kr, k);
+    sc_recode256(sr, s);
+    ge_p3 P[kLatLanes];
+    for (int r = 0; r < kLatLanes; r++) comb_partial(P[r], kr, sr, r, ac[v], bcomb);
+    for (int L = 1; L < kLatLanes; L <<= 1)
+      for (int r = 0; r + L < kLatLanes; r += 2 * L) ge_p3_add(P[r], P[r + L]);
+    fe xr, yr;
+    const bool rok = r_decode_strict(xr, yr, sw);
+    out[i] = (ok && rok && projective_matches(P[0].X, P[0].Y, P[0].Z, xr, yr)) ? 1 : 0;
+  }
+}
+
+void hostsim_verify_comb_batch(const uint8_t *keys, size_t nkeys, const uint32_t *key_idx, const uint8_t *sig,
+                               const uint8_t *msgs, const uint32_t *off, size_t n, uint8_t *out) {
+  const HostComb &bcomb = host_bcomb();
+  std::vector<HostComb> ac;
+  std::vector<uint8_t> kok;
+  build_key_combs(keys, nkeys, ac, kok);
   std::vector<ge_p2> pts(n);
 #pragma omp parallel for schedule(dynamic, 8)
   for (long i = 0; i < (long)n; i++) {

@@ -1,5 +1,6 @@
 """GPU parity: the gfx950 kernels through the C ABI vs the oracle (bit-exact decisions)."""
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -122,8 +123,31 @@ def test_product_signbytes_match_oracle():
         assert pvsb(cid, h, r, bid, ts, flag) == ovsb(cid, 2, h, r, bid if flag == 2 else None, ts)
 
 
-def test_keyset_golden_and_random(engine, golden):
-    """Key-cached comb path == generic path == oracle, on golden tuples grouped by key."""
+@pytest.fixture(params=["latency", "throughput"])
+def keyset_engine(request, engine):
+    """The default engine takes the latency kernels for key-cached batches up to TMED_LAT_MAX;
+    a second engine with TMED_LAT_MAX=0 forces the throughput kernels on the same inputs."""
+    if request.param == "latency":
+        yield engine
+        return
+    from tmed import Engine
+    old = os.environ.get("TMED_LAT_MAX")
+    os.environ["TMED_LAT_MAX"] = "0"
+    try:
+        e = Engine(0)
+    finally:
+        if old is None:
+            del os.environ["TMED_LAT_MAX"]
+        else:
+            os.environ["TMED_LAT_MAX"] = old
+    yield e
+    e.close()
+
+
+def test_keyset_golden_and_random(keyset_engine, golden):
+    """Key-cached comb path == generic path == oracle, on golden tuples grouped by key, through
+    both the latency kernels (strict R decode + projective compare) and the throughput ones."""
+    engine = keyset_engine
     vs = [v for v in golden if len(v["sig"]) == 128]
     keys = sorted({v["pub"] for v in vs})
     kidx = {k: i for i, k in enumerate(keys)}

@@ -111,12 +111,19 @@ def test_sign_matches_oracle(hostsim):
         assert pub[i].tobytes() == port.pubkey_from_seed(seeds[i].tobytes())
 
 
-def test_comb_path_hostsim(hostsim, golden):
+@pytest.mark.parametrize("fn", ["hostsim_verify_comb_batch", "hostsim_verify_comb_lat"])
+def test_comb_path_hostsim(hostsim, golden, fn):
     """Key-cached (radix-256 comb) verification, host build of the kernel code, vs the oracle:
-    golden tuples grouped by key (incl. small-order, non-canonical and undecodable keys)."""
-    vs = [v for v in golden if len(v["sig"]) == 128][::4]
-    keys = sorted({v["pub"] for v in vs})[:40]
-    vs = [v for v in vs if v["pub"] in keys]
+    golden tuples grouped by key (incl. small-order, non-canonical and undecodable keys).
+    _lat: latency mode (8 partial comb sums + cross-lane tree, strict R decode + projective
+    compare instead of the inversion) — covers the non-canonical / off-curve / x=0-sign R
+    classes of the golden set."""
+    per = {}
+    for v in golden:  # up to 5 tuples of every edge class, so each R / A / S class is hit
+        if len(v["sig"]) == 128 and len(per.setdefault(v["class"], [])) < 5:
+            per[v["class"]].append(v)
+    vs = [v for c in sorted(per) for v in per[c]]
+    keys = sorted({v["pub"] for v in vs})
     kidx = {k: i for i, k in enumerate(keys)}
     karr = np.array([np.frombuffer(bytes.fromhex(k), np.uint8) for k in keys])
     idx = np.array([kidx[v["pub"]] for v in vs], np.uint32)
@@ -126,8 +133,8 @@ def test_comb_path_hostsim(hostsim, golden):
     offs[1:] = np.cumsum([len(m) for m in ms])
     msgs = np.frombuffer(b"".join(ms) + b"\0", np.uint8)
     out = np.zeros(len(vs), np.uint8)
-    hostsim.hostsim_verify_comb_batch(_p(karr), ctypes.c_size_t(len(keys)), _p(idx), _p(sigs), _p(msgs), _p(offs),
-                                      ctypes.c_size_t(len(vs)), _p(out))
+    getattr(hostsim, fn)(_p(karr), ctypes.c_size_t(len(keys)), _p(idx), _p(sigs), _p(msgs), _p(offs),
+                         ctypes.c_size_t(len(vs)), _p(out))
     exp = np.array([v["valid"] for v in vs], np.uint8)
     assert (out == exp).all(), [vs[i]["class"] for i in np.nonzero(out != exp)[0]]
     assert exp.sum() > 10 and (exp == 0).sum() > 10
