@@ -14,6 +14,7 @@
 //   3. CanonicalVote sign-bytes (signbytes.hip), ONE device batch (tmed_verify_batch)
 //   4. replay of the reference loop over the validity bits — first-error index, early
 //      exit, Got/Needed and error kinds come out identical by construction.
+#include <chrono>
 #include <string.h>
 
 #include <algorithm>
@@ -39,6 +40,27 @@ bool block_id_equal(const tmed_block_id &a, const tmed_block_id &b) {  // types/
   if (a.psh_hash_len && memcmp(a.psh_hash, b.psh_hash, a.psh_hash_len) != 0) return false;
   return true;
 }
+
+// TMED_TRACE=1: per-phase wall times of every seam call on stderr (diagnostics only).
+static bool trace_on() {
+  static const bool on = getenv("TMED_TRACE") != nullptr;
+  return on;
+}
+struct PhaseClock {
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  char buf[512];
+  int len = 0;
+  void lap(const char *name) {
+    if (!trace_on()) return;
+    const auto now = std::chrono::steady_clock::now();
+    const double us = std::chrono::duration<double, std::micro>(now - t).count();
+    t = now;
+    if (len < (int)sizeof(buf) - 48) len += snprintf(buf + len, sizeof(buf) - len, " %s=%.0fus", name, us);
+  }
+  void emit(const char *what, size_t n, size_t m) {
+    if (trace_on()) fprintf(stderr, "[tmed] %s n=%zu m=%zu%.*s\n", what, n, m, len, buf);
+  }
+};
 
 // safeMul (types/validator_set.go:1086-1105)
 bool safe_mul(int64_t a, int64_t b, int64_t *out) {
@@ -434,11 +456,13 @@ static int seam_replay(const tmed_commit_request *reqs, size_t n, tmed_commit_re
 
 static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, const BatchVerifier &verify) {
   if (n && (!reqs || !out)) return TMED_EINVAL;
+  PhaseClock clk;
   std::vector<Plan> plans;
   std::vector<Cand> cands;
   AddrCache cache;
   int rc = seam_plan(reqs, n, out, plans, cands, cache);
   if (rc != TMED_OK) return rc;
+  clk.lap("plan");
   // ---- one device batch for every candidate of every request
   const size_t m = cands.size();
   std::vector<uint8_t> valid(m, 0);
@@ -446,7 +470,11 @@ static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_resul
     rc = verify(reqs, n, cands, valid.data());
     if (rc != TMED_OK) return rc;
   }
-  return seam_replay(reqs, n, out, plans, valid.data());
+  clk.lap("verify");
+  rc = seam_replay(reqs, n, out, plans, valid.data());
+  clk.lap("replay");
+  clk.emit("seam", n, m);
+  return rc;
 }
 
 extern "C" int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out,
@@ -569,11 +597,13 @@ static int device_templates(const tmed_commit_request *reqs, size_t n, const std
 // through the key-cached kernels, one launch sequence per distinct key set.
 static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands,
                       uint8_t *valid) {
+  PhaseClock clk;
   std::vector<uint8_t> tmpl;
   bool fits = true;
   int rc = device_templates(reqs, n, cands, tmpl, &fits);
   if (rc != TMED_OK) return rc;
   if (!fits) return ctx_verify_host_msgs(ctx, reqs, n, cands, valid);
+  clk.lap("templates");
   // group by key set (usually a single group)
   std::vector<uint64_t> gkeys;
   std::vector<std::vector<uint32_t>> gidx;
@@ -590,11 +620,17 @@ static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, 
     const uint32_t m = (uint32_t)ix.size();
     tmed::VoteStage st;
     rc = stage_group(ctx, reqs, n, cands, ix.data(), m, gkeys[g], tmpl.data(), 0, st);
+    clk.lap("stage");
     std::vector<uint8_t> out(m);
     if (rc == TMED_OK) rc = tmed::votes_launch(ctx, st, out.data());
     if (rc != TMED_OK) return rc;
+    clk.lap("device");
+    if (trace_on()) fprintf(stderr, "[tmed] group %zu: %u votes, assemble+verify kernels %.0fus\n", g, m,
+                            1000.0 * ctx->last_ms);
     scatter_bits(reqs, cands, ix.data(), m, out.data(), valid);
+    clk.lap("scatter");
   }
+  clk.emit("ctx_verify", n, cands.size());
   return TMED_OK;
 }
 

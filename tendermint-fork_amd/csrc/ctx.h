@@ -134,4 +134,14 @@ struct tmed_ctx {
   tmed::DevBuf d_merkle_a, d_merkle_b, d_merkle_idx;  // Merkle level digests (ping-pong) + level indexes
   std::unordered_map<uint64_t, tmed::Keyset> keysets;
   uint64_t next_keyset = 1;
+  // The verify scratch (slab, prep hand-off, finish buffers) is shared by every call on the
+  // context, but the device-pointer entry points run on the CALLER's stream: each user of
+  // the scratch first makes its stream wait for the previous user (scratch_ev, whatever its
+  // stream), then records itself.  Both under mu.
+  hipEvent_t scratch_ev = nullptr;
 };
+
+namespace tmed {
+inline hipError_t scratch_acquire(tmed_ctx *c, hipStream_t s) { return hipStreamWaitEvent(s, c->scratch_ev, 0); }
+inline hipError_t scratch_release(tmed_ctx *c, hipStream_t s) { return hipEventRecord(c->scratch_ev, s); }
+}  // namespace tmed

@@ -96,7 +96,8 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   VoteSlot &vs = c->vslot[st.slot];
   uint8_t *d = (uint8_t *)vs.d_votes.p;
   hipStream_t s = c->stream;
-  hipError_t e = hipMemcpyAsync(d, vs.h_votes.p, st.total, hipMemcpyHostToDevice, s);
+  hipError_t e = scratch_acquire(c, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(d, vs.h_votes.p, st.total, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipEventRecord(vs.ev0, s);
   if (e == hipSuccess)
     e = launch_assemble_votes(d + st.o_tmpl, (const uint32_t *)(d + st.o_tidx), d + st.o_flag,
@@ -112,6 +113,7 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
                         c->d_fin_pre, s, c->chunk, c->main_waves, /*msg_slots=*/true);
   }
   if (e == hipSuccess) e = hipEventRecord(vs.ev1, s);
+  if (e == hipSuccess) e = scratch_release(c, s);
   if (e == hipSuccess) e = hipMemcpyAsync(vs.h_out.p, vs.d_out.p, m, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipEventRecord(vs.done, s);
   return map_err(e);
@@ -195,12 +197,16 @@ int tmed_verify_batch_keyset_device(tmed_ctx *c, uint64_t handle, const uint32_t
   if (!c) return TMED_EINVAL;
   if (n == 0) return TMED_OK;
   if (!d_val_idx || !d_sigs || !d_msgs || !d_msg_off || !d_out || n > 0xffffffffu) return TMED_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
   auto it = c->keysets.find(handle);
   if (it == c->keysets.end()) return TMED_ENOKEYSET;
   const Keyset &k = it->second;
   (void)hipSetDevice(c->device);
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  return map_err(keyset_verify(c, k, d_val_idx, d_sigs, d_msgs, d_msg_off, (uint32_t)n, d_out, s, false));
+  hipError_t e = scratch_acquire(c, s);
+  if (e == hipSuccess) e = keyset_verify(c, k, d_val_idx, d_sigs, d_msgs, d_msg_off, (uint32_t)n, d_out, s, false);
+  if (e == hipSuccess) e = scratch_release(c, s);
+  return map_err(e);
 }
 
 int tmed_verify_batch_keyset(tmed_ctx *c, uint64_t handle, const uint32_t *val_idx, const uint8_t *sigs,
@@ -240,11 +246,13 @@ int tmed_verify_batch_keyset(tmed_ctx *c, uint64_t handle, const uint32_t *val_i
   if (e == hipSuccess) e = hipMemcpyAsync(c->d_b.p, c->h_b.p, n * 64, hipMemcpyHostToDevice, s);
   if (e == hipSuccess && mbytes) e = hipMemcpyAsync(c->d_msg.p, c->h_msg.p, mbytes, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemcpyAsync(c->d_off.p, c->h_off.p, moff, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = scratch_acquire(c, s);
   if (e == hipSuccess) e = hipEventRecord(c->ev0, s);
   if (e == hipSuccess)
     e = keyset_verify(c, k, (const uint32_t *)c->d_a.p, (const uint8_t *)c->d_b.p, (const uint8_t *)c->d_msg.p,
                       (const uint32_t *)c->d_off.p, (uint32_t)n, (uint8_t *)c->d_out.p, s, false);
   if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
+  if (e == hipSuccess) e = scratch_release(c, s);
   if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, n, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return map_err(e);

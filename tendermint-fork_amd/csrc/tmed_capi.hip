@@ -54,6 +54,7 @@ int tmed_init(int device, tmed_ctx **out) {
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->scratch_ev, hipEventDisableTiming);
   static ge_niels bt[kBTabSize];
   static std::once_flag bt_once;
   std::call_once(bt_once, [] { host_build_btab(bt); });
@@ -111,6 +112,7 @@ void tmed_destroy(tmed_ctx *c) {
   }
   for (auto &kv : c->keysets) free_keyset(kv.second);
   c->keysets.clear();
+  if (c->scratch_ev) hipEventDestroy(c->scratch_ev);
   if (c->d_bcomb) hipFree(c->d_bcomb);
   if (c->d_slab) hipFree(c->d_slab);
   if (c->d_prep) hipFree(c->d_prep);
@@ -160,11 +162,14 @@ int tmed_verify_batch_device(tmed_ctx *c, const uint8_t *d_pub, const uint8_t *d
   if (n == 0) return TMED_OK;
   if (!d_pub || !d_sig || !d_msgs || !d_off || !d_out || n > 0xffffffffu) return TMED_EINVAL;
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  std::lock_guard<std::mutex> lk(c->mu);
   hipSetDevice(c->device);
   if (c->timing) c->timer.n = 0;
-  hipError_t e = launch_verify(d_pub, d_sig, d_msgs, d_off, (uint32_t)n, d_out, c->d_slab, c->slab_slots,
-                               c->d_btab, c->d_prep, c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves, false,
-                               c->timing ? &c->timer : nullptr);
+  hipError_t e = scratch_acquire(c, s);
+  if (e == hipSuccess)
+    e = launch_verify(d_pub, d_sig, d_msgs, d_off, (uint32_t)n, d_out, c->d_slab, c->slab_slots, c->d_btab, c->d_prep,
+                      c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves, false, c->timing ? &c->timer : nullptr);
+  if (e == hipSuccess) e = scratch_release(c, s);
   return map_err(e);
 }
 
@@ -215,12 +220,14 @@ int tmed_verify_batch(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, const
   if (e == hipSuccess) e = hipMemcpyAsync(c->d_b.p, c->h_b.p, n * 64, hipMemcpyHostToDevice, s);
   if (e == hipSuccess && mbytes) e = hipMemcpyAsync(c->d_msg.p, c->h_msg.p, mbytes, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemcpyAsync(c->d_off.p, c->h_off.p, moff_bytes, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = scratch_acquire(c, s);
   if (e == hipSuccess) e = hipEventRecord(c->ev0, s);
   if (e == hipSuccess)
     e = launch_verify((const uint8_t *)c->d_a.p, (const uint8_t *)c->d_b.p, (const uint8_t *)c->d_msg.p,
                       (const uint32_t *)c->d_off.p, (uint32_t)n, (uint8_t *)c->d_out.p, c->d_slab, c->slab_slots,
                       c->d_btab, c->d_prep, c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves);
   if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
+  if (e == hipSuccess) e = scratch_release(c, s);
   if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, n, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return map_err(e);
