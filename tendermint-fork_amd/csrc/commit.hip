@@ -77,47 +77,35 @@ struct Cand {
   int32_t val_idx;
 };
 
-struct AddrKey {
-  uint64_t a, b;
-  uint32_t c;
-  bool operator==(const AddrKey &o) const { return a == o.a && b == o.b && c == o.c; }
-};
-struct AddrHash {
-  size_t operator()(const AddrKey &k) const { return k.a * 0x9E3779B97F4A7C15ull ^ k.b ^ ((uint64_t)k.c << 17); }
-};
-AddrKey addr_key(const uint8_t *p) {
-  AddrKey k;
-  memcpy(&k.a, p, 8);
-  memcpy(&k.b, p + 8, 8);
-  memcpy(&k.c, p + 16, 4);
-  return k;
-}
-
 // address -> first validator index with that address (GetByAddress, types/validator_set.go:270-278
 // returns the first match).  Flat open-addressing table: a light-client batch builds one per
 // trusted set (10k sets x 175 validators in C3), so construction cost matters.
 struct AddrIndex {
-  std::vector<AddrKey> keys;
-  std::vector<int32_t> vals;  // -1 = empty
+  const uint8_t *addrs = nullptr;  // the set's n x 20 address array (owned by the request)
+  std::vector<int32_t> vals;       // validator index, -1 = empty
   size_t mask = 0;
+  static size_t slot_of(const uint8_t *p) {  // addresses are SHA-256 truncations: 8 bytes mix well
+    uint64_t a;
+    memcpy(&a, p, 8);
+    return (size_t)((a * 0x9E3779B97F4A7C15ull) >> 20);
+  }
   void build(const uint8_t *addresses, size_t n) {
+    addrs = addresses;
     size_t cap = 16;
     while (cap < 2 * n + 1) cap <<= 1;
     mask = cap - 1;
-    keys.assign(cap, AddrKey{0, 0, 0});
     vals.assign(cap, -1);
     for (size_t v = 0; v < n; v++) {
-      const AddrKey k = addr_key(addresses + 20 * v);
-      size_t h = AddrHash()(k) & mask;
-      while (vals[h] >= 0 && !(keys[h] == k)) h = (h + 1) & mask;
-      if (vals[h] < 0) { keys[h] = k; vals[h] = (int32_t)v; }  // keep the first match
+      const uint8_t *a = addresses + 20 * v;
+      size_t h = slot_of(a) & mask;
+      while (vals[h] >= 0 && memcmp(addrs + 20 * (size_t)vals[h], a, 20) != 0) h = (h + 1) & mask;
+      if (vals[h] < 0) vals[h] = (int32_t)v;  // keep the first match
     }
   }
   int32_t find(const uint8_t *addr) const {
-    const AddrKey k = addr_key(addr);
-    size_t h = AddrHash()(k) & mask;
+    size_t h = slot_of(addr) & mask;
     while (vals[h] >= 0) {
-      if (keys[h] == k) return vals[h];
+      if (memcmp(addrs + 20 * (size_t)vals[h], addr, 20) == 0) return vals[h];
       h = (h + 1) & mask;
     }
     return -1;
@@ -127,8 +115,32 @@ struct AddrIndex {
 struct Plan {
   bool decided = false;
   int64_t needed = 0;
-  std::vector<int32_t> bit_of_sig;  // sig idx -> candidate slot (-1 = not sent)
+  int32_t *bit_of_sig = nullptr;  // sig idx -> candidate slot in its planning part (-1 = not sent)
+  size_t cand_off = 0;            // + the part's offset in the merged candidate list
   const AddrIndex *addr_index = nullptr;  // Trusting only (shared by requests on the same valset)
+};
+
+// The plans of one seam call; bit_of_sig of every request lives in one flat array.
+struct Plans {
+  std::vector<Plan> v;
+  std::vector<int32_t> bits;
+};
+
+// Per-thread "seen" marks of the Trusting loops (first index of each validator), reset in
+// O(1) per request by an epoch stamp instead of a fresh n-sized vector.
+struct SeenMarks {
+  std::vector<int32_t> idx;
+  std::vector<uint32_t> stamp;
+  uint32_t epoch = 0;
+  void reset(size_t n) {
+    if (++epoch == 0 || stamp.size() < n) {
+      stamp.assign(std::max(n, stamp.size()), 0);
+      idx.resize(stamp.size());
+      epoch = 1;
+    }
+  }
+  int32_t get(int32_t v) const { return stamp[v] == epoch ? idx[v] : -1; }
+  void set(int32_t v, int32_t i) { stamp[v] = epoch; idx[v] = i; }
 };
 
 int check_request(const tmed_commit_request &r) {
@@ -270,7 +282,7 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
   if (rc != TMED_OK) return rc;
   const tmed_valset &vs = *r.vals;
   const tmed_commit &c = *r.commit;
-  pl.bit_of_sig.assign(c.n_sigs, -1);
+  std::fill(pl.bit_of_sig, pl.bit_of_sig + c.n_sigs, -1);
   if (r.mode != TMED_MODE_LIGHT_TRUSTING) {
     if (vs.n != c.n_sigs) {
       o.code = TMED_COMMIT_WRONG_SET_SIZE; o.expected = (int64_t)vs.n; o.actual = (int64_t)c.n_sigs;
@@ -308,14 +320,15 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
     if (safe_mul(vs.total_power, r.trust_num, &prod)) { o.code = TMED_COMMIT_OVERFLOW; pl.decided = true; return TMED_OK; }
     pl.needed = prod / r.trust_den;  // Go int64 division truncates toward zero, as C++ does
     pl.addr_index = cache.at(r.vals).get();
-    std::vector<int32_t> seen(vs.n, -1);
+    thread_local SeenMarks seen;
+    seen.reset(vs.n);
     int64_t tally = 0;
     for (size_t i = 0; i < c.n_sigs; i++) {
       if (c.flags[i] != kCommit) continue;
       const int32_t v = pl.addr_index->find(c.addresses + 20 * i);
       if (v < 0) continue;
-      if (seen[v] >= 0) break;  // the loop returns the double-vote error here
-      seen[v] = (int32_t)i;
+      if (seen.get(v) >= 0) break;  // the loop returns the double-vote error here
+      seen.set(v, (int32_t)i);
       pl.bit_of_sig[i] = (int32_t)cands.size();
       cands.push_back({q, (int32_t)i, v});
       tally += vs.powers[v];
@@ -328,8 +341,13 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
 // Worker count for host loops over `items` units of work (requests x signatures).
 static unsigned host_threads(size_t items) {
   if (items < (1u << 16)) return 1;
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  return std::min(16u, hw);
+  static const unsigned cap = [] {
+    const char *v = getenv("TMED_HOST_THREADS");  // default 16: one GPU's share of a node's cores
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const unsigned want = v ? (unsigned)std::max(1, atoi(v)) : 16u;
+    return std::min(want, hw);
+  }();
+  return cap;
 }
 
 template <class F>
@@ -348,13 +366,26 @@ static size_t total_sigs(const tmed_commit_request *reqs, size_t n) {
 }
 
 // Candidates of requests [0, n) in request order (identical to a serial plan).
-static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, std::vector<Plan> &plans,
+static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, Plans &ps,
                      std::vector<Cand> &cands, AddrCache &cache) {
+  PhaseClock clk;
+  std::vector<Plan> &plans = ps.v;
   plans.assign(n, Plan());
   cands.clear();
-  for (size_t q = 0; q < n; q++)
+  size_t nbits = 0;
+  for (size_t q = 0; q < n; q++) {
     if (check_request(reqs[q]) != TMED_OK) return TMED_EINVAL;
+    nbits += reqs[q].commit->n_sigs;
+  }
+  ps.bits.resize(nbits);
+  nbits = 0;
+  for (size_t q = 0; q < n; q++) {
+    plans[q].bit_of_sig = ps.bits.data() + nbits;
+    nbits += reqs[q].commit->n_sigs;
+  }
+  clk.lap("check");
   build_addr_cache(reqs, n, cache);
+  clk.lap("addr_cache");
   const unsigned nt = host_threads(total_sigs(reqs, n));
   if (nt <= 1) {
     for (size_t q = 0; q < n; q++) {
@@ -368,22 +399,25 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
   std::vector<int> rcs(nt, TMED_OK);
   parallel_ranges(n, nt, [&](size_t lo, size_t hi, unsigned t) {
     lo_of[t] = lo; hi_of[t] = hi;
+    size_t cap = 0;
+    for (size_t q = lo; q < hi; q++) cap += reqs[q].commit->n_sigs;
+    part[t].reserve(cap);
     for (size_t q = lo; q < hi && rcs[t] == TMED_OK; q++) rcs[t] = plan_request(reqs, q, out[q], plans[q], part[t], cache);
   });
   for (int rc : rcs)
     if (rc != TMED_OK) return rc;
+  clk.lap("plan_requests");
   std::vector<size_t> base(nt + 1, 0);
   for (unsigned t = 0; t < nt; t++) base[t + 1] = base[t] + part[t].size();
   cands.resize(base[nt]);
   parallel_ranges(nt, nt, [&](size_t lo, size_t hi, unsigned) {
     for (size_t t = lo; t < hi; t++) {
       std::copy(part[t].begin(), part[t].end(), cands.begin() + base[t]);
-      if (base[t])
-        for (size_t q = lo_of[t]; q < hi_of[t]; q++)
-          for (int32_t &k : plans[q].bit_of_sig)
-            if (k >= 0) k += (int32_t)base[t];
+      for (size_t q = lo_of[t]; q < hi_of[t]; q++) plans[q].cand_off = base[t];
     }
   });
+  clk.lap("merge");
+  clk.emit("plan", n, cands.size());
   return TMED_OK;
 }
 
@@ -396,7 +430,7 @@ static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, c
     const int32_t k = pl.bit_of_sig[i];
     if (k < 0) { *ok = false; return false; }
     o.verified++;
-    return valid[(size_t)k] != 0;
+    return valid[pl.cand_off + (size_t)k] != 0;
   };
   bool ok = true;
   int64_t tally = 0;
@@ -420,16 +454,17 @@ static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, c
     }
     if (o.code < 0 && ok) { o.code = TMED_COMMIT_NOT_ENOUGH_POWER; o.got = tally; o.needed = pl.needed; }
   } else {
-    std::vector<int32_t> seen(vs.n, -1);
+    thread_local SeenMarks seen;
+    seen.reset(vs.n);
     for (size_t i = 0; i < c.n_sigs && o.code < 0; i++) {
       if (c.flags[i] != kCommit) continue;
       const int32_t v = pl.addr_index->find(c.addresses + 20 * i);
       if (v < 0) continue;
-      if (seen[v] >= 0) {
-        o.code = TMED_COMMIT_DOUBLE_VOTE; o.val_idx = v; o.idx_first = seen[v]; o.idx = (int32_t)i;
+      if (seen.get(v) >= 0) {
+        o.code = TMED_COMMIT_DOUBLE_VOTE; o.val_idx = v; o.idx_first = seen.get(v); o.idx = (int32_t)i;
         break;
       }
-      seen[v] = (int32_t)i;
+      seen.set(v, (int32_t)i);
       if (!bit(i, &ok)) { if (ok) { o.code = TMED_COMMIT_WRONG_SIGNATURE; o.idx = (int32_t)i; } break; }
       tally += vs.powers[v];
       if (tally > pl.needed) o.code = TMED_COMMIT_OK;
@@ -440,7 +475,8 @@ static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, c
 }
 
 static int seam_replay(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out,
-                       const std::vector<Plan> &plans, const uint8_t *valid) {
+                       const Plans &ps, const uint8_t *valid) {
+  const std::vector<Plan> &plans = ps.v;
   const unsigned nt = host_threads(total_sigs(reqs, n));
   std::vector<int> rcs(std::max(1u, nt), TMED_OK);
   parallel_ranges(n, nt, [&](size_t lo, size_t hi, unsigned t) {
@@ -457,7 +493,7 @@ static int seam_replay(const tmed_commit_request *reqs, size_t n, tmed_commit_re
 static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, const BatchVerifier &verify) {
   if (n && (!reqs || !out)) return TMED_EINVAL;
   PhaseClock clk;
-  std::vector<Plan> plans;
+  Plans plans;
   std::vector<Cand> cands;
   AddrCache cache;
   int rc = seam_plan(reqs, n, out, plans, cands, cache);
@@ -647,7 +683,7 @@ extern "C" int tmed_verify_commits(tmed_ctx *ctx, const tmed_commit_request *req
 namespace {
 struct BsBatch {
   size_t lo = 0, n = 0;
-  std::vector<Plan> plans;
+  Plans plans;
   std::vector<Cand> cands;
   AddrCache cache;
   std::vector<uint8_t> tmpl, bits, valid;
