@@ -68,16 +68,8 @@ def main():
     from tmed import Engine, lib
     from tmed.workload import c2_messages, c2_seeds
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    else:
-        torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    from tmed.launch import dist_setup
+    world, rank, local_rank, dev, coll = dist_setup()
     eng = Engine(local_rank)
     n = args.n
 
@@ -126,10 +118,10 @@ def main():
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     valid = int(d_out.sum().item())
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tally = torch.tensor([valid, n], dtype=torch.int64, device=dev)
+        tally = torch.tensor([valid, n], dtype=torch.int64, device=coll)
         dist.all_reduce(tally)  # int64 tally all-reduce
         valid_all, n_all = int(tally[0].item()), int(tally[1].item())
     else:

@@ -203,14 +203,8 @@ def main():
     import torch
     import torch.distributed as dist
     from tmed import Engine
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+    from tmed.launch import dist_setup
+    world, rank, local, dev, coll = dist_setup()
     eng = Engine(local)
     for cfg in args.config.split(","):
         if cfg == "c1" and rank == 0:
@@ -218,7 +212,7 @@ def main():
         elif cfg == "c3" and rank == 0:
             r = c3(eng, args.headers, args.gap, not args.no_keyset)
         elif cfg == "c4":
-            r = c4(eng, args.blocks, args.validators, rank, world, dev, args.window, args.batch)
+            r = c4(eng, args.blocks, args.validators, rank, world, coll, args.window, args.batch)
         else:
             continue
         if rank == 0:

@@ -1,0 +1,30 @@
+"""Process-group setup shared by the benches: one process per GPU (torchrun env), RCCL over
+xGMI for the small tally collectives.  TMED_DIST_BACKEND=gloo rehearses N ranks on fewer
+GPUs (rank r uses device LOCAL_RANK % device_count, collectives run on CPU tensors) — how
+the multi-rank paths are exercised on a one-GPU box; the driver's 8-GPU runs use RCCL."""
+from __future__ import annotations
+
+import os
+
+
+def dist_setup():
+    """Returns (world, rank, local_rank, device, collective_device)."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("TMED_DIST_BACKEND", "nccl")
+    ndev = max(1, torch.cuda.device_count())
+    local = local % ndev if backend == "gloo" else local
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    coll = dev
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+            coll = torch.device("cpu")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    return world, rank, local, dev, coll
