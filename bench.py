@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=150_000, help="signatures timed on the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-peak", action="store_true")
+    ap.add_argument("--mix", choices=["c2", "c5"], default="c2",
+                    help="c5: 1%% of the batch replaced by edge-case / invalid tuples (BASELINE C5)")
     return ap.parse_args()
 
 
@@ -90,6 +92,14 @@ def main():
     stream = torch_stream.cuda_stream
     eng.sign_device(d_seed, d_msg, d_off, d_sig, d_pub, n, stream)
     torch.cuda.synchronize(dev)
+    n_adv = 0
+    if args.mix == "c5":
+        from tmed.workload import c5_mix
+        hp, hs = d_pub.cpu().numpy(), d_sig.cpu().numpy()
+        n_adv = len(c5_mix(hp, hs, seed=0x5EED + rank))
+        d_pub.copy_(torch.from_numpy(hp))
+        d_sig.copy_(torch.from_numpy(hs))
+        torch.cuda.synchronize(dev)
     t_gen = time.time() - t_gen
 
     def step():
@@ -163,7 +173,7 @@ def main():
                     "algorithmic_bytes_per_verify": 32 + 64 + int(offs[-1]) // n + 4 + 1}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(eng, d_pub, d_sig, msgs, offs, min(args.cpu_sample, n))
+            cpu = cpu_baseline(eng, d_pub, d_sig, msgs, offs, min(args.cpu_sample, n), d_out)
         result = {
             "metric": "ed25519 verifies/sec at 1/8 MI355X",
             "value": round(value, 1),
@@ -176,11 +186,14 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32 (GF(2^255-19) radix 2^25.5 limbs, int64 accumulate)",
-            "data": "synthetic (C2: distinct key per signature, CanonicalVote sign-bytes, GPU RFC 8032 signer)",
-            "config": {"workload": "C2: raw batch of %d ed25519 signatures per GPU" % n,
+            "data": "synthetic (C2: distinct key per signature, CanonicalVote sign-bytes, GPU RFC 8032 signer%s)"
+                    % (", 1% replaced by edge-case/invalid tuples" if n_adv else ""),
+            "config": {"workload": ("C5: adversarial mix, %d ed25519 signatures per GPU with %d edge-case/invalid"
+                                    % (n, n_adv)) if n_adv else "C2: raw batch of %d ed25519 signatures per GPU" % n,
                        "signatures_per_gpu": n, "avg_msg_bytes": round(int(offs[-1]) / n, 1),
                        "key_cache": False, "parallelism": "shard-per-gpu x%d" % world},
             "valid": valid_all, "checked": n_all, "all_valid": valid_all == n_all and ok_first == n,
+            "adversarial_per_gpu": n_adv,
             "roofline": roof,
             "cpu_baseline": cpu,
             "setup_s": round(t_gen, 2),
@@ -208,8 +221,9 @@ def pmc_traffic(sigs_per_launch):
     return None, None
 
 
-def cpu_baseline(eng, d_pub, d_sig, msgs, offs, m):
-    """Single-thread C restatement of the Go verify on the first m tuples (oracle/ed25519_port.c)."""
+def cpu_baseline(eng, d_pub, d_sig, msgs, offs, m, d_out):
+    """Single-thread C restatement of the Go verify on the first m tuples (oracle/ed25519_port.c);
+    its decisions are also compared with the GPU's on that sample."""
     sys.path.insert(0, ROOT)
     from oracle import port  # cpu_baseline leg only
     pubs = d_pub[:m].cpu().numpy()
@@ -219,9 +233,11 @@ def cpu_baseline(eng, d_pub, d_sig, msgs, offs, m):
     out = port.verify_batch(pubs, sigs, msgs, o, nthreads=1)
     dt = time.perf_counter() - t
     ncores = os.cpu_count() or 1
+    gpu = d_out[:m].cpu().numpy()
     return {"value": round(m / dt, 1), "unit": "verifies/s", "cores": 1, "kind": "port",
-            "sample": "first %d signatures of the same C2 batch, 1 thread, %.1f s; all_valid=%s; host cpu_count=%d"
-                      % (m, dt, bool(out.all()), ncores)}
+            "sample": "first %d signatures of the same batch, 1 thread, %.1f s; valid=%d; host cpu_count=%d"
+                      % (m, dt, int(out.sum()), ncores),
+            "gpu_decisions_match": bool((gpu == out).all())}
 
 
 if __name__ == "__main__":

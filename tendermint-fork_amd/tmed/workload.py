@@ -118,3 +118,43 @@ def sign_commits(engine, chain_id: str, specs, sign_upto: int | None = None):
         out.append(PackedCommit(height, round_, bid, fl, a, sec, nan, s, lens))
         k += ns
     return out
+
+
+# The eight small-order points of edwards25519 (canonical encodings, and the two with the
+# x = 0 sign bit set): public constants, the same set as the oracle's small_order_points().
+SMALL_ORDER = [bytes.fromhex(h) for h in (
+    "0100000000000000000000000000000000000000000000000000000000000000",
+    "ecffffffffffffffffffffffffffffffffffffffffffffffffffffffffffff7f",
+    "0000000000000000000000000000000000000000000000000000000000000000",
+    "0000000000000000000000000000000000000000000000000000000000000080",
+    "c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac037a",
+    "26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05",
+    "26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc85",
+    "c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac03fa")]
+_L = 2 ** 252 + 27742317777372353535851937790883648493
+_P = 2 ** 255 - 19
+
+
+def c5_mix(pubs: np.ndarray, sigs: np.ndarray, seed: int = 0x5EED, frac: float = 0.01) -> np.ndarray:
+    """BASELINE C5 in place: `frac` of the tuples (uniform, seeded) replaced, cycling over the
+    edge classes of SURVEY §8c — R/S/M bit flip, S + L, small-order A, small-order R,
+    non-canonical A (y = p + small), R sign flip.  Returns the modified indices."""
+    n = pubs.shape[0]
+    rng = np.random.default_rng(seed)
+    idx = rng.choice(n, int(n * frac), replace=False)
+    for j, i in enumerate(idx):
+        k = j % 6
+        if k == 0:
+            sigs[i, rng.integers(0, 64)] ^= np.uint8(1 << int(rng.integers(0, 8)))
+        elif k == 1:
+            s = int.from_bytes(sigs[i, 32:].tobytes(), "little") + _L
+            sigs[i, 32:] = np.frombuffer(s.to_bytes(32, "little"), np.uint8)
+        elif k == 2:
+            pubs[i] = np.frombuffer(SMALL_ORDER[j % 8], np.uint8)
+        elif k == 3:
+            sigs[i, :32] = np.frombuffer(SMALL_ORDER[j % 8], np.uint8)
+        elif k == 4:
+            pubs[i] = np.frombuffer((int(rng.integers(0, 19)) + _P).to_bytes(32, "little"), np.uint8)
+        else:
+            sigs[i, 31] ^= np.uint8(0x80)
+    return idx
