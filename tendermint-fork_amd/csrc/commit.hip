@@ -75,6 +75,10 @@ struct Cand {
   size_t req;
   int32_t sig_idx;
   int32_t val_idx;
+  // no zero-fill: the merged candidate list of a large call (tens of MB) is resized and
+  // then overwritten in parallel, so value-initialising it would be a serial memset
+  Cand() {}
+  Cand(size_t r, int32_t s, int32_t v) : req(r), sig_idx(s), val_idx(v) {}
 };
 
 // address -> first validator index with that address (GetByAddress, types/validator_set.go:270-278
@@ -120,10 +124,24 @@ struct Plan {
   const AddrIndex *addr_index = nullptr;  // Trusting only (shared by requests on the same valset)
 };
 
-// The plans of one seam call; bit_of_sig of every request lives in one flat array.
+// Growable array without value-initialisation (every element is written before use).
+template <class T>
+struct RawBuf {
+  std::unique_ptr<T[]> p;
+  size_t cap = 0;
+  T *ensure(size_t n) {
+    if (n > cap) { p.reset(new T[n]); cap = n; }
+    return p.get();
+  }
+};
+
+// The plans of one seam call; bit_of_sig of every request lives in one flat array.  The
+// per-thread candidate parts are kept between calls (blocksync plans batch after batch),
+// so their pages are touched once.
 struct Plans {
   std::vector<Plan> v;
-  std::vector<int32_t> bits;
+  RawBuf<int32_t> bits;
+  std::vector<std::vector<Cand>> parts;
 };
 
 // Per-thread "seen" marks of the Trusting loops (first index of each validator), reset in
@@ -302,14 +320,14 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
         if (f == kAbsent) continue;
         if (f != kCommit && f != kNil) return TMED_EINVAL;  // CommitSig.BlockID panics (types/block.go:663)
         pl.bit_of_sig[i] = (int32_t)cands.size();
-        cands.push_back({q, (int32_t)i, (int32_t)i});
+        cands.emplace_back(q, (int32_t)i, (int32_t)i);
       }
     } else {
       int64_t tally = 0;
       for (size_t i = 0; i < c.n_sigs; i++) {
         if (c.flags[i] != kCommit) continue;
         pl.bit_of_sig[i] = (int32_t)cands.size();
-        cands.push_back({q, (int32_t)i, (int32_t)i});
+        cands.emplace_back(q, (int32_t)i, (int32_t)i);
         tally += vs.powers[i];
         if (tally > pl.needed) break;
       }
@@ -330,7 +348,7 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
       if (seen.get(v) >= 0) break;  // the loop returns the double-vote error here
       seen.set(v, (int32_t)i);
       pl.bit_of_sig[i] = (int32_t)cands.size();
-      cands.push_back({q, (int32_t)i, v});
+      cands.emplace_back(q, (int32_t)i, v);
       tally += vs.powers[v];
       if (tally > pl.needed) break;
     }
@@ -377,10 +395,10 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
     if (check_request(reqs[q]) != TMED_OK) return TMED_EINVAL;
     nbits += reqs[q].commit->n_sigs;
   }
-  ps.bits.resize(nbits);
+  int32_t *bits = ps.bits.ensure(std::max<size_t>(nbits, 1));
   nbits = 0;
   for (size_t q = 0; q < n; q++) {
-    plans[q].bit_of_sig = ps.bits.data() + nbits;
+    plans[q].bit_of_sig = bits + nbits;
     nbits += reqs[q].commit->n_sigs;
   }
   clk.lap("check");
@@ -394,7 +412,9 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
     }
     return TMED_OK;
   }
-  std::vector<std::vector<Cand>> part(nt);
+  if (ps.parts.size() < nt) ps.parts.resize(nt);
+  std::vector<std::vector<Cand>> &part = ps.parts;
+  for (unsigned t = 0; t < nt; t++) part[t].clear();
   std::vector<size_t> lo_of(nt, 0), hi_of(nt, 0);
   std::vector<int> rcs(nt, TMED_OK);
   parallel_ranges(n, nt, [&](size_t lo, size_t hi, unsigned t) {
@@ -606,13 +626,15 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
 // Collected bits -> valid[] (signatures of length != 64 are false: ed25519.go:150-152).
 static void scatter_bits(const tmed_commit_request *reqs, const std::vector<Cand> &cands, const uint32_t *ix,
                          uint32_t m, const uint8_t *bits, uint8_t *valid) {
-  for (uint32_t j = 0; j < m; j++) {
-    const uint32_t k = ix ? ix[j] : j;
-    const Cand &cd = cands[k];
-    const tmed_commit &c = *reqs[cd.req].commit;
-    const uint32_t sl = c.sig_lens ? c.sig_lens[cd.sig_idx] : 64;
-    valid[k] = sl == 64 ? bits[j] : 0;
-  }
+  parallel_ranges(m, host_threads(m), [&](size_t lo, size_t hi, unsigned) {
+    for (size_t j = lo; j < hi; j++) {
+      const uint32_t k = ix ? ix[j] : (uint32_t)j;
+      const Cand &cd = cands[k];
+      const tmed_commit &c = *reqs[cd.req].commit;
+      const uint32_t sl = c.sig_lens ? c.sig_lens[cd.sig_idx] : 64;
+      valid[k] = sl == 64 ? bits[j] : 0;
+    }
+  });
 }
 
 // Device templates of the requests that have candidates; false if one does not fit.
@@ -731,20 +753,25 @@ extern "C" int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window 
   std::unique_lock<std::mutex> lk(ctx->mu);
   size_t idx = 0;
   for (size_t lo = 0; lo < nb && rc == TMED_OK; lo += bsz, idx++) {
+    PhaseClock clk;
     BsBatch &b = slots[idx & 1];
     BsBatch &prev = slots[(idx + 1) & 1];
     b.lo = lo;
     b.n = std::min(bsz, nb - lo);
     const tmed_commit_request *rq = reqs.data() + lo;
     rc = seam_plan(rq, b.n, out + lo, b.plans, b.cands, b.cache);
+    clk.lap("plan");
     const size_t m = b.cands.size();
     b.valid.assign(m, 0);
     bool fits = true;
     if (rc == TMED_OK && m) rc = device_templates(rq, b.n, b.cands, b.tmpl, &fits);
+    clk.lap("templates");
     if (rc == TMED_OK && m) {
       if (fits && m <= 0xffffffffu) {
         rc = stage_group(ctx, rq, b.n, b.cands, nullptr, (uint32_t)m, keyset, b.tmpl.data(), (int)(idx & 1), b.st);
+        clk.lap("stage");
         if (rc == TMED_OK) rc = tmed::votes_enqueue(ctx, b.st);
+        clk.lap("enqueue");
         b.device = rc == TMED_OK;
       } else {  // oversize template: host-assembled messages, synchronous (drain the pipeline first)
         rc = finish(prev);
@@ -754,6 +781,10 @@ extern "C" int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window 
       }
     }
     if (rc == TMED_OK) rc = finish(prev);  // overlaps the device work of batch b
+    clk.lap("finish_prev");
+    if (trace_on() && prev.st.m)
+      fprintf(stderr, "[tmed] blocksync prev batch kernels %.0fus\n", 1000.0 * ctx->last_ms);
+    clk.emit("blocksync batch", b.n, m);
   }
   for (BsBatch &b : slots)
     if (rc == TMED_OK) rc = finish(b);
