@@ -14,6 +14,7 @@
 //   3. CanonicalVote sign-bytes (signbytes.hip), ONE device batch (tmed_verify_batch)
 //   4. replay of the reference loop over the validity bits — first-error index, early
 //      exit, Got/Needed and error kinds come out identical by construction.
+#include <atomic>
 #include <chrono>
 #include <string.h>
 
@@ -175,6 +176,12 @@ int check_request(const tmed_commit_request &r) {
 
 }  // namespace
 
+// host worker pool helpers (defined below)
+static unsigned host_threads(size_t items);
+template <class F>
+static void parallel_ranges(size_t n, unsigned nt, F &&f);
+
+
 // Flattened candidates of one seam call.
 struct CandBatch {
   size_t m = 0;
@@ -211,7 +218,9 @@ static int init_encoders(const tmed_commit_request *reqs, size_t n, const std::v
   enc.assign(n, tmed::VoteEncoder());
   used.assign(n, 0);
   for (const Cand &cd : cands) used[cd.req] = 1;
-  for (size_t q = 0; q < n; q++) {
+  std::atomic<int> bad{0};
+  parallel_ranges(n, n >= 64 ? host_threads(cands.size()) : 1, [&](size_t lo, size_t hi, unsigned) {
+  for (size_t q = lo; q < hi; q++) {
     if (!used[q]) continue;
     const tmed_commit &c = *reqs[q].commit;
     tmed_vote_template t;
@@ -224,9 +233,10 @@ static int init_encoders(const tmed_commit_request *reqs, size_t n, const std::v
     t.psh_total = c.block_id.psh_total;
     t.psh_hash = c.block_id.psh_hash;
     t.psh_hash_len = c.block_id.psh_hash_len;
-    if (enc[q].init(&t) != TMED_OK) return TMED_EINVAL;
+    if (enc[q].init(&t) != TMED_OK) bad = 1;
   }
-  return TMED_OK;
+  });
+  return bad ? TMED_EINVAL : TMED_OK;
 }
 
 // Flatten candidates with host-assembled sign-bytes (callback verifiers; oversize templates).
@@ -270,9 +280,6 @@ static int build_cand_batch(const tmed_commit_request *reqs, size_t n, const std
 // Address indexes for every LightTrusting valset of the call (built once, read-only after).
 using AddrCache = std::unordered_map<const tmed_valset *, std::unique_ptr<AddrIndex>>;
 
-static unsigned host_threads(size_t items);
-template <class F>
-static void parallel_ranges(size_t n, unsigned nt, F &&f);
 
 static void build_addr_cache(const tmed_commit_request *reqs, size_t n, AddrCache &cache) {
   std::vector<std::pair<const tmed_valset *, AddrIndex *>> todo;
@@ -645,9 +652,12 @@ static int device_templates(const tmed_commit_request *reqs, size_t n, const std
   int rc = init_encoders(reqs, n, cands, enc, used);
   if (rc != TMED_OK) return rc;
   tmpl.assign(n * tmed::kVoteTmplBytes, 0);
-  *fits = true;
-  for (size_t q = 0; q < n; q++)
-    if (used[q] && !enc[q].device_template(&tmpl[q * tmed::kVoteTmplBytes], tmed::kVoteTmplBytes)) *fits = false;
+  std::atomic<bool> ok{true};
+  parallel_ranges(n, n >= 64 ? host_threads(cands.size()) : 1, [&](size_t lo, size_t hi, unsigned) {
+    for (size_t q = lo; q < hi; q++)
+      if (used[q] && !enc[q].device_template(&tmpl[q * tmed::kVoteTmplBytes], tmed::kVoteTmplBytes)) ok = false;
+  });
+  *fits = ok;
   return TMED_OK;
 }
 

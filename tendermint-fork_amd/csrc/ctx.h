@@ -106,12 +106,14 @@ struct VoteSlot {
   HostBuf h_votes, h_out;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the device work of the slot's last batch
   hipEvent_t done = nullptr;                // after its copy-out
+  hipEvent_t copied = nullptr;              // its staged votes are on the device (copy stream)
 };
 }  // namespace tmed
 
 struct tmed_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;  // H2D of staged votes, so batch b's copy overlaps b-1's kernels
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
   std::mutex mu;

@@ -76,6 +76,7 @@ int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteSta
   if (e == hipSuccess && !vs.ev0) e = hipEventCreate(&vs.ev0);
   if (e == hipSuccess && !vs.ev1) e = hipEventCreate(&vs.ev1);
   if (e == hipSuccess && !vs.done) e = hipEventCreateWithFlags(&vs.done, hipEventDisableTiming);
+  if (e == hipSuccess && !vs.copied) e = hipEventCreateWithFlags(&vs.copied, hipEventDisableTiming);
   if (e != hipSuccess) return map_err(e);
   uint8_t *h = (uint8_t *)vs.h_votes.p;
   st.key = h + st.o_key;
@@ -96,8 +97,12 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   VoteSlot &vs = c->vslot[st.slot];
   uint8_t *d = (uint8_t *)vs.d_votes.p;
   hipStream_t s = c->stream;
-  hipError_t e = scratch_acquire(c, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(d, vs.h_votes.p, st.total, hipMemcpyHostToDevice, s);
+  // the copy runs on the copy stream, so it overlaps the kernels of the batch queued before
+  // (the other slot); this slot's previous batch was collected before it was restaged
+  hipError_t e = hipMemcpyAsync(d, vs.h_votes.p, st.total, hipMemcpyHostToDevice, c->copy_stream);
+  if (e == hipSuccess) e = hipEventRecord(vs.copied, c->copy_stream);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s, vs.copied, 0);
+  if (e == hipSuccess) e = scratch_acquire(c, s);
   if (e == hipSuccess) e = hipEventRecord(vs.ev0, s);
   if (e == hipSuccess)
     e = launch_assemble_votes(d + st.o_tmpl, (const uint32_t *)(d + st.o_tidx), d + st.o_flag,

@@ -52,6 +52,7 @@ int tmed_init(int device, tmed_ctx **out) {
   tmed_ctx *c = new tmed_ctx();
   c->device = device;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->scratch_ev, hipEventDisableTiming);
@@ -100,6 +101,7 @@ void tmed_destroy(tmed_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
   for (DevBuf *b : {&c->d_a, &c->d_b, &c->d_msg, &c->d_off, &c->d_out, &c->d_c}) b->release();
   for (HostBuf *b : {&c->h_a, &c->h_b, &c->h_msg, &c->h_off, &c->h_out, &c->h_c}) b->release();
   for (DevBuf *b : {&c->d_merkle_a, &c->d_merkle_b, &c->d_merkle_idx}) b->release();
@@ -109,6 +111,7 @@ void tmed_destroy(tmed_ctx *c) {
     if (v.ev0) hipEventDestroy(v.ev0);
     if (v.ev1) hipEventDestroy(v.ev1);
     if (v.done) hipEventDestroy(v.done);
+    if (v.copied) hipEventDestroy(v.copied);
   }
   for (auto &kv : c->keysets) free_keyset(kv.second);
   c->keysets.clear();
@@ -122,6 +125,7 @@ void tmed_destroy(tmed_ctx *c) {
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->stream) hipStreamDestroy(c->stream);
+  if (c->copy_stream) hipStreamDestroy(c->copy_stream);
   delete c;
 }
 
