@@ -141,9 +141,25 @@ struct tmed_ctx {
   // the scratch first makes its stream wait for the previous user (scratch_ev, whatever its
   // stream), then records itself.  Both under mu.
   hipEvent_t scratch_ev = nullptr;
+  bool scratch_foreign = false;  // the last user was a caller's stream (scratch_ev marks its end)
 };
 
 namespace tmed {
-inline hipError_t scratch_acquire(tmed_ctx *c, hipStream_t s) { return hipStreamWaitEvent(s, c->scratch_ev, 0); }
-inline hipError_t scratch_release(tmed_ctx *c, hipStream_t s) { return hipEventRecord(c->scratch_ev, s); }
+// Calls on the context's own stream are ordered by the stream itself; an event is recorded
+// or waited on only when the user changes to or from a caller's stream.  (A caller's stream
+// is only ever recorded on inside that caller's own call: it may be gone afterwards.)
+inline hipError_t scratch_acquire(tmed_ctx *c, hipStream_t s) {
+  hipError_t e = hipSuccess;
+  if (s == c->stream) {
+    if (c->scratch_foreign) e = hipStreamWaitEvent(s, c->scratch_ev, 0);
+  } else {
+    if (!c->scratch_foreign) e = hipEventRecord(c->scratch_ev, c->stream);  // the tail covers its last use
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, c->scratch_ev, 0);
+  }
+  return e;
+}
+inline hipError_t scratch_release(tmed_ctx *c, hipStream_t s) {
+  c->scratch_foreign = s != c->stream;
+  return c->scratch_foreign ? hipEventRecord(c->scratch_ev, s) : hipSuccess;
+}
 }  // namespace tmed

@@ -97,11 +97,18 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   VoteSlot &vs = c->vslot[st.slot];
   uint8_t *d = (uint8_t *)vs.d_votes.p;
   hipStream_t s = c->stream;
-  // the copy runs on the copy stream, so it overlaps the kernels of the batch queued before
-  // (the other slot); this slot's previous batch was collected before it was restaged
-  hipError_t e = hipMemcpyAsync(d, vs.h_votes.p, st.total, hipMemcpyHostToDevice, c->copy_stream);
-  if (e == hipSuccess) e = hipEventRecord(vs.copied, c->copy_stream);
-  if (e == hipSuccess) e = hipStreamWaitEvent(s, vs.copied, 0);
+  // A large copy runs on the copy stream, so it overlaps the kernels of the batch queued
+  // before (the other slot; this slot's previous batch was collected before it was
+  // restaged).  A small one (a single commit) stays on the kernel stream: the cross-stream
+  // event would cost more latency than the copy.
+  hipError_t e = hipSuccess;
+  if (st.total >= (1u << 20)) {
+    e = hipMemcpyAsync(d, vs.h_votes.p, st.total, hipMemcpyHostToDevice, c->copy_stream);
+    if (e == hipSuccess) e = hipEventRecord(vs.copied, c->copy_stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, vs.copied, 0);
+  } else {
+    e = hipMemcpyAsync(d, vs.h_votes.p, st.total, hipMemcpyHostToDevice, s);
+  }
   if (e == hipSuccess) e = scratch_acquire(c, s);
   if (e == hipSuccess) e = hipEventRecord(vs.ev0, s);
   if (e == hipSuccess)
