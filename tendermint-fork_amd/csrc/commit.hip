@@ -702,9 +702,34 @@ static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, 
   return TMED_OK;
 }
 
+static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t nb, size_t bsz, uint64_t keyset,
+                         tmed_commit_result *out);
+
+// A large call whose sets share one key set (a light-client or evidence backlog) goes through
+// the two-slot pipeline in batches of ~2^19 signatures (env TMED_PIPE_SIGS), so the host
+// planning, staging and replay of one batch overlap the device work of the next.
+static size_t pipe_batch_sigs() {
+  const char *e = getenv("TMED_PIPE_SIGS");
+  return e ? std::max<size_t>(1, strtoull(e, nullptr, 10)) : (size_t)1 << 19;
+}
+
 extern "C" int tmed_verify_commits(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
                                    tmed_commit_result *out) {
   if (!ctx) return TMED_EINVAL;
+  const size_t kPipeBatchSigs = pipe_batch_sigs();
+  if (n > 1 && reqs && out) {
+    bool ok = true;
+    size_t sigs = 0;
+    const uint64_t ks = reqs[0].vals ? reqs[0].vals->keyset : 0;
+    for (size_t q = 0; q < n && ok; q++) {
+      ok = check_request(reqs[q]) == TMED_OK && reqs[q].vals->keyset == ks;
+      if (ok) sigs += reqs[q].commit->n_sigs;
+    }
+    if (ok && sigs >= 2 * kPipeBatchSigs) {
+      const size_t bsz = std::max<size_t>(16, kPipeBatchSigs / std::max<size_t>(1, sigs / n));
+      if (n > bsz) return run_pipelined(ctx, reqs, n, bsz, ks, out);
+    }
+  }
   return run_seam(reqs, n, out,
                   [&](const tmed_commit_request *rq, size_t nr, const std::vector<Cand> &cands, uint8_t *valid) {
                     return ctx_verify(ctx, rq, nr, cands, valid);
@@ -724,26 +749,12 @@ struct BsBatch {
 };
 }  // namespace
 
-extern "C" int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t batch_blocks,
-                                     tmed_commit_result *out) {
-  if (!ctx || !w || (w->n_blocks && (!w->vals || !w->block_ids || !w->heights || !w->commits || !out)))
-    return TMED_EINVAL;
-  const size_t nb = w->n_blocks;
-  if (nb == 0) return TMED_OK;
-  const size_t bsz = batch_blocks ? batch_blocks : 256;
-  std::vector<tmed_commit_request> reqs(nb);
-  for (size_t h = 0; h < nb; h++) {
-    tmed_commit_request &r = reqs[h];
-    memset(&r, 0, sizeof r);
-    r.mode = TMED_MODE_LIGHT;
-    r.chain_id = w->chain_id;
-    r.chain_id_len = w->chain_id_len;
-    r.vals = w->vals;
-    r.block_id = &w->block_ids[h];
-    r.height = w->heights[h];
-    r.commit = &w->commits[h];
-  }
-  const uint64_t keyset = w->vals->keyset;
+// Two-slot pipeline over batches of bsz requests whose validator sets share one key set
+// (0 = generic keys): batch b is planned, staged and queued while the device verifies batch
+// b-1, which is then collected and replayed (f4).  Same results as one run_seam over all
+// requests; the caller has checked every request (check_request) beforehand.
+static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t nb, size_t bsz, uint64_t keyset,
+                         tmed_commit_result *out) {
   BsBatch slots[2];
   int rc = TMED_OK;
   auto finish = [&](BsBatch &b) -> int {
@@ -753,9 +764,9 @@ extern "C" int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window 
       b.bits.resize(m);
       int r = tmed::votes_collect(ctx, b.st, b.bits.data());
       if (r != TMED_OK) return r;
-      scatter_bits(reqs.data() + b.lo, b.cands, nullptr, (uint32_t)m, b.bits.data(), b.valid.data());
+      scatter_bits(reqs + b.lo, b.cands, nullptr, (uint32_t)m, b.bits.data(), b.valid.data());
     }
-    int r = seam_replay(reqs.data() + b.lo, b.n, out + b.lo, b.plans, b.valid.data());
+    int r = seam_replay(reqs + b.lo, b.n, out + b.lo, b.plans, b.valid.data());
     b.n = 0;
     b.device = false;
     return r;
@@ -768,7 +779,7 @@ extern "C" int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window 
     BsBatch &prev = slots[(idx + 1) & 1];
     b.lo = lo;
     b.n = std::min(bsz, nb - lo);
-    const tmed_commit_request *rq = reqs.data() + lo;
+    const tmed_commit_request *rq = reqs + lo;
     rc = seam_plan(rq, b.n, out + lo, b.plans, b.cands, b.cache);
     clk.lap("plan");
     const size_t m = b.cands.size();
@@ -794,10 +805,32 @@ extern "C" int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window 
     clk.lap("finish_prev");
     if (trace_on() && prev.st.m)
       fprintf(stderr, "[tmed] blocksync prev batch kernels %.0fus\n", 1000.0 * ctx->last_ms);
-    clk.emit("blocksync batch", b.n, m);
+    clk.emit("pipelined batch", b.n, m);
   }
   for (BsBatch &b : slots)
     if (rc == TMED_OK) rc = finish(b);
   if (rc != TMED_OK) (void)hipStreamSynchronize(ctx->stream);
   return rc;
+}
+
+extern "C" int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t batch_blocks,
+                                     tmed_commit_result *out) {
+  if (!ctx || !w || (w->n_blocks && (!w->vals || !w->block_ids || !w->heights || !w->commits || !out)))
+    return TMED_EINVAL;
+  const size_t nb = w->n_blocks;
+  if (nb == 0) return TMED_OK;
+  std::vector<tmed_commit_request> reqs(nb);
+  for (size_t h = 0; h < nb; h++) {
+    tmed_commit_request &r = reqs[h];
+    memset(&r, 0, sizeof r);
+    r.mode = TMED_MODE_LIGHT;
+    r.chain_id = w->chain_id;
+    r.chain_id_len = w->chain_id_len;
+    r.vals = w->vals;
+    r.block_id = &w->block_ids[h];
+    r.height = w->heights[h];
+    r.commit = &w->commits[h];
+    if (check_request(r) != TMED_OK) return TMED_EINVAL;
+  }
+  return run_pipelined(ctx, reqs.data(), nb, batch_blocks ? batch_blocks : 256, w->vals->keyset, out);
 }

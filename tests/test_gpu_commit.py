@@ -19,6 +19,25 @@ def test_seam_matches_reference_loops_gpu(engine):
         assert same(T.verify_commits(engine, [reqs[q]])[0], exp[q])
 
 
+def test_pipelined_seam_gpu(engine):
+    """Large tmed_verify_commits calls go through the two-slot pipeline (batches planned and
+    staged while the previous batch runs); TMED_PIPE_SIGS=64 forces many tiny batches, and the
+    pipelined path must reproduce the reference loops on every scenario, batch boundaries
+    included."""
+    import os
+    reqs, exp = [], []
+    for mode, vs, pv, chain, bid, h, cm, pc, num, den in scenarios(seed=3, count=90):
+        exp.append(oracle_result(mode, vs, chain, bid, h, cm, num, den))
+        reqs.append((mode, pv, chain, pbid(bid), h, pc, num, den))
+    os.environ["TMED_PIPE_SIGS"] = "64"
+    try:
+        got = T.verify_commits(engine, reqs)
+    finally:
+        del os.environ["TMED_PIPE_SIGS"]
+    bad = [(q, str(g), str(e)) for q, (g, e) in enumerate(zip(got, exp)) if not same(g, e)]
+    assert not bad, bad[:5]
+
+
 def test_index_sliced_commit_gpu(engine):
     """§8e latency mode on one rank: the slice verifier runs on the GPU (tmed_verify_batch) and
     the first-failure replay must give the reference loop's exact error."""
