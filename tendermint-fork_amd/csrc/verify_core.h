@@ -8,13 +8,13 @@
 //   S >= L -> reject; R' = [k](-A) + [S]B (cofactorless); accept iff enc(R') == R bytes.
 // (len(sig) != 64 is decided on the host, before a tuple reaches the device.)
 //
-// SIMT shape: the double-scalar multiplication is a Straus interleave with
-// FIXED signed radix-16 windows for both scalars (64 windows: 4 doublings, one
-// cached add from the per-lane table of -A, one niels add from the shared B
-// table).  Unlike the reference's wNAF (whose data-dependent add positions
-// would make every lane of a 64-wide wave pay for every other lane's adds),
-// every lane runs exactly the same instruction stream; digit 0 adds the
-// identity, which the complete formulas handle exactly.
+// SIMT shape: the double-scalar multiplication is a Straus interleave with FIXED
+// signed windows — radix 16 for k (64 windows: 4 doublings + one cached add from the
+// per-lane table of -A) and radix 256 for S (32 niels adds from the shared LDS table of
+// j*B, one per 8 doublings).  Unlike the reference's wNAF (whose data-dependent add
+// positions would make every lane of a 64-wide wave pay for every other lane's adds),
+// every lane runs exactly the same instruction stream; digit 0 adds the identity,
+// which the complete formulas handle exactly.
 #pragma once
 #include "ge25519.h"
 #include "sc25519.h"
