@@ -19,8 +19,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <deque>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <string>
 #include <unordered_map>
@@ -375,13 +378,62 @@ static unsigned host_threads(size_t items) {
   return cap;
 }
 
+// Persistent host workers: a seam call runs ~8 parallel phases per batch, and spawning and
+// joining 16 threads for each was a measurable share of a blocksync batch.  The pool is
+// started on first use and deliberately never torn down (its idle workers end with the
+// process).  Tasks never call parallel_ranges themselves; a call made from a worker (or
+// while the caller is itself a worker) runs serially instead of waiting on the pool.
+namespace {
+struct HostPool {
+  std::mutex m;
+  std::condition_variable cv;
+  std::deque<std::function<void()>> q;
+  static thread_local bool in_worker;
+  explicit HostPool(unsigned n) {
+    for (unsigned i = 0; i < n; i++)
+      std::thread([this] {
+        in_worker = true;
+        for (;;) {
+          std::function<void()> f;
+          {
+            std::unique_lock<std::mutex> lk(m);
+            cv.wait(lk, [&] { return !q.empty(); });
+            f = std::move(q.front());
+            q.pop_front();
+          }
+          f();
+        }
+      }).detach();
+  }
+  static HostPool &get() {
+    static HostPool *p = new HostPool(std::max(1u, host_threads(~(size_t)0) - 1));
+    return *p;
+  }
+};
+thread_local bool HostPool::in_worker = false;
+}  // namespace
+
 template <class F>
 static void parallel_ranges(size_t n, unsigned nt, F &&f) {
-  if (nt <= 1 || n < 2) { f(0, n, 0u); return; }
+  if (nt <= 1 || n < 2 || HostPool::in_worker) { f(0, n, 0u); return; }
   if (nt > n) nt = (unsigned)n;
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < nt; t++) th.emplace_back(f, n * t / nt, n * (t + 1) / nt, t);
-  for (auto &x : th) x.join();
+  HostPool &pool = HostPool::get();
+  std::mutex dm;
+  std::condition_variable dcv;
+  unsigned left = nt - 1;
+  {
+    std::lock_guard<std::mutex> lk(pool.m);
+    for (unsigned t = 1; t < nt; t++)
+      pool.q.emplace_back([&, t] {
+        f(n * t / nt, n * (t + 1) / nt, t);
+        std::lock_guard<std::mutex> g(dm);
+        if (--left == 0) dcv.notify_one();
+      });
+  }
+  pool.cv.notify_all();
+  f(0, n / nt, 0u);
+  std::unique_lock<std::mutex> lk(dm);
+  dcv.wait(lk, [&] { return left == 0; });
 }
 
 static size_t total_sigs(const tmed_commit_request *reqs, size_t n) {
