@@ -195,7 +195,7 @@ def main():
     ap.add_argument("--gap", type=int, default=2)
     ap.add_argument("--blocks", type=int, default=100_000)
     ap.add_argument("--window", type=int, default=1000, help="blocks generated and verified per seam call")
-    ap.add_argument("--batch", type=int, default=256, help="blocks per device batch inside the seam")
+    ap.add_argument("--batch", type=int, default=128, help="blocks per device batch inside the seam")
     ap.add_argument("--validators", type=int, default=10_000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-keyset", action="store_true")

@@ -335,7 +335,7 @@ typedef struct {
  * over TMED_MODE_LIGHT requests — computed speculatively for the whole window, so the
  * caller applies blocks in order and stops at the first non-OK one (the reactor then
  * redoes that request, reactor.go:368-388).  The window is processed in device batches
- * of batch_blocks blocks (0 = 256) through a two-slot pipeline: while the device verifies
+ * of batch_blocks blocks (0 = 128, the measured best) through a two-slot pipeline: while the device verifies
  * batch b, the host plans and stages batch b+1 and replays batch b-1.
  */
 int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t batch_blocks,

@@ -884,5 +884,5 @@ extern "C" int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window 
     r.commit = &w->commits[h];
     if (check_request(r) != TMED_OK) return TMED_EINVAL;
   }
-  return run_pipelined(ctx, reqs.data(), nb, batch_blocks ? batch_blocks : 256, w->vals->keyset, out);
+  return run_pipelined(ctx, reqs.data(), nb, batch_blocks ? batch_blocks : 128, w->vals->keyset, out);
 }
