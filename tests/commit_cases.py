@@ -18,14 +18,14 @@ def pbid(b: C.BlockID):
     return T.BlockID(b.hash, b.psh_total, b.psh_hash)
 
 
-def scenarios(seed=1, count=60):
+def scenarios(seed=1, count=60, chains=("test_chain_id", "Lalande21185", "")):
     """Yield (mode, oracle_vs, product_vs, chain, oracle_bid, height, oracle_commit, product_commit, num, den)."""
     rng = random.Random(seed)
     for k in range(count):
         n = rng.choice([1, 2, 3, 4, 7, 10, 31])
         powers = [rng.choice([1, 10, 10, 100]) for _ in range(n)]
         vs, seeds = make_valset([seed_of("sc%d" % k, i) for i in range(n)], powers)
-        chain = rng.choice(["test_chain_id", "Lalande21185", ""])
+        chain = rng.choice(list(chains))
         bid = make_block_id("sc%d" % k)
         h = rng.randrange(1, 10**6)
         flags = [rng.choice([C.FLAG_COMMIT] * 6 + [C.FLAG_NIL, C.FLAG_ABSENT]) for _ in range(n)]

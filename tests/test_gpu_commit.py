@@ -38,6 +38,33 @@ def test_pipelined_seam_gpu(engine):
     assert not bad, bad[:5]
 
 
+def test_oversize_chain_ids_and_mixed_key_sets_gpu(engine):
+    """One seam call mixing generic requests, requests on several key sets (one launch group
+    per key set) and chain IDs too long for the device sign-bytes template (host-assembled
+    fallback; VerifyCommit itself does not bound the chain ID) — every decision and error
+    equal to the reference loops."""
+    import numpy as np
+    long_chain = "c" * 200
+    reqs, exp, handles = [], [], []
+    try:
+        for k, (mode, vs, pv, chain, bid, h, cm, pc, num, den) in enumerate(
+                scenarios(seed=11, count=48, chains=("test_chain_id", long_chain))):
+            if k % 3 == 1:  # key-cached: a key set per request (keys in set order)
+                pubs = np.array([np.frombuffer(v.pub_key, np.uint8) for v in pv.validators])
+                pv.keyset = engine.keyset_load(pubs)
+                pv.keyset_index = np.arange(len(pubs), dtype=np.uint32)
+                handles.append(pv.keyset)
+            exp.append(oracle_result(mode, vs, chain, bid, h, cm, num, den))
+            reqs.append((mode, pv, chain, pbid(bid), h, pc, num, den))
+        got = T.verify_commits(engine, reqs)
+        bad = [(q, str(g), str(e)) for q, (g, e) in enumerate(zip(got, exp)) if not same(g, e)]
+        assert not bad, bad[:5]
+        assert any(r[2] == long_chain for r in reqs) and handles
+    finally:
+        for hnd in handles:
+            engine.keyset_free(hnd)
+
+
 def test_index_sliced_commit_gpu(engine):
     """§8e latency mode on one rank: the slice verifier runs on the GPU (tmed_verify_batch) and
     the first-failure replay must give the reference loop's exact error."""
