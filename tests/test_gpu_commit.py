@@ -135,12 +135,13 @@ def test_keyset_seam_and_packed_commits(engine):
         engine.keyset_free(ks)
 
 
-@pytest.mark.parametrize("batch", [1, 3, 256])
+@pytest.mark.parametrize("batch,chain", [(1, "bs-chain"), (3, "bs-chain"), (256, "bs-chain"), (3, "c" * 200)])
 @pytest.mark.parametrize("keyed", [False, True])
-def test_blocksync_window_matches_light_loops(engine, batch, keyed):
+def test_blocksync_window_matches_light_loops(engine, batch, chain, keyed):
     """tmed_blocksync_verify (f4: pipelined LIGHT batches over one validator set) gives the
     reference VerifyCommitLight outcome for every block: valid commits, a bad signature
-    before and after the 2/3 crossing, wrong height, wrong BlockID, not enough power."""
+    before and after the 2/3 crossing, wrong height, wrong BlockID, not enough power; a
+    200-character chain ID takes the pipeline's synchronous host-assembled fallback."""
     import numpy as np
     from oracle.fixtures import make_block_id, make_commit, make_valset, resign, seed_of
     from commit_cases import to_product
@@ -148,7 +149,7 @@ def test_blocksync_window_matches_light_loops(engine, batch, keyed):
     blocks, exp, bids, heights = [], [], [], []
     for h in range(11):
         bid = make_block_id("bs%d" % h)
-        cm = make_commit(vs, seeds, "bs-chain", 50 + h, 0, bid)
+        cm = make_commit(vs, seeds, chain, 50 + h, 0, bid)
         want_h, want_bid = 50 + h, bid
         if h == 2:
             resign(cm, 0, seeds[0], "bad")          # before the crossing -> wrong signature (#0)
@@ -162,22 +163,22 @@ def test_blocksync_window_matches_light_loops(engine, batch, keyed):
             for i in range(3, 7):                   # absent -> not enough power
                 cm.signatures[i].flag = 1
                 cm.signatures[i].signature = b""
-        exp.append(oracle_result(T.MODE_LIGHT, vs, "bs-chain", want_bid, want_h, cm, 0, 0))
+        exp.append(oracle_result(T.MODE_LIGHT, vs, chain, want_bid, want_h, cm, 0, 0))
         _, pc = to_product(vs, cm)
         blocks.append(pc)
         bids.append(pbid(want_bid))
         heights.append(want_h)
-    pv = to_product(vs, make_commit(vs, seeds, "bs-chain", 1, 0, make_block_id("x")))[0]
+    pv = to_product(vs, make_commit(vs, seeds, chain, 1, 0, make_block_id("x")))[0]
     ks = 0
     if keyed:
         ks = engine.keyset_load(np.array([np.frombuffer(v.pub_key, np.uint8) for v in pv.validators]))
         pv.keyset = ks
     try:
-        w = T.BlocksyncWindow(pv, "bs-chain", bids, heights, blocks)
+        w = T.BlocksyncWindow(pv, chain, bids, heights, blocks)
         w.run(engine, batch)
         for h, (g, e) in enumerate(zip(w.errors(), exp)):
             assert same(g, e), (h, g, e)
-        ref = T.verify_commits(engine, [(T.MODE_LIGHT, pv, "bs-chain", b, hh, c, 0, 0)
+        ref = T.verify_commits(engine, [(T.MODE_LIGHT, pv, chain, b, hh, c, 0, 0)
                                         for b, hh, c in zip(bids, heights, blocks)])
         assert all(same(a, b) for a, b in zip(ref, w.errors()))
     finally:
