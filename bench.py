@@ -36,7 +36,11 @@ sys.path.insert(0, os.path.join(ROOT, "tendermint-fork_amd"))
 # v_mad_i64_i32 per verification of the generic (no key cache) kernel, counted from its
 # formulas (DESIGN.md "Roofline"); field mul = 100 mads, square = 55 (radix 2^25.5).
 MUL, SQ = 100, 55
-MADS_STRAUS = 32 * (32 * SQ + 47 * MUL)     # 32 x (8 dbl + 2 cached adds (-A) + 1 niels add (B))
+# Straus per byte of the scalars: 8 dbl (32 S + 26 M) + 2 cached (-A) adds with their conversions
+# (14 M), plus, where a B window ends, p1p1->p3 + niels add + p1p1->p2 instead of one p1p1->p2 (+7 M)
+MAIN_VARIANT = int(os.environ.get("TMED_MAIN_WAVES", "5"))
+B_WINDOWS = 16 if MAIN_VARIANT == 5 else 32     # radix-2^16 (default) or radix-256 B windows
+MADS_STRAUS = 32 * (32 * SQ + 40 * MUL) + B_WINDOWS * 7 * MUL
 MADS_TABLE = 64 * MUL                        # 1..8 x (-A), cached form
 MADS_DECODE = 255 * SQ + 21 * MUL + MUL      # Point.SetBytes (sqrt-ratio chain) + T = XY
 # batched finish: one inversion (254 sq + 11 mul) per group of 16 + 3 mul (prefix, 1/Z_j,

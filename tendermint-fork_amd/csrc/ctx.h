@@ -119,13 +119,14 @@ struct tmed_ctx {
   std::mutex mu;
   tmed::ge_niels *d_btab = nullptr;
   int4 *d_bcomb = nullptr;  // signed radix-256 comb of +B (shared)
+  int4 *d_b16 = nullptr;    // j*B, j = 0..32768 (main-kernel variant 5), built at init
   int4 *d_slab = nullptr;
   int4 *d_prep = nullptr;
   int4 *d_fin = nullptr;      // batched-finish hand-off (kFinBytes)
   int4 *d_fin_pre = nullptr;  // batched-finish prefix products (kFinPreBytes)
   uint32_t slab_slots = 0;
   uint32_t chunk = 0;     // signatures per prep/main launch pair (0 = slab_slots); env TMED_CHUNK
-  int main_waves = 2;     // register budget variant of the main kernel; env TMED_MAIN_WAVES
+  int main_waves = 5;     // main-kernel variant (5: radix-2^16 B windows, the measured best); env TMED_MAIN_WAVES
   uint32_t lat_max = 24576;  // key-cached batches up to this size take the latency kernels (crossover ~32k,
                              // profiles/r01/session3/lat_sweep.jsonl); env TMED_LAT_MAX
   bool timing = false;    // tmed_set_kernel_timing

@@ -38,8 +38,18 @@ constexpr uint32_t kFinPreStride = kFinCap + 64;
 constexpr size_t kFinBytes = (size_t)kFinCap * kFinInt4 * 16;
 constexpr size_t kFinPreBytes = (size_t)kFinPreStride * 3 * 16;
 
+// The shared B tables of the generic main kernel: the radix-256 table staged in LDS and the
+// radix-2^16 table in HBM (main-kernel variant 5).
+struct BTabs {
+  const ge_niels *lds;
+  const int4 *b16;
+};
+constexpr uint32_t kB16Entries = 32769;
+constexpr size_t kB16Bytes = (size_t)kB16Entries * 128;
+hipError_t launch_build_b16(int4 *tab, hipStream_t stream);
+
 hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
-                         uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
+                         uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, BTabs btab,
                          int4 *prep, int4 *fin, int4 *fin_pre, hipStream_t stream, uint32_t chunk = 0,
                          int main_waves = 2, bool msg_slots = false, KernelTimer *timer = nullptr);
 

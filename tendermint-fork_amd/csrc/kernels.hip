@@ -106,8 +106,42 @@ struct SlabTabPf {
 using SlabTab = SlabTabT<false>;
 
 struct LdsBTab {
+  static constexpr int kBits = 8;
   const ge_niels *t;
+  int pf = 0;
   __device__ __forceinline__ void load(int j, ge_niels &n) const { n = t[j]; }
+  __device__ __forceinline__ void prefetch(int j) { pf = j; }
+  __device__ __forceinline__ void take(ge_niels &n) const { n = t[pf]; }
+};
+
+// Radix-2^16 B table (double_scalarmult<16>): j*B, j = 0..32768, affine niels in 128-B rows
+// (kCombEntryInt4 int4, 4.2 MB, L2/MALL-resident).  The entry of the next B window is fetched
+// into LDS with global_load_lds_dwordx4 right after the current B addition, 16 doublings
+// before it is needed; buf is this wave's [8][64] int4 region (lane l's piece q at q*64+l).
+struct B16Pf {
+  static constexpr int kBits = 16;
+  const int4 *tab;
+  int4 *buf;
+  uint32_t lane;
+  __device__ __forceinline__ void prefetch(int j) const {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the previous take's LDS reads are done
+#pragma unroll
+    for (int q = 0; q < 8; q++)
+      __builtin_amdgcn_global_load_lds((global_void *)(tab + (size_t)j * 8 + q), (lds_void *)(buf + q * 64), 16, 0, 0);
+  }
+  __device__ __forceinline__ void take(ge_niels &e) const {
+    fe *fs[3] = {&e.YpX, &e.YmX, &e.XY2d};
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int4 v = buf[q * 64 + lane];
+      const int32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const int f = 4 * q + c;
+        if (f < 30) fs[f / 10]->v[f % 10] = w[c];
+      }
+    }
+  }
 };
 
 constexpr int kBTabEntries = 129;  // j*B, j = 0..128 (niels) — 15.5 KB of LDS
@@ -263,27 +297,37 @@ __device__ __forceinline__ void fin_store(int4 *fin, uint32_t stride, uint32_t s
 // WAVES = minimum waves per SIMD the register allocation must allow.
 // PF: the per-lane A table is lane-major and its next entry is prefetched into LDS
 // (SlabTabPf, 40 KB per 256-lane block on top of the 15.5 KB B table).
-template <int WAVES, bool LANE_MAJOR, bool PF = false>
+// BB: B window width (8: LDS table; 16: the HBM table with LDS prefetch, B16Pf).
+template <int WAVES, bool LANE_MAJOR, bool PF = false, int BB = 8>
 __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_main_kernel(
     uint32_t base, uint32_t count, const int4 *__restrict__ prep, uint32_t stride, int4 *__restrict__ slab,
-    const ge_niels *__restrict__ btab_g, int4 *__restrict__ fin, uint32_t fin_base, uint8_t *__restrict__ out) {
-  __shared__ ge_niels sbt[kBTabEntries];
+    BTabs bts, int4 *__restrict__ fin, uint32_t fin_base, uint8_t *__restrict__ out) {
+  __shared__ ge_niels sbt[BB == 8 ? kBTabEntries : 1];
   __shared__ int4 spf[PF ? kThreadsPerBlock / 64 : 1][PF ? 10 * 64 : 1];
-  stage_btab(sbt, btab_g);
+  __shared__ int4 sb16[BB == 16 ? kThreadsPerBlock / 64 : 1][BB == 16 ? 8 * 64 : 1];
+  if constexpr (BB == 8) stage_btab(sbt, bts.lds);
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   if (slot >= count) return;
   const uint32_t i = base + slot;
   uint32_t k[8], s[8];
   ge_p3 A;
   const bool ok = prep_load(prep, stride, slot, k, s, A);
-  const LdsBTab bt{sbt};
   ge_p2 R;
-  if constexpr (PF) {
-    SlabTabPf tab{SlabTabT<true>{slab, stride, slot}, spf[threadIdx.x >> 6], threadIdx.x & 63u};
-    verify_main_point(R, k, s, A, tab, bt);
+  auto run = [&](auto &bt) {
+    if constexpr (PF) {
+      SlabTabPf tab{SlabTabT<true>{slab, stride, slot}, spf[threadIdx.x >> 6], threadIdx.x & 63u};
+      verify_main_point(R, k, s, A, tab, bt);
+    } else {
+      SlabTabT<LANE_MAJOR> tab{slab, stride, slot};
+      verify_main_point(R, k, s, A, tab, bt);
+    }
+  };
+  if constexpr (BB == 16) {
+    B16Pf bt{bts.b16, sb16[threadIdx.x >> 6], threadIdx.x & 63u};
+    run(bt);
   } else {
-    SlabTabT<LANE_MAJOR> tab{slab, stride, slot};
-    verify_main_point(R, k, s, A, tab, bt);
+    LdsBTab bt{sbt};
+    run(bt);
   }
   fin_store(fin, kFinCap, i - fin_base, R.X, R.Y, R.Z);
   out[i] = ok ? 1 : 0;
@@ -396,7 +440,7 @@ uint32_t grid_for(size_t n, uint32_t max_blocks) {
 }
 
 hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
-                         uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, const ge_niels *btab,
+                         uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, BTabs btab,
                          int4 *prep, int4 *fin, int4 *fin_pre, hipStream_t stream, uint32_t chunk, int main_waves,
                          bool msg_slots, KernelTimer *timer) {
   const MsgSrc ms{msgs, off, msg_slots};
@@ -412,9 +456,13 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
       hipLaunchKernelGGL(verify_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, pub, sig, ms, base,
                          count, prep, slab_stride);
       if (timer) timer->mark(stream, 0);
-      // default: 2 waves/SIMD, lane-major per-lane tables (+3.7 % over the slot-interleaved
-      // layout, profiles/r01/variants.txt); the others are kept as measured A/B variants.
-      if (main_waves == 4)  // lane-major + LDS prefetch of the next A entry
+      // default (5): 2 waves/SIMD, lane-major per-lane tables (+3.7 % over the slot-interleaved
+      // layout), radix-2^16 B windows from the HBM table (+3.3 % over the LDS radix-256
+      // table, profiles/r01/session3/variants_b16.txt); the others are measured A/B variants.
+      if (main_waves == 5)  // radix-2^16 B windows from the HBM table (16 fewer B additions)
+        hipLaunchKernelGGL((verify_main_kernel<2, true, false, 16>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream,
+                           base, count, prep, slab_stride, slab, btab, fin, fbase, out);
+      else if (main_waves == 4)  // lane-major + LDS prefetch of the next A entry
         hipLaunchKernelGGL((verify_main_kernel<2, true, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream,
                            base, count, prep, slab_stride, slab, btab, fin, fbase, out);
       else if (main_waves >= 3)
@@ -446,6 +494,36 @@ hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t
 }
 
 void host_build_btab(ge_niels out[129]) { build_btab_niels(out); }
+
+// j*B for j = 0..kB16Entries-1 into 128-B rows (one lane per entry; once per context).
+__global__ __launch_bounds__(256) void b16_fill_kernel(int4 *__restrict__ tab) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= kB16Entries) return;
+  ge_niels e;
+  if (j == 0) {
+    ge_niels_0(e);
+  } else {
+    ge_p3 B;
+    ge_base_point(B);
+    comb_entry(e, B, j, 16);
+  }
+  const fe *fs[3] = {&e.YpX, &e.YmX, &e.XY2d};
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    int32_t w[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int f = 4 * q + c;
+      w[c] = f < 30 ? fs[f / 10]->v[f % 10] : 0;
+    }
+    tab[(size_t)j * 8 + q] = make_int4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+hipError_t launch_build_b16(int4 *tab, hipStream_t stream) {
+  hipLaunchKernelGGL(b16_fill_kernel, dim3((kB16Entries + 255) / 256), dim3(256), 0, stream, tab);
+  return hipGetLastError();
+}
 
 // ============================================================ fixed-base combs
 

@@ -81,6 +81,8 @@ int tmed_init(int device, tmed_ctx **out) {
   const uint8_t benc[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
                             0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
                             0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
+  if (e == hipSuccess) e = hipMalloc((void **)&c->d_b16, kB16Bytes);
+  if (e == hipSuccess) e = launch_build_b16(c->d_b16, c->stream);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_bcomb, kCombBytesPerKey);
   if (e == hipSuccess) e = hipMalloc((void **)&d_bpub, 32);
   if (e == hipSuccess) e = hipMalloc((void **)&d_bok, 1);
@@ -117,6 +119,7 @@ void tmed_destroy(tmed_ctx *c) {
   c->keysets.clear();
   if (c->scratch_ev) hipEventDestroy(c->scratch_ev);
   if (c->d_bcomb) hipFree(c->d_bcomb);
+  if (c->d_b16) hipFree(c->d_b16);
   if (c->d_slab) hipFree(c->d_slab);
   if (c->d_prep) hipFree(c->d_prep);
   if (c->d_fin) hipFree(c->d_fin);
@@ -171,7 +174,7 @@ int tmed_verify_batch_device(tmed_ctx *c, const uint8_t *d_pub, const uint8_t *d
   if (c->timing) c->timer.n = 0;
   hipError_t e = scratch_acquire(c, s);
   if (e == hipSuccess)
-    e = launch_verify(d_pub, d_sig, d_msgs, d_off, (uint32_t)n, d_out, c->d_slab, c->slab_slots, c->d_btab, c->d_prep,
+    e = launch_verify(d_pub, d_sig, d_msgs, d_off, (uint32_t)n, d_out, c->d_slab, c->slab_slots, BTabs{c->d_btab, c->d_b16}, c->d_prep,
                       c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves, false, c->timing ? &c->timer : nullptr);
   if (e == hipSuccess) e = scratch_release(c, s);
   return map_err(e);
@@ -229,7 +232,7 @@ int tmed_verify_batch(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, const
   if (e == hipSuccess)
     e = launch_verify((const uint8_t *)c->d_a.p, (const uint8_t *)c->d_b.p, (const uint8_t *)c->d_msg.p,
                       (const uint32_t *)c->d_off.p, (uint32_t)n, (uint8_t *)c->d_out.p, c->d_slab, c->slab_slots,
-                      c->d_btab, c->d_prep, c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves);
+                      BTabs{c->d_btab, c->d_b16}, c->d_prep, c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves);
   if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
   if (e == hipSuccess) e = scratch_release(c, s);
   if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, n, hipMemcpyDeviceToHost, s);

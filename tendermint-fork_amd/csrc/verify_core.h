@@ -71,14 +71,31 @@ TMED_HD void build_table_negA(T &tab, const ge_p3 &A) {
 
 // out = [k](-A) + [S]B  (Straus, most-significant first).
 // k: signed radix-16 digits (64 windows) from the per-lane table of j*(-A), j=0..8;
-// S: signed radix-256 digits (32 windows) from the shared table of j*B, j=0..128
-// (BT::load(j, niels)), added once per 8 doublings — half the B additions of a
-// radix-16 B window, for a 15.5 KB LDS table.
-template <class T, class BT>
-TMED_HD void double_scalarmult(ge_p2 &out, const uint32_t k[8], const uint32_t s[8], T &tab, const BT &btab) {
+// S: signed radix-2^BBITS digits from a shared table of j*B (niels), added once per
+// BBITS doublings:
+//   BBITS = 8:  32 windows, j = 0..128 (the 15.5 KB table staged in LDS);
+//   BBITS = 16: 16 windows, j = 0..32768 (a 4.2 MB table in HBM, L2/MALL-resident),
+//               16 fewer mixed additions per signature.
+// Both tables expose prefetch(j) / take(niels&): the next B digit is known one window
+// ahead, so a global table's entry can be fetched while the doublings run.
+template <int BBITS>
+TMED_HD void sc_recode_b(uint32_t r[8], const uint32_t s[8]) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t t = (uint64_t)s[i] + (BBITS == 8 ? 0x80808080u : 0x80008000u) + c;
+    r[i] = (uint32_t)t;
+    c = t >> 32;
+  }
+}
+
+template <int BBITS, class T, class BT>
+TMED_HD void double_scalarmult(ge_p2 &out, const uint32_t k[8], const uint32_t s[8], T &tab, BT &btab) {
+  constexpr int kBias = 1 << (BBITS - 1);
+  constexpr uint32_t kMask = (1u << BBITS) - 1u;
   uint32_t kr[8], sr[8];
   sc_recode16(kr, k);
-  sc_recode256(sr, s);
+  sc_recode_b<BBITS>(sr, s);
   ge_p2 q;
   ge_p2_0(q);
   ge_p1p1 t;
@@ -88,16 +105,17 @@ TMED_HD void double_scalarmult(ge_p2 &out, const uint32_t k[8], const uint32_t s
   {
     const int da0 = (int)(kr[7] >> 28) - 8;
     tab.prefetch(da0 < 0 ? -da0 : da0);
+    const int db0 = (int)(sr[7] >> (32 - BBITS)) - kBias;
+    btab.prefetch(db0 < 0 ? -db0 : db0);
   }
 #pragma unroll 1
   for (int j = 0; j < 8; j++) {  // 32-bit word of the scalars, most significant first
-    uint32_t kc = kr[7], sc = sr[7];
+    uint32_t kc = kr[7];
+    const uint32_t sw = sr[7];
 #pragma unroll
     for (int m = 7; m > 0; m--) { kr[m] = kr[m - 1]; sr[m] = sr[m - 1]; }
 #pragma unroll 1
-    for (int i = 0; i < 4; i++) {  // byte of the word: two radix-16 A windows, one radix-256 B window
-      const int db = (int)(sc >> 24) - 128;
-      sc <<= 8;
+    for (int i = 0; i < 4; i++) {  // byte of the word: two radix-16 A windows
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const int da = (int)(kc >> 28) - 8;
@@ -121,10 +139,20 @@ TMED_HD void double_scalarmult(ge_p2 &out, const uint32_t k[8], const uint32_t s
         tab.prefetch(dn < 0 ? -dn : dn);
         if (h == 0) ge_p1p1_to_p2(q, t);
       }
-      ge_p1p1_to_p3(r, t);
-      btab.load(db < 0 ? -db : db, nb);
-      niels_apply_sign(nb, db < 0);
-      ge_madd_niels(t, r, nb, false);
+      const bool badd = BBITS == 8 || (i & 1);  // a B window ends after this byte
+      if (badd) {
+        // B digit of the window ending here: bits [32 - 8(i+1), 32 - 8(i+1) + BBITS) of sw
+        const int sh = 32 - 8 * (i + 1);
+        const int db = (int)((sw >> sh) & kMask) - kBias;
+        // next B digit: same word, or the next word's first window after the last one
+        const int dbn = (i == 3) ? (int)(sr[7] >> (32 - BBITS)) - kBias
+                                 : (int)((sw >> (sh - BBITS)) & kMask) - kBias;
+        ge_p1p1_to_p3(r, t);
+        btab.take(nb);
+        btab.prefetch(dbn < 0 ? -dbn : dbn);
+        niels_apply_sign(nb, db < 0);
+        ge_madd_niels(t, r, nb, false);
+      }
       ge_p1p1_to_p2(q, t);
     }
   }
@@ -160,9 +188,9 @@ TMED_HD bool verify_prep(const uint32_t pubw[8], const uint32_t sigw[16], const 
 // canonical encoding of R' (one inversion) is left to the batched finish below.
 template <class T, class BT>
 TMED_HD void verify_main_point(ge_p2 &R, const uint32_t k[8], const uint32_t s[8], const ge_p3 &A, T &tab,
-                               const BT &btab) {
+                               BT &btab) {
   build_table_negA(tab, A);
-  double_scalarmult(R, k, s, tab, btab);
+  double_scalarmult<BT::kBits>(R, k, s, tab, btab);
 }
 
 // enc(X/Z, Y/Z) == R bytes, given zi = 1/Z.
@@ -182,7 +210,7 @@ TMED_HD bool encoding_matches(const fe &X, const fe &Y, const fe &zi, const uint
 // Unbatched phase 2 + compare (one inversion per signature).
 template <class T, class BT>
 TMED_HD bool verify_main(const uint32_t k[8], const uint32_t s[8], const ge_p3 &A, const uint32_t Rw[8], T &tab,
-                         const BT &btab) {
+                         BT &btab) {
   ge_p2 R;
   verify_main_point(R, k, s, A, tab, btab);
   fe zi;
@@ -236,7 +264,7 @@ TMED_HD void finish_group(Acc &a) {
 // One verification.  pubw: 8 words of A; sigw: 16 words (R = 0..7, S = 8..15).
 template <class T, class BT>
 TMED_HD bool verify_one(const uint32_t pubw[8], const uint32_t sigw[16], const uint8_t *msg, uint32_t mlen,
-                        T &tab, const BT &btab) {
+                        T &tab, BT &btab) {
   uint32_t k[8], s[8];
   ge_p3 A;
   const bool ok = verify_prep(pubw, sigw, msg, mlen, k, s, A);
@@ -246,7 +274,7 @@ TMED_HD bool verify_one(const uint32_t pubw[8], const uint32_t sigw[16], const u
 // [s]B for s < 2^255 via the same window schedule (k = 0 uses the identity
 // table; used by the signer and key generation only).
 template <class T, class BT>
-TMED_HD void scalarmult_base(uint32_t enc[8], const uint32_t s[8], T &tab, const BT &btab) {
+TMED_HD void scalarmult_base(uint32_t enc[8], const uint32_t s[8], T &tab, BT &btab) {
   uint32_t zero[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) zero[i] = 0;
@@ -254,7 +282,7 @@ TMED_HD void scalarmult_base(uint32_t enc[8], const uint32_t s[8], T &tab, const
   ge_p3_0(id);
   build_table_negA(tab, id);
   ge_p2 R;
-  double_scalarmult(R, zero, s, tab, btab);
+  double_scalarmult<BT::kBits>(R, zero, s, tab, btab);
   ge_tobytes(enc, R.X, R.Y, R.Z);
 }
 
@@ -292,7 +320,7 @@ TMED_HD void sign_one_bm(uint32_t sig[16], uint32_t pub[8], const uint32_t seed[
 // Signing with [s]B by the Straus schedule (k = 0) — the host test build's signer.
 template <class T, class BT>
 TMED_HD void sign_one(uint32_t sig[16], uint32_t pub[8], const uint32_t seed[8], const uint8_t *msg,
-                      uint32_t mlen, T &tab, const BT &btab) {
+                      uint32_t mlen, T &tab, BT &btab) {
   sign_one_bm(sig, pub, seed, msg, mlen, [&](uint32_t enc[8], const uint32_t s[8]) {
     scalarmult_base(enc, s, tab, btab);
   });
@@ -315,7 +343,7 @@ TMED_HD void ge_mul256(ge_p3 &P) {
 }
 
 // out = j * base (j in 1..255) in niels form; branch-free double-and-add.
-TMED_HD void comb_entry(ge_niels &out, const ge_p3 &base, uint32_t j) {
+TMED_HD void comb_entry(ge_niels &out, const ge_p3 &base, uint32_t j, int nbits = 8) {
   ge_cached cP;
   ge_p3_to_cached(cP, base);
   ge_p3 acc, sum;
@@ -323,7 +351,7 @@ TMED_HD void comb_entry(ge_niels &out, const ge_p3 &base, uint32_t j) {
   ge_p1p1 t;
   ge_p2 q;
 #pragma unroll 1
-  for (int b = 7; b >= 0; b--) {
+  for (int b = nbits - 1; b >= 0; b--) {
     ge_p3_to_p2(q, acc);
     ge_p2_dbl(t, q);
     ge_p1p1_to_p3(acc, t);
@@ -505,6 +533,15 @@ TMED_HD bool verify_one_comb(const uint32_t pubw[8], bool key_ok, const uint32_t
   uint32_t k[8], s[8];
   const bool ok = verify_prep_comb(pubw, key_ok, sigw, msg, mlen, k, s);
   return verify_main_comb(k, s, sigw, acomb, bcomb) && ok;
+}
+
+// The base point B = (x, 4/5), x even, from its encoding.
+TMED_HD void ge_base_point(ge_p3 &B) {
+  uint32_t w[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = 0x66666666u;
+  w[0] = 0x66666658u;
+  ge_frombytes_go(B, w);
 }
 
 // Construction of the shared B table: out[j] = j*B (niels, affine), j = 0..128.

@@ -24,12 +24,35 @@ struct HostTab {
 };
 struct HostBTab {
   ge_niels e[129];
-  void load(int j, ge_niels &n) const { n = e[j]; }
 };
 HostBTab &btab() {
   static HostBTab t;
   static bool init = false;
   if (!init) { build_btab_niels(t.e); init = true; }
+  return t;
+}
+// Per-lane view of a shared B table (prefetch/take state is the lane's own).
+template <int BITS>
+struct HostBRef {
+  static constexpr int kBits = BITS;
+  const ge_niels *e;
+  int pf = 0;
+  void prefetch(int j) { pf = j; }
+  void take(ge_niels &n) const { n = e[pf]; }
+};
+// The radix-2^16 table of main-kernel variant 5 (j*B, j = 0..32768), built like the device's.
+const std::vector<ge_niels> &b16tab() {
+  static std::vector<ge_niels> t;
+  static bool init = false;
+  if (!init) {
+    t.resize(32769);
+    ge_p3 B;
+    ge_base_point(B);
+    ge_niels_0(t[0]);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (long j = 1; j < 32769; j++) comb_entry(t[j], B, (uint32_t)j, 16);
+    init = true;
+  }
   return t;
 }
 // The device finish's accessor, on host arrays: lane l owns slots l, l + L, ... < m.
@@ -67,13 +90,16 @@ extern "C" {
 
 // group = 0: per-signature encoding (verify_one); group >= 1: prep + main point per
 // signature, then the batched finish with that group size (the device path).
-void hostsim_verify_batch_g(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
-                            size_t n, uint8_t *out, int group) {
-  HostBTab &bt = btab();
+static void verify_batch_impl(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
+                              size_t n, uint8_t *out, int group, int bbits) {
+  const ge_niels *b8 = btab().e;
+  const ge_niels *b16 = bbits == 16 ? b16tab().data() : nullptr;
   std::vector<ge_p2> pts(group > 0 ? n : 0);
 #pragma omp parallel for schedule(dynamic, 16)
   for (long i = 0; i < (long)n; i++) {
     HostTab tab;
+    HostBRef<8> bt{b8};
+    HostBRef<16> bt16{b16};
     uint32_t pw[8], sw[16];
     load_words8(pw, pub + 32 * i);
     load_words8(sw, sig + 64 * i);
@@ -84,11 +110,23 @@ void hostsim_verify_batch_g(const uint8_t *pub, const uint8_t *sig, const uint8_
       uint32_t k[8], s[8];
       ge_p3 A;
       const bool ok = verify_prep(pw, sw, msgs + off[i], off[i + 1] - off[i], k, s, A);
-      verify_main_point(pts[i], k, s, A, tab, bt);
+      if (bbits == 16) verify_main_point(pts[i], k, s, A, tab, bt16);
+      else verify_main_point(pts[i], k, s, A, tab, bt);
       out[i] = ok ? 1 : 0;
     }
   }
   if (group > 0) host_finish(pts, sig, out, (uint32_t)n, (uint32_t)group);
+}
+
+void hostsim_verify_batch_g(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
+                            size_t n, uint8_t *out, int group) {
+  verify_batch_impl(pub, sig, msgs, off, n, out, group, 8);
+}
+
+// Main-kernel variant 5: radix-2^16 B windows (16 B additions) + the batched finish.
+void hostsim_verify_batch_b16(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
+                              size_t n, uint8_t *out) {
+  verify_batch_impl(pub, sig, msgs, off, n, out, 16, 16);
 }
 
 void hostsim_verify_batch(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
@@ -98,10 +136,11 @@ void hostsim_verify_batch(const uint8_t *pub, const uint8_t *sig, const uint8_t 
 
 void hostsim_sign_batch(const uint8_t *seeds, const uint8_t *msgs, const uint32_t *off, size_t n,
                         uint8_t *sig_out, uint8_t *pub_out) {
-  HostBTab &bt = btab();
+  const ge_niels *b8 = btab().e;
 #pragma omp parallel for schedule(dynamic, 16)
   for (long i = 0; i < (long)n; i++) {
     HostTab tab;
+    HostBRef<8> bt{b8};
     uint32_t seed[8], sg[16], pb[8];
     load_words8(seed, seeds + 32 * i);
     sign_one(sg, pb, seed, msgs + off[i], off[i + 1] - off[i], tab, bt);

@@ -72,15 +72,19 @@ def test_decode_matches_go_rule(hostsim):
 def _verify(l, pubs, sigs, msgs, offs, group=16):
     n = len(pubs)
     out = np.zeros(n, np.uint8)
+    if group == "b16":  # main-kernel variant 5: radix-2^16 B windows from the 32769-entry table
+        l.hostsim_verify_batch_b16(_p(pubs), _p(sigs), _p(msgs), _p(offs), ctypes.c_size_t(n), _p(out))
+        return out
     l.hostsim_verify_batch_g(_p(pubs), _p(sigs), _p(msgs), _p(offs), ctypes.c_size_t(n), _p(out),
                              ctypes.c_int(group))
     return out
 
 
-@pytest.mark.parametrize("group", [0, 1, 5, 16])
+@pytest.mark.parametrize("group", [0, 1, 5, 16, "b16"])
 def test_golden_vectors_hostsim(hostsim, golden, group):
     """Every golden tuple, with per-signature encoding (group 0) and through the batched
-    finish (Montgomery inversion over groups of 1, 5 and 16 signatures, partial last group)."""
+    finish (Montgomery inversion over groups of 1, 5 and 16 signatures, partial last group);
+    "b16": the radix-2^16 B-window variant of the main kernel."""
     vs = [v for v in golden if len(v["sig"]) == 128]
     pubs = np.array([np.frombuffer(bytes.fromhex(v["pub"]), np.uint8) for v in vs])
     sigs = np.array([np.frombuffer(bytes.fromhex(v["sig"]), np.uint8) for v in vs])
