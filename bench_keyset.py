@@ -18,8 +18,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "tendermint-fork_amd"))
 
 MUL, SQ = 100, 55
-# key-cached main kernel: 64 mixed additions (3M) each followed by p1p1->p3 (4M)
-MADS_KEYSET_MAIN = 64 * 7 * MUL
+# key-cached main kernel: 32 A-comb + 16 radix-2^16 B-comb mixed additions (3M), each followed
+# by p1p1->p3 (4M)
+MADS_KEYSET_MAIN = 48 * 7 * MUL
 
 
 def main():

@@ -120,6 +120,7 @@ struct tmed_ctx {
   tmed::ge_niels *d_btab = nullptr;
   int4 *d_bcomb = nullptr;  // signed radix-256 comb of +B (shared)
   int4 *d_b16 = nullptr;    // j*B, j = 0..32768 (main-kernel variant 5), built at init
+  int4 *d_bcomb16 = nullptr;  // radix-2^16 comb of +B (key-cached throughput kernel), 67 MB
   int4 *d_slab = nullptr;
   int4 *d_prep = nullptr;
   int4 *d_fin = nullptr;      // batched-finish hand-off (kFinBytes)

@@ -47,6 +47,10 @@ struct BTabs {
 constexpr uint32_t kB16Entries = 32769;
 constexpr size_t kB16Bytes = (size_t)kB16Entries * 128;
 hipError_t launch_build_b16(int4 *tab, hipStream_t stream);
+// Radix-2^16 comb of +B for the key-cached throughput kernel (16 x kB16Entries x 128 B).
+constexpr size_t kBComb16Bytes = 16 * kB16Bytes;
+void host_bcomb16_bases(int32_t out[16 * 40]);
+hipError_t launch_build_bcomb16(const int32_t *d_bases, int4 *comb, hipStream_t stream);
 
 hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                          uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, BTabs btab,

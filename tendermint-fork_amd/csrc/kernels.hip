@@ -601,11 +601,54 @@ __global__ __launch_bounds__(128) void comb_fill_kernel(const int32_t *__restric
 }
 
 struct GlobalComb {
+  static constexpr int kBits = 8;
   const int4 *base;  // 32 windows x 129 entries x 8 int4
   __device__ __forceinline__ void load(int w, int j, ge_niels &e) const {
     niels_load(e, base + ((size_t)w * kCombEntries + j) * kCombEntryInt4);
   }
 };
+
+// Radix-2^16 comb of +B for the key-cached throughput kernel: 16 windows x 32769 entries
+// (j * 2^(16w) * B) x 8 int4 = 67 MB in HBM, built once per context.
+struct GlobalComb16 {
+  static constexpr int kBits = 16;
+  const int4 *base;
+  __device__ __forceinline__ void load(int w, int j, ge_niels &e) const {
+    niels_load(e, base + ((size_t)w * kB16Entries + j) * kCombEntryInt4);
+  }
+};
+
+// Lane (w, j) of the radix-2^16 B comb: j * bases[w] (bases[w] = 2^(16w) B, p3 words).
+__global__ __launch_bounds__(256) void bcomb16_fill_kernel(const int32_t *__restrict__ bases, int4 *__restrict__ comb) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= 16u * kB16Entries) return;
+  const uint32_t w = g / kB16Entries, j = g % kB16Entries;
+  ge_niels e;
+  if (j == 0) {
+    ge_niels_0(e);
+  } else {
+    ge_p3 P;
+    p3_load(P, bases + (size_t)w * 40);
+    comb_entry(e, P, j, 16);
+  }
+  niels_store(comb + (size_t)g * kCombEntryInt4, e);
+}
+
+void host_bcomb16_bases(int32_t out[16 * 40]) {
+  ge_p3 P;
+  ge_base_point(P);
+  for (int w = 0; w < 16; w++) {
+    const fe *fs[4] = {&P.X, &P.Y, &P.Z, &P.T};
+    for (int f = 0; f < 40; f++) out[w * 40 + f] = fs[f / 10]->v[f % 10];
+    ge_mul256(P);
+    ge_mul256(P);
+  }
+}
+
+hipError_t launch_build_bcomb16(const int32_t *d_bases, int4 *comb, hipStream_t stream) {
+  hipLaunchKernelGGL(bcomb16_fill_kernel, dim3((16u * kB16Entries + 255) / 256), dim3(256), 0, stream, d_bases, comb);
+  return hipGetLastError();
+}
 
 __device__ void comb_sign_one(uint32_t sg[16], uint32_t pb[8], const uint32_t seed[8], const uint8_t *m,
                               uint32_t mlen, const int4 *bcomb) {
@@ -633,7 +676,8 @@ __global__ __launch_bounds__(kThreadsPerBlock) void verify_keyset_prep_kernel(
   prep_store(prep, stride, slot, k, s, dummy, ok);
 }
 
-__global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_keyset_main_kernel(
+template <int WAVES>
+__global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_keyset_main_kernel(
     const uint32_t *__restrict__ val_idx, const int4 *__restrict__ acomb, const int4 *__restrict__ bcomb,
     uint32_t base, uint32_t count, const int4 *__restrict__ prep, uint32_t stride, int4 *__restrict__ fin,
     uint32_t fin_base, uint8_t *__restrict__ out) {
@@ -652,7 +696,7 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_keyset_main_kernel
 #pragma unroll
   for (int j = 0; j < 8; j++) { k[j] = (uint32_t)w[j]; s[j] = (uint32_t)w[8 + j]; }
   const GlobalComb ac{acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4};
-  const GlobalComb bc{bcomb};
+  const GlobalComb16 bc{bcomb};
   ge_p3 R;
   verify_main_comb_point(R, k, s, ac, bc);
   fin_store(fin, kFinCap, i - fin_base, R.X, R.Y, R.Z);
@@ -791,8 +835,16 @@ hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub,
       const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
       hipLaunchKernelGGL(verify_keyset_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx,
                          key_pub, key_ok, sig, ms, base, count, prep, stride);
-      hipLaunchKernelGGL(verify_keyset_main_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx, acomb,
-                         bcomb, base, count, prep, stride, fin, fbase, out);
+      static const int ks_waves = [] {  // A/B: waves/SIMD the key-cached main kernel is compiled for
+        const char *v = getenv("TMED_KS_WAVES");
+        return v ? atoi(v) : 2;
+      }();
+      if (ks_waves >= 3)
+        hipLaunchKernelGGL(verify_keyset_main_kernel<3>, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx,
+                           acomb, bcomb, base, count, prep, stride, fin, fbase, out);
+      else
+        hipLaunchKernelGGL(verify_keyset_main_kernel<2>, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx,
+                           acomb, bcomb, base, count, prep, stride, fin, fbase, out);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }

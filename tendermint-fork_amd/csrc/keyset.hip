@@ -42,7 +42,7 @@ static hipError_t keyset_verify(tmed_ctx *c, const Keyset &k, const uint32_t *d_
   if (n <= c->lat_max)
     return launch_verify_keyset_lat(d_idx, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb, d_sig, d_msgs, d_off, n, d_out,
                                     c->d_fin, c->d_fin_pre, s, msg_slots);
-  return launch_verify_keyset(d_idx, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb, d_sig, d_msgs, d_off, n, d_out, c->d_prep,
+  return launch_verify_keyset(d_idx, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb16, d_sig, d_msgs, d_off, n, d_out, c->d_prep,
                               c->slab_slots, c->d_fin, c->d_fin_pre, s, msg_slots);
 }
 

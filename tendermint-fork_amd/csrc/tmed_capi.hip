@@ -83,6 +83,18 @@ int tmed_init(int device, tmed_ctx **out) {
                             0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_b16, kB16Bytes);
   if (e == hipSuccess) e = launch_build_b16(c->d_b16, c->stream);
+  if (e == hipSuccess) e = hipMalloc((void **)&c->d_bcomb16, kBComb16Bytes);
+  {
+    static int32_t bases[16 * 40];
+    static std::once_flag bases_once;
+    std::call_once(bases_once, [] { host_bcomb16_bases(bases); });
+    int32_t *d_bases = nullptr;
+    if (e == hipSuccess) e = hipMalloc((void **)&d_bases, sizeof(bases));
+    if (e == hipSuccess) e = hipMemcpy(d_bases, bases, sizeof(bases), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_build_bcomb16(d_bases, c->d_bcomb16, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (d_bases) (void)hipFree(d_bases);
+  }
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_bcomb, kCombBytesPerKey);
   if (e == hipSuccess) e = hipMalloc((void **)&d_bpub, 32);
   if (e == hipSuccess) e = hipMalloc((void **)&d_bok, 1);
@@ -120,6 +132,7 @@ void tmed_destroy(tmed_ctx *c) {
   if (c->scratch_ev) hipEventDestroy(c->scratch_ev);
   if (c->d_bcomb) hipFree(c->d_bcomb);
   if (c->d_b16) hipFree(c->d_b16);
+  if (c->d_bcomb16) hipFree(c->d_bcomb16);
   if (c->d_slab) hipFree(c->d_slab);
   if (c->d_prep) hipFree(c->d_prep);
   if (c->d_fin) hipFree(c->d_fin);

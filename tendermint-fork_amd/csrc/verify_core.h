@@ -391,9 +391,36 @@ TMED_HD bool verify_prep_comb(const uint32_t pubw[8], bool key_ok, const uint32_
 // Key-cached verification, phase 2: [k](-A) from the key's comb, [s]B from the shared
 // comb: 32 + 32 mixed additions (projective result; encoding by the batched finish).
 // AC/BC provide  void load(int window, int j, ge_niels&) const  for j in 0..128.
+// BC::kBits = 16 (the throughput kernel): [s]B from the radix-2^16 comb of B (16 windows of
+// j * 2^(16w) * B, j = 0..32768), so 32 + 16 mixed additions; kBits = 8: 32 + 32.
 template <class AC, class BC>
 TMED_HD void verify_main_comb_point(ge_p3 &acc, const uint32_t k[8], const uint32_t s[8], const AC &acomb,
                                     const BC &bcomb) {
+  if constexpr (BC::kBits == 16) {
+    uint32_t kr[8], sr[8];
+    sc_recode256(kr, k);
+    sc_recode_b<16>(sr, s);
+    ge_p3_0(acc);
+    ge_p1p1 t;
+    ge_niels e;
+#pragma unroll 1
+    for (int w = 0; w < 32; w++) {
+      const int da = (int)((kr[w >> 2] >> (8 * (w & 3))) & 0xffu) - 128;
+      acomb.load(w, da < 0 ? -da : da, e);
+      niels_apply_sign(e, da < 0);
+      ge_madd_niels(t, acc, e, false);
+      ge_p1p1_to_p3(acc, t);
+      if (w & 1) {  // B window w/2 (16 bits) after every second A window
+        const int wb = w >> 1;
+        const int db = (int)((sr[wb >> 1] >> (16 * (wb & 1))) & 0xffffu) - 32768;
+        bcomb.load(wb, db < 0 ? -db : db, e);
+        niels_apply_sign(e, db < 0);
+        ge_madd_niels(t, acc, e, false);
+        ge_p1p1_to_p3(acc, t);
+      }
+    }
+    return;
+  }
   uint32_t kr[8], sr[8];
   sc_recode256(kr, k);
   sc_recode256(sr, s);

@@ -152,8 +152,24 @@ void hostsim_sign_batch(const uint8_t *seeds, const uint8_t *msgs, const uint32_
 // Key-cached (comb) verification on the host: builds every comb with the kernel's
 // comb_entry/ge_mul256 and runs verify_one_comb.
 struct HostComb {
+  static constexpr int kBits = 8;
   std::vector<ge_niels> e;  // 32 x 129
   void load(int w, int j, ge_niels &out) const { out = e[(size_t)w * 129 + j]; }
+};
+// The radix-2^16 comb of B (16 windows x 32769 entries): entries computed on demand with the
+// device builder's comb_entry from the same bases (host_bcomb16_bases restated).
+struct HostComb16 {
+  static constexpr int kBits = 16;
+  ge_p3 bases[16];
+  HostComb16() {
+    ge_p3 P;
+    ge_base_point(P);
+    for (int w = 0; w < 16; w++) { bases[w] = P; ge_mul256(P); ge_mul256(P); }
+  }
+  void load(int w, int j, ge_niels &out) const {
+    if (j == 0) ge_niels_0(out);
+    else comb_entry(out, bases[w], (uint32_t)j, 16);
+  }
 };
 
 static void build_host_comb(HostComb &c, const uint32_t pw[8], bool negate, bool *ok) {
@@ -225,9 +241,11 @@ void hostsim_verify_comb_lat(const uint8_t *keys, size_t nkeys, const uint32_t *
   }
 }
 
-void hostsim_verify_comb_batch(const uint8_t *keys, size_t nkeys, const uint32_t *key_idx, const uint8_t *sig,
-                               const uint8_t *msgs, const uint32_t *off, size_t n, uint8_t *out) {
-  const HostComb &bcomb = host_bcomb();
+}  // extern "C"
+
+template <class BC>
+static void verify_comb_batch_impl(const uint8_t *keys, size_t nkeys, const uint32_t *key_idx, const uint8_t *sig,
+                                   const uint8_t *msgs, const uint32_t *off, size_t n, uint8_t *out, const BC &bcomb) {
   std::vector<HostComb> ac;
   std::vector<uint8_t> kok;
   build_key_combs(keys, nkeys, ac, kok);
@@ -246,6 +264,20 @@ void hostsim_verify_comb_batch(const uint8_t *keys, size_t nkeys, const uint32_t
     out[i] = ok ? 1 : 0;
   }
   host_finish(pts, sig, out, (uint32_t)n, 3);
+}
+
+extern "C" {
+
+void hostsim_verify_comb_batch(const uint8_t *keys, size_t nkeys, const uint32_t *key_idx, const uint8_t *sig,
+                               const uint8_t *msgs, const uint32_t *off, size_t n, uint8_t *out) {
+  verify_comb_batch_impl(keys, nkeys, key_idx, sig, msgs, off, n, out, host_bcomb());
+}
+
+// The key-cached throughput kernel's schedule: 32 A-comb + 16 radix-2^16 B-comb additions.
+void hostsim_verify_comb_batch16(const uint8_t *keys, size_t nkeys, const uint32_t *key_idx, const uint8_t *sig,
+                                 const uint8_t *msgs, const uint32_t *off, size_t n, uint8_t *out) {
+  static const HostComb16 b16;
+  verify_comb_batch_impl(keys, nkeys, key_idx, sig, msgs, off, n, out, b16);
 }
 
 // Field-level probes: inputs/outputs are 32-byte LE encodings.

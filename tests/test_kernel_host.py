@@ -115,7 +115,7 @@ def test_sign_matches_oracle(hostsim):
         assert pub[i].tobytes() == port.pubkey_from_seed(seeds[i].tobytes())
 
 
-@pytest.mark.parametrize("fn", ["hostsim_verify_comb_batch", "hostsim_verify_comb_lat"])
+@pytest.mark.parametrize("fn", ["hostsim_verify_comb_batch", "hostsim_verify_comb_batch16", "hostsim_verify_comb_lat"])
 def test_comb_path_hostsim(hostsim, golden, fn):
     """Key-cached (radix-256 comb) verification, host build of the kernel code, vs the oracle:
     golden tuples grouped by key (incl. small-order, non-canonical and undecodable keys).
