@@ -341,6 +341,21 @@ typedef struct {
 int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t batch_blocks,
                           tmed_commit_result *out);
 
+/* ------------------------------------------ several GPUs in ONE process (§8e) */
+
+/*
+ * A Tendermint node is one process: with one context per GPU (tmed_init(0..N-1)), these
+ * split the work into contiguous shards balanced by signature count, run every shard on
+ * its own context concurrently, and write each result in place — no collective is needed
+ * because the host memory is shared.  Results are identical to the single-context calls.
+ * A key-set handle in a request must be loaded on EVERY context under the same handle
+ * value (load the set on each context in the same order).  Returns the first error.
+ */
+int tmed_verify_commits_multi(tmed_ctx *const *ctxs, size_t n_ctx, const tmed_commit_request *reqs, size_t n,
+                              tmed_commit_result *out);
+int tmed_blocksync_verify_multi(tmed_ctx *const *ctxs, size_t n_ctx, const tmed_blocksync_window *w,
+                                uint32_t batch_blocks, tmed_commit_result *out);
+
 #ifdef __cplusplus
 }
 #endif

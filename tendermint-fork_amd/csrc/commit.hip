@@ -886,3 +886,63 @@ extern "C" int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window 
   }
   return run_pipelined(ctx, reqs.data(), nb, batch_blocks ? batch_blocks : 128, w->vals->keyset, out);
 }
+
+// ---- several GPUs in one process (§8e): contiguous shards balanced by signature count ----
+
+// Shard boundaries over n items whose weights are w(i): shard t = [cut[t], cut[t+1]).
+template <class W>
+static std::vector<size_t> weighted_cuts(size_t n, size_t parts, W &&w) {
+  size_t total = 0;
+  for (size_t i = 0; i < n; i++) total += w(i);
+  std::vector<size_t> cut(parts + 1, n);
+  cut[0] = 0;
+  size_t acc = 0, t = 1;
+  for (size_t i = 0; i < n && t < parts; i++) {
+    acc += w(i);
+    while (t < parts && acc * parts >= total * t) cut[t++] = i + 1;
+  }
+  return cut;
+}
+
+template <class F>
+static int run_shards(size_t n_ctx, const std::vector<size_t> &cut, F &&f) {
+  std::vector<int> rcs(n_ctx, TMED_OK);
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < n_ctx; t++)
+    if (cut[t + 1] > cut[t]) th.emplace_back([&, t] { rcs[t] = f(t, cut[t], cut[t + 1]); });
+  for (auto &x : th) x.join();
+  for (int rc : rcs)
+    if (rc != TMED_OK) return rc;
+  return TMED_OK;
+}
+
+extern "C" int tmed_verify_commits_multi(tmed_ctx *const *ctxs, size_t n_ctx, const tmed_commit_request *reqs,
+                                         size_t n, tmed_commit_result *out) {
+  if (!ctxs || n_ctx == 0 || (n && (!reqs || !out))) return TMED_EINVAL;
+  for (size_t t = 0; t < n_ctx; t++)
+    if (!ctxs[t]) return TMED_EINVAL;
+  for (size_t q = 0; q < n; q++)
+    if (check_request(reqs[q]) != TMED_OK) return TMED_EINVAL;
+  const auto cut = weighted_cuts(n, n_ctx, [&](size_t q) { return (size_t)reqs[q].commit->n_sigs + 1; });
+  return run_shards(n_ctx, cut, [&](size_t t, size_t lo, size_t hi) {
+    return tmed_verify_commits(ctxs[t], reqs + lo, hi - lo, out + lo);
+  });
+}
+
+extern "C" int tmed_blocksync_verify_multi(tmed_ctx *const *ctxs, size_t n_ctx, const tmed_blocksync_window *w,
+                                           uint32_t batch_blocks, tmed_commit_result *out) {
+  if (!ctxs || n_ctx == 0 || !w) return TMED_EINVAL;
+  for (size_t t = 0; t < n_ctx; t++)
+    if (!ctxs[t]) return TMED_EINVAL;
+  const size_t nb = w->n_blocks;
+  if (nb && (!w->vals || !w->block_ids || !w->heights || !w->commits || !out)) return TMED_EINVAL;
+  const auto cut = weighted_cuts(nb, n_ctx, [&](size_t h) { return (size_t)w->commits[h].n_sigs + 1; });
+  return run_shards(n_ctx, cut, [&](size_t t, size_t lo, size_t hi) {
+    tmed_blocksync_window s = *w;
+    s.n_blocks = hi - lo;
+    s.block_ids = w->block_ids + lo;
+    s.heights = w->heights + lo;
+    s.commits = w->commits + lo;
+    return tmed_blocksync_verify(ctxs[t], &s, batch_blocks, out + lo);
+  });
+}

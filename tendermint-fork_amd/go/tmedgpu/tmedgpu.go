@@ -193,6 +193,14 @@ func (e *Engine) FreeKeyset(h uint64) { C.tmed_keyset_free(e.ctx, C.uint64_t(h))
 
 // VerifyCommits verifies many commits with ONE device batch.
 func (e *Engine) VerifyCommits(reqs []Request) ([]Result, error) {
+	return e.verifyCommitsWith(reqs, func(a *arena, creqs *C.tmed_commit_request, n C.size_t,
+		res *C.tmed_commit_result) C.int {
+		return C.tmed_verify_commits(e.ctx, creqs, n, res)
+	})
+}
+
+func (e *Engine) verifyCommitsWith(reqs []Request, call func(*arena, *C.tmed_commit_request, C.size_t,
+	*C.tmed_commit_result) C.int) ([]Result, error) {
 	n := len(reqs)
 	if n == 0 {
 		return nil, nil
@@ -223,16 +231,10 @@ func (e *Engine) VerifyCommits(reqs []Request) ([]Result, error) {
 			trust_num: C.int64_t(r.TrustNum), trust_den: C.int64_t(r.TrustDen)}
 	}
 	res := make([]C.tmed_commit_result, n)
-	if rc := C.tmed_verify_commits(e.ctx, &creqs[0], C.size_t(n), &res[0]); rc != 0 {
+	if rc := call(&a, &creqs[0], C.size_t(n), &res[0]); rc != 0 {
 		return nil, errors.New(C.GoString(C.tmed_strerror(rc)))
 	}
-	out := make([]Result, n)
-	for i := range res {
-		out[i] = Result{Code: int(res[i].code), Got: int64(res[i].got), Needed: int64(res[i].needed),
-			Expected: int64(res[i].expected), Actual: int64(res[i].actual), Idx: int32(res[i].idx),
-			IdxFirst: int32(res[i].idx_first), ValIdx: int32(res[i].val_idx)}
-	}
-	return out, nil
+	return toResults(res), nil
 }
 
 func toResults(res []C.tmed_commit_result) []Result {
@@ -336,4 +338,62 @@ func (e *Engine) MerkleRoots(trees [][][]byte) ([][32]byte, error) {
 		return nil, errors.New(C.GoString(C.tmed_strerror(rc)))
 	}
 	return append([][32]byte(nil), out...), nil
+}
+
+// Pool is one engine per GPU of the node, used from ONE process (a Tendermint node):
+// tmed_verify_commits_multi / tmed_blocksync_verify_multi shard the work over the contexts
+// concurrently; no collective is needed since host memory is shared.
+type Pool struct{ engines []*Engine }
+
+// NewPool opens devices 0..n-1.
+func NewPool(n int) (*Pool, error) {
+	p := &Pool{}
+	for d := 0; d < n; d++ {
+		var ctx *C.tmed_ctx
+		if rc := C.tmed_init(C.int(d), &ctx); rc != 0 {
+			for _, e := range p.engines {
+				C.tmed_destroy(e.ctx)
+			}
+			return nil, errors.New(C.GoString(C.tmed_strerror(rc)))
+		}
+		p.engines = append(p.engines, &Engine{ctx: ctx})
+	}
+	return p, nil
+}
+
+func (p *Pool) ctxs(a *arena) **C.tmed_ctx {
+	arr := (*[1 << 10]*C.tmed_ctx)(a.alloc(uintptr(len(p.engines)) * unsafe.Sizeof((*C.tmed_ctx)(nil))))[:len(p.engines):len(p.engines)]
+	for i, e := range p.engines {
+		arr[i] = e.ctx
+	}
+	return &arr[0]
+}
+
+// LoadKeyset loads the same key set on every GPU; the handles agree when every pool
+// member loads the same sets in the same order (the pool is the only loader).
+func (p *Pool) LoadKeyset(pubKeys []byte) (uint64, error) {
+	var h uint64
+	for i, e := range p.engines {
+		hi, err := e.LoadKeyset(pubKeys)
+		if err != nil {
+			return 0, err
+		}
+		if i > 0 && hi != h {
+			return 0, errors.New("tmedgpu: key-set handles diverged across GPUs")
+		}
+		h = hi
+	}
+	return h, nil
+}
+
+// VerifyCommits is Engine.VerifyCommits sharded over the pool's GPUs.
+func (p *Pool) VerifyCommits(reqs []Request) ([]Result, error) {
+	if len(reqs) == 0 {
+		return nil, nil
+	}
+	// the request structs are built exactly as Engine.VerifyCommits does
+	return p.engines[0].verifyCommitsWith(reqs, func(a *arena, creqs *C.tmed_commit_request, n C.size_t,
+		res *C.tmed_commit_result) C.int {
+		return C.tmed_verify_commits_multi(p.ctxs(a), C.size_t(len(p.engines)), creqs, n, res)
+	})
 }

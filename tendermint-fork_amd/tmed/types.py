@@ -251,7 +251,19 @@ def _bind():
         l.tmed_verify_commits_with.restype = ctypes.c_int
         l.tmed_verify_commits_with.argtypes = [ctypes.POINTER(_RequestC), ctypes.c_size_t,
                                                ctypes.POINTER(_ResultC), VERIFY_FN, ctypes.c_void_p]
+        l.tmed_verify_commits_multi.restype = ctypes.c_int
+        l.tmed_verify_commits_multi.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t,
+                                                ctypes.POINTER(_RequestC), ctypes.c_size_t, ctypes.POINTER(_ResultC)]
+        l.tmed_blocksync_verify_multi.restype = ctypes.c_int
+        l.tmed_blocksync_verify_multi.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t,
+                                                  ctypes.POINTER(_BlocksyncWindowC), ctypes.c_uint32,
+                                                  ctypes.POINTER(_ResultC)]
     return l
+
+
+def _ctx_array(engines):
+    """ctypes array of the contexts of several engines (one per GPU, the same process)."""
+    return (ctypes.c_void_p * len(engines))(*[e._h for e in engines])
 
 
 def _ptr(a):
@@ -363,6 +375,8 @@ def verify_commits(engine, requests: Sequence[tuple], verifier=None, stats: Opti
     """Verify many commits with one device batch.
 
     requests: (mode, ValidatorSet, chain_id, BlockID|None, height, Commit, trust_num, trust_den).
+    engine: an Engine, or a list of Engines (one per GPU: tmed_verify_commits_multi shards the
+    requests over them in this process).
     verifier: None -> the engine's GPU path (tmed_verify_commits); otherwise a Python callable
     ``(pubs, sigs, lens, msgs, offs) -> uint8 array`` (used by the CPU test-suite with the oracle).
     Returns one Go-style error (or None) per request.
@@ -384,7 +398,9 @@ def verify_commits(engine, requests: Sequence[tuple], verifier=None, stats: Opti
         reqs[q] = _RequestC(mode, cid, len(cid), ctypes.pointer(vs),
                             ctypes.pointer(bid) if bid is not None else None, height, ctypes.pointer(cc), num, den)
     res = (_ResultC * max(n, 1))()
-    if verifier is None:
+    if verifier is None and isinstance(engine, (list, tuple)):  # several GPUs, one process
+        rc = l.tmed_verify_commits_multi(_ctx_array(engine), len(engine), reqs, n, res)
+    elif verifier is None:
         rc = l.tmed_verify_commits(engine._h, reqs, n, res)
     else:
         def cb(user, pubs, sigs, lens, msgs, offs, m, out):
@@ -440,7 +456,12 @@ class BlocksyncWindow:
         self.res = (_ResultC * max(n, 1))()
 
     def run(self, engine, batch_blocks: int = 0):
-        rc = _bind().tmed_blocksync_verify(engine._h, ctypes.byref(self.win), batch_blocks, self.res)
+        """engine: one Engine, or a list of Engines (one per GPU): the window is sharded over them."""
+        if isinstance(engine, (list, tuple)):
+            rc = _bind().tmed_blocksync_verify_multi(_ctx_array(engine), len(engine), ctypes.byref(self.win),
+                                                     batch_blocks, self.res)
+        else:
+            rc = _bind().tmed_blocksync_verify(engine._h, ctypes.byref(self.win), batch_blocks, self.res)
         if rc != TMED_OK:
             raise TmedError(rc, "tmed_blocksync_verify")
         return self.res

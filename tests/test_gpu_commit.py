@@ -65,6 +65,52 @@ def test_oversize_chain_ids_and_mixed_key_sets_gpu(engine):
             engine.keyset_free(hnd)
 
 
+def test_multi_context_sharding_gpu(engine):
+    """tmed_verify_commits_multi / tmed_blocksync_verify_multi: requests sharded over several
+    contexts in one process (here three contexts on the one GPU of the test box; on a node,
+    one per GPU) give exactly the single-context results, key-set handles included."""
+    import numpy as np
+    from tmed import Engine
+    engines = [Engine(0) for _ in range(3)]  # fresh contexts: key-set handles count up in step
+    try:
+        reqs, exp = [], []
+        for mode, vs, pv, chain, bid, h, cm, pc, num, den in scenarios(seed=13, count=70):
+            exp.append(oracle_result(mode, vs, chain, bid, h, cm, num, den))
+            reqs.append((mode, pv, chain, pbid(bid), h, pc, num, den))
+        got = T.verify_commits(engines, reqs)
+        bad = [(q, str(g), str(e)) for q, (g, e) in enumerate(zip(got, exp)) if not same(g, e)]
+        assert not bad, bad[:5]
+        # blocksync window over one key set, loaded on every context (same handle everywhere)
+        from oracle.fixtures import make_block_id, make_commit, make_valset, resign, seed_of
+        from commit_cases import to_product
+        vs, seeds = make_valset([seed_of("mc", i) for i in range(7)], [10] * 7)
+        blocks, bids, heights, wexp = [], [], [], []
+        for h in range(9):
+            bid = make_block_id("mc%d" % h)
+            cm = make_commit(vs, seeds, "mc-chain", 10 + h, 0, bid)
+            if h == 4:
+                resign(cm, 1, seeds[1], "bad")
+            wexp.append(oracle_result(T.MODE_LIGHT, vs, "mc-chain", bid, 10 + h, cm, 0, 0))
+            blocks.append(to_product(vs, cm)[1])
+            bids.append(pbid(bid))
+            heights.append(10 + h)
+        pv = to_product(vs, make_commit(vs, seeds, "mc-chain", 1, 0, make_block_id("y")))[0]
+        pubs = np.array([np.frombuffer(v.pub_key, np.uint8) for v in pv.validators])
+        hs = [e.keyset_load(pubs) for e in engines]
+        assert len(set(hs)) == 1
+        pv.keyset = hs[0]
+        try:
+            w = T.BlocksyncWindow(pv, "mc-chain", bids, heights, blocks)
+            w.run(engines, 2)
+            assert all(same(g, e) for g, e in zip(w.errors(), wexp))
+        finally:
+            for e, hnd in zip(engines, hs):
+                e.keyset_free(hnd)
+    finally:
+        for e in engines:
+            e.close()
+
+
 def test_index_sliced_commit_gpu(engine):
     """§8e latency mode on one rank: the slice verifier runs on the GPU (tmed_verify_batch) and
     the first-failure replay must give the reference loop's exact error."""
