@@ -175,9 +175,10 @@ def main():
                     "finish_kernel_ms": round(fin_ms, 4), "finish_launches": fin_launches,
                     "step_kernel_ms": round(kernel_ms, 3),
                     "algorithmic_bytes_per_verify": 32 + 64 + int(offs[-1]) // n + 4 + 1}
-        cpu = None
+        cpu = cpu_all = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(eng, d_pub, d_sig, msgs, offs, min(args.cpu_sample, n), d_out)
+            cpu_all = cpu_baseline_threads(d_pub, d_sig, msgs, offs, n, d_out)
         result = {
             "metric": "ed25519 verifies/sec at 1/8 MI355X",
             "value": round(value, 1),
@@ -200,6 +201,7 @@ def main():
             "adversarial_per_gpu": n_adv,
             "roofline": roof,
             "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_all,
             "setup_s": round(t_gen, 2),
         }
         print(json.dumps(result), flush=True)
@@ -223,6 +225,35 @@ def pmc_traffic(sigs_per_launch):
         if k.startswith("verify_main_kernel") and "hbm_bytes_per_sig" in d:
             return round(d["hbm_bytes_per_sig"] * sigs_per_launch), "profiles/pmc_summary.json[%s]" % k
     return None, None
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_threads(d_pub, d_sig, msgs, offs, m, d_out):
+    """The same port on one GPU's share of the host (16 threads, or fewer cores): the
+    embarrassingly parallel upper bound SURVEY.md §8d asks for beside the 1-core figure."""
+    sys.path.insert(0, ROOT)
+    from oracle import port  # cpu_baseline leg only
+    nt = min(16, os.cpu_count() or 1)
+    pubs = d_pub[:m].cpu().numpy()
+    sigs = d_sig[:m].cpu().numpy()
+    o = offs[: m + 1].astype(np.uint64)
+    t = time.perf_counter()
+    out = port.verify_batch(pubs, sigs, msgs, o, nthreads=nt)
+    dt = time.perf_counter() - t
+    return {"value": round(m / dt, 1), "unit": "verifies/s", "cores": nt, "kind": "port",
+            "sample": "all %d signatures of the batch, %d threads, %.1f s; %s; host cpu_count=%d"
+                      % (m, nt, dt, _cpu_model(), os.cpu_count() or 1),
+            "gpu_decisions_match": bool((d_out[:m].cpu().numpy() == out).all())}
 
 
 def cpu_baseline(eng, d_pub, d_sig, msgs, offs, m, d_out):
