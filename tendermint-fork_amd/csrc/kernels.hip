@@ -1,17 +1,18 @@
 // kernels.hip — gfx950 kernels: batch ed25519 verify and RFC 8032 sign.
 //
-// One signature per lane (64 per wave).  The work per signature is ~2.7e5
-// 32x32->64 integer multiply-adds, entirely VALU; HBM traffic
-// is ~212 B per verify, so the kernel is bound by integer-VALU issue, not by
-// memory and not by MFMA (which has no 32x32->64 integer path).
+// One signature per lane (64 per wave) on the throughput paths.  The work per signature
+// is ~2.2e5 32x32->64 integer multiply-adds, entirely VALU; the
+// algorithmic HBM traffic is ~214 B per verify, so the kernels are bound by integer-VALU
+// issue, not by memory and not by MFMA (which has no 32x32->64 integer path).
 //
 // Memory layout
 //   pub   n x 32 B, sig n x 64 B (16-B aligned rows -> dwordx4 loads)
-//   msgs  concatenated bytes, off[n+1] u32
-//   slab  per-lane variable-base table: 9 cached points x 160 B, stored as
-//         [entry j][chunk q (16 B)][lane slot] so that lanes of a wave that pick
-//         the same entry read contiguous 16-B chunks.
-//   btab  9 niels multiples of B, staged once per workgroup in LDS (1080 B).
+//   msgs  concatenated bytes, off[n+1] u32 (or fixed 256-B vote slots)
+//   slab  per-lane variable-base table: 9 cached points x 160 B, lane-major
+//         [slot][entry][chunk] (default) or [entry][chunk][slot] (variant -2)
+//   btab  129 niels multiples of B, staged per workgroup in LDS (15.5 KB; variants 2-4)
+//   b16   32769 niels multiples of B in 128-B rows in HBM (4.2 MB; default variant 5)
+//   combs key-set combs [key][window][entry] and the shared combs of B (radix 256, radix 2^16)
 #include "kernels.h"
 #include "verify_core.h"
 
