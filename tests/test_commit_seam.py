@@ -79,3 +79,42 @@ def test_parallel_plan_and_replay_equal_serial():
         one = T.verify_commits(None, [reqs[q]], verifier=bitfn)[0]
         assert same(got[q], one), (q, got[q], one)
     assert len({type(e).__name__ for e in got}) >= 2
+
+
+def _one_commit(flag_override=None):
+    from oracle.fixtures import make_block_id, make_commit, make_valset, seed_of
+    from commit_cases import to_product
+    vs, seeds = make_valset([seed_of("ei", i) for i in range(4)], [10] * 4)
+    bid = make_block_id("ei")
+    cm = make_commit(vs, seeds, "ei-chain", 7, 0, bid)
+    pv, pc = to_product(vs, cm)
+    if flag_override is not None:
+        pc.signatures[2].flag = flag_override
+    return vs, pv, cm, pc, bid
+
+
+def test_inputs_the_reference_panics_on_return_einval():
+    """Where the reference would panic — an unknown BlockIDFlag reaching CommitSig.BlockID
+    (types/block.go:652-662) in VerifyCommit — the seam returns TMED_EINVAL so the caller takes
+    the original Go path (which then panics exactly as before); an unknown flag in the Light
+    loops is skipped like any non-Commit flag, as the reference does (validator_set.go:742)."""
+    import pytest
+    from tmed import TmedError
+    from tmed._native import TMED_EINVAL
+    vs, pv, cm, pc, bid = _one_commit(flag_override=9)
+    with pytest.raises(TmedError) as ei:
+        T.verify_commits(None, [(T.MODE_COMMIT, pv, "ei-chain", pbid(bid), 7, pc, 0, 0)], verifier=oracle_verifier)
+    assert ei.value.code == TMED_EINVAL
+    # Light: flag 9 is not BlockIDFlagCommit -> skipped; 3 of 4 equal powers still cross 2/3
+    got = T.verify_commits(None, [(T.MODE_LIGHT, pv, "ei-chain", pbid(bid), 7, pc, 0, 0)], verifier=oracle_verifier)
+    assert got == [None]
+
+
+def test_bad_mode_and_missing_block_id_return_einval():
+    import pytest
+    from tmed import TmedError
+    vs, pv, cm, pc, bid = _one_commit()
+    with pytest.raises(TmedError):
+        T.verify_commits(None, [(7, pv, "ei-chain", pbid(bid), 7, pc, 0, 0)], verifier=oracle_verifier)
+    with pytest.raises(TmedError):  # VerifyCommit / Light need a BlockID
+        T.verify_commits(None, [(T.MODE_LIGHT, pv, "ei-chain", None, 7, pc, 0, 0)], verifier=oracle_verifier)
