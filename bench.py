@@ -38,7 +38,7 @@ sys.path.insert(0, os.path.join(ROOT, "tendermint-fork_amd"))
 MUL, SQ = 100, 55
 # Straus per byte of the scalars: 8 dbl (32 S + 26 M) + 2 cached (-A) adds with their conversions
 # (14 M), plus, where a B window ends, p1p1->p3 + niels add + p1p1->p2 instead of one p1p1->p2 (+7 M)
-MAIN_VARIANT = int(os.environ.get("TMED_MAIN_WAVES", "5"))
+MAIN_VARIANT = int(os.environ.get("TMED_MAIN_WAVES", "6"))
 B_WINDOWS = 16 if MAIN_VARIANT == 5 else 32     # radix-2^16 (default) or radix-256 B windows
 MADS_STRAUS = 32 * (32 * SQ + 40 * MUL) + B_WINDOWS * 7 * MUL
 MADS_TABLE = 64 * MUL                        # 1..8 x (-A), cached form
@@ -50,6 +50,18 @@ MADS_SCALAR = 188                            # mod-L Barrett (v_mad_u64_u32)
 MADS_PER_VERIFY_GENERIC = MADS_STRAUS + MADS_TABLE + MADS_DECODE + MADS_ENCODE + MADS_SCALAR
 # the dominant kernel (verify_main_kernel): table + Straus + T = XY of the hand-off
 MADS_MAIN = MADS_STRAUS + MADS_TABLE + MUL
+MAIN_KERNEL = "verify_main_kernel"
+if MAIN_VARIANT == 6:
+    # half-size scalars (verify_hs.h, the default): W = 33 radix-16 windows (the usual wave
+    # maximum; some waves run 34) of 4 dbl (16 S + 13 M) and two cached adds with their
+    # conversions (15 M), 8 B steps of two niels adds (+14 M each), two tables (-A, -sign(d) R)
+    # and T = XY of A and R; no finish.  Outside the main kernel: decode of A and strict decode
+    # of R, the mod-L work (Barrett + |d| S).  The lattice step (fp64 quotient estimates,
+    # ~130 Euclid steps) is not counted in mads.
+    HS_W = 33
+    MADS_MAIN = (HS_W - 1) * (16 * SQ + 13 * MUL) + HS_W * 15 * MUL + 8 * 14 * MUL + 2 * MADS_TABLE + 2 * MUL
+    MADS_PER_VERIFY_GENERIC = MADS_MAIN + 2 * MADS_DECODE + MADS_SCALAR + 64 + 188
+    MAIN_KERNEL = "verify_main_hs_kernel"
 
 
 def parse():
@@ -159,11 +171,11 @@ def main():
             eng.set_kernel_timing(True)
             step()
             torch.cuda.synchronize(dev)
-            (prep_ms, main_ms, fin_ms), (launches, _, fin_launches) = eng.kernel_times()
+            (prep_ms, main_ms, fin_ms), (prep_launches, launches, fin_launches) = eng.kernel_times()
             eng.set_kernel_timing(False)
             achieved = n * MADS_MAIN / (main_ms * 1e-3) / 1e12
             traffic, traffic_src = pmc_traffic(n / max(1, launches))
-            roof = {"bound": "valu", "kernel": "verify_main_kernel", "achieved": round(achieved, 3),
+            roof = {"bound": "valu", "kernel": MAIN_KERNEL, "achieved": round(achieved, 3),
                     "peak": round(peak, 3) if peak else None,
                     "unit": "Tmad/s (v_mad_i64_i32 lane-ops; peak = measured sustained rate)",
                     "frac": round(achieved / peak, 4) if peak else None,
@@ -171,7 +183,7 @@ def main():
                     "traffic_source": traffic_src,
                     "mads_per_verify_main": MADS_MAIN, "mads_per_verify_total": MADS_PER_VERIFY_GENERIC,
                     "kernel_avg_ms": round(main_ms / max(1, launches), 4), "launches_per_step": launches,
-                    "prep_kernel_avg_ms": round(prep_ms / max(1, launches), 4),
+                    "prep_kernels_ms": round(prep_ms / max(1, launches), 4), "prep_launches": prep_launches,
                     "finish_kernel_ms": round(fin_ms, 4), "finish_launches": fin_launches,
                     "step_kernel_ms": round(kernel_ms, 3),
                     "algorithmic_bytes_per_verify": 32 + 64 + int(offs[-1]) // n + 4 + 1}
@@ -222,7 +234,7 @@ def pmc_traffic(sigs_per_launch):
     except (OSError, ValueError):
         return None, None
     for k, d in pmc.items():
-        if k.startswith("verify_main_kernel") and "hbm_bytes_per_sig" in d:
+        if k.split("<")[0] == MAIN_KERNEL and "hbm_bytes_per_sig" in d:
             return round(d["hbm_bytes_per_sig"] * sigs_per_launch), "profiles/pmc_summary.json[%s]" % k
     return None, None
 

@@ -127,7 +127,7 @@ struct tmed_ctx {
   int4 *d_fin_pre = nullptr;  // batched-finish prefix products (kFinPreBytes)
   uint32_t slab_slots = 0;
   uint32_t chunk = 0;     // signatures per prep/main launch pair (0 = slab_slots); env TMED_CHUNK
-  int main_waves = 5;     // main-kernel variant (5: radix-2^16 B windows, the measured best); env TMED_MAIN_WAVES
+  int main_waves = 6;     // main-kernel variant (6: half-size scalars, verify_hs.h; 5: full-length Straus); env TMED_MAIN_WAVES
   uint32_t lat_max = 24576;  // key-cached batches up to this size take the latency kernels (crossover ~32k,
                              // profiles/r01/session3/lat_sweep.jsonl); env TMED_LAT_MAX
   bool timing = false;    // tmed_set_kernel_timing

@@ -26,6 +26,9 @@ constexpr uint32_t kThreadsPerBlock = 256;
 // Variable-base table slab: lane slots (grid-stride loop bounds the grid to
 // slab_slots / kThreadsPerBlock blocks).  9 entries x 160 B per slot.
 constexpr uint32_t kSlabSlotBytes = 9 * 160;
+// The half-size path (main variant 6) keeps two per-lane tables (-A and -sign(d) R): the slab
+// is allocated with kSlabTables slot regions.
+constexpr uint32_t kSlabTables = 2;
 
 // Batched finish (verify_core.h finish_group): the main kernels hand projective R' over in
 // fin ([q][slot], kFinInt4 int4 per signature, kFinCap slots); the finish kernel runs once per
@@ -43,6 +46,7 @@ constexpr size_t kFinPreBytes = (size_t)kFinPreStride * 3 * 16;
 struct BTabs {
   const ge_niels *lds;
   const int4 *b16;
+  const int4 *comb16 = nullptr;  // radix-2^16 comb of B (windows 0 and 8: the half-size path)
 };
 constexpr uint32_t kB16Entries = 32769;
 constexpr size_t kB16Bytes = (size_t)kB16Entries * 128;
@@ -64,7 +68,7 @@ hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t
 // Shared fixed-base table j*B, j = 0..128 (niels), staged in LDS by the kernels.
 constexpr int kBTabSize = 129;
 // prep hand-off bytes per signature slot (k, s, A.x, A.y, ok)
-constexpr uint32_t kPrepSlotBytes = 160;
+constexpr uint32_t kPrepSlotBytes = 352;  // 10 int4 (k, s, A) + 11 int4 (the half-size hand-off), padded
 void host_build_btab(ge_niels out[129]);
 
 // ---- fixed-base combs (key cache) -------------------------------

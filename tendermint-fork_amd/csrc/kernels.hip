@@ -15,6 +15,7 @@
 //   combs key-set combs [key][window][entry] and the shared combs of B (radix 256, radix 2^16)
 #include "kernels.h"
 #include "verify_core.h"
+#include "verify_hs.h"
 
 namespace tmed {
 
@@ -334,6 +335,114 @@ __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_main_kernel(
   out[i] = ok ? 1 : 0;
 }
 
+// ---- half-size path (verify_hs.h; main variant 6, the default) -----------------------
+// verify_prep_kernel writes k, s, A, ok to the first prep region (10 int4 per slot); the
+// R kernel adds, in the second region (kPrepHsInt4 int4 per slot, [q][slot]): recoded c
+// (words 0-7), recoded |d| (8-12), recoded e (13-20), R.x (21-30), R.y (31-40), flags (41:
+// bit 0 ok, bit 1 d < 0, bits 8.. window count).
+constexpr int kPrepHsInt4 = 11;
+static_assert((kPrepInt4 + kPrepHsInt4) * 16 <= kPrepSlotBytes, "prep slot too small for the half-size hand-off");
+
+__global__ __launch_bounds__(kThreadsPerBlock) void verify_prep_r_kernel(
+    const uint8_t *__restrict__ sig, uint32_t base, uint32_t count, const int4 *__restrict__ prep,
+    int4 *__restrict__ prep2, uint32_t stride) {
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= count) return;
+  int32_t w[44];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {  // k (words 0-7), s (8-15)
+    const int4 v = prep[(size_t)q * stride + slot];
+    w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+  }
+  const bool ok = prep[(size_t)9 * stride + slot].x != 0;  // word 36
+  uint32_t k[8], s[8], Rw[8], cr[8], dr[8], er[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) { k[j] = (uint32_t)w[j]; s[j] = (uint32_t)w[8 + j]; }
+  load_row_words(Rw, sig + 64 * (size_t)(base + slot), 2);
+  fe Rx, Ry;
+  bool dneg;
+  int W;
+  const bool rok = hs_prep_r(k, s, Rw, cr, dr, er, dneg, Rx, Ry, W);
+#pragma unroll
+  for (int j = 0; j < 8; j++) { w[j] = (int32_t)cr[j]; w[13 + j] = (int32_t)er[j]; }
+#pragma unroll
+  for (int j = 0; j < 5; j++) w[8 + j] = (int32_t)dr[j];
+#pragma unroll
+  for (int j = 0; j < 10; j++) { w[21 + j] = Rx.v[j]; w[31 + j] = Ry.v[j]; }
+  w[41] = ((ok && rok) ? 1 : 0) | (dneg ? 2 : 0) | (W << 8);
+  w[42] = w[43] = 0;
+#pragma unroll
+  for (int q = 0; q < kPrepHsInt4; q++)
+    prep2[(size_t)q * stride + slot] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
+// Digits of the recoded c / |d| straight from the hand-off (one dword per eight windows).
+struct HsDigitsDev {
+  const int4 *p2;
+  uint32_t stride, slot;
+  __device__ __forceinline__ uint32_t word(int w) const {
+    return reinterpret_cast<const uint32_t *>(p2 + (size_t)(w >> 2) * stride + slot)[w & 3];
+  }
+  __device__ __forceinline__ uint32_t cword(int w) const { return word(w); }
+  __device__ __forceinline__ uint32_t dword(int w) const { return w < 5 ? word(8 + w) : 0x88888888u; }
+};
+
+// Phase 2: tables of -A and -sign(d) R in the slab (two lane-major regions), the 3-point
+// Straus sum over the wave's largest window count, B digits from windows 0 and 8 of the
+// radix-2^16 comb (each entry fetched into LDS 16 doublings ahead), identity test.  Every
+// lane of the grid stays to the end (the wave maximum of W is a shuffle reduction); lanes
+// past count run on the identity and store nothing.
+__global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_hs_kernel(
+    uint32_t base, uint32_t count, const int4 *__restrict__ prep, const int4 *__restrict__ prep2, uint32_t stride,
+    int4 *__restrict__ slab, const int4 *__restrict__ comb16, uint8_t *__restrict__ out) {
+  __shared__ int4 sbl[kThreadsPerBlock / 64][8 * 64];
+  __shared__ int4 sbh[kThreadsPerBlock / 64][8 * 64];
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = slot < count;
+  int32_t w[44];
+#pragma unroll
+  for (int q = 3; q < kPrepHsInt4; q++) {  // e, R, flags (words 12..43)
+    const int4 v = active ? prep2[(size_t)q * stride + slot] : make_int4(0, 0, 0, 0);
+    w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+  }
+  uint32_t er[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) er[j] = (uint32_t)w[13 + j];
+  fe Rx, Ry;
+#pragma unroll
+  for (int j = 0; j < 10; j++) { Rx.v[j] = w[21 + j]; Ry.v[j] = w[31 + j]; }
+  int32_t a[20];
+#pragma unroll
+  for (int q = 4; q < 9; q++) {  // A.x, A.y: words 16..35 of the first region
+    const int4 v = active ? prep[(size_t)q * stride + slot] : make_int4(0, 0, 0, 0);
+    a[4 * q - 16] = v.x; a[4 * q - 15] = v.y; a[4 * q - 14] = v.z; a[4 * q - 13] = v.w;
+  }
+  ge_p3 A;
+#pragma unroll
+  for (int j = 0; j < 10; j++) { A.X.v[j] = a[j]; A.Y.v[j] = a[10 + j]; }
+  if (!active) { fe_1(A.Y); fe_1(Ry); }
+  fe_1(A.Z);
+  fe_mul(A.T, A.X, A.Y);
+  const int flags = w[41];
+  int W = active ? (flags >> 8) : 29;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int x = __shfl_xor(W, o);
+    W = x > W ? x : W;
+  }
+  W = __builtin_amdgcn_readfirstlane(W);
+  if (W < 29) W = 29;
+  if (W > 64) W = 64;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const HsDigitsDev ds{prep2, stride, slot};
+  SlabTabT<true> ta{slab, stride, slot};
+  SlabTabT<true> tr{slab + (size_t)stride * 90, stride, slot};
+  B16Pf bl{comb16, sbl[wv], lane};
+  B16Pf bh{comb16 + (size_t)8 * kB16Entries * kCombEntryInt4, sbh[wv], lane};
+  const bool id = verify_main_hs(ds, (flags & 2) != 0, er, W, A, Rx, Ry, ta, tr, bl, bh);
+  if (active) out[base + slot] = ((flags & 1) && id) ? 1 : 0;
+}
+
 // Phase 3: batched finish.  Lane l owns slots l, l + L, l + 2L, ... (< m) of the block of m
 // signatures starting at fin_base (coalesced [q][slot] loads); finish_group inverts their
 // Z with one inversion and compares each canonical encoding with R.
@@ -454,9 +563,22 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
     for (uint32_t base = fbase; base < fbase + m; base += chunk) {
       const uint32_t count = (fbase + m - base) < chunk ? (fbase + m - base) : chunk;
       const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
+
       hipLaunchKernelGGL(verify_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, pub, sig, ms, base,
                          count, prep, slab_stride);
       if (timer) timer->mark(stream, 0);
+      if (main_waves == 6) {  // half-size scalars (verify_hs.h): R decode + lattice, main; no finish
+        int4 *prep2 = prep + (size_t)kPrepInt4 * slab_stride;
+        hipLaunchKernelGGL(verify_prep_r_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base, count,
+                           prep, prep2, slab_stride);
+        if (timer) timer->mark(stream, 0);
+        hipLaunchKernelGGL(verify_main_hs_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base, count, prep,
+                           prep2, slab_stride, slab, btab.comb16, out);
+        if (timer) timer->mark(stream, 1);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        continue;
+      }
       // default (5): 2 waves/SIMD, lane-major per-lane tables (+3.7 % over the slot-interleaved
       // layout), radix-2^16 B windows from the HBM table (+3.3 % over the LDS radix-256
       // table, profiles/r01/session3/variants_b16.txt); the others are measured A/B variants.
@@ -479,7 +601,7 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
-    hipError_t e = launch_finish(fin, fin_pre, sig, out, fbase, m, stream);
+    hipError_t e = main_waves == 6 ? hipSuccess : launch_finish(fin, fin_pre, sig, out, fbase, m, stream);
     if (timer) timer->mark(stream, 2);
     if (e != hipSuccess) return e;
   }

@@ -72,7 +72,7 @@ int tmed_init(int device, tmed_ctx **out) {
   if (const char *v = getenv("TMED_SLAB_SLOTS")) c->slab_slots = (uint32_t)strtoul(v, nullptr, 10);
   if (const char *v = getenv("TMED_LAT_MAX")) c->lat_max = (uint32_t)strtoul(v, nullptr, 10);
   if (c->lat_max > kLatMax) c->lat_max = kLatMax;
-  if (e == hipSuccess) e = hipMalloc((void **)&c->d_slab, (size_t)c->slab_slots * kSlabSlotBytes);
+  if (e == hipSuccess) e = hipMalloc((void **)&c->d_slab, (size_t)c->slab_slots * kSlabSlotBytes * kSlabTables);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_prep, (size_t)c->slab_slots * kPrepSlotBytes);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_fin, kFinBytes);          // 128 MB: projective R'
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_fin_pre, kFinPreBytes);   // 48 MB: prefix products
@@ -187,7 +187,7 @@ int tmed_verify_batch_device(tmed_ctx *c, const uint8_t *d_pub, const uint8_t *d
   if (c->timing) c->timer.n = 0;
   hipError_t e = scratch_acquire(c, s);
   if (e == hipSuccess)
-    e = launch_verify(d_pub, d_sig, d_msgs, d_off, (uint32_t)n, d_out, c->d_slab, c->slab_slots, BTabs{c->d_btab, c->d_b16}, c->d_prep,
+    e = launch_verify(d_pub, d_sig, d_msgs, d_off, (uint32_t)n, d_out, c->d_slab, c->slab_slots, BTabs{c->d_btab, c->d_b16, c->d_bcomb16}, c->d_prep,
                       c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves, false, c->timing ? &c->timer : nullptr);
   if (e == hipSuccess) e = scratch_release(c, s);
   return map_err(e);
@@ -245,7 +245,7 @@ int tmed_verify_batch(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, const
   if (e == hipSuccess)
     e = launch_verify((const uint8_t *)c->d_a.p, (const uint8_t *)c->d_b.p, (const uint8_t *)c->d_msg.p,
                       (const uint32_t *)c->d_off.p, (uint32_t)n, (uint8_t *)c->d_out.p, c->d_slab, c->slab_slots,
-                      BTabs{c->d_btab, c->d_b16}, c->d_prep, c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves);
+                      BTabs{c->d_btab, c->d_b16, c->d_bcomb16}, c->d_prep, c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves);
   if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
   if (e == hipSuccess) e = scratch_release(c, s);
   if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, n, hipMemcpyDeviceToHost, s);

@@ -1,0 +1,343 @@
+// verify_hs.h — half-size-scalar verification (the generic throughput path).
+//
+// Same decision as verify_core.h's verify_one (crypto/ed25519/ed25519.go:148-155 ->
+// Go 1.18 crypto/ed25519.Verify), with half the doublings:
+//
+//   Go accepts iff enc([S]B - [k]A) == R_bytes.  enc() is canonical, so this holds iff
+//   R_bytes is the canonical encoding of a curve point R (strict decode: y < p, on the
+//   curve, not x = 0 with the sign bit set) and D := [S]B - [k]A - R is the identity.
+//
+//   The curve group has order N = 8L and is cyclic, so [d] is injective for every odd d
+//   with |d| < L.  Pick (c, d) with c = d*k (mod N), d odd and |c|, |d| ~ 2^128 (a short
+//   vector of the lattice {(c, d) : c = d k mod N}); then
+//       D = 0  <=>  [d]D = 0  <=>  [e]B - [c]A - [d]R = 0,   e = d*S mod L
+//   exactly — for every A, including keys with a torsion component, because c = dk
+//   holds modulo the full group order 8L, not only modulo L.  B has order L, so e can
+//   be reduced mod L.
+//
+//   The check is then a 3-point Straus sum with ~130-bit scalars for A and R (4 doublings
+//   and two cached additions per radix-16 window, ~33 windows instead of 64) and the full
+//   scalar e for B from two radix-2^16 tables (j*B and j*2^128*B, 8 windows each), and
+//   the comparison with the identity is projective (X = 0, Y = Z): no inversion.
+//
+// (c, d) comes from the extended Euclidean algorithm on (N, k): r_i = t_i k (mod N),
+// stopped at the first r_i < 2^128, where |t_i| <= N / r_{i-1} <= 2^127.  If t_i is
+// even (t_{i-1} and t_i are coprime, so t_{i-1} is odd), the vector
+// (r_{i-1} - j r_i, t_{i-1} - j t_i) with j in [0, floor(r_{i-1}/r_i)] balancing the two
+// magnitudes is taken instead (odd t, at most a few bits longer).  Quotients come from
+// fp64 estimates corrected to the exact floor; any step the estimate cannot settle
+// (quotient >= 2^32, or an estimate off by more than one) falls back to (c, d) = (k, 1),
+// the unshortened equation — so the decision never depends on the lattice step, only
+// the length of the loop does.  The loop length W (radix-16 windows) is per lane here and
+// the wave maximum on the device.
+#pragma once
+#include <math.h>
+
+#include "verify_core.h"
+
+namespace tmed {
+
+// N = 8L (little-endian words).
+TMED_HD void sc_const_8L(uint32_t n[8]) {
+  const uint32_t c[8] = {0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa6f7cef5u, 0u, 0u, 0u, 0x80000000u};
+#pragma unroll
+  for (int i = 0; i < 8; i++) n[i] = c[i];
+}
+
+TMED_HD int bitlen_words(const uint32_t *x, int n) {
+  int b = 0;
+#pragma unroll
+  for (int i = 0; i < n; i++)
+    if (x[i]) b = 32 * i + 32 - __builtin_clz(x[i]);
+  return b;
+}
+
+TMED_HD double words_to_double(const uint32_t *x, int n) {
+  double r = 0.0;
+#pragma unroll
+  for (int i = n - 1; i >= 0; i--) r = r * 4294967296.0 + (double)x[i];
+  return r;
+}
+
+// r = a - q*b (8 words); returns true if the result went negative (wrapped mod 2^256).
+TMED_HD bool words8_submul(uint32_t r[8], const uint32_t a[8], uint32_t q, const uint32_t b[8]) {
+  uint64_t carry = 0;
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t p = (uint64_t)q * b[i] + carry;
+    carry = p >> 32;
+    const uint64_t d = (uint64_t)a[i] - (uint32_t)p - borrow;
+    r[i] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+  return (carry + borrow) != 0;
+}
+
+// r += b; returns the carry out.
+TMED_HD uint32_t words8_add(uint32_t r[8], const uint32_t b[8]) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t t = (uint64_t)r[i] + b[i] + c;
+    r[i] = (uint32_t)t;
+    c = t >> 32;
+  }
+  return (uint32_t)c;
+}
+
+// r -= b; returns the borrow out.
+TMED_HD uint32_t words8_sub(uint32_t r[8], const uint32_t b[8]) {
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t d = (uint64_t)r[i] - b[i] - borrow;
+    r[i] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+  return borrow;
+}
+
+// a >= b
+TMED_HD bool words8_ge(const uint32_t a[8], const uint32_t b[8]) {
+  uint32_t t[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = a[i];
+  return words8_sub(t, b) == 0;
+}
+
+// Magnitudes of the cofactors t_i (< 2^160): r = a + q*b (5 words).
+constexpr int kHsTW = 5;
+TMED_HD void words5_muladd(uint32_t r[kHsTW], const uint32_t a[kHsTW], uint32_t q, const uint32_t b[kHsTW]) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < kHsTW; i++) {
+    const uint64_t t = (uint64_t)q * b[i] + a[i] + c;
+    r[i] = (uint32_t)t;
+    c = t >> 32;
+  }
+}
+
+// Half-size decomposition of k (< L): c >= 0, |d| = dm odd, dneg = (d < 0), c = d k mod 8L.
+// Returns the radix-16 window count the pair needs (29..64; 64 for the (k, 1) fallback).
+TMED_HD int sc_halfsize(uint32_t c[8], uint32_t dm[8], bool &dneg, const uint32_t k[8]) {
+  uint32_t a[8], b[8], ta[kHsTW], tb[kHsTW], nb[8], nt[kHsTW];
+  sc_const_8L(a);
+#pragma unroll
+  for (int i = 0; i < 8; i++) b[i] = k[i];
+#pragma unroll
+  for (int i = 0; i < kHsTW; i++) { ta[i] = 0; tb[i] = i == 0 ? 1u : 0u; }
+  double fa = words_to_double(a, 8), fb = words_to_double(b, 8);
+  bool fail = false, iodd = true;  // i = 1: b = r_1 = k, t_1 = +1
+#pragma unroll 1
+  for (int it = 0; it < 190; it++) {
+    if ((b[4] | b[5] | b[6] | b[7]) == 0) break;  // r_i < 2^128
+    const double qd = floor(fa / fb);
+    if (!(qd < 4294967294.0)) { fail = true; break; }
+    uint32_t q = (uint32_t)qd;
+    if (words8_submul(nb, a, q, b)) {      // estimate one too high
+      q -= 1;
+      if (words8_add(nb, b) == 0) { fail = true; break; }
+    } else if (words8_ge(nb, b)) {          // estimate one too low
+      q += 1;
+      words8_sub(nb, b);
+      if (words8_ge(nb, b)) { fail = true; break; }
+    }
+    words5_muladd(nt, ta, q, tb);
+#pragma unroll
+    for (int i = 0; i < 8; i++) { a[i] = b[i]; b[i] = nb[i]; }
+#pragma unroll
+    for (int i = 0; i < kHsTW; i++) { ta[i] = tb[i]; tb[i] = nt[i]; }
+    fa = fb;
+    fb = words_to_double(b, 8);
+    iodd = !iodd;
+  }
+  if ((b[4] | b[5] | b[6] | b[7]) != 0) fail = true;
+  if (!fail && (tb[0] & 1u) == 0) {
+    // t_i even: (r_{i-1} - j r_i, t_{i-1} - j t_i), sign of t_{i-1} (negative iff i odd)
+    const double fta = words_to_double(ta, kHsTW), ftb = words_to_double(tb, kHsTW);
+    const double qmax = floor(fa / fb);
+    double j0 = floor((fa - fta) / (fb + ftb));
+    if (!(qmax < 4294967294.0)) fail = true;
+    if (j0 < 0.0) j0 = 0.0;
+    if (j0 > qmax) j0 = qmax;
+    const double j1 = j0 + 1.0 > qmax ? qmax : j0 + 1.0;
+    const double m0 = fmax(fa - j0 * fb, fta + j0 * ftb), m1 = fmax(fa - j1 * fb, fta + j1 * ftb);
+    const uint32_t j = fail ? 0u : (uint32_t)(m1 < m0 ? j1 : j0);
+    if (words8_submul(nb, a, j, b)) fail = true;  // the estimate of floor(a/b) was high
+    words5_muladd(nt, ta, j, tb);
+#pragma unroll
+    for (int i = 0; i < 8; i++) b[i] = nb[i];
+#pragma unroll
+    for (int i = 0; i < kHsTW; i++) tb[i] = nt[i];
+    iodd = !iodd;  // sign(t_{i-1}) = -sign(t_i)
+  }
+  if (fail) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) { c[i] = k[i]; dm[i] = i == 0 ? 1u : 0u; }
+    dneg = false;
+    return 64;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) { c[i] = b[i]; dm[i] = i < kHsTW ? tb[i] : 0u; }
+  dneg = !iodd;  // t_i = (-1)^(i+1) |t_i|
+  const int bc = bitlen_words(c, 8), bd = bitlen_words(dm, 8);
+  if (bd > 150) {  // keeps the recoded |d| within five words (never seen: |d| ~ 2^128)
+#pragma unroll
+    for (int i = 0; i < 8; i++) { c[i] = k[i]; dm[i] = i == 0 ? 1u : 0u; }
+    dneg = false;
+    return 64;
+  }
+  const int bits = bc > bd ? bc : bd;
+  int W = (bits + 2 + 3) / 4;  // |x| < 2^(4W-2): no carry out of the W recoded nibbles
+  return W < 29 ? 29 : W;
+}
+
+// Phase 1b of the half-size path (after verify_prep's hash / S check / decode of A): strict
+// decode of R, the lattice step and e = d S mod L.  Writes the recoded scalars — cr, dr:
+// signed radix-16 (sc_recode16; dr words 5..7 are 0x88888888, i.e. zero digits, since
+// |d| < 2^150), er: signed radix-2^16 — R (affine; the identity when it does not decode)
+// and the window count; returns the R verdict.
+TMED_HD bool hs_prep_r(const uint32_t k[8], const uint32_t s[8], const uint32_t Rw[8], uint32_t cr[8],
+                       uint32_t dr[8], uint32_t er[8], bool &dneg, fe &Rx, fe &Ry, int &W) {
+  const bool rok = r_decode_strict(Rx, Ry, Rw);
+  if (!rok) { fe_0(Rx); fe_1(Ry); }
+  uint32_t c[8], dm[8], e[8];
+  W = sc_halfsize(c, dm, dneg, k);
+  uint32_t zero[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) zero[i] = 0;
+  sc_muladd(e, dm, s, zero);  // |d| S mod L
+  uint32_t L[8], ne[8];
+  sc_const_L(L);
+#pragma unroll
+  for (int i = 0; i < 8; i++) ne[i] = L[i];
+  words8_sub(ne, e);
+  uint32_t nz = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) nz |= e[i];
+#pragma unroll
+  for (int i = 0; i < 8; i++) e[i] = (dneg && nz) ? ne[i] : e[i];
+  sc_recode16(cr, c);
+  sc_recode16(dr, dm);
+  sc_recode_b<16>(er, e);
+  return rok;
+}
+
+// Host-side digit source over the recoded words (the device reads them from the hand-off).
+struct HsDigits {
+  uint32_t cr[8], dr[8];
+  TMED_HDM uint32_t cword(int w) const { return cr[w]; }
+  TMED_HDM uint32_t dword(int w) const { return dr[w]; }
+};
+
+// Both phases of the half-size prep (the host simulation's single pass).
+TMED_HD bool verify_prep_hs(const uint32_t pubw[8], const uint32_t sigw[16], const uint8_t *msg, uint32_t mlen,
+                            HsDigits &dg, uint32_t er[8], bool &dneg, ge_p3 &A, fe &Rx, fe &Ry, int &W) {
+  uint32_t k[8], s[8];
+  const bool ok = verify_prep(pubw, sigw, msg, mlen, k, s, A);
+  const bool rok = hs_prep_r(k, s, sigw, dg.cr, dg.dr, er, dneg, Rx, Ry, W);
+  return ok && rok;
+}
+
+TMED_HD void words4_shl16(uint32_t x[4]) {
+#pragma unroll
+  for (int i = 3; i > 0; i--) x[i] = (x[i] << 16) | (x[i - 1] >> 16);
+  x[0] <<= 16;
+}
+
+// Q = [e]B + [c](-A) + [|d|](-sign(d) R) over W radix-16 windows (Straus, most significant
+// first).  DS: cword(w) / dword(w), word w (0..7) of the recoded c / |d| — read once per
+// eight windows, before the doublings that hide the read.  TA / TR: per-lane cached tables
+// of j*(-A) and j*(-sign(d) R), j = 0..8 (build_table_negA), prefetch(j) / take(ge_cached&).
+// BL / BH: niels tables of j*B and j*2^128*B, j = 0..32768, prefetch(j) / take(ge_niels&);
+// the 16-bit digits of e (er, recoded) are added at windows 28, 24, ..., 0 (16 doublings
+// apart): low-table digit m and high-table digit m + 8 at window 4m, each entry prefetched
+// one B step ahead.  Needs 29 <= W <= 64.
+template <class DS, class TA, class TR, class BL, class BH>
+TMED_HD void hs_straus(ge_p2 &out, const DS &ds, const uint32_t er[8], int W, TA &ta, TR &tr, BL &bl, BH &bh) {
+  uint32_t el[4] = {er[0], er[1], er[2], er[3]}, eh[4] = {er[4], er[5], er[6], er[7]};
+  {
+    const int dl = (int)(el[3] >> 16) - 32768, dh = (int)(eh[3] >> 16) - 32768;
+    bl.prefetch(dl < 0 ? -dl : dl);
+    bh.prefetch(dh < 0 ? -dh : dh);
+  }
+  ge_p2 q;
+  ge_p1p1 t;
+  ge_p3 r;
+  ge_cached ca;
+  ge_niels nb;
+  uint32_t cw = 0, dw = 0;
+#pragma unroll 1
+  for (int n = W - 1; n >= 0; n--) {
+    if (n == W - 1 || (n & 7) == 7) {
+      cw = ds.cword(n >> 3);
+      dw = ds.dword(n >> 3);
+    }
+    const int sh = 4 * (n & 7);
+    const int dc = (int)((cw >> sh) & 15u) - 8, dd = (int)((dw >> sh) & 15u) - 8;
+    if (n == W - 1) {
+      ge_p3_0(r);
+    } else {
+#pragma unroll 1
+      for (int k = 0; k < 3; k++) {
+        ge_p2_dbl(t, q);
+        ge_p1p1_to_p2(q, t);
+      }
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p3(r, t);
+    }
+    ta.prefetch(dc < 0 ? -dc : dc);
+    ta.take(ca);
+    ge_add_cached(t, r, ca, dc < 0);
+    ge_p1p1_to_p3(r, t);
+    tr.prefetch(dd < 0 ? -dd : dd);
+    tr.take(ca);
+    ge_add_cached(t, r, ca, dd < 0);
+    if ((n & 3) == 0 && n <= 28) {
+      const int dl = (int)(el[3] >> 16) - 32768, dh = (int)(eh[3] >> 16) - 32768;
+      words4_shl16(el);
+      words4_shl16(eh);
+      ge_p1p1_to_p3(r, t);
+      bl.take(nb);
+      {
+        const int dn = (int)(el[3] >> 16) - 32768;
+        bl.prefetch(dn < 0 ? -dn : dn);
+      }
+      niels_apply_sign(nb, dl < 0);
+      ge_madd_niels(t, r, nb, false);
+      ge_p1p1_to_p3(r, t);
+      bh.take(nb);
+      {
+        const int dn = (int)(eh[3] >> 16) - 32768;
+        bh.prefetch(dn < 0 ? -dn : dn);
+      }
+      niels_apply_sign(nb, dh < 0);
+      ge_madd_niels(t, r, nb, false);
+    }
+    ge_p1p1_to_p2(q, t);
+  }
+  out = q;
+}
+
+// (X : Y : Z) is the identity: X = 0 and Y = Z (Z != 0 for the complete formulas).
+TMED_HD bool p2_is_identity(const ge_p2 &q) { return fe_iszero(q.X) && fe_equal(q.Y, q.Z) && !fe_iszero(q.Z); }
+
+// Phase 2 of the half-size path: tables of -A and -sign(d) R, the 3-point sum, the
+// identity test.  A: extended (T set); R: affine (x, y).
+template <class DS, class TA, class TR, class BL, class BH>
+TMED_HD bool verify_main_hs(const DS &ds, bool dneg, const uint32_t er[8], int W, const ge_p3 &A, const fe &Rx,
+                            const fe &Ry, TA &ta, TR &tr, BL &bl, BH &bh) {
+  build_table_negA(ta, A);
+  ge_p3 R;
+  if (dneg) fe_neg(R.X, Rx); else fe_copy(R.X, Rx);
+  fe_copy(R.Y, Ry);
+  fe_1(R.Z);
+  fe_mul(R.T, R.X, R.Y);
+  build_table_negA(tr, R);
+  ge_p2 q;
+  hs_straus(q, ds, er, W, ta, tr, bl, bh);
+  return p2_is_identity(q);
+}
+
+}  // namespace tmed

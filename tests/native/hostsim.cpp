@@ -9,6 +9,7 @@
 
 #include <vector>
 #include "verify_core.h"
+#include "verify_hs.h"
 #include "sha256.h"
 
 using namespace tmed;
@@ -127,6 +128,62 @@ void hostsim_verify_batch_g(const uint8_t *pub, const uint8_t *sig, const uint8_
 void hostsim_verify_batch_b16(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                               size_t n, uint8_t *out) {
   verify_batch_impl(pub, sig, msgs, off, n, out, 16, 16);
+}
+
+// Half-size-scalar path (verify_hs.h): prep_hs + main_hs per signature, B digits from the
+// j*B and j*2^128*B tables (the device's radix-2^16 comb windows 0 and 8).
+static const std::vector<ge_niels> &b16hi_tab() {
+  static std::vector<ge_niels> t;
+  static bool init = false;
+  if (!init) {
+    t.resize(32769);
+    ge_p3 P;
+    ge_base_point(P);
+    for (int i = 0; i < 16; i++) ge_mul256(P);  // 2^128 B
+    ge_niels_0(t[0]);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (long j = 1; j < 32769; j++) comb_entry(t[j], P, (uint32_t)j, 16);
+    init = true;
+  }
+  return t;
+}
+
+void hostsim_verify_batch_hs(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
+                             size_t n, uint8_t *out, int32_t *wins) {
+  const ge_niels *lo = b16tab().data();
+  const ge_niels *hi = b16hi_tab().data();
+#pragma omp parallel for schedule(dynamic, 16)
+  for (long i = 0; i < (long)n; i++) {
+    HostTab ta, tr;
+    HostBRef<16> bl{lo}, bh{hi};
+    uint32_t pw[8], sw[16], er[8];
+    load_words8(pw, pub + 32 * i);
+    load_words8(sw, sig + 64 * i);
+    load_words8(sw + 8, sig + 64 * i + 32);
+    bool dneg;
+    ge_p3 A;
+    fe Rx, Ry;
+    int W;
+    HsDigits dg;
+    const bool ok = verify_prep_hs(pw, sw, msgs + off[i], off[i + 1] - off[i], dg, er, dneg, A, Rx, Ry, W);
+    const bool id = verify_main_hs(dg, dneg, er, W, A, Rx, Ry, ta, tr, bl, bh);
+    out[i] = ok && id ? 1 : 0;
+    if (wins) wins[i] = W;
+  }
+}
+
+// The lattice step alone: c, |d| (32-byte LE each), dneg, window count.
+int hostsim_halfsize(const uint8_t *k32, uint8_t *c32, uint8_t *d32, int *dneg) {
+  uint32_t k[8], c[8], dm[8];
+  load_words8(k, k32);
+  bool neg;
+  const int W = sc_halfsize(c, dm, neg, k);
+  for (int i = 0; i < 32; i++) {
+    c32[i] = (uint8_t)(c[i / 4] >> (8 * (i % 4)));
+    d32[i] = (uint8_t)(dm[i / 4] >> (8 * (i % 4)));
+  }
+  *dneg = neg ? 1 : 0;
+  return W;
 }
 
 void hostsim_verify_batch(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,

@@ -72,6 +72,9 @@ def test_decode_matches_go_rule(hostsim):
 def _verify(l, pubs, sigs, msgs, offs, group=16):
     n = len(pubs)
     out = np.zeros(n, np.uint8)
+    if group == "hs":  # main variant 6 (default): half-size scalars, verify_hs.h
+        l.hostsim_verify_batch_hs(_p(pubs), _p(sigs), _p(msgs), _p(offs), ctypes.c_size_t(n), _p(out), None)
+        return out
     if group == "b16":  # main-kernel variant 5: radix-2^16 B windows from the 32769-entry table
         l.hostsim_verify_batch_b16(_p(pubs), _p(sigs), _p(msgs), _p(offs), ctypes.c_size_t(n), _p(out))
         return out
@@ -80,7 +83,7 @@ def _verify(l, pubs, sigs, msgs, offs, group=16):
     return out
 
 
-@pytest.mark.parametrize("group", [0, 1, 5, 16, "b16"])
+@pytest.mark.parametrize("group", [0, 1, 5, 16, "b16", "hs"])
 def test_golden_vectors_hostsim(hostsim, golden, group):
     """Every golden tuple, with per-signature encoding (group 0) and through the batched
     finish (Montgomery inversion over groups of 1, 5 and 16 signatures, partial last group);
@@ -142,3 +145,73 @@ def test_comb_path_hostsim(hostsim, golden, fn):
     exp = np.array([v["valid"] for v in vs], np.uint8)
     assert (out == exp).all(), [vs[i]["class"] for i in np.nonzero(out != exp)[0]]
     assert exp.sum() > 10 and (exp == 0).sum() > 10
+
+
+def test_halfsize_lattice(hostsim):
+    """verify_hs.h sc_halfsize: c = d k (mod 8L), d odd, both within the window count's range
+    (|x| < 2^(4W-2)); W = 64 only for the (k, 1) fallback; typical W is 32..34."""
+    L = E.L
+    rng = random.Random(3)
+    ks = [0, 1, 2, 3, 8, 16, L - 1, L - 2, 2**127, 2**128 - 1, 2**128, 2**200, 2**252 - 1, 5 * 2**128 + 3]
+    ks += [rng.randrange(L) for _ in range(4000)]
+    ws = []
+    for k in ks:
+        c, d = ctypes.create_string_buffer(32), ctypes.create_string_buffer(32)
+        neg = ctypes.c_int()
+        W = hostsim.hostsim_halfsize(k.to_bytes(32, "little"), c, d, ctypes.byref(neg))
+        ci, di = int.from_bytes(c.raw, "little"), int.from_bytes(d.raw, "little")
+        if neg.value:
+            di = -di
+        assert (ci - di * k) % (8 * L) == 0, k
+        assert di % 2 == 1 and 0 < abs(di) < L, k
+        assert 29 <= W <= 64 and max(ci.bit_length(), abs(di).bit_length()) <= 4 * W - 2, (k, W)
+        if W == 64:
+            assert (ci, di) == (k, 1)
+        ws.append(W)
+    rand = ws[14:]
+    assert max(rand) <= 36 and sum(rand) / len(rand) < 33.2
+
+
+def test_halfsize_torsion_keys(hostsim):
+    """The half-size equation multiplies by d modulo the full group order 8L, so keys with a
+    torsion component keep the reference's cofactorless decision: A = A0 + T (T of order 2, 4
+    or 8) with R = [r]B - [k]T (valid) or R = [r]B (invalid unless [k]T = 0)."""
+    rng = random.Random(9)
+    small = E.small_order_points()
+    pubs, sigs, msgs, exp = [], [], [], []
+    for i in range(96):
+        a = rng.randrange(1, E.L)
+        T = small[i % 8]
+        A = E.pt_add(E.pt_mul(a, E.BASE), T)
+        pub = E.encode(A)
+        m = rng.randbytes(40)
+        r = rng.randrange(1, E.L)
+        for mode in range(2):
+            R0 = E.pt_mul(r, E.BASE)
+            # k depends on R's bytes: pick R first, then S = r + k a (mod L)
+            R = R0
+            if mode == 0:
+                # R = [r]B - [k]T requires k: iterate once with the k of the torsion-corrected R
+                for _ in range(4):
+                    Rb = E.encode(R)
+                    k = int.from_bytes(hashlib.sha512(Rb + pub + m).digest(), "little") % E.L
+                    R_new = E.pt_add(R0, E.pt_neg(E.pt_mul(k, T)))
+                    if E.encode(R_new) == Rb:
+                        break
+                    R = R_new
+            Rb = E.encode(R)
+            k = int.from_bytes(hashlib.sha512(Rb + pub + m).digest(), "little") % E.L
+            S = (r + k * a) % E.L
+            pubs.append(pub)
+            sigs.append(Rb + S.to_bytes(32, "little"))
+            msgs.append(m)
+            exp.append(1 if E.verify(pub, m, sigs[-1]) else 0)
+    n = len(pubs)
+    P = np.array([np.frombuffer(p, np.uint8) for p in pubs])
+    Sg = np.array([np.frombuffer(s, np.uint8) for s in sigs])
+    offs = np.zeros(n + 1, np.uint32)
+    offs[1:] = np.cumsum([len(m) for m in msgs])
+    M = np.frombuffer(b"".join(msgs) + b"\0", np.uint8)
+    out = _verify(hostsim, P, Sg, M, offs, "hs")
+    assert (out == np.array(exp, np.uint8)).all()
+    assert 0 < sum(exp) < n

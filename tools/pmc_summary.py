@@ -14,7 +14,7 @@ import json
 import os
 import sys
 
-KERNELS = ("verify_main_kernel", "verify_prep_kernel", "verify_finish_kernel", "verify_keyset_main_kernel",
+KERNELS = ("verify_main_hs_kernel", "verify_prep_r_kernel", "verify_main_kernel", "verify_prep_kernel", "verify_finish_kernel", "verify_keyset_main_kernel",
            "verify_keyset_prep_kernel", "sign_kernel", "merkle", "sha256")
 
 
