@@ -18,7 +18,12 @@ Extra JSON fields:
                 against the measured device peak of that instruction.
   cpu_baseline  the C restatement of Go 1.18 crypto/ed25519.Verify (oracle/ed25519_port.c,
                 "port"), single thread (the reference verifies on one goroutine), timed on
-                a bounded sample of the same workload.
+                a bounded sample of the same workload; beside it OpenSSL 3 EVP_DigestVerify
+                (anchor_openssl), an independent implementation, on the same sample.
+  c2_keyset_variant    the second C2 variant: 10k reused keys, key cache on.
+  c1_verifycommit_p50  the metric's second half: VerifyCommit p50 latency @175 validators
+                through the seam, generic and key-cached, with its 1-thread CPU baseline.
+`--gpus N` without a torchrun environment starts N ranks itself (a child torch.distributed.run).
 """
 from __future__ import annotations
 
@@ -38,7 +43,7 @@ sys.path.insert(0, os.path.join(ROOT, "tendermint-fork_amd"))
 MUL, SQ = 100, 55
 # Straus per byte of the scalars: 8 dbl (32 S + 26 M) + 2 cached (-A) adds with their conversions
 # (14 M), plus, where a B window ends, p1p1->p3 + niels add + p1p1->p2 instead of one p1p1->p2 (+7 M)
-MAIN_VARIANT = int(os.environ.get("TMED_MAIN_WAVES", "6"))
+MAIN_VARIANT = 5 if os.environ.get("TMED_MAIN_WAVES") == "5" else 6  # tmed_init reads the same knob
 B_WINDOWS = 16 if MAIN_VARIANT == 5 else 32     # radix-2^16 (default) or radix-256 B windows
 MADS_STRAUS = 32 * (32 * SQ + 40 * MUL) + B_WINDOWS * 7 * MUL
 MADS_TABLE = 64 * MUL                        # 1..8 x (-A), cached form
@@ -62,24 +67,74 @@ if MAIN_VARIANT == 6:
     MADS_MAIN = (HS_W - 1) * (16 * SQ + 13 * MUL) + HS_W * 15 * MUL + 8 * 14 * MUL + 2 * MADS_TABLE + 2 * MUL
     MADS_PER_VERIFY_GENERIC = MADS_MAIN + 2 * MADS_DECODE + MADS_SCALAR + 64 + 188
     MAIN_KERNEL = "verify_main_hs_kernel"
+# key-cached main kernel (C2 variant): 32 A-comb + 16 radix-2^16 B-comb mixed additions (3M),
+# each followed by p1p1->p3 (4M)
+MADS_KEYSET_MAIN = 48 * 7 * MUL
 
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node; without a torchrun environment bench.py starts N ranks itself")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=1 << 20, help="signatures per GPU")
-    ap.add_argument("--cpu-sample", type=int, default=150_000, help="signatures timed on the CPU baseline")
+    ap.add_argument("--sigs", type=int, default=1 << 20, help="signatures per GPU (C2: 2^20)")
+    ap.add_argument("--cpu-sample", type=int, default=150_000, help="signatures timed on the 1-thread CPU baseline")
+    ap.add_argument("--openssl-sample", type=int, default=60_000, help="signatures timed on the OpenSSL anchor")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-peak", action="store_true")
+    ap.add_argument("--no-c1", action="store_true", help="skip the VerifyCommit p50 @175 validators leg")
+    ap.add_argument("--no-keyset", action="store_true", help="skip the 10k-reused-key C2 variant")
+    ap.add_argument("--c1-reps", type=int, default=1000)
     ap.add_argument("--mix", choices=["c2", "c5"], default="c2",
                     help="c5: 1%% of the batch replaced by edge-case / invalid tuples (BASELINE C5)")
     return ap.parse_args()
 
 
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` outside torchrun: start N ranks (one process per GPU) with
+    torch.distributed.run as a CHILD process — before anything here touches the GPU — and return
+    its exit code (the driver's own N>1 command is this same torchrun line)."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def mads_main_hs(w: float) -> float:
+    """v_mad_i64_i32 of verify_main_hs_kernel per signature at a wave loop length of w windows."""
+    return (w - 1) * (16 * SQ + 13 * MUL) + w * 15 * MUL + 8 * 14 * MUL + 2 * MADS_TABLE + 2 * MUL
+
+
+def window_summary(eng):
+    """Loop-length statistics of the last half-size chunk (tmed_window_stats): the lattice step's
+    per-signature window count W and the per-wave maximum the main kernel ran (W = 64 = fallback)."""
+    try:
+        lh, wh = eng.window_stats()
+    except AttributeError:  # an older library build (A/B runs through TMED_LIB)
+        return None
+    nl, nw = int(lh.sum()), int(wh.sum())
+    if nl == 0 or nw == 0:
+        return None
+    ws = np.arange(65)
+    return {"lanes": nl, "waves": nw, "lane_W_mean": round(float((lh * ws).sum()) / nl, 3),
+            "wave_W_mean": round(float((wh * ws).sum()) / nw, 3),
+            "lane_fallback_W64": int(lh[64]), "wave_W64": int(wh[64]),
+            "wave_W_hist": {str(w): int(wh[w]) for w in range(65) if wh[w]}}
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args.gpus)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world_env), file=sys.stderr)
+        return 2
     import torch
     import torch.distributed as dist
 
@@ -89,7 +144,7 @@ def main():
     from tmed.launch import dist_setup
     world, rank, local_rank, dev, coll = dist_setup()
     eng = Engine(local_rank)
-    n = args.n
+    n = args.sigs
 
     # ---- synthetic workload (untimed): shard [rank*n, (rank+1)*n) of the C2 stream
     t_gen = time.time()
@@ -157,8 +212,9 @@ def main():
 
     result = None
     if rank == 0:
-        verifies_per_s_kernel = n / (kernel_ms * 1e-3)
+        wstats = window_summary(eng) if MAIN_VARIANT != 5 else None
         roof = None
+        peak = None
         if not args.no_peak:
             import ctypes
             l = lib()
@@ -173,7 +229,8 @@ def main():
             torch.cuda.synchronize(dev)
             (prep_ms, main_ms, fin_ms), (prep_launches, launches, fin_launches) = eng.kernel_times()
             eng.set_kernel_timing(False)
-            achieved = n * MADS_MAIN / (main_ms * 1e-3) / 1e12
+            mads_main = MADS_MAIN if wstats is None else mads_main_hs(wstats["wave_W_mean"])
+            achieved = n * mads_main / (main_ms * 1e-3) / 1e12
             traffic, traffic_src = pmc_traffic(n / max(1, launches))
             roof = {"bound": "valu", "kernel": MAIN_KERNEL, "achieved": round(achieved, 3),
                     "peak": round(peak, 3) if peak else None,
@@ -181,18 +238,28 @@ def main():
                     "frac": round(achieved / peak, 4) if peak else None,
                     "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                     "traffic_source": traffic_src,
-                    "mads_per_verify_main": MADS_MAIN, "mads_per_verify_total": MADS_PER_VERIFY_GENERIC,
+                    "mads_per_verify_main": round(mads_main), "mads_per_verify_total": MADS_PER_VERIFY_GENERIC,
+                    "mads_basis": ("wave-mean window count %.3f (tmed_window_stats)" % wstats["wave_W_mean"])
+                                  if wstats else "formula",
                     "kernel_avg_ms": round(main_ms / max(1, launches), 4), "launches_per_step": launches,
                     "prep_kernels_ms": round(prep_ms / max(1, launches), 4), "prep_launches": prep_launches,
                     "finish_kernel_ms": round(fin_ms, 4), "finish_launches": fin_launches,
                     "step_kernel_ms": round(kernel_ms, 3),
-                    "algorithmic_bytes_per_verify": 32 + 64 + int(offs[-1]) // n + 4 + 1}
+                    "algorithmic_bytes_per_verify": 32 + 64 + int(offs[-1]) // n + 4 + 1,
+                    "window_stats": wstats}
         cpu = cpu_all = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(eng, d_pub, d_sig, msgs, offs, min(args.cpu_sample, n), d_out)
+            cpu = cpu_baseline(d_pub, d_sig, msgs, offs, min(args.cpu_sample, n), d_out,
+                               min(args.openssl_sample, n))
             cpu_all = cpu_baseline_threads(d_pub, d_sig, msgs, offs, n, d_out)
+        keyset = None
+        if not args.no_keyset and world == 1:
+            keyset = c2_keyset(eng, dev, torch_stream, n, args.steps, args.warmup, peak)
+        c1 = None
+        if not args.no_c1 and world == 1:
+            c1 = c1_latency(eng, args.c1_reps, not args.no_cpu_baseline)
         result = {
-            "metric": "ed25519 verifies/sec at 1/8 MI355X",
+            "metric": "ed25519 verifies/sec at %d/8 MI355X" % world,
             "value": round(value, 1),
             "unit": "verifies/s",
             "n_gpus": world,
@@ -214,13 +281,88 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
+            "c2_keyset_variant": keyset,
+            "c1_verifycommit_p50": c1,
             "setup_s": round(t_gen, 2),
         }
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
     eng.close()
-    return result
+    return 0
+
+
+def c2_keyset(eng, dev, torch_stream, n, steps, warmup, peak):
+    """C2's second variant: n signatures by 10,000 validators with the key cache
+    on (tmed_verify_batch_keyset_device: [k](-A) from each key's comb, no doublings), inputs in HBM;
+    verifies/s over `steps` timed passes and the roofline of its main kernel (HIP events)."""
+    import torch
+    from tmed.workload import c2_messages, seeds_from_tag
+    nk = 10_000
+    kseeds = seeds_from_tag(b"tmed-c2k-key", 0, nk)
+    rng = np.random.default_rng(7)
+    val_idx = rng.integers(0, nk, n).astype(np.uint32)
+    msgs, offs = c2_messages(0, n)
+    d_seed = torch.from_numpy(kseeds[val_idx]).to(dev)
+    d_msg = torch.from_numpy(np.concatenate([msgs, np.zeros(16, np.uint8)])).to(dev)
+    d_off = torch.from_numpy(offs.view(np.int32)).to(dev)
+    d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    d_pub = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    d_out = torch.zeros(n, dtype=torch.uint8, device=dev)
+    d_vi = torch.from_numpy(val_idx.view(np.int32)).to(dev)
+    st = torch_stream.cuda_stream
+    eng.sign_device(d_seed, d_msg, d_off, d_sig, d_pub, n, st)
+    torch.cuda.synchronize(dev)
+    pubs = np.zeros((nk, 32), np.uint8)
+    pubs[val_idx] = d_pub.cpu().numpy()
+    del d_seed, d_pub
+    t_ks = time.perf_counter()
+    ks = eng.keyset_load(pubs)
+    t_ks = time.perf_counter() - t_ks
+
+    def step():
+        eng.verify_keyset_device(ks, d_vi, d_sig, d_msg, d_off, d_out, n, st)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ok_first = int(d_out.sum().item())
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    valid = int(d_out.sum().item())
+    eng.set_kernel_timing(True)
+    step()
+    torch.cuda.synchronize(dev)
+    (prep_ms, main_ms, fin_ms), (pl, ml, fl) = eng.kernel_times()
+    eng.set_kernel_timing(False)
+    eng.keyset_free(ks)
+    achieved = n * MADS_KEYSET_MAIN / (main_ms * 1e-3) / 1e12 if main_ms > 0 else None
+    return {"metric": "ed25519 verifies/sec at 1/8 MI355X, key cache on (C2 variant: 10k reused keys)",
+            "value": round(n * steps / dt, 1), "unit": "verifies/s", "steps": steps,
+            "ms_per_step": round(dt / steps * 1e3, 3), "all_valid": valid == n and ok_first == n,
+            "keyset_build_s": round(t_ks, 3),
+            "roofline": {"bound": "valu", "kernel": "verify_keyset_main_kernel",
+                         "achieved": round(achieved, 3) if achieved else None,
+                         "peak": round(peak, 3) if peak else None, "unit": "Tmad/s",
+                         "frac": round(achieved / peak, 4) if (achieved and peak) else None,
+                         "mads_per_verify_main": MADS_KEYSET_MAIN,
+                         "kernel_avg_ms": round(main_ms / max(1, ml), 4), "launches_per_step": ml,
+                         "prep_kernel_ms": round(prep_ms, 4), "finish_kernel_ms": round(fin_ms, 4)},
+            "config": {"workload": "C2 variant: %d signatures by %d validators (seeded), key cache on" % (n, nk)}}
+
+
+def c1_latency(eng, reps, cpu):
+    """BASELINE metric, second half: VerifyCommit p50 latency @175 validators through the seam
+    (bench_commits.c1: generic and key-cached paths, `reps` repetitions each, 1-thread CPU port
+    beside it)."""
+    sys.path.insert(0, ROOT)
+    import bench_commits
+    r = bench_commits.c1(eng, reps, cpu)
+    return {k: r[k] for k in ("metric", "unit", "value", "paths", "reps", "config", "cpu_baseline", "speedup_vs_cpu")
+            if k in r}
 
 
 def pmc_traffic(sigs_per_launch):
@@ -268,9 +410,11 @@ def cpu_baseline_threads(d_pub, d_sig, msgs, offs, m, d_out):
             "gpu_decisions_match": bool((d_out[:m].cpu().numpy() == out).all())}
 
 
-def cpu_baseline(eng, d_pub, d_sig, msgs, offs, m, d_out):
+def cpu_baseline(d_pub, d_sig, msgs, offs, m, d_out, m_ossl):
     """Single-thread C restatement of the Go verify on the first m tuples (oracle/ed25519_port.c);
-    its decisions are also compared with the GPU's on that sample."""
+    its decisions are also compared with the GPU's on that sample.  Beside it, the independent
+    anchor BASELINE.md plans: OpenSSL 3 EVP_DigestVerify(ED25519), 1 thread, on the first m_ossl
+    tuples of the same sample (oracle/openssl_anchor.c; absent without libcrypto)."""
     sys.path.insert(0, ROOT)
     from oracle import port  # cpu_baseline leg only
     pubs = d_pub[:m].cpu().numpy()
@@ -281,11 +425,20 @@ def cpu_baseline(eng, d_pub, d_sig, msgs, offs, m, d_out):
     dt = time.perf_counter() - t
     ncores = os.cpu_count() or 1
     gpu = d_out[:m].cpu().numpy()
-    return {"value": round(m / dt, 1), "unit": "verifies/s", "cores": 1, "kind": "port",
-            "sample": "first %d signatures of the same batch, 1 thread, %.1f s; valid=%d; host cpu_count=%d"
-                      % (m, dt, int(out.sum()), ncores),
-            "gpu_decisions_match": bool((gpu == out).all())}
+    res = {"value": round(m / dt, 1), "unit": "verifies/s", "cores": 1, "kind": "port",
+           "sample": "first %d signatures of the same batch, 1 thread, %.1f s; valid=%d; %s; host cpu_count=%d"
+                     % (m, dt, int(out.sum()), _cpu_model(), ncores),
+           "gpu_decisions_match": bool((gpu == out).all())}
+    t = time.perf_counter()
+    oo = port.openssl_verify_batch(pubs[:m_ossl], sigs[:m_ossl], msgs, o[: m_ossl + 1], nthreads=1)
+    dt = time.perf_counter() - t
+    if oo is not None:
+        res["anchor_openssl"] = {"value": round(m_ossl / dt, 1), "unit": "verifies/s", "cores": 1,
+                                 "kind": "OpenSSL 3 EVP_DigestVerify (ED25519), independent implementation",
+                                 "sample": "first %d signatures of the same batch, 1 thread, %.1f s" % (m_ossl, dt),
+                                 "decisions_match_port": bool((oo == out[:m_ossl]).all())}
+    return res
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -88,6 +88,15 @@ int tmed_sign_batch(tmed_ctx *ctx, const uint8_t *seeds, const uint8_t *msgs, co
 int tmed_sign_batch_device(tmed_ctx *ctx, const uint8_t *d_seeds, const uint8_t *d_msgs, const uint32_t *d_msg_off,
                            size_t n, uint8_t *d_sigs_out, uint8_t *d_pubkeys_out, void *stream);
 
+/*
+ * Diagnostics of the default (half-size scalar) path: for the last chunk of the last
+ * tmed_verify_batch / _device call, histograms of the radix-16 window count W the lattice step
+ * gave each signature (lane_hist[W]) and of the per-wave maximum the main kernel ran
+ * (wave_hist[W], 64 signatures per wave; W = 64 is the unshortened (k, 1) fallback).
+ * All zero when the last call took another path.
+ */
+int tmed_window_stats(tmed_ctx *ctx, uint32_t lane_hist[65], uint32_t wave_hist[65]);
+
 /* Device time (ms) of the last verify/sign launch on this context (HIP events). */
 float tmed_last_kernel_ms(tmed_ctx *ctx);
 
@@ -177,7 +186,9 @@ typedef struct {
   size_t n;
   const uint8_t *pubkeys;   /* n x 32 (ed25519 keys; other key types stay on the Go path) */
   const int64_t *powers;    /* n voting powers */
-  const uint8_t *addresses; /* n x 20, PubKey.Address(); needed by LightTrusting only (may be NULL otherwise) */
+  const uint8_t *addresses; /* n x 20, PubKey.Address(); needed by LightTrusting only (may be NULL otherwise).
+                               Every validator address must be 20 bytes (Validator.ValidateBasic,
+                               types/validator.go:49): a caller holding another length takes the Go path */
   int64_t total_power;      /* vals.TotalVotingPower() (its panics stay in Go, :298-321) */
   uint64_t keyset;          /* 0, or a tmed_keyset_load handle holding these pubkeys (key-cached path) */
   const uint32_t *keyset_index; /* NULL: validator i is key i of the key set; else its index there
@@ -196,6 +207,10 @@ typedef struct {
   const int32_t *ts_nanos;    /* Timestamp.Nanosecond() */
   const uint8_t *sigs;        /* n_sigs x 64 (first sig_lens[i] bytes meaningful) */
   const uint32_t *sig_lens;   /* NULL = all 64 */
+  const uint32_t *address_lens; /* NULL = all 20; else len(ValidatorAddress) per signature.  GetByAddress
+                                   compares with bytes.Equal (types/validator_set.go:270-277): an address
+                                   whose length is not 20 matches no validator, so LightTrusting skips
+                                   that signature (its 20-byte slot is then ignored) */
 } tmed_commit;
 
 #define TMED_MODE_COMMIT 0         /* ValidatorSet.VerifyCommit              :667-714 */
@@ -223,12 +238,18 @@ typedef struct {
 #define TMED_COMMIT_DOUBLE_VOTE 6      /* "double vote from %v (%d and %d)" (val_idx, idx_first, idx) */
 #define TMED_COMMIT_ZERO_DENOMINATOR 7 /* "trustLevel has zero Denominator" */
 #define TMED_COMMIT_OVERFLOW 8         /* "int64 overflow while calculating voting power needed..." */
+#define TMED_COMMIT_PANIC 9            /* the reference loop PANICS when it reaches signature idx: an unknown
+                                          BlockIDFlag in VerifyCommit (CommitSig.BlockID, types/block.go:652-665)
+                                          or a malformed BlockID hash in the sign-bytes of a Commit-flag vote
+                                          (CanonicalizeBlockID, types/canonical.go:18-22).  Every earlier
+                                          signature the loop reached was valid.  The caller runs the original
+                                          Go method for this request, which panics exactly as before. */
 
 typedef struct {
   int code;
   int64_t got, needed;     /* NOT_ENOUGH_POWER */
   int64_t expected, actual;/* WRONG_SET_SIZE / WRONG_HEIGHT */
-  int32_t idx;             /* WRONG_SIGNATURE index; DOUBLE_VOTE second index */
+  int32_t idx;             /* WRONG_SIGNATURE / PANIC index; DOUBLE_VOTE second index */
   int32_t idx_first;       /* DOUBLE_VOTE first index */
   int32_t val_idx;         /* DOUBLE_VOTE validator index */
   uint32_t verified;       /* signatures sent to the device for this request */
@@ -241,8 +262,10 @@ typedef struct {
  * LIGHT_TRUSTING, stopping at a double vote), build their CanonicalVote
  * sign-bytes, verify them on the GPU, then replay each reference loop over the
  * validity bits — same first-error index, same early exit, same Got/Needed.
- * TMED_EINVAL for inputs on which the reference panics (unknown BlockIDFlag,
- * malformed hashes): the caller must take the original code path.
+ * Inputs on which the reference loop panics (unknown BlockIDFlag, malformed BlockID
+ * hash) give that request the outcome TMED_COMMIT_PANIC at the index where the loop
+ * would panic — only if the loop reaches it; the other requests are unaffected.
+ * TMED_EINVAL is reserved for malformed calls (null pointers, unknown mode).
  */
 int tmed_verify_commits(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, tmed_commit_result *out);
 

@@ -92,3 +92,26 @@ def sha512(m: bytes) -> bytes:
     out = ctypes.create_string_buffer(64)
     lib().port_sha512(m, len(m), out)
     return out.raw
+
+
+def openssl_verify_batch(pubs: np.ndarray, sigs: np.ndarray, msgs: np.ndarray, offs: np.ndarray,
+                         nthreads: int = 1):
+    """OpenSSL 3 EVP_DigestVerify(ED25519) over the batch (oracle/openssl_anchor.c): the independent
+    CPU anchor of bench.py's cpu_baseline leg — not the reference semantics.  None when the anchor
+    library (OpenSSL 3) is unavailable."""
+    path = os.path.join(_HERE, "_build", "libossl_anchor.so")
+    try:
+        l = ctypes.CDLL(path)
+    except OSError:
+        return None
+    P = ctypes.c_void_p
+    l.ossl_verify_batch.restype = None
+    l.ossl_verify_batch.argtypes = [P, P, P, P, ctypes.c_size_t, P, ctypes.c_int]
+    n = pubs.shape[0]
+    pubs = np.ascontiguousarray(pubs, np.uint8)
+    sigs = np.ascontiguousarray(sigs, np.uint8)
+    msgs = np.ascontiguousarray(msgs, np.uint8)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    out = np.zeros(n, np.uint8)
+    l.ossl_verify_batch(_ptr(pubs), _ptr(sigs), _ptr(msgs), _ptr(offs), n, _ptr(out), nthreads)
+    return out

@@ -123,6 +123,7 @@ struct AddrIndex {
 struct Plan {
   bool decided = false;
   int64_t needed = 0;
+  int32_t panic_idx = -1;         // the loop panics on reaching this signature (TMED_COMMIT_PANIC)
   int32_t *bit_of_sig = nullptr;  // sig idx -> candidate slot in its planning part (-1 = not sent)
   size_t cand_off = 0;            // + the part's offset in the merged candidate list
   const AddrIndex *addr_index = nullptr;  // Trusting only (shared by requests on the same valset)
@@ -175,6 +176,19 @@ int check_request(const tmed_commit_request &r) {
   if (r.mode != TMED_MODE_LIGHT_TRUSTING && !r.block_id) return TMED_EINVAL;
   if (r.mode < TMED_MODE_COMMIT || r.mode > TMED_MODE_LIGHT_TRUSTING) return TMED_EINVAL;
   return TMED_OK;
+}
+
+// ValidateHash (types/validation.go:32-40): BlockIDFromProto, called by CanonicalizeBlockID
+// (types/canonical.go:18-22) for every Commit-flag vote's sign-bytes, panics otherwise.
+bool block_hashes_valid(const tmed_block_id &b) {
+  return (b.hash_len == 0 || b.hash_len == 32) && (b.psh_hash_len == 0 || b.psh_hash_len == 32);
+}
+
+// GetByAddress(commitSig.ValidatorAddress) (types/validator_set.go:270-277): bytes.Equal against
+// 20-byte validator addresses, so an address of any other length matches nothing.
+int32_t lookup_address(const AddrIndex &ix, const tmed_commit &c, size_t i) {
+  if (c.address_lens && c.address_lens[i] != 20) return -1;
+  return ix.find(c.addresses + 20 * i);
 }
 
 }  // namespace
@@ -311,6 +325,7 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
   const tmed_valset &vs = *r.vals;
   const tmed_commit &c = *r.commit;
   std::fill(pl.bit_of_sig, pl.bit_of_sig + c.n_sigs, -1);
+  const bool bid_ok = block_hashes_valid(c.block_id);
   if (r.mode != TMED_MODE_LIGHT_TRUSTING) {
     if (vs.n != c.n_sigs) {
       o.code = TMED_COMMIT_WRONG_SET_SIZE; o.expected = (int64_t)vs.n; o.actual = (int64_t)c.n_sigs;
@@ -328,7 +343,9 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
       for (size_t i = 0; i < c.n_sigs; i++) {
         const uint8_t f = c.flags[i];
         if (f == kAbsent) continue;
-        if (f != kCommit && f != kNil) return TMED_EINVAL;  // CommitSig.BlockID panics (types/block.go:663)
+        // CommitSig.BlockID panics on an unknown flag (types/block.go:652-665), sign-bytes of a
+        // Commit vote on a malformed hash: the loop stops there if it gets that far
+        if ((f != kCommit && f != kNil) || (f == kCommit && !bid_ok)) { pl.panic_idx = (int32_t)i; break; }
         pl.bit_of_sig[i] = (int32_t)cands.size();
         cands.emplace_back(q, (int32_t)i, (int32_t)i);
       }
@@ -336,6 +353,7 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
       int64_t tally = 0;
       for (size_t i = 0; i < c.n_sigs; i++) {
         if (c.flags[i] != kCommit) continue;
+        if (!bid_ok) { pl.panic_idx = (int32_t)i; break; }
         pl.bit_of_sig[i] = (int32_t)cands.size();
         cands.emplace_back(q, (int32_t)i, (int32_t)i);
         tally += vs.powers[i];
@@ -353,10 +371,11 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
     int64_t tally = 0;
     for (size_t i = 0; i < c.n_sigs; i++) {
       if (c.flags[i] != kCommit) continue;
-      const int32_t v = pl.addr_index->find(c.addresses + 20 * i);
+      const int32_t v = lookup_address(*pl.addr_index, c, i);
       if (v < 0) continue;
       if (seen.get(v) >= 0) break;  // the loop returns the double-vote error here
       seen.set(v, (int32_t)i);
+      if (!bid_ok) { pl.panic_idx = (int32_t)i; break; }
       pl.bit_of_sig[i] = (int32_t)cands.size();
       cands.emplace_back(q, (int32_t)i, v);
       tally += vs.powers[v];
@@ -511,12 +530,19 @@ static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, c
     o.verified++;
     return valid[pl.cand_off + (size_t)k] != 0;
   };
+  auto panics = [&](size_t i) -> bool {
+    if ((int32_t)i != pl.panic_idx) return false;
+    o.code = TMED_COMMIT_PANIC;
+    o.idx = (int32_t)i;
+    return true;
+  };
   bool ok = true;
   int64_t tally = 0;
   o.code = -1;
   if (r.mode == TMED_MODE_COMMIT) {
     for (size_t i = 0; i < c.n_sigs && o.code < 0; i++) {
       if (c.flags[i] == kAbsent) continue;
+      if (panics(i)) break;
       if (!bit(i, &ok)) { if (ok) { o.code = TMED_COMMIT_WRONG_SIGNATURE; o.idx = (int32_t)i; } break; }
       if (c.flags[i] == kCommit) tally += vs.powers[i];
     }
@@ -527,6 +553,7 @@ static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, c
   } else if (r.mode == TMED_MODE_LIGHT) {
     for (size_t i = 0; i < c.n_sigs && o.code < 0; i++) {
       if (c.flags[i] != kCommit) continue;
+      if (panics(i)) break;
       if (!bit(i, &ok)) { if (ok) { o.code = TMED_COMMIT_WRONG_SIGNATURE; o.idx = (int32_t)i; } break; }
       tally += vs.powers[i];
       if (tally > pl.needed) o.code = TMED_COMMIT_OK;
@@ -537,13 +564,14 @@ static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, c
     seen.reset(vs.n);
     for (size_t i = 0; i < c.n_sigs && o.code < 0; i++) {
       if (c.flags[i] != kCommit) continue;
-      const int32_t v = pl.addr_index->find(c.addresses + 20 * i);
+      const int32_t v = lookup_address(*pl.addr_index, c, i);
       if (v < 0) continue;
       if (seen.get(v) >= 0) {
         o.code = TMED_COMMIT_DOUBLE_VOTE; o.val_idx = v; o.idx_first = seen.get(v); o.idx = (int32_t)i;
         break;
       }
       seen.set(v, (int32_t)i);
+      if (panics(i)) break;
       if (!bit(i, &ok)) { if (ok) { o.code = TMED_COMMIT_WRONG_SIGNATURE; o.idx = (int32_t)i; } break; }
       tally += vs.powers[v];
       if (tally > pl.needed) o.code = TMED_COMMIT_OK;

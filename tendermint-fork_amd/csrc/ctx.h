@@ -117,7 +117,6 @@ struct tmed_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
   std::mutex mu;
-  tmed::ge_niels *d_btab = nullptr;
   int4 *d_bcomb = nullptr;  // signed radix-256 comb of +B (shared)
   int4 *d_b16 = nullptr;    // j*B, j = 0..32768 (main-kernel variant 5), built at init
   int4 *d_bcomb16 = nullptr;  // radix-2^16 comb of +B (key-cached throughput kernel), 67 MB
@@ -127,10 +126,11 @@ struct tmed_ctx {
   int4 *d_fin_pre = nullptr;  // batched-finish prefix products (kFinPreBytes)
   uint32_t slab_slots = 0;
   uint32_t chunk = 0;     // signatures per prep/main launch pair (0 = slab_slots); env TMED_CHUNK
-  int main_waves = 6;     // main-kernel variant (6: half-size scalars, verify_hs.h; 5: full-length Straus); env TMED_MAIN_WAVES
+  int main_waves = 6;     // main-kernel path (6: half-size scalars, verify_hs.h; 5: full-length Straus + finish); env TMED_MAIN_WAVES
   uint32_t lat_max = 24576;  // key-cached batches up to this size take the latency kernels (crossover ~32k,
                              // profiles/r01/session3/lat_sweep.jsonl); env TMED_LAT_MAX
   bool timing = false;    // tmed_set_kernel_timing
+  uint32_t last_hs_count = 0;  // signatures of the last half-size chunk in d_prep (tmed_window_stats)
   tmed::KernelTimer timer;
   tmed::DevBuf d_a, d_b, d_msg, d_off, d_out, d_c;
   tmed::HostBuf h_a, h_b, h_msg, h_off, h_out, h_c;
@@ -159,6 +159,13 @@ inline hipError_t scratch_acquire(tmed_ctx *c, hipStream_t s) {
     if (e == hipSuccess) e = hipStreamWaitEvent(s, c->scratch_ev, 0);
   }
   return e;
+}
+// Signatures in the last chunk launch_verify runs for an n-signature call (chunks of `chunk`
+// inside blocks of kFinCap).
+inline uint32_t last_chunk_count(uint32_t n, uint32_t chunk) {
+  if (n == 0) return 0;
+  const uint32_t m = n - (n - 1) / kFinCap * kFinCap;
+  return m - (m - 1) / chunk * chunk;
 }
 inline hipError_t scratch_release(tmed_ctx *c, hipStream_t s) {
   c->scratch_foreign = s != c->stream;

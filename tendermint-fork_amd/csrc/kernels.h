@@ -26,9 +26,9 @@ constexpr uint32_t kThreadsPerBlock = 256;
 // Variable-base table slab: lane slots (grid-stride loop bounds the grid to
 // slab_slots / kThreadsPerBlock blocks).  9 entries x 160 B per slot.
 constexpr uint32_t kSlabSlotBytes = 9 * 160;
-// The half-size path (main variant 6) keeps two per-lane tables (-A and -sign(d) R): the slab
-// is allocated with kSlabTables slot regions.
-constexpr uint32_t kSlabTables = 2;
+// The half-size path (main variant 6, the default) keeps two per-lane tables (-A and
+// -sign(d) R): its slab has two slot regions; the full-length fallback (variant 5) one.
+inline uint32_t slab_tables(int main_waves) { return main_waves == 5 ? 1u : 2u; }
 
 // Batched finish (verify_core.h finish_group): the main kernels hand projective R' over in
 // fin ([q][slot], kFinInt4 int4 per signature, kFinCap slots); the finish kernel runs once per
@@ -41,12 +41,11 @@ constexpr uint32_t kFinPreStride = kFinCap + 64;
 constexpr size_t kFinBytes = (size_t)kFinCap * kFinInt4 * 16;
 constexpr size_t kFinPreBytes = (size_t)kFinPreStride * 3 * 16;
 
-// The shared B tables of the generic main kernel: the radix-256 table staged in LDS and the
-// radix-2^16 table in HBM (main-kernel variant 5).
+// The shared B tables of the generic main kernels: the radix-2^16 table of j*B (full-length
+// fallback, variant 5) and the radix-2^16 comb of B (windows 0 and 8: the half-size default).
 struct BTabs {
-  const ge_niels *lds;
   const int4 *b16;
-  const int4 *comb16 = nullptr;  // radix-2^16 comb of B (windows 0 and 8: the half-size path)
+  const int4 *comb16;
 };
 constexpr uint32_t kB16Entries = 32769;
 constexpr size_t kB16Bytes = (size_t)kB16Entries * 128;
@@ -59,17 +58,14 @@ hipError_t launch_build_bcomb16(const int32_t *d_bases, int4 *comb, hipStream_t 
 hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                          uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, BTabs btab,
                          int4 *prep, int4 *fin, int4 *fin_pre, hipStream_t stream, uint32_t chunk = 0,
-                         int main_waves = 2, bool msg_slots = false, KernelTimer *timer = nullptr);
+                         int main_waves = 6, bool msg_slots = false, KernelTimer *timer = nullptr);
 
 // RFC 8032 signer (synthetic commits) on the shared comb of B.
 hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t *off, uint32_t n, uint8_t *sig_out,
                        uint8_t *pub_out, const int4 *bcomb, hipStream_t stream);
 
-// Shared fixed-base table j*B, j = 0..128 (niels), staged in LDS by the kernels.
-constexpr int kBTabSize = 129;
 // prep hand-off bytes per signature slot (k, s, A.x, A.y, ok)
 constexpr uint32_t kPrepSlotBytes = 352;  // 10 int4 (k, s, A) + 11 int4 (the half-size hand-off), padded
-void host_build_btab(ge_niels out[129]);
 
 // ---- fixed-base combs (key cache) -------------------------------
 // Signed radix-256 comb of a point P: entry [w][j] = j * 256^w * P (niels, affine),
@@ -90,7 +86,13 @@ hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStr
 hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
                                 const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                 const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
-                                int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots = false);
+                                int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots = false,
+                                KernelTimer *timer = nullptr);
+
+// Window-count statistics of the last half-size chunk in the prep hand-off (count lanes):
+// d_hist[0..64] per-lane W, d_hist[65..129] per-wave maximum W.
+hipError_t launch_window_stats(const int4 *prep, uint32_t stride, uint32_t count, uint32_t *d_hist,
+                               hipStream_t stream);
 
 // Latency mode for small key-cached batches (n <= kLatMax): 8 lanes per signature for the
 // comb sum, strict decode of R on other lanes instead of the inversion; two launches.

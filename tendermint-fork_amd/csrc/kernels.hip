@@ -8,10 +8,8 @@
 // Memory layout
 //   pub   n x 32 B, sig n x 64 B (16-B aligned rows -> dwordx4 loads)
 //   msgs  concatenated bytes, off[n+1] u32 (or fixed 256-B vote slots)
-//   slab  per-lane variable-base table: 9 cached points x 160 B, lane-major
-//         [slot][entry][chunk] (default) or [entry][chunk][slot] (variant -2)
-//   btab  129 niels multiples of B, staged per workgroup in LDS (15.5 KB; variants 2-4)
-//   b16   32769 niels multiples of B in 128-B rows in HBM (4.2 MB; default variant 5)
+//   slab  per-lane variable-base tables: 9 cached points x 160 B, lane-major [slot][entry][chunk]
+//   b16   32769 niels multiples of B in 128-B rows in HBM (4.2 MB; the full-length fallback, variant 5)
 //   combs key-set combs [key][window][entry] and the shared combs of B (radix 256, radix 2^16)
 #include "kernels.h"
 #include "verify_core.h"
@@ -19,18 +17,14 @@
 
 namespace tmed {
 
-// LANE_MAJOR = false: [entry][chunk][slot] (lanes with equal digits read contiguous 16-B
-// pieces); true: [slot][entry][chunk] (each lane's 160-B entry is contiguous, so a
-// divergent lookup reads whole lines instead of one 16-B piece per line).
-template <bool LANE_MAJOR>
-struct SlabTabT {
+// Per-lane table in the HBM slab, lane-major [slot][entry][chunk]: each lane's 160-B entry is
+// contiguous, so a divergent lookup reads whole lines (+3.7 % over the slot-interleaved
+// [entry][chunk][slot] layout, profiles/r01/variants.txt).
+struct SlabTab {
   int4 *base;
-  uint32_t stride;  // lane slots in the slab
   uint32_t slot;
 
-  __device__ __forceinline__ size_t idx(int j, int q) const {
-    return LANE_MAJOR ? ((size_t)slot * 9 + j) * 10 + q : (size_t)(j * 10 + q) * stride + slot;
-  }
+  __device__ __forceinline__ size_t idx(int j, int q) const { return ((size_t)slot * 9 + j) * 10 + q; }
 
   __device__ __forceinline__ void store(int j, const ge_cached &c) const {
     const fe *fs[4] = {&c.YpX, &c.YmX, &c.Z, &c.T2d};
@@ -66,56 +60,6 @@ struct SlabTabT {
 typedef __attribute__((address_space(1))) void global_void;
 typedef __attribute__((address_space(3))) void lds_void;
 
-__device__ __forceinline__ void unpack_cached(ge_cached &c, const int4 v[10]) {
-  fe *fs[4] = {&c.YpX, &c.YmX, &c.Z, &c.T2d};
-#pragma unroll
-  for (int q = 0; q < 10; q++) {
-    const int32_t w[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-      const int f = 4 * q + e;
-      fs[f / 10]->v[f % 10] = w[e];
-    }
-  }
-}
-
-// Lane-major slab whose next entry is fetched asynchronously into LDS
-// (global_load_lds_dwordx4, gfx950): the fetch is issued right after an A addition and
-// consumed by the next one, four doublings later, so the entry's HBM/MALL latency is
-// hidden without holding 40 VGPRs across the doublings (the kernel has none to spare at
-// 2 waves/SIMD).  buf is this wave's [10][64] int4 region: lane l's 16-B piece q lands at
-// buf[q * 64 + l] (M0 = buf + q * 1 KB, LDS address = M0 + 16 * lane).  Single-buffered:
-// the next prefetch is issued only after take()'s values have been consumed.
-struct SlabTabPf {
-  SlabTabT<true> s;
-  int4 *buf;
-  uint32_t lane;
-  __device__ __forceinline__ void store(int j, const ge_cached &c) const { s.store(j, c); }
-  __device__ __forceinline__ void prefetch(int j) const {
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the previous take's LDS reads are done
-#pragma unroll
-    for (int q = 0; q < 10; q++)
-      __builtin_amdgcn_global_load_lds((global_void *)(s.base + s.idx(j, q)), (lds_void *)(buf + q * 64), 16, 0, 0);
-  }
-  __device__ __forceinline__ void take(ge_cached &c) const {
-    int4 v[10];
-#pragma unroll
-    for (int q = 0; q < 10; q++) v[q] = buf[q * 64 + lane];
-    unpack_cached(c, v);
-  }
-};
-
-using SlabTab = SlabTabT<false>;
-
-struct LdsBTab {
-  static constexpr int kBits = 8;
-  const ge_niels *t;
-  int pf = 0;
-  __device__ __forceinline__ void load(int j, ge_niels &n) const { n = t[j]; }
-  __device__ __forceinline__ void prefetch(int j) { pf = j; }
-  __device__ __forceinline__ void take(ge_niels &n) const { n = t[pf]; }
-};
-
 // Radix-2^16 B table (double_scalarmult<16>): j*B, j = 0..32768, affine niels in 128-B rows
 // (kCombEntryInt4 int4, 4.2 MB, L2/MALL-resident).  The entry of the next B window is fetched
 // into LDS with global_load_lds_dwordx4 right after the current B addition, 16 doublings
@@ -145,15 +89,6 @@ struct B16Pf {
     }
   }
 };
-
-constexpr int kBTabEntries = 129;  // j*B, j = 0..128 (niels) — 15.5 KB of LDS
-
-__device__ __forceinline__ void stage_btab(ge_niels *sbt, const ge_niels *btab_g) {
-  int32_t *dst = reinterpret_cast<int32_t *>(sbt);
-  const int32_t *src = reinterpret_cast<const int32_t *>(btab_g);
-  for (int i = threadIdx.x; i < kBTabEntries * 30; i += blockDim.x) dst[i] = src[i];
-  __syncthreads();
-}
 
 // Per-signature hand-off from the prep to the main kernel: k, s, A.x, A.y, ok
 // (37 words padded to 10 x int4), stored [chunk q][slot] for coalescing.
@@ -295,19 +230,13 @@ __device__ __forceinline__ void fin_store(int4 *fin, uint32_t stride, uint32_t s
     fin[(size_t)q * stride + slot] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 
-// Phase 2: table of -A, Straus [k](-A) + [s]B -> projective R' (hand-off to the finish).
-// WAVES = minimum waves per SIMD the register allocation must allow.
-// PF: the per-lane A table is lane-major and its next entry is prefetched into LDS
-// (SlabTabPf, 40 KB per 256-lane block on top of the 15.5 KB B table).
-// BB: B window width (8: LDS table; 16: the HBM table with LDS prefetch, B16Pf).
-template <int WAVES, bool LANE_MAJOR, bool PF = false, int BB = 8>
-__global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_main_kernel(
+// Phase 2 of the full-length fallback (TMED_MAIN_WAVES=5): table of -A, Straus [k](-A) + [s]B
+// (radix-2^16 B windows from the HBM table, each entry fetched into LDS 16 doublings ahead)
+// -> projective R' (hand-off to the batched finish).
+__global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_kernel(
     uint32_t base, uint32_t count, const int4 *__restrict__ prep, uint32_t stride, int4 *__restrict__ slab,
-    BTabs bts, int4 *__restrict__ fin, uint32_t fin_base, uint8_t *__restrict__ out) {
-  __shared__ ge_niels sbt[BB == 8 ? kBTabEntries : 1];
-  __shared__ int4 spf[PF ? kThreadsPerBlock / 64 : 1][PF ? 10 * 64 : 1];
-  __shared__ int4 sb16[BB == 16 ? kThreadsPerBlock / 64 : 1][BB == 16 ? 8 * 64 : 1];
-  if constexpr (BB == 8) stage_btab(sbt, bts.lds);
+    const int4 *__restrict__ b16, int4 *__restrict__ fin, uint32_t fin_base, uint8_t *__restrict__ out) {
+  __shared__ int4 sb16[kThreadsPerBlock / 64][8 * 64];
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   if (slot >= count) return;
   const uint32_t i = base + slot;
@@ -315,22 +244,9 @@ __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_main_kernel(
   ge_p3 A;
   const bool ok = prep_load(prep, stride, slot, k, s, A);
   ge_p2 R;
-  auto run = [&](auto &bt) {
-    if constexpr (PF) {
-      SlabTabPf tab{SlabTabT<true>{slab, stride, slot}, spf[threadIdx.x >> 6], threadIdx.x & 63u};
-      verify_main_point(R, k, s, A, tab, bt);
-    } else {
-      SlabTabT<LANE_MAJOR> tab{slab, stride, slot};
-      verify_main_point(R, k, s, A, tab, bt);
-    }
-  };
-  if constexpr (BB == 16) {
-    B16Pf bt{bts.b16, sb16[threadIdx.x >> 6], threadIdx.x & 63u};
-    run(bt);
-  } else {
-    LdsBTab bt{sbt};
-    run(bt);
-  }
+  B16Pf bt{b16, sb16[threadIdx.x >> 6], threadIdx.x & 63u};
+  SlabTab tab{slab, slot};
+  verify_main_point(R, k, s, A, tab, bt);
   fin_store(fin, kFinCap, i - fin_base, R.X, R.Y, R.Z);
   out[i] = ok ? 1 : 0;
 }
@@ -435,12 +351,44 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_hs_kernel(
   if (W > 64) W = 64;
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const HsDigitsDev ds{prep2, stride, slot};
-  SlabTabT<true> ta{slab, stride, slot};
-  SlabTabT<true> tr{slab + (size_t)stride * 90, stride, slot};
+  SlabTab ta{slab, slot};
+  SlabTab tr{slab + (size_t)stride * 90, slot};
   B16Pf bl{comb16, sbl[wv], lane};
   B16Pf bh{comb16 + (size_t)8 * kB16Entries * kCombEntryInt4, sbh[wv], lane};
   const bool id = verify_main_hs(ds, (flags & 2) != 0, er, W, A, Rx, Ry, ta, tr, bl, bh);
   if (active) out[base + slot] = ((flags & 1) && id) ? 1 : 0;
+}
+
+// Diagnostics (tmed_window_stats): the lattice step's window count W of every lane of the last
+// half-size chunk (hand-off flags, bits 8..), as a per-lane histogram and a histogram of the
+// wave maxima — the loop length each wave of verify_main_hs_kernel actually ran (W = 64: the
+// (k, 1) fallback).  Same 64-slot waves as the main kernel.
+__global__ __launch_bounds__(kThreadsPerBlock) void window_stats_kernel(const int4 *__restrict__ prep2, uint32_t stride,
+                                                                       uint32_t count, uint32_t *__restrict__ lane_hist,
+                                                                       uint32_t *__restrict__ wave_hist) {
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = slot < count;
+  int W = active ? (prep2[(size_t)10 * stride + slot].y >> 8) : 0;  // word 41
+  if (W < 0 || W > 64) W = 64;
+  if (active) atomicAdd(&lane_hist[W], 1u);
+  int m = W;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int x = __shfl_xor(m, o);
+    m = x > m ? x : m;
+  }
+  if ((threadIdx.x & 63u) == 0 && slot < count) atomicAdd(&wave_hist[m], 1u);
+}
+
+hipError_t launch_window_stats(const int4 *prep, uint32_t stride, uint32_t count, uint32_t *d_hist,
+                               hipStream_t stream) {
+  if (count == 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(d_hist, 0, 2 * 65 * sizeof(uint32_t), stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(window_stats_kernel, dim3((count + kThreadsPerBlock - 1) / kThreadsPerBlock),
+                     dim3(kThreadsPerBlock), 0, stream, prep + (size_t)kPrepInt4 * stride, stride, count, d_hist,
+                     d_hist + 65);
+  return hipGetLastError();
 }
 
 // Phase 3: batched finish.  Lane l owns slots l, l + L, l + 2L, ... (< m) of the block of m
@@ -554,9 +502,13 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
                          int4 *prep, int4 *fin, int4 *fin_pre, hipStream_t stream, uint32_t chunk, int main_waves,
                          bool msg_slots, KernelTimer *timer) {
   const MsgSrc ms{msgs, off, msg_slots};
-  // Chunks of at most slab_stride signatures: the per-lane tables (slab) and the
-  // prep hand-off are sized for one chunk.  The finish runs once per kFinCap block.
+  // Chunks of at most slab_stride signatures (the per-lane tables and the prep hand-off are
+  // sized for one chunk; tmed_init keeps both multiples of kThreadsPerBlock, so every lane of
+  // every launched block owns a slot below slab_stride).  The finish (variant 5 only) runs
+  // once per kFinCap block.
   if (chunk == 0 || chunk > slab_stride) chunk = slab_stride;
+  if (chunk % kThreadsPerBlock != 0 || slab_stride % kThreadsPerBlock != 0) return hipErrorInvalidValue;
+  const bool hs = main_waves != 5;
   if (timer) timer->mark(stream, -1);
   for (uint32_t fbase = 0; fbase < n; fbase += kFinCap) {
     const uint32_t m = (n - fbase) < kFinCap ? (n - fbase) : kFinCap;
@@ -567,41 +519,22 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
       hipLaunchKernelGGL(verify_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, pub, sig, ms, base,
                          count, prep, slab_stride);
       if (timer) timer->mark(stream, 0);
-      if (main_waves == 6) {  // half-size scalars (verify_hs.h): R decode + lattice, main; no finish
+      if (hs) {  // default: half-size scalars (verify_hs.h): R decode + lattice, main; no finish
         int4 *prep2 = prep + (size_t)kPrepInt4 * slab_stride;
         hipLaunchKernelGGL(verify_prep_r_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base, count,
                            prep, prep2, slab_stride);
         if (timer) timer->mark(stream, 0);
         hipLaunchKernelGGL(verify_main_hs_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base, count, prep,
                            prep2, slab_stride, slab, btab.comb16, out);
-        if (timer) timer->mark(stream, 1);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        continue;
+      } else {  // fallback 5: full-length Straus + batched finish
+        hipLaunchKernelGGL(verify_main_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base, count, prep,
+                           slab_stride, slab, btab.b16, fin, fbase, out);
       }
-      // default (5): 2 waves/SIMD, lane-major per-lane tables (+3.7 % over the slot-interleaved
-      // layout), radix-2^16 B windows from the HBM table (+3.3 % over the LDS radix-256
-      // table, profiles/r01/session3/variants_b16.txt); the others are measured A/B variants.
-      if (main_waves == 5)  // radix-2^16 B windows from the HBM table (16 fewer B additions)
-        hipLaunchKernelGGL((verify_main_kernel<2, true, false, 16>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream,
-                           base, count, prep, slab_stride, slab, btab, fin, fbase, out);
-      else if (main_waves == 4)  // lane-major + LDS prefetch of the next A entry
-        hipLaunchKernelGGL((verify_main_kernel<2, true, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream,
-                           base, count, prep, slab_stride, slab, btab, fin, fbase, out);
-      else if (main_waves >= 3)
-        hipLaunchKernelGGL((verify_main_kernel<3, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base,
-                           count, prep, slab_stride, slab, btab, fin, fbase, out);
-      else if (main_waves == -2)  // slot-interleaved slab layout
-        hipLaunchKernelGGL((verify_main_kernel<2, false>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base,
-                           count, prep, slab_stride, slab, btab, fin, fbase, out);
-      else
-        hipLaunchKernelGGL((verify_main_kernel<2, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base,
-                           count, prep, slab_stride, slab, btab, fin, fbase, out);
       if (timer) timer->mark(stream, 1);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
-    hipError_t e = main_waves == 6 ? hipSuccess : launch_finish(fin, fin_pre, sig, out, fbase, m, stream);
+    hipError_t e = hs ? hipSuccess : launch_finish(fin, fin_pre, sig, out, fbase, m, stream);
     if (timer) timer->mark(stream, 2);
     if (e != hipSuccess) return e;
   }
@@ -615,8 +548,6 @@ hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t
                      pub_out, bcomb);
   return hipGetLastError();
 }
-
-void host_build_btab(ge_niels out[129]) { build_btab_niels(out); }
 
 // j*B for j = 0..kB16Entries-1 into 128-B rows (one lane per entry; once per context).
 __global__ __launch_bounds__(256) void b16_fill_kernel(int4 *__restrict__ tab) {
@@ -948,9 +879,10 @@ hipError_t launch_verify_keyset_lat(const uint32_t *val_idx, const uint8_t *key_
 hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
                                 const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                 const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
-                                int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots) {
+                                int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots, KernelTimer *timer) {
   const MsgSrc ms{msgs, off, msg_slots};
   if (stride > kFinCap) stride = kFinCap;
+  if (timer) timer->mark(stream, -1);
   for (uint32_t fbase = 0; fbase < n; fbase += kFinCap) {
     const uint32_t m = (n - fbase) < kFinCap ? (n - fbase) : kFinCap;
     for (uint32_t base = fbase; base < fbase + m; base += stride) {
@@ -958,6 +890,7 @@ hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub,
       const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
       hipLaunchKernelGGL(verify_keyset_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx,
                          key_pub, key_ok, sig, ms, base, count, prep, stride);
+      if (timer) timer->mark(stream, 0);
       static const int ks_waves = [] {  // A/B: waves/SIMD the key-cached main kernel is compiled for
         const char *v = getenv("TMED_KS_WAVES");
         return v ? atoi(v) : 2;
@@ -968,10 +901,12 @@ hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub,
       else
         hipLaunchKernelGGL(verify_keyset_main_kernel<2>, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx,
                            acomb, bcomb, base, count, prep, stride, fin, fbase, out);
+      if (timer) timer->mark(stream, 1);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
     hipError_t e = launch_finish(fin, fin_pre, sig, out, fbase, m, stream);
+    if (timer) timer->mark(stream, 2);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;

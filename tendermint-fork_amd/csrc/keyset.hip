@@ -39,11 +39,13 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 static hipError_t keyset_verify(tmed_ctx *c, const Keyset &k, const uint32_t *d_idx, const uint8_t *d_sig,
                                 const uint8_t *d_msgs, const uint32_t *d_off, uint32_t n, uint8_t *d_out,
                                 hipStream_t s, bool msg_slots) {
+  c->last_hs_count = 0;  // d_prep now holds another path's hand-off (tmed_window_stats)
   if (n <= c->lat_max)
     return launch_verify_keyset_lat(d_idx, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb, d_sig, d_msgs, d_off, n, d_out,
                                     c->d_fin, c->d_fin_pre, s, msg_slots);
   return launch_verify_keyset(d_idx, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb16, d_sig, d_msgs, d_off, n, d_out, c->d_prep,
-                              c->slab_slots, c->d_fin, c->d_fin_pre, s, msg_slots);
+                              c->slab_slots, c->d_fin, c->d_fin_pre, s, msg_slots,
+                              (c->timing && !msg_slots) ? &c->timer : nullptr);
 }
 
 int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st, int slot) {
@@ -96,6 +98,7 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
       if (((const uint32_t *)st.key)[j] >= st.ks->n) return TMED_EINVAL;
   VoteSlot &vs = c->vslot[st.slot];
   uint8_t *d = (uint8_t *)vs.d_votes.p;
+  c->last_hs_count = 0;  // the commit seam reuses d_prep (tmed_window_stats)
   hipStream_t s = c->stream;
   // A large copy runs on the copy stream, so it overlaps the kernels of the batch queued
   // before (the other slot; this slot's previous batch was collected before it was
@@ -121,7 +124,7 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
                         (const uint32_t *)vs.d_off.p, m, (uint8_t *)vs.d_out.p, s, /*msg_slots=*/true);
     else
       e = launch_verify(d + st.o_key, d + st.o_sig, (const uint8_t *)vs.d_vmsg.p, (const uint32_t *)vs.d_off.p, m,
-                        (uint8_t *)vs.d_out.p, c->d_slab, c->slab_slots, BTabs{c->d_btab, c->d_b16, c->d_bcomb16}, c->d_prep, c->d_fin,
+                        (uint8_t *)vs.d_out.p, c->d_slab, c->slab_slots, BTabs{c->d_b16, c->d_bcomb16}, c->d_prep, c->d_fin,
                         c->d_fin_pre, s, c->chunk, c->main_waves, /*msg_slots=*/true);
   }
   if (e == hipSuccess) e = hipEventRecord(vs.ev1, s);
@@ -215,6 +218,7 @@ int tmed_verify_batch_keyset_device(tmed_ctx *c, uint64_t handle, const uint32_t
   const Keyset &k = it->second;
   (void)hipSetDevice(c->device);
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  if (c->timing) c->timer.n = 0;
   hipError_t e = scratch_acquire(c, s);
   if (e == hipSuccess) e = keyset_verify(c, k, d_val_idx, d_sigs, d_msgs, d_msg_off, (uint32_t)n, d_out, s, false);
   if (e == hipSuccess) e = scratch_release(c, s);

@@ -13,6 +13,7 @@ struct VoteEncoder {
   int pre_len = 0;
   uint8_t bid[160];
   int bid_body = 0, bid_field = 0;
+  bool bid_ok = true;  // block/part-set hashes pass ValidateHash (else only Absent/Nil votes encode)
   const char *cid = nullptr;
   uint32_t cid_len = 0;
   int cid_field = 0;

@@ -41,9 +41,11 @@ namespace tmed {
 
 int VoteEncoder::init(const tmed_vote_template *t) {
   if (!t) return TMED_EINVAL;
-  if ((t->block_hash_len != 0 && t->block_hash_len != 32) || (t->psh_hash_len != 0 && t->psh_hash_len != 32))
-    return TMED_EINVAL;  // ValidateHash: BlockIDFromProto would panic (types/canonical.go:19-22)
   if (t->chain_id_len && !t->chain_id) return TMED_EINVAL;
+  // ValidateHash: CanonicalizeBlockID panics on a malformed hash (types/canonical.go:18-22), which
+  // only a Commit-flag vote reaches (Absent / Nil votes sign the zero BlockID): such a template
+  // can still encode those, and write()/size() must never be asked for a Commit vote.
+  bid_ok = (t->block_hash_len == 0 || t->block_hash_len == 32) && (t->psh_hash_len == 0 || t->psh_hash_len == 32);
   uint8_t *p = pre;
   *p++ = 0x08; *p++ = 0x02;  // SignedMsgType Precommit (Commit.GetVote, types/block.go:787)
   if (t->height != 0) { *p++ = 0x11; p = put_le64(p, (uint64_t)t->height); }
@@ -52,7 +54,7 @@ int VoteEncoder::init(const tmed_vote_template *t) {
   // CanonicalBlockID body; a zero BlockID is omitted (CanonicalizeBlockID -> nil)
   const bool zero = t->block_hash_len == 0 && t->psh_total == 0 && t->psh_hash_len == 0;
   bid_body = 0;
-  if (!zero) {
+  if (!zero && bid_ok) {
     uint8_t psh[64];
     uint8_t *q = psh;
     if (t->psh_total != 0) { *q++ = 0x08; q = put_uvarint(q, t->psh_total); }
@@ -119,6 +121,7 @@ extern "C" int tmed_vote_sign_bytes(const tmed_vote_template *t, size_t n, const
   for (size_t i = 0; i < n; i++) {
     const int f = flags ? flags[i] : 2;
     if (f < 1 || f > 3) return TMED_EINVAL;  // CommitSig.BlockID panics on unknown flags (types/block.go:663)
+    if (f == 2 && !enc.bid_ok) return TMED_EINVAL;  // CanonicalizeBlockID panics (types/canonical.go:18-22)
     const size_t total = enc.size(f, ts_seconds[i], ts_nanos[i]);
     out_off[i] = (uint32_t)pos;
     if (out && pos + total <= out_cap) enc.write(out + pos, f, ts_seconds[i], ts_nanos[i]);

@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <string>
 
@@ -56,23 +57,27 @@ int tmed_init(int device, tmed_ctx **out) {
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->scratch_ev, hipEventDisableTiming);
-  static ge_niels bt[kBTabSize];
-  static std::once_flag bt_once;
-  std::call_once(bt_once, [] { host_build_btab(bt); });
-  if (e == hipSuccess) e = hipMalloc((void **)&c->d_btab, sizeof(bt));
-  if (e == hipSuccess) e = hipMemcpy(c->d_btab, bt, sizeof(bt), hipMemcpyHostToDevice);
   // Lane slots for the per-lane tables and the prep hand-off: 2^20 signatures per
-  // prep/main pair (1.5 GB slab + 168 MB hand-off of the 288 GB HBM), so a BASELINE C2
-  // batch is one prep, one main and one finish launch: +2.6 % over 131,072-signature
+  // prep/main pair (default path: 3.0 GB slab of two tables + 369 MB hand-off, of the 288 GB
+  // HBM), so a BASELINE C2 batch is one launch of each kernel: +2.6 % over 131,072-signature
   // chunks, which paid a drain/ramp bubble per launch (profiles/r01/session2/variants_chunk.txt).
+  // Both sizes are kept multiples of the block size (every lane of a launched block owns a slot
+  // of the slab; a zero size would never make progress).
+  auto round_up = [](uint32_t v) {
+    if (v < kThreadsPerBlock) v = kThreadsPerBlock;
+    if (v > (1u << 24)) v = 1u << 24;
+    return (v + kThreadsPerBlock - 1) / kThreadsPerBlock * kThreadsPerBlock;
+  };
   c->slab_slots = 4096 * kThreadsPerBlock;
   c->chunk = c->slab_slots;
-  if (const char *v = getenv("TMED_CHUNK")) c->chunk = (uint32_t)strtoul(v, nullptr, 10);
-  if (const char *v = getenv("TMED_MAIN_WAVES")) c->main_waves = atoi(v);
-  if (const char *v = getenv("TMED_SLAB_SLOTS")) c->slab_slots = (uint32_t)strtoul(v, nullptr, 10);
+  if (const char *v = getenv("TMED_SLAB_SLOTS")) c->slab_slots = round_up((uint32_t)strtoul(v, nullptr, 10));
+  c->chunk = c->slab_slots;
+  if (const char *v = getenv("TMED_CHUNK")) c->chunk = std::min(c->slab_slots, round_up((uint32_t)strtoul(v, nullptr, 10)));
+  if (const char *v = getenv("TMED_MAIN_WAVES")) c->main_waves = atoi(v) == 5 ? 5 : 6;
   if (const char *v = getenv("TMED_LAT_MAX")) c->lat_max = (uint32_t)strtoul(v, nullptr, 10);
   if (c->lat_max > kLatMax) c->lat_max = kLatMax;
-  if (e == hipSuccess) e = hipMalloc((void **)&c->d_slab, (size_t)c->slab_slots * kSlabSlotBytes * kSlabTables);
+  if (e == hipSuccess)
+    e = hipMalloc((void **)&c->d_slab, (size_t)c->slab_slots * kSlabSlotBytes * slab_tables(c->main_waves));
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_prep, (size_t)c->slab_slots * kPrepSlotBytes);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_fin, kFinBytes);          // 128 MB: projective R'
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_fin_pre, kFinPreBytes);   // 48 MB: prefix products
@@ -137,7 +142,6 @@ void tmed_destroy(tmed_ctx *c) {
   if (c->d_prep) hipFree(c->d_prep);
   if (c->d_fin) hipFree(c->d_fin);
   if (c->d_fin_pre) hipFree(c->d_fin_pre);
-  if (c->d_btab) hipFree(c->d_btab);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -187,10 +191,31 @@ int tmed_verify_batch_device(tmed_ctx *c, const uint8_t *d_pub, const uint8_t *d
   if (c->timing) c->timer.n = 0;
   hipError_t e = scratch_acquire(c, s);
   if (e == hipSuccess)
-    e = launch_verify(d_pub, d_sig, d_msgs, d_off, (uint32_t)n, d_out, c->d_slab, c->slab_slots, BTabs{c->d_btab, c->d_b16, c->d_bcomb16}, c->d_prep,
+    e = launch_verify(d_pub, d_sig, d_msgs, d_off, (uint32_t)n, d_out, c->d_slab, c->slab_slots, BTabs{c->d_b16, c->d_bcomb16}, c->d_prep,
                       c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves, false, c->timing ? &c->timer : nullptr);
   if (e == hipSuccess) e = scratch_release(c, s);
+  if (e == hipSuccess) c->last_hs_count = c->main_waves == 5 ? 0 : last_chunk_count((uint32_t)n, c->chunk);
   return map_err(e);
+}
+
+int tmed_window_stats(tmed_ctx *c, uint32_t lane_hist[65], uint32_t wave_hist[65]) {
+  if (!c || !lane_hist || !wave_hist) return TMED_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  for (int w = 0; w < 65; w++) lane_hist[w] = wave_hist[w] = 0;
+  if (c->last_hs_count == 0) return TMED_OK;
+  (void)hipSetDevice(c->device);
+  uint32_t *d = nullptr;
+  hipError_t e = hipMalloc((void **)&d, 2 * 65 * sizeof(uint32_t));
+  if (e == hipSuccess) e = scratch_acquire(c, c->stream);
+  if (e == hipSuccess) e = launch_window_stats(c->d_prep, c->slab_slots, c->last_hs_count, d, c->stream);
+  if (e == hipSuccess) e = scratch_release(c, c->stream);
+  uint32_t h[130];
+  if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (d) (void)hipFree(d);
+  if (e != hipSuccess) return map_err(e);
+  for (int w = 0; w < 65; w++) { lane_hist[w] = h[w]; wave_hist[w] = h[65 + w]; }
+  return TMED_OK;
 }
 
 int tmed_sign_batch_device(tmed_ctx *c, const uint8_t *d_seeds, const uint8_t *d_msgs, const uint32_t *d_off,
@@ -245,12 +270,13 @@ int tmed_verify_batch(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, const
   if (e == hipSuccess)
     e = launch_verify((const uint8_t *)c->d_a.p, (const uint8_t *)c->d_b.p, (const uint8_t *)c->d_msg.p,
                       (const uint32_t *)c->d_off.p, (uint32_t)n, (uint8_t *)c->d_out.p, c->d_slab, c->slab_slots,
-                      BTabs{c->d_btab, c->d_b16, c->d_bcomb16}, c->d_prep, c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves);
+                      BTabs{c->d_b16, c->d_bcomb16}, c->d_prep, c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves);
   if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
   if (e == hipSuccess) e = scratch_release(c, s);
   if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, n, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return map_err(e);
+  c->last_hs_count = c->main_waves == 5 ? 0 : last_chunk_count((uint32_t)n, c->chunk);
   hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
   memcpy(out, c->h_out.p, n);
   if (sig_lens)

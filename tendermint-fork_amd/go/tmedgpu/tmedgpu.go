@@ -69,6 +69,9 @@ const (
 	DoubleVote      = C.TMED_COMMIT_DOUBLE_VOTE
 	ZeroDenominator = C.TMED_COMMIT_ZERO_DENOMINATOR
 	Overflow        = C.TMED_COMMIT_OVERFLOW
+	// Panic: the reference loop panics when it reaches signature Idx (unknown BlockIDFlag,
+	// malformed BlockID hash); the caller runs the original Go method, which panics as before.
+	Panic = C.TMED_COMMIT_PANIC
 )
 
 // ValSet / CommitData are flat copies of types.ValidatorSet / types.Commit
@@ -76,7 +79,7 @@ const (
 type ValSet struct {
 	PubKeys     []byte  // n x 32
 	Powers      []int64 // n
-	Addresses   []byte  // n x 20
+	Addresses   []byte  // n x 20 (every Validator.Address is 20 bytes; see verifyCommitGPU)
 	TotalPower  int64
 	Keyset      uint64   // 0 or a LoadKeyset handle (cache key: ValidatorSet.Hash())
 	KeysetIndex []uint32 // nil, or validator i -> index in the key set
@@ -93,7 +96,8 @@ type CommitData struct {
 	Round     int32
 	BlockID   BlockID
 	Flags     []byte  // BlockIDFlag per signature
-	Addresses []byte  // n x 20
+	Addresses []byte  // n x 20 (zero-padded slots; AddrLens gives the real lengths)
+	AddrLens  []uint32 // len(ValidatorAddress) per signature: only 20 can match (bytes.Equal)
 	TsSeconds []int64
 	TsNanos   []int32
 	Sigs      []byte // n x 64 (zero padded)
@@ -219,7 +223,8 @@ func (e *Engine) verifyCommitsWith(reqs []Request, call func(*arena, *C.tmed_com
 		c := r.Commit
 		cs[i] = C.tmed_commit{height: C.int64_t(c.Height), round: C.int32_t(c.Round), block_id: a.blockID(&c.BlockID),
 			n_sigs: C.size_t(len(c.Flags)), flags: a.bytes(c.Flags), addresses: a.bytes(c.Addresses),
-			ts_seconds: a.i64(c.TsSeconds), ts_nanos: a.i32(c.TsNanos), sigs: a.bytes(c.Sigs), sig_lens: a.u32(c.SigLens)}
+			ts_seconds: a.i64(c.TsSeconds), ts_nanos: a.i32(c.TsNanos), sigs: a.bytes(c.Sigs), sig_lens: a.u32(c.SigLens),
+			address_lens: a.u32(c.AddrLens)}
 		bids[i] = C.tmed_block_id{}
 		if r.BlockID != nil {
 			bids[i] = a.blockID(r.BlockID)
@@ -277,7 +282,8 @@ func (e *Engine) BlocksyncVerify(w *BlocksyncWindow, batchBlocks int) ([]Result,
 	for i, c := range w.Commits {
 		cs[i] = C.tmed_commit{height: C.int64_t(c.Height), round: C.int32_t(c.Round), block_id: a.blockID(&c.BlockID),
 			n_sigs: C.size_t(len(c.Flags)), flags: a.bytes(c.Flags), addresses: a.bytes(c.Addresses),
-			ts_seconds: a.i64(c.TsSeconds), ts_nanos: a.i32(c.TsNanos), sigs: a.bytes(c.Sigs), sig_lens: a.u32(c.SigLens)}
+			ts_seconds: a.i64(c.TsSeconds), ts_nanos: a.i32(c.TsNanos), sigs: a.bytes(c.Sigs), sig_lens: a.u32(c.SigLens),
+			address_lens: a.u32(c.AddrLens)}
 		bids[i] = a.blockID(&w.BlockIDs[i])
 	}
 	cid := C.CString(w.ChainID)

@@ -76,6 +76,8 @@ def lib() -> ctypes.CDLL:
     l.tmed_kernel_times.argtypes = [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
     l.tmed_last_kernel_ms.restype = ctypes.c_float
     l.tmed_last_kernel_ms.argtypes = [P]
+    l.tmed_window_stats.restype = I
+    l.tmed_window_stats.argtypes = [P, P, P]
     _lib = l
     return l
 
@@ -89,5 +91,5 @@ EXPORTED_SYMBOLS = [
     "tmed_keyset_load", "tmed_keyset_free", "tmed_verify_batch_keyset", "tmed_verify_batch_keyset_device",
     "tmed_set_kernel_timing", "tmed_kernel_times", "tmed_blocksync_verify",
     "tmed_merkle_roots", "tmed_valset_hashes", "tmed_header_hashes", "tmed_partset_roots",
-    "tmed_verify_commits_multi", "tmed_blocksync_verify_multi",
+    "tmed_verify_commits_multi", "tmed_blocksync_verify_multi", "tmed_window_stats",
 ]

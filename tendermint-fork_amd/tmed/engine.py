@@ -169,5 +169,13 @@ class Engine:
             raise TmedError(rc, "tmed_kernel_times")
         return list(ms), list(n)
 
+    def window_stats(self):
+        """(lane_hist, wave_hist): window counts W of the last half-size chunk (tmed_window_stats)."""
+        lh, wh = np.zeros(65, np.uint32), np.zeros(65, np.uint32)
+        rc = lib().tmed_window_stats(self._h, _p(lh), _p(wh))
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_window_stats")
+        return lh, wh
+
     def last_kernel_ms(self) -> float:
         return float(lib().tmed_last_kernel_ms(self._h))

@@ -80,6 +80,7 @@ class PackedCommit:
     ts_nanos: np.ndarray     # i32[n]
     sigs: np.ndarray         # u8[n,64]
     sig_lens: np.ndarray     # u32[n]
+    address_lens: Optional[np.ndarray] = None  # u32[n] len(ValidatorAddress); None = all 20
 
     @property
     def signatures(self):
@@ -95,7 +96,9 @@ class _PackedSigs:
 
     def __getitem__(self, i):
         pc = self.pc
-        return CommitSig(int(pc.flags[i]), pc.addresses[i].tobytes(), (int(pc.ts_seconds[i]), int(pc.ts_nanos[i])),
+        al = 20 if pc.address_lens is None else int(pc.address_lens[i])
+        addr = pc.addresses[i].tobytes() if al == 20 else bytes(al)  # other lengths: content never compared
+        return CommitSig(int(pc.flags[i]), addr, (int(pc.ts_seconds[i]), int(pc.ts_nanos[i])),
                          pc.sigs[i, :int(pc.sig_lens[i])].tobytes())
 
 
@@ -153,13 +156,19 @@ class ValidatorSet:
 
     # reference method names
     def verify_commit(self, engine, chain_id: str, block_id: BlockID, height: int, commit: Commit):
-        return verify_commits(engine, [(MODE_COMMIT, self, chain_id, block_id, height, commit, 0, 0)])[0]
+        return _raise_panic(verify_commits(engine, [(MODE_COMMIT, self, chain_id, block_id, height, commit, 0, 0)])[0])
 
     def verify_commit_light(self, engine, chain_id: str, block_id: BlockID, height: int, commit: Commit):
-        return verify_commits(engine, [(MODE_LIGHT, self, chain_id, block_id, height, commit, 0, 0)])[0]
+        return _raise_panic(verify_commits(engine, [(MODE_LIGHT, self, chain_id, block_id, height, commit, 0, 0)])[0])
 
     def verify_commit_light_trusting(self, engine, chain_id: str, commit: Commit, num: int, den: int):
-        return verify_commits(engine, [(MODE_LIGHT_TRUSTING, self, chain_id, None, 0, commit, num, den)])[0]
+        return _raise_panic(verify_commits(engine, [(MODE_LIGHT_TRUSTING, self, chain_id, None, 0, commit, num, den)])[0])
+
+
+def _raise_panic(res):
+    if isinstance(res, GoPanic):
+        raise res
+    return res
 
 
 # --------------------------------------------------------------------------- errors
@@ -196,6 +205,17 @@ class ErrNotEnoughVotingPowerSigned(GoError):  # types/validator_set.go:856-863
         super().__init__("invalid commit -- insufficient voting power: got %d, needed more than %d" % (got, needed))
 
 
+class GoPanic(RuntimeError):
+    """The reference loop panics at signature ``idx`` (TMED_COMMIT_PANIC): an unknown BlockIDFlag in
+    VerifyCommit (types/block.go:652-665) or a malformed BlockID hash reaching CanonicalizeBlockID
+    (types/canonical.go:18-22).  The reference-named methods raise it, like Go's panic; the batch
+    functions return it in that request's slot."""
+
+    def __init__(self, idx):
+        self.idx = idx
+        super().__init__("reference panics at signature #%d" % idx)
+
+
 # --------------------------------------------------------------------------- ABI structs
 
 class _BlockIDC(ctypes.Structure):
@@ -213,7 +233,7 @@ class _CommitC(ctypes.Structure):
     _fields_ = [("height", ctypes.c_int64), ("round", ctypes.c_int32), ("block_id", _BlockIDC),
                 ("n_sigs", ctypes.c_size_t), ("flags", ctypes.c_void_p), ("addresses", ctypes.c_void_p),
                 ("ts_seconds", ctypes.c_void_p), ("ts_nanos", ctypes.c_void_p), ("sigs", ctypes.c_void_p),
-                ("sig_lens", ctypes.c_void_p)]
+                ("sig_lens", ctypes.c_void_p), ("address_lens", ctypes.c_void_p)]
 
 
 class _RequestC(ctypes.Structure):
@@ -282,8 +302,10 @@ def _commit_c(c, keep):
         arrs = [np.ascontiguousarray(c.flags, np.uint8), np.ascontiguousarray(c.addresses, np.uint8),
                 np.ascontiguousarray(c.ts_seconds, np.int64), np.ascontiguousarray(c.ts_nanos, np.int32),
                 np.ascontiguousarray(c.sigs, np.uint8), np.ascontiguousarray(c.sig_lens, np.uint32)]
-        keep.extend(arrs)
-        return _CommitC(c.height, c.round, _block_id_c(c.block_id, keep), arrs[0].shape[0], *[_ptr(a) for a in arrs])
+        al = None if c.address_lens is None else np.ascontiguousarray(c.address_lens, np.uint32)
+        keep.extend(arrs + [al])
+        return _CommitC(c.height, c.round, _block_id_c(c.block_id, keep), arrs[0].shape[0], *[_ptr(a) for a in arrs],
+                        None if al is None else _ptr(al))
     n = len(c.signatures)
     m = max(n, 1)
     flags = np.zeros(m, np.uint8)
@@ -292,8 +314,10 @@ def _commit_c(c, keep):
     nan = np.zeros(m, np.int32)
     sigs = np.zeros((m, 64), np.uint8)
     lens = np.zeros(m, np.uint32)
+    alens = np.zeros(m, np.uint32)
     for i, cs in enumerate(c.signatures):
         flags[i] = cs.flag
+        alens[i] = len(cs.address)  # only a 20-byte address can equal a validator's (GetByAddress)
         if len(cs.address) == 20:
             addrs[i] = np.frombuffer(cs.address, np.uint8)
         sec[i], nan[i] = cs.timestamp
@@ -301,9 +325,9 @@ def _commit_c(c, keep):
         if s:
             sigs[i, :len(s)] = np.frombuffer(s, np.uint8)
         lens[i] = len(cs.signature)
-    keep.extend([flags, addrs, sec, nan, sigs, lens])
+    keep.extend([flags, addrs, sec, nan, sigs, lens, alens])
     return _CommitC(c.height, c.round, _block_id_c(c.block_id, keep), n, _ptr(flags), _ptr(addrs), _ptr(sec),
-                    _ptr(nan), _ptr(sigs), _ptr(lens))
+                    _ptr(nan), _ptr(sigs), _ptr(lens), _ptr(alens))
 
 
 def _to_error(code, r: _ResultC, vals: ValidatorSet, block_id, commit: Commit):
@@ -325,6 +349,8 @@ def _to_error(code, r: _ResultC, vals: ValidatorSet, block_id, commit: Commit):
         return GoError("trustLevel has zero Denominator")
     if code == 8:
         return GoError("int64 overflow while calculating voting power needed. please provide smaller trustLevel numerator")
+    if code == 9:
+        return GoPanic(r.idx)  # a batch reports it per request; the reference-named methods raise it
     raise RuntimeError("tmed: unknown commit outcome %d" % code)
 
 

@@ -93,21 +93,85 @@ def _one_commit(flag_override=None):
     return vs, pv, cm, pc, bid
 
 
-def test_inputs_the_reference_panics_on_return_einval():
-    """Where the reference would panic — an unknown BlockIDFlag reaching CommitSig.BlockID
-    (types/block.go:652-662) in VerifyCommit — the seam returns TMED_EINVAL so the caller takes
-    the original Go path (which then panics exactly as before); an unknown flag in the Light
-    loops is skipped like any non-Commit flag, as the reference does (validator_set.go:742)."""
+def test_inputs_the_reference_panics_on_are_per_request():
+    """Where the reference loop would panic — an unknown BlockIDFlag reaching CommitSig.BlockID
+    (types/block.go:652-665) in VerifyCommit — the request gets TMED_COMMIT_PANIC at that index
+    (the Go shim then runs the original method, which panics exactly as before) — but only if the
+    loop gets that far: a bad signature before it is reported as such.  An unknown flag in the
+    Light loops is skipped like any non-Commit flag, as the reference does (validator_set.go:742).
+    Other requests of the same batch are unaffected."""
     import pytest
-    from tmed import TmedError
-    from tmed._native import TMED_EINVAL
     vs, pv, cm, pc, bid = _one_commit(flag_override=9)
-    with pytest.raises(TmedError) as ei:
-        T.verify_commits(None, [(T.MODE_COMMIT, pv, "ei-chain", pbid(bid), 7, pc, 0, 0)], verifier=oracle_verifier)
-    assert ei.value.code == TMED_EINVAL
+    good = (T.MODE_COMMIT, *_one_commit()[1:2], "ei-chain", pbid(bid), 7, _one_commit()[3], 0, 0)
+    got = T.verify_commits(None, [(T.MODE_COMMIT, pv, "ei-chain", pbid(bid), 7, pc, 0, 0), good],
+                           verifier=oracle_verifier)
+    assert isinstance(got[0], T.GoPanic) and got[0].idx == 2
+    assert got[1] is None
+    with pytest.raises(T.GoPanic):
+        T._raise_panic(got[0])
+    # a bad signature at index 1 comes first: the reference returns "wrong signature (#1)"
+    s = bytearray(pc.signatures[1].signature)
+    s[0] ^= 1
+    pc.signatures[1].signature = bytes(s)
+    got = T.verify_commits(None, [(T.MODE_COMMIT, pv, "ei-chain", pbid(bid), 7, pc, 0, 0)], verifier=oracle_verifier)
+    assert str(got[0]).startswith("wrong signature (#1)")
     # Light: flag 9 is not BlockIDFlagCommit -> skipped; 3 of 4 equal powers still cross 2/3
+    vs, pv, cm, pc, bid = _one_commit(flag_override=9)
     got = T.verify_commits(None, [(T.MODE_LIGHT, pv, "ei-chain", pbid(bid), 7, pc, 0, 0)], verifier=oracle_verifier)
     assert got == [None]
+
+
+def test_edge_scenarios_match_reference_loops_cpu():
+    """Unknown flags, malformed BlockID hashes and ValidatorAddress lengths 0/19/21 (including
+    the 19-byte prefix of an address ending in 0x00) through the seam vs the oracle loops —
+    panics reported per request at the reference's index, addresses matched by bytes.Equal."""
+    from commit_cases import edge_scenarios, oracle_outcome, same_outcome
+    reqs, exp = [], []
+    for mode, vs, pv, chain, bid, h, cm, pc, num, den in edge_scenarios(seed=7, count=60):
+        exp.append(oracle_outcome(mode, vs, chain, bid, h, cm, num, den))
+        reqs.append((mode, pv, chain, pbid(bid), h, pc, num, den))
+    got = T.verify_commits(None, reqs, verifier=oracle_verifier)
+    bad = [(q, got[q], exp[q]) for q in range(len(reqs)) if not same_outcome(got[q], exp[q])]
+    assert not bad, bad[:5]
+    kinds = {"panic" if isinstance(e, tuple) else (type(e).__name__ if e is not None else "ok") for e in exp}
+    assert {"panic", "ok"} <= kinds, kinds
+
+
+def test_address_prefix_of_zero_ending_address_is_not_a_match():
+    """A ForBlock CommitSig whose ValidatorAddress is the 19-byte prefix of a validator address
+    ending in 0x00 must be skipped by LightTrusting (bytes.Equal, types/validator_set.go:270-277):
+    with the signature otherwise valid the tally lacks that validator's power."""
+    from oracle import commit as C
+    from oracle.fixtures import make_block_id, make_commit, make_valset, seed_of
+    from commit_cases import address_ending_in_zero, oracle_outcome, to_product
+    zs, zp = address_ending_in_zero()
+    vs, seeds = make_valset([zs, seed_of("zp", 1), seed_of("zp", 2)], [10, 10, 10])
+    cm = make_commit(vs, seeds, "zc", 5, 0, make_block_id("zc"))
+    zi = next(i for i, v in enumerate(vs.validators) if v.pub_key == zp)
+    assert vs.validators[zi].address[19] == 0
+    cm.signatures[zi].address = vs.validators[zi].address[:19]
+    exp = oracle_outcome(2, vs, "zc", None, 0, cm, 2, 3)
+    pv, pc = to_product(vs, cm)
+    got = T.verify_commits(None, [(T.MODE_LIGHT_TRUSTING, pv, "zc", None, 0, pc, 2, 3)], verifier=oracle_verifier)[0]
+    assert str(got) == str(exp) == "invalid commit -- insufficient voting power: got 20, needed more than 20"
+    # the bytes a fixed 20-byte slot holds for that address ARE the validator's address: only the
+    # length crossing the ABI (address_lens) keeps them apart
+    n = len(pc.signatures)
+    addrs = np.zeros((n, 20), np.uint8)
+    for i, cs in enumerate(pc.signatures):
+        addrs[i, :len(cs.address[:20])] = np.frombuffer(cs.address[:20], np.uint8)
+    assert addrs[zi].tobytes() == vs.validators[zi].address
+    packed = T.PackedCommit(pc.height, pc.round, pc.block_id, np.array([s.flag for s in pc.signatures], np.uint8),
+                            addrs, np.array([s.timestamp[0] for s in pc.signatures], np.int64),
+                            np.array([s.timestamp[1] for s in pc.signatures], np.int32),
+                            np.array([np.frombuffer(s.signature, np.uint8) for s in pc.signatures]),
+                            np.full(n, 64, np.uint32),
+                            np.array([len(s.address) for s in pc.signatures], np.uint32))
+    got = T.verify_commits(None, [(T.MODE_LIGHT_TRUSTING, pv, "zc", None, 0, packed, 2, 3)], verifier=oracle_verifier)[0]
+    assert str(got) == str(exp)
+    packed.address_lens = None  # all 20: now the prefix slot matches, as a 20-byte shim would make it
+    got = T.verify_commits(None, [(T.MODE_LIGHT_TRUSTING, pv, "zc", None, 0, packed, 2, 3)], verifier=oracle_verifier)[0]
+    assert got is None
 
 
 def test_bad_mode_and_missing_block_id_return_einval():

@@ -230,3 +230,19 @@ def test_blocksync_window_matches_light_loops(engine, batch, chain, keyed):
     finally:
         if ks:
             engine.keyset_free(ks)
+
+
+def test_edge_scenarios_gpu(engine):
+    """Unknown BlockIDFlags, malformed BlockID hashes and odd-length ValidatorAddresses (0/19/21
+    bytes, and the 19-byte prefix of an address ending in 0x00) through the GPU seam: panics are
+    reported per request at the reference loop's index (TMED_COMMIT_PANIC), GetByAddress matches by
+    bytes.Equal, every other outcome equals the reference loops."""
+    from commit_cases import edge_scenarios, oracle_outcome, same_outcome
+    reqs, exp = [], []
+    for mode, vs, pv, chain, bid, h, cm, pc, num, den in edge_scenarios(seed=8, count=60):
+        exp.append(oracle_outcome(mode, vs, chain, bid, h, cm, num, den))
+        reqs.append((mode, pv, chain, pbid(bid), h, pc, num, den))
+    got = T.verify_commits(engine, reqs)
+    bad = [(q, got[q], exp[q]) for q in range(len(reqs)) if not same_outcome(got[q], exp[q])]
+    assert not bad, bad[:5]
+    assert any(isinstance(e, tuple) for e in exp)

@@ -1,0 +1,201 @@
+"""GPU parity at the BASELINE.json shapes (C1, C3, C4) through the drop-in seam, against the
+oracle's restatement of the reference loops (types/validator_set.go:667-826) with the C port as
+the per-signature verifier.  Invalid signatures are placed where the loops' early exits make them
+matter: index 0, the last index, right at and after the >2/3 crossing, and a header whose
+trusted-set overlap is below the trust level (light/verifier.go:58-62: ErrNotEnoughVotingPowerSigned
+with exact Got/Needed).  Synthetic keys and votes come from the GPU signer (checked against the
+oracle signer in test_gpu_verify.py)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import commit as C
+from oracle import port
+import tmed.types as T
+from tmed.workload import make_valset, pubkeys_of, seeds_from_tag, sign_commits
+
+pytestmark = pytest.mark.gpu
+
+T2023 = 1672531200
+CHAIN = "test_chain_id"
+
+
+def _bid(tag: bytes):
+    return T.BlockID(hashlib.sha256(tag).digest(), 123, hashlib.sha256(tag + b"/psh").digest())
+
+
+def _ovals(vals: T.ValidatorSet) -> C.ValidatorSet:
+    return C.ValidatorSet([C.Validator(v.pub_key, v.voting_power, v.proposer_priority, v.address)
+                           for v in vals.validators])
+
+
+def _ocommit(pc: T.PackedCommit) -> C.Commit:
+    sigs = []
+    for i in range(pc.flags.shape[0]):
+        sigs.append(C.CommitSig(int(pc.flags[i]), pc.addresses[i].tobytes(),
+                                (int(pc.ts_seconds[i]), int(pc.ts_nanos[i])),
+                                pc.sigs[i, :int(pc.sig_lens[i])].tobytes()))
+    b = pc.block_id
+    return C.Commit(pc.height, pc.round, C.BlockID(b.hash, b.psh_total, b.psh_hash), sigs)
+
+
+def _obid(b: T.BlockID) -> C.BlockID:
+    return C.BlockID(b.hash, b.psh_total, b.psh_hash)
+
+
+def _port_verify(pub, msg, sig):
+    return port.verify(pub, msg, sig)
+
+
+def _oracle(req, ovs, oc):
+    mode, vals, chain, bid, h, pc, num, den = req
+    if mode == T.MODE_COMMIT:
+        return C.verify_commit(ovs, chain, _obid(bid), h, oc, _port_verify)
+    if mode == T.MODE_LIGHT:
+        return C.verify_commit_light(ovs, chain, _obid(bid), h, oc, _port_verify)
+    return C.verify_commit_light_trusting(ovs, chain, oc, num, den, _port_verify)
+
+
+def _same(a, b):
+    if a is None or b is None:
+        return a is None and b is None
+    return type(a).__name__ == type(b).__name__ and str(a) == str(b)
+
+
+def _corrupt(pc: T.PackedCommit, i: int):
+    pc.sigs[i, 7] ^= 0x20
+
+
+@pytest.fixture(scope="module")
+def c1_data(engine):
+    n = 175
+    seeds = seeds_from_tag(b"tmed-bench-key", 0, n)
+    pubs = pubkeys_of(engine, seeds)
+    vals, order = make_valset(pubs, [10] * n)
+    addrs = np.array([np.frombuffer(v.address, np.uint8) for v in vals.validators])
+    bid = _bid(b"tmed-c1")
+    base = sign_commits(engine, CHAIN, [(seeds[order], addrs, 3, 0, bid, T2023, None)])[0]
+    return vals, bid, base
+
+
+def _copy(pc):
+    return T.PackedCommit(pc.height, pc.round, pc.block_id, pc.flags.copy(), pc.addresses.copy(),
+                          pc.ts_seconds.copy(), pc.ts_nanos.copy(), pc.sigs.copy(), pc.sig_lens.copy())
+
+
+@pytest.mark.parametrize("path", ["generic", "keyset"])
+def test_c1_175_validators(engine, c1_data, path):
+    """C1: one 175-validator commit (equal power 10; needed = 1166, crossed after 117 signatures),
+    VerifyCommit / Light / Trusting(1/3) through tmed_verify_commits, generic and key-cached (the
+    latency kernels), with a bad signature at index 0, at 174, at 116 (the crossing signature) and
+    at 150 (after the crossing: Light and Trusting still succeed, VerifyCommit fails)."""
+    vals, bid, base = c1_data
+    if path == "keyset":
+        vals = T.ValidatorSet(list(vals.validators))
+        vals.keyset = engine.keyset_load(np.array([np.frombuffer(v.pub_key, np.uint8) for v in vals.validators]))
+    try:
+        ovs = _ovals(vals)
+        reqs, exp = [], []
+        for bad in (None, 0, 174, 116, 150):
+            pc = _copy(base)
+            if bad is not None:
+                _corrupt(pc, bad)
+            oc = _ocommit(pc)
+            for req in ((T.MODE_COMMIT, vals, CHAIN, bid, 3, pc, 0, 0), (T.MODE_LIGHT, vals, CHAIN, bid, 3, pc, 0, 0),
+                        (T.MODE_LIGHT_TRUSTING, vals, CHAIN, None, 0, pc, 1, 3)):
+                reqs.append(req)
+                exp.append(_oracle(req, ovs, oc))
+        got = T.verify_commits(engine, reqs)                     # one batch
+        one = [T.verify_commits(engine, [r])[0] for r in reqs]   # one commit per call (C1's latency shape)
+        for q in range(len(reqs)):
+            assert _same(got[q], exp[q]), (q, got[q], exp[q])
+            assert _same(one[q], exp[q]), (q, one[q], exp[q])
+        texts = [str(e) for e in exp]
+        assert "wrong signature (#0)" in " ".join(texts) and "wrong signature (#174)" in " ".join(texts)
+        assert exp[3 * 4 + 1] is None and str(exp[3 * 4]).startswith("wrong signature (#150)")
+    finally:
+        if path == "keyset":
+            engine.keyset_free(vals.keyset)
+
+
+def test_c3_light_client_changing_sets(engine):
+    """C3 shape: 48 headers x 175 validators, the set changing by one key per height, one shared key
+    set indexed per validator set (keyset_index); per header Trusting(1/3) against the set of h and
+    Light against the set of h + 2.  Header 5 is checked against a trusted set 120 heights back
+    (overlap 53 validators: Got 530 <= Needed 583), headers 9 and 17 carry bad signatures inside
+    the Trusting prefix, header 23 a bad signature after the Light crossing."""
+    nv, H, gap, far = 175, 48, 2, 120
+    pool_seeds = seeds_from_tag(b"tmed-c3-key", 0, H + gap + nv + far)
+    pool_pubs = pubkeys_of(engine, pool_seeds)
+    ks = engine.keyset_load(pool_pubs)
+    try:
+        sets, specs = {}, []
+        hs = sorted(set(range(H + gap)) | {far + 5 + gap})
+        for h in hs:
+            vals, order = make_valset(pool_pubs[h:h + nv], [10] * nv)
+            vals.keyset = ks
+            vals.keyset_index = (order + h).astype(np.uint32)
+            sets[h] = vals
+            addrs = np.array([np.frombuffer(v.address, np.uint8) for v in vals.validators])
+            specs.append((pool_seeds[h:h + nv][order], addrs, h + 1, 0, _bid(b"c3-%d" % (h + 1)), T2023 + h, None))
+        commits = dict(zip(hs, sign_commits(engine, CHAIN, specs)))
+        _corrupt(commits[9 + gap], 3)
+        _corrupt(commits[17 + gap], 40)
+        _corrupt(commits[23 + gap], 160)
+        reqs, exp, osets = [], [], {h: _ovals(v) for h, v in sets.items()}
+        for h in range(H):
+            u = h + gap if h != 5 else far + 5 + gap
+            pc = commits[u]
+            oc = _ocommit(pc)
+            for req, ovs in (((T.MODE_LIGHT_TRUSTING, sets[h], CHAIN, None, 0, pc, 1, 3), osets[h]),
+                             ((T.MODE_LIGHT, sets[u], CHAIN, pc.block_id, u + 1, pc, 0, 0), osets[u])):
+                reqs.append(req)
+                exp.append(_oracle(req, ovs, oc))
+        got = T.verify_commits(engine, reqs)
+        bad = [(q, str(got[q]), str(exp[q])) for q in range(len(reqs)) if not _same(got[q], exp[q])]
+        assert not bad, bad[:4]
+        assert isinstance(exp[10], C.ErrNotEnoughVotingPowerSigned)
+        assert (exp[10].got, exp[10].needed) == (10 * (nv - far - gap), 583)
+        assert sum(str(e).startswith("wrong signature") for e in exp) >= 2 and exp[2 * 23 + 1] is None
+    finally:
+        engine.keyset_free(ks)
+
+
+def test_c4_10k_validator_light_window(engine):
+    """C4 shape: a blocksync window of 6 blocks x 10,000 validators (equal power 10: needed 66,666,
+    crossed by the 6,667th signature, index 6,666), VerifyCommitLight per block through the pipelined
+    blocksync seam (key-cached) and through tmed_verify_commits (generic keys).  Blocks carry a bad
+    signature at index 100, at 6,666 (the crossing signature itself), at 6,667 (just after the
+    crossing: never reached) and at 9,999; one block is all valid and one has a wrong BlockID."""
+    nv = 10_000
+    seeds = seeds_from_tag(b"tmed-c4-key", 0, nv)
+    pubs = pubkeys_of(engine, seeds)
+    vals, order = make_valset(pubs, [10] * nv)
+    addrs = np.array([np.frombuffer(v.address, np.uint8) for v in vals.validators])
+    specs = [(seeds[order], addrs, b + 1, 0, _bid(b"c4-%d" % (b + 1)), T2023 + b, None) for b in range(6)]
+    commits = sign_commits(engine, CHAIN, specs)
+    for b, i in ((0, 100), (1, 6666), (2, 6667), (3, 9999)):
+        _corrupt(commits[b], i)
+    bids = [c.block_id for c in commits]
+    bids[5] = _bid(b"c4-other")
+    heights = [c.height for c in commits]
+    ovs = _ovals(vals)
+    exp = [C.verify_commit_light(ovs, CHAIN, _obid(bids[b]), heights[b], _ocommit(commits[b]), _port_verify)
+           for b in range(6)]
+    assert str(exp[0]).startswith("wrong signature (#100)") and str(exp[1]).startswith("wrong signature (#6666)")
+    assert exp[2] is None and exp[3] is None and exp[4] is None and "wrong block ID" in str(exp[5])
+    generic = T.verify_commits(engine, [(T.MODE_LIGHT, vals, CHAIN, bids[b], heights[b], commits[b], 0, 0)
+                                        for b in range(6)])
+    vals.keyset = engine.keyset_load(np.array([np.frombuffer(v.pub_key, np.uint8) for v in vals.validators]))
+    try:
+        win = T.BlocksyncWindow(vals, CHAIN, bids, heights, commits)
+        win.run(engine, 2)
+        keyed = win.errors()
+        stats = win.verified()
+    finally:
+        engine.keyset_free(vals.keyset)
+    for b in range(6):
+        assert _same(generic[b], exp[b]), (b, generic[b], exp[b])
+        assert _same(keyed[b], exp[b]), (b, keyed[b], exp[b])
+    assert stats.tolist() == [101, 6667, 6667, 6667, 6667, 0]

@@ -79,3 +79,36 @@ def test_c5_mix(vengine):
     out = vengine.verify_arrays(pubs, sigs, msgs, offs.astype(np.uint32))
     exp = port.verify_batch(pubs, sigs, msgs, offs, 16)
     assert int((out != exp).sum()) == 0
+
+
+@pytest.mark.parametrize("slots,chunk", [("1000", None), ("300", "100")])
+def test_odd_slab_and_chunk_sizes(slots, chunk):
+    """TMED_SLAB_SLOTS / TMED_CHUNK that are not multiples of the 256-lane block: the
+    context rounds them up, so every lane of every launched block owns a slab slot and a batch
+    larger than the slab runs as several chunks with decisions equal to the oracle."""
+    from tmed import Engine
+    saved = {k: os.environ.get(k) for k in ("TMED_SLAB_SLOTS", "TMED_CHUNK")}
+    os.environ["TMED_SLAB_SLOTS"] = slots
+    if chunk:
+        os.environ["TMED_CHUNK"] = chunk
+    try:
+        e = Engine(0)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    try:
+        n = 2600
+        rng = np.random.default_rng(99)
+        seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        offs = (np.arange(n + 1) * 114).astype(np.uint64)
+        msgs = rng.integers(0, 256, int(offs[-1]) + 16, dtype=np.uint8)
+        sigs, pubs = e.sign_arrays(seeds, msgs, offs.astype(np.uint32))
+        sigs[::7, 40] ^= 0x01
+        out = e.verify_arrays(pubs, sigs, msgs, offs.astype(np.uint32))
+        exp = port.verify_batch(pubs, sigs, msgs, offs, 16)
+        assert int((out != exp).sum()) == 0 and exp.sum() == n - len(range(0, n, 7))
+    finally:
+        e.close()

@@ -39,6 +39,23 @@ def test_sign_kernel_matches_oracle(engine):
     assert (sigs == esig).all() and (pubs == epub).all()
 
 
+def test_sign_kernel_privval_known_answer(engine):
+    """The GPU signer's key derivation pinned to the reference's one fixed ed25519 datum
+    (privval/msgs_test.go:62,85: GenPrivKeyFromSecret("it's a secret") -> 556a436f...c5fcf230),
+    and a vote signed by it verifies on the GPU."""
+    import json
+    with open(os.path.join(os.path.dirname(__file__), "golden", "privval_kat.json")) as f:
+        kat = json.load(f)
+    seed = np.frombuffer(hashlib.sha256(kat["secret_utf8"].encode()).digest(), np.uint8).reshape(1, 32)
+    msg = np.frombuffer(b"privval vote" + bytes(16), np.uint8)
+    offs = np.array([0, 12], np.uint32)
+    sigs, pubs = engine.sign_arrays(seed, msg, offs)
+    assert pubs[0].tobytes().hex() == kat["pubkey"]
+    assert sigs[0].tobytes() == port.sign(seed[0].tobytes(), b"privval vote")
+    out = engine.verify_arrays(pubs, sigs, msg, offs)
+    assert out.tolist() == [1]
+
+
 @pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 257, 1000])
 def test_batch_sizes(engine, n):
     rng, seeds, msgs, offs = _random_batch(n, 100 + n)
