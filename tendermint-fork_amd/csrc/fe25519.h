@@ -74,17 +74,9 @@ TMED_HD void fe_select(fe &h, const fe &f, const fe &g, bool b) {
 // one 64-bit shift, one 32-bit and, one 64-bit add per carry (+ one 32-bit sub per limb).
 TMED_HD int64_t fe_bias(int k) { return (k & 1) ? ((int64_t)1 << 24) : ((int64_t)1 << 25); }
 
-// The same constant hidden from constant folding: as a known constant LLVM re-associates
-// the bias to the END of the column sum (one extra 64-bit add per column, 10 per mul);
-// opaque, it stays the addend of the column's first v_mad_i64_i32.  (The empty asm is
-// not volatile, so it is CSE'd and hoisted: two SGPR pairs for the whole kernel.)
-TMED_HD int64_t fe_bias_acc(int k) {
-  int64_t b = fe_bias(k);
-#if defined(__HIP_DEVICE_COMPILE__)
-  asm("" : "+s"(b));
-#endif
-  return b;
-}
+// The column sums of fe_mul / fe_sq / fe_sq2 as explicit v_mad_i64_i32 schedules, bias in
+// each column's first mad (generated: tools/gen_fe_asm.py).
+#include "fe_cols.h"
 
 // Carry pass over BIASED 64-bit column sums H_k = h_k + B_k -> carried limbs.  Two
 // interleaved chains (0..4 and 4..9) give the scheduler independent work.
@@ -119,7 +111,8 @@ TMED_HD void fe_carry(fe &h, const fe &f) {
   fe_carry64(h, t);
 }
 
-// h = f * g  (100 v_mad_i64_i32)
+// h = f * g  (100 v_mad_i64_i32; operand pairs (i, j) carry x2 when both are odd and x19 on g_j
+// when i + j >= 10 — fe_mul_cols)
 TMED_HD void fe_mul(fe &h, const fe &f, const fe &g) {
   int32_t g19[10], f2[10];
 #pragma unroll
@@ -127,73 +120,43 @@ TMED_HD void fe_mul(fe &h, const fe &f, const fe &g) {
 #pragma unroll
   for (int i = 0; i < 10; i++) f2[i] = (int32_t)(2u * (uint32_t)f.v[i]);
   int64_t acc[10];
-#pragma unroll
-  for (int k = 0; k < 10; k++) acc[k] = fe_bias_acc(k);
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-#pragma unroll
-    for (int j = 0; j < 10; j++) {
-      const int k = i + j;
-      const int32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
-      const int32_t b = (k >= 10) ? g19[j] : g.v[j];
-      acc[k >= 10 ? k - 10 : k] += (int64_t)a * (int64_t)b;
-    }
-  }
+  fe_mul_cols(acc, f.v, f2, g.v, g19);
   fe_carry64(h, acc);
 }
 
-// Column sums of f^2 (55 products).  Pair (i,j), i<=j, carries the coefficient
-// (i<j ? 2 : 1) * (i,j odd ? 2 : 1) * (i+j>=10 ? 19 : 1); the factor 19 (and
-// its companion 2 for odd-odd pairs) is put on the odd-index operand where
-// there is one, so every pre-multiplied operand stays inside int32.
-TMED_HD void fe_sq_acc(int64_t acc[10], const fe &f, bool biased) {
-  int32_t x2[10], x19[10], x38[10];
+// Column sums of D f^2, D = 1 (square) or 2 (the doubling's 2 Z^2): 55 products.  Pair (i, j),
+// i <= j, carries the coefficient D * (i<j ? 2 : 1) * (i,j odd ? 2 : 1) * (i+j>=10 ? 19 : 1),
+// spread over the two operands as pre-multiplied copies x2, x4, x19, x38 = 2 * x19 (the split:
+// tools/gen_fe_asm.py sq_products): the 19 on the odd-index operand where there is one, with a
+// factor 2 only on an odd (25-bit) limb, so every operand stays inside int32 for inputs up to
+// three carried values (D = 1) or one (D = 2).
+struct fe_premul {
+  int32_t x[10], x2[10], x4[10], x19[10], x38[10];
+  TMED_HDM explicit fe_premul(const fe &f) {
 #pragma unroll
-  for (int i = 0; i < 10; i++) {
-    const uint32_t u = (uint32_t)f.v[i];
-    x2[i] = (int32_t)(2u * u); x19[i] = mul19(f.v[i]); x38[i] = mul38(f.v[i]);
-  }
-#pragma unroll
-  for (int k = 0; k < 10; k++) acc[k] = biased ? fe_bias_acc(k) : 0;
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-#pragma unroll
-    for (int j = i; j < 10; j++) {
-      const int k = i + j;
-      const bool wrap = k >= 10;
-      const bool oo = (i & 1) && (j & 1);
-      const bool off = i < j;
-      // operands a (index i) and b (index j)
-      int32_t a = f.v[i], b = f.v[j];
-      if (!wrap) {
-        // coefficient: (off?2:1)*(oo?2:1)  in {1,2,4}
-        if (off && oo) { a = x2[i]; b = x2[j]; }
-        else if (off || oo) { a = x2[i]; }
-      } else {
-        // coefficient: (off?2:1)*(oo?2:1)*19 in {19,38,76}
-        if (off && oo) { a = x2[i]; b = x38[j]; }          // 76 = 2 * 38
-        else if (oo) { b = x38[j]; }                        // i == j odd: 38
-        else if (off) {                                      // 38: 19 on the odd one
-          if (j & 1) { a = x2[i]; b = x19[j]; } else { a = x19[i]; b = x2[j]; }
-        } else { b = x19[j]; }                               // i == j even: 19
-      }
-      acc[wrap ? k - 10 : k] += (int64_t)a * (int64_t)b;
+    for (int i = 0; i < 10; i++) {
+      const uint32_t u = (uint32_t)f.v[i];
+      x[i] = f.v[i];
+      x2[i] = (int32_t)(2u * u);
+      x4[i] = (int32_t)(4u * u);
+      x19[i] = mul19(f.v[i]);
+      x38[i] = (int32_t)((uint32_t)x19[i] << 1);  // a shift, not a second v_mul_lo_u32
     }
   }
-}
+};
 
 TMED_HD void fe_sq(fe &h, const fe &f) {
+  const fe_premul p(f);
   int64_t acc[10];
-  fe_sq_acc(acc, f, true);
+  fe_sq1_cols(acc, p.x, p.x2, p.x4, p.x19, p.x38);
   fe_carry64(h, acc);
 }
 
-// h = 2 f^2
+// h = 2 f^2 (f carried)
 TMED_HD void fe_sq2(fe &h, const fe &f) {
+  const fe_premul p(f);
   int64_t acc[10];
-  fe_sq_acc(acc, f, false);
-#pragma unroll
-  for (int k = 0; k < 10; k++) acc[k] = 2 * acc[k] + fe_bias(k);
+  fe_sq2_cols(acc, p.x, p.x2, p.x4, p.x19, p.x38);
   fe_carry64(h, acc);
 }
 
