@@ -59,42 +59,60 @@ TMED_HD double words_to_double(const uint32_t *x, int n) {
   return r;
 }
 
+// 32-bit add / subtract with carry (device: the carry-chain builtins, which become one
+// v_addc / v_subb each; the 64-bit spelling costs a sign extension and register moves per word).
+TMED_HD uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t &cout) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  unsigned int co;
+  const uint32_t r = __builtin_addc(a, b, cin, &co);
+  cout = co;
+  return r;
+#else
+  const uint64_t t = (uint64_t)a + b + cin;
+  cout = (uint32_t)(t >> 32);
+  return (uint32_t)t;
+#endif
+}
+TMED_HD uint32_t subb32(uint32_t a, uint32_t b, uint32_t bin, uint32_t &bout) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  unsigned int bo;
+  const uint32_t r = __builtin_subc(a, b, bin, &bo);
+  bout = bo;
+  return r;
+#else
+  const uint64_t d = (uint64_t)a - b - bin;
+  bout = (uint32_t)(d >> 63);
+  return (uint32_t)d;
+#endif
+}
+
 // r = a - q*b (8 words); returns true if the result went negative (wrapped mod 2^256).
+// Two borrow chains: the low halves of q*b[i] and the high halves of q*b[i-1].
 TMED_HD bool words8_submul(uint32_t r[8], const uint32_t a[8], uint32_t q, const uint32_t b[8]) {
-  uint64_t carry = 0;
-  uint32_t borrow = 0;
+  uint32_t b1 = 0, b2 = 0, hi = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    const uint64_t p = (uint64_t)q * b[i] + carry;
-    carry = p >> 32;
-    const uint64_t d = (uint64_t)a[i] - (uint32_t)p - borrow;
-    r[i] = (uint32_t)d;
-    borrow = (uint32_t)(d >> 63);
+    const uint64_t p = (uint64_t)q * b[i];
+    const uint32_t t = subb32(a[i], (uint32_t)p, b1, b1);
+    r[i] = subb32(t, hi, b2, b2);
+    hi = (uint32_t)(p >> 32);
   }
-  return (carry + borrow) != 0;
+  return (hi | b1 | b2) != 0;
 }
 
 // r += b; returns the carry out.
 TMED_HD uint32_t words8_add(uint32_t r[8], const uint32_t b[8]) {
-  uint64_t c = 0;
+  uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint64_t t = (uint64_t)r[i] + b[i] + c;
-    r[i] = (uint32_t)t;
-    c = t >> 32;
-  }
-  return (uint32_t)c;
+  for (int i = 0; i < 8; i++) r[i] = addc32(r[i], b[i], c, c);
+  return c;
 }
 
 // r -= b; returns the borrow out.
 TMED_HD uint32_t words8_sub(uint32_t r[8], const uint32_t b[8]) {
   uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint64_t d = (uint64_t)r[i] - b[i] - borrow;
-    r[i] = (uint32_t)d;
-    borrow = (uint32_t)(d >> 63);
-  }
+  for (int i = 0; i < 8; i++) r[i] = subb32(r[i], b[i], borrow, borrow);
   return borrow;
 }
 
@@ -106,20 +124,70 @@ TMED_HD bool words8_ge(const uint32_t a[8], const uint32_t b[8]) {
   return words8_sub(t, b) == 0;
 }
 
-// Magnitudes of the cofactors t_i (< 2^160): r = a + q*b (5 words).
+// Magnitudes of the cofactors t_i (< 2^160): r = a + q*b (5 words, carry out dropped).
 constexpr int kHsTW = 5;
 TMED_HD void words5_muladd(uint32_t r[kHsTW], const uint32_t a[kHsTW], uint32_t q, const uint32_t b[kHsTW]) {
-  uint64_t c = 0;
+  uint32_t c1 = 0, c2 = 0, hi = 0;
 #pragma unroll
   for (int i = 0; i < kHsTW; i++) {
-    const uint64_t t = (uint64_t)q * b[i] + a[i] + c;
-    r[i] = (uint32_t)t;
-    c = t >> 32;
+    const uint64_t p = (uint64_t)q * b[i];
+    const uint32_t t = addc32(a[i], (uint32_t)p, c1, c1);
+    r[i] = addc32(t, hi, c2, c2);
+    hi = (uint32_t)(p >> 32);
+  }
+}
+
+// floor(x / y) to within one (x, y > 0, quotient < 2^32): on the device a reciprocal with one
+// Newton step (relative error ~2^-50, against ~2^-52 for the IEEE division it replaces, whose
+// scale / fixup sequence is twice as long); the caller corrects the floor exactly.
+TMED_HD double quot_estimate(double x, double y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r = __builtin_amdgcn_rcp(y);
+  r = fma(r, fma(-y, r, 1.0), r);
+  return floor(x * r);
+#else
+  return floor(x / y);
+#endif
+}
+
+TMED_HD bool words8_high_zero(const uint32_t x[8]) { return (x[4] | x[5] | x[6] | x[7]) == 0; }  // x < 2^128
+
+// One exact Euclid step in place: q = floor(x / y) (x > y), x <- x - q y, tx <- tx + q ty,
+// fx <- double(x).  fx, fy approximate x, y to double precision, so the estimate floor(fx / fy)
+// is off by at most one for q < 2^32; it is corrected exactly (the y-subtraction / comparison
+// runs only when the remainder came out negative, or within 2^-30 of y).  Sets fail when q is
+// out of range or the estimate was off by more.
+TMED_HD void hs_euclid_step(uint32_t x[8], const uint32_t y[8], uint32_t tx[kHsTW], const uint32_t ty[kHsTW],
+                            double &fx, double fy, bool &fail) {
+  const double qd = quot_estimate(fx, fy);
+  if (!(qd < 4294967294.0)) { fail = true; return; }
+  const uint32_t q = (uint32_t)qd;
+  const bool neg = words8_submul(x, x, q, y);  // x - q y (wrapped mod 2^256 when negative)
+  words5_muladd(tx, tx, q, ty);
+  if (neg) {  // q one too high
+    if (words8_add(x, y) == 0) fail = true;    // still negative: the estimate was off by more
+    uint32_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < kHsTW; i++) tx[i] = subb32(tx[i], ty[i], borrow, borrow);  // tx -= ty
+  }
+  fx = words_to_double(x, 8);
+  if (!neg && fx >= fy * (1.0 - 0x1p-30) && words8_ge(x, y)) {  // q one too low
+    words8_sub(x, y);
+    uint32_t cy = 0;
+#pragma unroll
+    for (int i = 0; i < kHsTW; i++) tx[i] = addc32(tx[i], ty[i], cy, cy);  // tx += ty
+    if (words8_ge(x, y)) fail = true;
+    fx = words_to_double(x, 8);
   }
 }
 
 // Half-size decomposition of k (< L): c >= 0, |d| = dm odd, dneg = (d < 0), c = d k mod 8L.
 // Returns the radix-16 window count the pair needs (29..64; 64 for the (k, 1) fallback).
+// The Euclid phase runs two in-place steps per iteration (the remainders and cofactors swap
+// roles instead of being moved: the round-1 loop spent ~300 instructions a step, ~0.5 ms per
+// 2^20 signatures, mostly register moves and control flow).  FAST = false: that round-1 loop,
+// kept as the reference of tests/test_kernel_host.py.
+template <bool FAST = true>
 TMED_HD int sc_halfsize(uint32_t c[8], uint32_t dm[8], bool &dneg, const uint32_t k[8]) {
   uint32_t a[8], b[8], ta[kHsTW], tb[kHsTW], nb[8], nt[kHsTW];
   sc_const_8L(a);
@@ -129,8 +197,29 @@ TMED_HD int sc_halfsize(uint32_t c[8], uint32_t dm[8], bool &dneg, const uint32_
   for (int i = 0; i < kHsTW; i++) { ta[i] = 0; tb[i] = i == 0 ? 1u : 0u; }
   double fa = words_to_double(a, 8), fb = words_to_double(b, 8);
   bool fail = false, iodd = true;  // i = 1: b = r_1 = k, t_1 = +1
+  if (FAST) {
+    int steps = 0;
+    bool swapped = false;  // the last step left r_i in a (roles of a/b and ta/tb exchanged)
 #pragma unroll 1
-  for (int it = 0; it < 190; it++) {
+    for (int it = 0; it < 96 && !fail; it++) {
+      if (words8_high_zero(b)) break;
+      hs_euclid_step(a, b, ta, tb, fa, fb, fail);  // a <- r_{i+1}
+      steps++;
+      if (fail || words8_high_zero(a)) { swapped = true; break; }
+      hs_euclid_step(b, a, tb, ta, fb, fa, fail);  // b <- r_{i+2}
+      steps++;
+    }
+    if (swapped) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) { const uint32_t t = a[i]; a[i] = b[i]; b[i] = t; }
+#pragma unroll
+      for (int i = 0; i < kHsTW; i++) { const uint32_t t = ta[i]; ta[i] = tb[i]; tb[i] = t; }
+      const double t = fa; fa = fb; fb = t;
+    }
+    if (steps & 1) iodd = !iodd;
+  }
+#pragma unroll 1
+  for (int it = 0; it < (FAST ? 0 : 190); it++) {
     if ((b[4] | b[5] | b[6] | b[7]) == 0) break;  // r_i < 2^128
     const double qd = floor(fa / fb);
     if (!(qd < 4294967294.0)) { fail = true; break; }
@@ -249,7 +338,7 @@ TMED_HD void words4_shl16(uint32_t x[4]) {
 // Q = [e]B + [c](-A) + [|d|](-sign(d) R) over W radix-16 windows (Straus, most significant
 // first).  DS: cword(w) / dword(w), word w (0..7) of the recoded c / |d| — read once per
 // eight windows, before the doublings that hide the read.  TA / TR: per-lane cached tables
-// of j*(-A) and j*(-sign(d) R), j = 0..8 (build_table_negA), prefetch(j) / take(ge_cached&).
+// of j*(-A) and j*(-sign(d) R), j = 0..8 (build_table_affine), prefetch(j) / take(ge_cached&).
 // BL / BH: niels tables of j*B and j*2^128*B, j = 0..32768, prefetch(j) / take(ge_niels&);
 // the 16-bit digits of e (er, recoded) are added at windows 28, 24, ..., 0 (16 doublings
 // apart): low-table digit m and high-table digit m + 8 at window 4m, each entry prefetched
@@ -324,17 +413,20 @@ TMED_HD void hs_straus(ge_p2 &out, const DS &ds, const uint32_t er[8], int W, TA
 TMED_HD bool p2_is_identity(const ge_p2 &q) { return fe_iszero(q.X) && fe_equal(q.Y, q.Z) && !fe_iszero(q.Z); }
 
 // Phase 2 of the half-size path: tables of -A and -sign(d) R, the 3-point sum, the
-// identity test.  A: extended (T set); R: affine (x, y).
+// identity test.  A: affine extended (Z = 1, T set); R: affine (x, y).
 template <class DS, class TA, class TR, class BL, class BH>
 TMED_HD bool verify_main_hs(const DS &ds, bool dneg, const uint32_t er[8], int W, const ge_p3 &A, const fe &Rx,
                             const fe &Ry, TA &ta, TR &tr, BL &bl, BH &bh) {
-  build_table_negA(ta, A);
-  ge_p3 R;
-  if (dneg) fe_neg(R.X, Rx); else fe_copy(R.X, Rx);
-  fe_copy(R.Y, Ry);
-  fe_1(R.Z);
-  fe_mul(R.T, R.X, R.Y);
-  build_table_negA(tr, R);
+  ge_p3 P;  // -A (affine: the decoded key)
+  fe_neg(P.X, A.X);
+  fe_copy(P.Y, A.Y);
+  fe_1(P.Z);
+  fe_neg(P.T, A.T);
+  build_table_affine(ta, P);
+  if (dneg) fe_copy(P.X, Rx); else fe_neg(P.X, Rx);  // -sign(d) R (affine)
+  fe_copy(P.Y, Ry);
+  fe_mul(P.T, P.X, P.Y);
+  build_table_affine(tr, P);
   ge_p2 q;
   hs_straus(q, ds, er, W, ta, tr, bl, bh);
   return p2_is_identity(q);

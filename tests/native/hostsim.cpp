@@ -173,17 +173,25 @@ void hostsim_verify_batch_hs(const uint8_t *pub, const uint8_t *sig, const uint8
 }
 
 // The lattice step alone: c, |d| (32-byte LE each), dneg, window count.
-int hostsim_halfsize(const uint8_t *k32, uint8_t *c32, uint8_t *d32, int *dneg) {
+int hostsim_halfsize_impl(const uint8_t *k32, uint8_t *c32, uint8_t *d32, int *dneg, int fast) {
   uint32_t k[8], c[8], dm[8];
   load_words8(k, k32);
   bool neg;
-  const int W = sc_halfsize(c, dm, neg, k);
+  const int W = fast ? sc_halfsize<true>(c, dm, neg, k) : sc_halfsize<false>(c, dm, neg, k);
   for (int i = 0; i < 32; i++) {
     c32[i] = (uint8_t)(c[i / 4] >> (8 * (i % 4)));
     d32[i] = (uint8_t)(dm[i / 4] >> (8 * (i % 4)));
   }
   *dneg = neg ? 1 : 0;
   return W;
+}
+
+int hostsim_halfsize(const uint8_t *k32, uint8_t *c32, uint8_t *d32, int *dneg) {
+  return hostsim_halfsize_impl(k32, c32, d32, dneg, 1);
+}
+
+int hostsim_halfsize_plain(const uint8_t *k32, uint8_t *c32, uint8_t *d32, int *dneg) {
+  return hostsim_halfsize_impl(k32, c32, d32, dneg, 0);
 }
 
 void hostsim_verify_batch(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,

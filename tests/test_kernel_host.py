@@ -215,3 +215,23 @@ def test_halfsize_torsion_keys(hostsim):
     out = _verify(hostsim, P, Sg, M, offs, "hs")
     assert (out == np.array(exp, np.uint8)).all()
     assert 0 < sum(exp) < n
+
+
+def test_halfsize_fast_euclid_equals_reference_loop(hostsim):
+    """verify_hs.h's two-steps-per-iteration Euclid phase (in-place, roles swapping) must stop at
+    exactly the same remainder as the round-1 loop, so (c, d, W) are equal on every k — random k
+    and the boundary values of the lattice test."""
+    L = E.L
+    rng = random.Random(11)
+    ks = [0, 1, 2, 3, 8, 16, L - 1, L - 2, 2**127, 2**128 - 1, 2**128, 2**128 + 1, 2**160, 2**200,
+          2**252 - 1, 5 * 2**128 + 3, (8 * L) // 3, (8 * L) // 5 + 1]
+    ks += [rng.randrange(L) for _ in range(6000)]
+    ks += [rng.randrange(2**129) for _ in range(300)] + [rng.randrange(2**170) for _ in range(300)]
+    for k in ks:
+        out = []
+        for fn in (hostsim.hostsim_halfsize, hostsim.hostsim_halfsize_plain):
+            c, d = ctypes.create_string_buffer(32), ctypes.create_string_buffer(32)
+            neg = ctypes.c_int()
+            W = fn(k.to_bytes(32, "little"), c, d, ctypes.byref(neg))
+            out.append((W, c.raw, d.raw, neg.value))
+        assert out[0] == out[1], k
