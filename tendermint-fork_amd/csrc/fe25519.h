@@ -244,6 +244,54 @@ TMED_HD void fe_to_words(uint32_t w[8], const fe &f) {
   for (int i = 0; i < 8; i++) w[i] = (uint32_t)acc[i];
 }
 
+// 256-bit storage form (the main kernel's per-lane tables: one 128-B line per cached point).
+// Input: at most a 2-sum of carried values.  Limb 9 is first floor-carried with the
+// 2^255 = 19 wrap (limb 9 in [0, 2^25), limb 0 grows by 19 * {-2..0}), then one floor-carry pass
+// over limbs 0..8 without a wrap: limbs 0..8 end in [0, 2^26) / [0, 2^25) and limb 9 keeps that
+// pass's carry (limb 9 in [-2, 2^25], 26 bits signed): 5*26 + 4*25 + 26 = 256 bits, at the same
+// bit offsets as fe_from_words.  The value changes by a multiple of p only.
+TMED_HD void fe_pack256(uint32_t w[8], const fe &f) {
+  int32_t h[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) h[i] = f.v[i];
+  {
+    const int32_t c = h[9] >> 25;
+    h[9] -= (int32_t)((uint32_t)c << 25);
+    h[0] += mul19(c);
+  }
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int s = (i & 1) ? 25 : 26;
+    const int32_t c = h[i] >> s;
+    h[i] -= (int32_t)((uint32_t)c << s);
+    h[i + 1] += c;
+  }
+  const uint32_t *u = reinterpret_cast<const uint32_t *>(h);
+  w[0] = u[0] | (u[1] << 26);
+  w[1] = (u[1] >> 6) | (u[2] << 19);
+  w[2] = (u[2] >> 13) | (u[3] << 13);
+  w[3] = (u[3] >> 19) | (u[4] << 6);
+  w[4] = u[5] | (u[6] << 25);
+  w[5] = (u[6] >> 7) | (u[7] << 19);
+  w[6] = (u[7] >> 13) | (u[8] << 12);
+  w[7] = (u[8] >> 20) | (u[9] << 6);
+}
+
+// Inverse of fe_pack256 (field extraction only, no carry): limbs at most twice a carried limb,
+// inside the mul / sq operand bound of a 2-sum.
+TMED_HD void fe_unpack256(fe &h, const uint32_t w[8]) {
+  h.v[0] = (int32_t)(w[0] & 0x3ffffffu);
+  h.v[1] = (int32_t)(((w[0] >> 26) | (w[1] << 6)) & 0x1ffffffu);
+  h.v[2] = (int32_t)(((w[1] >> 19) | (w[2] << 13)) & 0x3ffffffu);
+  h.v[3] = (int32_t)(((w[2] >> 13) | (w[3] << 19)) & 0x1ffffffu);
+  h.v[4] = (int32_t)(w[3] >> 6);
+  h.v[5] = (int32_t)(w[4] & 0x1ffffffu);
+  h.v[6] = (int32_t)(((w[4] >> 25) | (w[5] << 7)) & 0x3ffffffu);
+  h.v[7] = (int32_t)(((w[5] >> 19) | (w[6] << 13)) & 0x1ffffffu);
+  h.v[8] = (int32_t)(((w[6] >> 12) | (w[7] << 20)) & 0x3ffffffu);
+  h.v[9] = (int32_t)w[7] >> 6;
+}
+
 TMED_HD bool fe_isnegative(const fe &f) {
   uint32_t w[8];
   fe_to_words(w, f);

@@ -8,7 +8,7 @@
 // Memory layout
 //   pub   n x 32 B, sig n x 64 B (16-B aligned rows -> dwordx4 loads)
 //   msgs  concatenated bytes, off[n+1] u32 (or fixed 256-B vote slots)
-//   slab  per-lane variable-base tables: 9 cached points x 160 B, lane-major [slot][entry][chunk]
+//   slab  per-lane variable-base tables: 9 cached points x 128 B (fe_pack256), lane-major [slot][entry][chunk]
 //   b16   32769 niels multiples of B in 128-B rows in HBM (4.2 MB; the full-length fallback, variant 5)
 //   combs key-set combs [key][window][entry] and the shared combs of B (radix 256, radix 2^16)
 #include "kernels.h"
@@ -17,39 +17,37 @@
 
 namespace tmed {
 
-// Per-lane table in the HBM slab, lane-major [slot][entry][chunk]: each lane's 160-B entry is
-// contiguous, so a divergent lookup reads whole lines (+3.7 % over the slot-interleaved
-// [entry][chunk][slot] layout, profiles/r01/variants.txt).
+// Per-lane table in the HBM slab, lane-major [slot][entry][chunk]: each lane's entry is one
+// aligned 128-B line (the four coordinates in fe_pack256 form), so a divergent lookup reads
+// exactly one line.  The slab does not fit L2/MALL at full occupancy; the 160-B int32 form
+// read 2.25 lines per lookup, and its traffic cost ~10 % of the clock (profiles/r02/s4).
 struct SlabTab {
   int4 *base;
   uint32_t slot;
 
-  __device__ __forceinline__ size_t idx(int j, int q) const { return ((size_t)slot * 9 + j) * 10 + q; }
+  __device__ __forceinline__ size_t idx(int j, int q) const { return ((size_t)slot * 9 + j) * 8 + q; }
 
   __device__ __forceinline__ void store(int j, const ge_cached &c) const {
     const fe *fs[4] = {&c.YpX, &c.YmX, &c.Z, &c.T2d};
 #pragma unroll
-    for (int q = 0; q < 10; q++) {
-      int32_t w[4];
-#pragma unroll
-      for (int e = 0; e < 4; e++) {
-        const int f = 4 * q + e;
-        w[e] = fs[f / 10]->v[f % 10];
-      }
-      base[idx(j, q)] = make_int4(w[0], w[1], w[2], w[3]);
+    for (int f = 0; f < 4; f++) {
+      uint32_t w[8];
+      fe_pack256(w, *fs[f]);
+      base[idx(j, 2 * f)] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+      base[idx(j, 2 * f + 1)] = make_int4((int)w[4], (int)w[5], (int)w[6], (int)w[7]);
     }
   }
   __device__ __forceinline__ void load(int j, ge_cached &c) const {
     fe *fs[4] = {&c.YpX, &c.YmX, &c.Z, &c.T2d};
+    int4 v[8];
 #pragma unroll
-    for (int q = 0; q < 10; q++) {
-      const int4 v = base[idx(j, q)];
-      const int32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (int q = 0; q < 8; q++) v[q] = base[idx(j, q)];
 #pragma unroll
-      for (int e = 0; e < 4; e++) {
-        const int f = 4 * q + e;
-        fs[f / 10]->v[f % 10] = w[e];
-      }
+    for (int f = 0; f < 4; f++) {
+      const uint32_t w[8] = {(uint32_t)v[2 * f].x, (uint32_t)v[2 * f].y, (uint32_t)v[2 * f].z,
+                             (uint32_t)v[2 * f].w, (uint32_t)v[2 * f + 1].x, (uint32_t)v[2 * f + 1].y,
+                             (uint32_t)v[2 * f + 1].z, (uint32_t)v[2 * f + 1].w};
+      fe_unpack256(*fs[f], w);
     }
   }
   int pf = 0;
@@ -352,7 +350,7 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_hs_kernel(
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const HsDigitsDev ds{prep2, stride, slot};
   SlabTab ta{slab, slot};
-  SlabTab tr{slab + (size_t)stride * 90, slot};
+  SlabTab tr{slab + (size_t)stride * 72, slot};
   B16Pf bl{comb16, sbl[wv], lane};
   B16Pf bh{comb16 + (size_t)8 * kB16Entries * kCombEntryInt4, sbh[wv], lane};
   const bool id = verify_main_hs(ds, (flags & 2) != 0, er, W, A, Rx, Ry, ta, tr, bl, bh);

@@ -369,6 +369,22 @@ void hostsim_fe_op(int op, const uint8_t *a, const uint8_t *b, uint8_t *out) {
   to_bytes(out, wo);
 }
 
+// fe_pack256 / fe_unpack256 on raw limbs (the main kernel's table storage form): unpacked limbs
+// out, and the product of the unpacked value with the carried g (32-byte LE) as a canonical encoding.
+void hostsim_pack256(const int32_t *limbs, const uint8_t *g, int32_t *out_limbs, uint8_t *prod) {
+  fe f, u, gf, o;
+  for (int i = 0; i < 10; i++) f.v[i] = limbs[i];
+  uint32_t w[8], wg[8], wo[8];
+  fe_pack256(w, f);
+  fe_unpack256(u, w);
+  for (int i = 0; i < 10; i++) out_limbs[i] = u.v[i];
+  load_words8(wg, g);
+  fe_from_words(gf, wg);
+  fe_mul(o, u, gf);
+  fe_to_words(wo, o);
+  to_bytes(prod, wo);
+}
+
 int hostsim_decode(const uint8_t *p, uint8_t *out_enc) {
   uint32_t w[8], e[8];
   load_words8(w, p);

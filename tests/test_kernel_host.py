@@ -38,6 +38,40 @@ def test_field_ops_vs_bigint(hostsim):
                 assert _fe(hostsim, op, a, b) == e, (op, hex(a), hex(b))
 
 
+def test_pack256_roundtrip_at_the_limb_extremes(hostsim):
+    """fe_pack256 / fe_unpack256 (the 128-B per-lane table entries of verify_main_hs_kernel):
+    for 2-sums of carried values at the ends of their limb ranges, the unpacked value is congruent
+    mod p, its limbs sit in [0, 2^26) / [0, 2^25) (limb 9 in [-2, 2^25]), and it multiplies
+    correctly as a fe_mul operand."""
+    P = E.P
+    off = [0, 26, 51, 77, 102, 128, 153, 179, 204, 230]
+    # carried ranges (fe_carry64): even [-2^25, 2^25), odd [-2^24, 2^24), limbs 1 and 5 one wider
+    lo = [-(2**25) if i % 2 == 0 else -(2**24) for i in range(10)]
+    hi = [2**25 - 1 if i % 2 == 0 else 2**24 - 1 for i in range(10)]
+    lo[1] -= 1; lo[5] -= 1; hi[1] += 1; hi[5] += 1
+    rng = random.Random(5)
+    cases = [[2 * lo[i] for i in range(10)], [2 * hi[i] for i in range(10)], [0] * 10,
+             [2 * lo[i] if i % 2 else 2 * hi[i] for i in range(10)], [2 * hi[i] if i % 2 else 2 * lo[i] for i in range(10)]]
+    for i in range(10):
+        for v in (2 * lo[i], 2 * hi[i]):
+            c = [0] * 10
+            c[i] = v
+            cases.append(c)
+    cases += [[rng.randint(2 * lo[i], 2 * hi[i]) for i in range(10)] for _ in range(800)]
+    g = rng.randrange(P)
+    out = (ctypes.c_int32 * 10)()
+    prod = ctypes.create_string_buffer(32)
+    for c in cases:
+        hostsim.hostsim_pack256((ctypes.c_int32 * 10)(*c), g.to_bytes(32, "little"), out, prod)
+        val = sum(x << o for x, o in zip(c, off))
+        u = list(out)
+        for i in range(9):
+            assert 0 <= u[i] < (2**25 if i % 2 else 2**26), (c, u)
+        assert -2 <= u[9] <= 2**25, (c, u)
+        assert sum(x << o for x, o in zip(u, off)) % P == val % P
+        assert int.from_bytes(prod.raw, "little") == val * g % P
+
+
 def test_sha512_and_reduce(hostsim):
     rng = random.Random(5)
     for n in [0, 1, 17, 111, 112, 113, 127, 128, 129, 200, 239, 240, 241, 300, 400]:
