@@ -129,6 +129,8 @@ struct tmed_ctx {
   int main_waves = 6;     // main-kernel path (6: half-size scalars, verify_hs.h; 5: full-length Straus + finish); env TMED_MAIN_WAVES
   uint32_t lat_max = 24576;  // key-cached batches up to this size take the latency kernels (crossover ~32k,
                              // profiles/r01/session3/lat_sweep.jsonl); env TMED_LAT_MAX
+  int4 *d_glat = nullptr;    // generic latency mode hand-off (kGLatHandBytes)
+  uint32_t glat_max = 4096;  // generic batches up to this size take the latency kernels; env TMED_GLAT_MAX
   bool timing = false;    // tmed_set_kernel_timing
   uint32_t last_hs_count = 0;  // signatures of the last half-size chunk in d_prep (tmed_window_stats)
   tmed::KernelTimer timer;
@@ -166,6 +168,20 @@ inline uint32_t last_chunk_count(uint32_t n, uint32_t chunk) {
   if (n == 0) return 0;
   const uint32_t m = n - (n - 1) / kFinCap * kFinCap;
   return m - (m - 1) / chunk * chunk;
+}
+// A generic (uncached-key) batch on stream s: the latency kernels (latency.hip) up to
+// c->glat_max signatures, the throughput pipeline above.  Inside a scratch_acquire/release pair.
+inline hipError_t generic_verify(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs,
+                                 const uint32_t *off, uint32_t n, uint8_t *out, hipStream_t s, bool msg_slots,
+                                 KernelTimer *timer) {
+  if (n <= c->glat_max) {
+    c->last_hs_count = 0;  // no half-size hand-off in d_prep (tmed_window_stats)
+    return launch_verify_glat(pub, sig, msgs, off, n, out, c->d_bcomb16, c->d_glat, s, msg_slots, timer);
+  }
+  hipError_t e = launch_verify(pub, sig, msgs, off, n, out, c->d_slab, c->slab_slots, BTabs{c->d_b16, c->d_bcomb16},
+                               c->d_prep, c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves, msg_slots, timer);
+  c->last_hs_count = (e != hipSuccess || c->main_waves == 5) ? 0 : last_chunk_count(n, c->chunk);
+  return e;
 }
 inline hipError_t scratch_release(tmed_ctx *c, hipStream_t s) {
   c->scratch_foreign = s != c->stream;

@@ -103,6 +103,14 @@ hipError_t launch_verify_keyset_lat(const uint32_t *val_idx, const uint8_t *key_
                                     const uint32_t *off, uint32_t n, uint8_t *out, int4 *fin, int4 *dec,
                                     hipStream_t stream, bool msg_slots = false);
 
+// Latency mode of the generic path (latency.hip; n <= kGLatMax): decode / hash roles, then
+// 8 lanes per signature (two quads, 4-way point formulas).  hand: kGLatHandBytes of scratch.
+constexpr uint32_t kGLatMax = 1u << 16;
+constexpr size_t kGLatHandBytes = (size_t)kGLatMax * (6 * 2 + 7) * 16;
+hipError_t launch_verify_glat(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
+                              uint32_t n, uint8_t *out, const int4 *comb16, int4 *hand, hipStream_t stream,
+                              bool msg_slots = false, KernelTimer *timer = nullptr);
+
 // f1: on-device CanonicalVote assembly.  Templates are kVoteTmplBytes records
 // ([pre_len, bid_len, cid_len, 0] + bytes); message i is written to out + i * kVoteSlot
 // and its length to out_len[i].  With msg_slots = true the verify launchers read

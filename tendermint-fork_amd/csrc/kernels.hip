@@ -14,6 +14,7 @@
 #include "kernels.h"
 #include "verify_core.h"
 #include "verify_hs.h"
+#include "kernel_util.h"
 
 namespace tmed {
 
@@ -122,35 +123,6 @@ __device__ __forceinline__ bool prep_load(const int4 *prep, uint32_t stride, uin
   fe_mul(A.T, A.X, A.Y);
   return w[36] != 0;
 }
-
-__device__ __forceinline__ void load_row_words(uint32_t *w, const uint8_t *p, int nwords16) {
-  const uint4 *q = reinterpret_cast<const uint4 *>(p);
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    if (i < nwords16) {
-      const uint4 v = q[i];
-      w[4 * i + 0] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
-    }
-  }
-}
-
-// Where message i lives: packed (off[i] .. off[i+1]) or fixed-stride slots written by
-// the on-device vote assembler (msgs + i * kVoteSlot, length len[i]).
-struct MsgSrc {
-  const uint8_t *msgs;
-  const uint32_t *off;  // packed mode (len == nullptr): n + 1 offsets; slot mode: lengths
-  bool slots;
-  __device__ __forceinline__ void get(uint32_t i, const uint8_t *&p, uint32_t &len) const {
-    if (slots) {
-      p = msgs + (size_t)i * kVoteSlot;
-      len = off[i];
-    } else {
-      const uint32_t o0 = off[i], o1 = off[i + 1];
-      p = msgs + o0;
-      len = o1 - o0;
-    }
-  }
-};
 
 // Phase 1: SHA-512(R||A||M) mod L, S < L, A = Point.SetBytes(pub)  (one lane per signature
 // of the chunk [base, base + count)).

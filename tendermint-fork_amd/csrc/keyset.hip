@@ -123,9 +123,8 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
       e = keyset_verify(c, *st.ks, (const uint32_t *)(d + st.o_key), d + st.o_sig, (const uint8_t *)vs.d_vmsg.p,
                         (const uint32_t *)vs.d_off.p, m, (uint8_t *)vs.d_out.p, s, /*msg_slots=*/true);
     else
-      e = launch_verify(d + st.o_key, d + st.o_sig, (const uint8_t *)vs.d_vmsg.p, (const uint32_t *)vs.d_off.p, m,
-                        (uint8_t *)vs.d_out.p, c->d_slab, c->slab_slots, BTabs{c->d_b16, c->d_bcomb16}, c->d_prep, c->d_fin,
-                        c->d_fin_pre, s, c->chunk, c->main_waves, /*msg_slots=*/true);
+      e = generic_verify(c, d + st.o_key, d + st.o_sig, (const uint8_t *)vs.d_vmsg.p, (const uint32_t *)vs.d_off.p, m,
+                         (uint8_t *)vs.d_out.p, s, /*msg_slots=*/true, nullptr);
   }
   if (e == hipSuccess) e = hipEventRecord(vs.ev1, s);
   if (e == hipSuccess) e = scratch_release(c, s);

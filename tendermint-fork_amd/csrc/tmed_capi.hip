@@ -76,11 +76,14 @@ int tmed_init(int device, tmed_ctx **out) {
   if (const char *v = getenv("TMED_MAIN_WAVES")) c->main_waves = atoi(v) == 5 ? 5 : 6;
   if (const char *v = getenv("TMED_LAT_MAX")) c->lat_max = (uint32_t)strtoul(v, nullptr, 10);
   if (c->lat_max > kLatMax) c->lat_max = kLatMax;
+  if (const char *v = getenv("TMED_GLAT_MAX")) c->glat_max = (uint32_t)strtoul(v, nullptr, 10);
+  if (c->glat_max > kGLatMax) c->glat_max = kGLatMax;
   if (e == hipSuccess)
     e = hipMalloc((void **)&c->d_slab, (size_t)c->slab_slots * kSlabSlotBytes * slab_tables(c->main_waves));
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_prep, (size_t)c->slab_slots * kPrepSlotBytes);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_fin, kFinBytes);          // 128 MB: projective R'
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_fin_pre, kFinPreBytes);   // 48 MB: prefix products
+  if (e == hipSuccess) e = hipMalloc((void **)&c->d_glat, kGLatHandBytes);     // 20 MB: latency-mode hand-off
   // Shared signed radix-256 comb of +B (528 KB, L2-resident) for the key-cached path.
   uint8_t *d_bpub = nullptr, *d_bok = nullptr;
   const uint8_t benc[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
@@ -142,6 +145,7 @@ void tmed_destroy(tmed_ctx *c) {
   if (c->d_prep) hipFree(c->d_prep);
   if (c->d_fin) hipFree(c->d_fin);
   if (c->d_fin_pre) hipFree(c->d_fin_pre);
+  if (c->d_glat) hipFree(c->d_glat);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -191,10 +195,8 @@ int tmed_verify_batch_device(tmed_ctx *c, const uint8_t *d_pub, const uint8_t *d
   if (c->timing) c->timer.n = 0;
   hipError_t e = scratch_acquire(c, s);
   if (e == hipSuccess)
-    e = launch_verify(d_pub, d_sig, d_msgs, d_off, (uint32_t)n, d_out, c->d_slab, c->slab_slots, BTabs{c->d_b16, c->d_bcomb16}, c->d_prep,
-                      c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves, false, c->timing ? &c->timer : nullptr);
+    e = generic_verify(c, d_pub, d_sig, d_msgs, d_off, (uint32_t)n, d_out, s, false, c->timing ? &c->timer : nullptr);
   if (e == hipSuccess) e = scratch_release(c, s);
-  if (e == hipSuccess) c->last_hs_count = c->main_waves == 5 ? 0 : last_chunk_count((uint32_t)n, c->chunk);
   return map_err(e);
 }
 
@@ -268,15 +270,13 @@ int tmed_verify_batch(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, const
   if (e == hipSuccess) e = scratch_acquire(c, s);
   if (e == hipSuccess) e = hipEventRecord(c->ev0, s);
   if (e == hipSuccess)
-    e = launch_verify((const uint8_t *)c->d_a.p, (const uint8_t *)c->d_b.p, (const uint8_t *)c->d_msg.p,
-                      (const uint32_t *)c->d_off.p, (uint32_t)n, (uint8_t *)c->d_out.p, c->d_slab, c->slab_slots,
-                      BTabs{c->d_b16, c->d_bcomb16}, c->d_prep, c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves);
+    e = generic_verify(c, (const uint8_t *)c->d_a.p, (const uint8_t *)c->d_b.p, (const uint8_t *)c->d_msg.p,
+                       (const uint32_t *)c->d_off.p, (uint32_t)n, (uint8_t *)c->d_out.p, s, false, nullptr);
   if (e == hipSuccess) e = hipEventRecord(c->ev1, s);
   if (e == hipSuccess) e = scratch_release(c, s);
   if (e == hipSuccess) e = hipMemcpyAsync(c->h_out.p, c->d_out.p, n, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return map_err(e);
-  c->last_hs_count = c->main_waves == 5 ? 0 : last_chunk_count((uint32_t)n, c->chunk);
   hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
   memcpy(out, c->h_out.p, n);
   if (sig_lens)

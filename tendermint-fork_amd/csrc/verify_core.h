@@ -532,14 +532,20 @@ TMED_HD void ge_p3_add(ge_p3 &acc, const ge_p3 &o) {
 
 // Strict decode of R (the set of byte strings Point.Bytes can produce): false unless R is
 // a canonical encoding of a curve point; then (x, y) is that point.
-TMED_HD bool r_decode_strict(fe &x, fe &y, const uint32_t Rw[8]) {
+// The checks strict decoding adds to Point.SetBytes for the encoding Rw of a decoded point
+// with x-coordinate X: y < p, and not x = 0 with the sign bit set.
+TMED_HD bool r_strict_extra(const fe &X, const uint32_t Rw[8]) {
   bool ones = (Rw[7] & 0x7fffffffu) == 0x7fffffffu;
 #pragma unroll
   for (int i = 1; i < 7; i++) ones = ones && Rw[i] == 0xffffffffu;
   const bool canonical = !(ones && Rw[0] >= 0xffffffedu);  // y < p = 2^255 - 19
+  return canonical && !(fe_iszero(X) && (Rw[7] >> 31) != 0);
+}
+
+TMED_HD bool r_decode_strict(fe &x, fe &y, const uint32_t Rw[8]) {
   ge_p3 P;
   bool ok = ge_frombytes_go(P, Rw);
-  ok = ok && canonical && !(fe_iszero(P.X) && (Rw[7] >> 31) != 0);
+  ok = ok && r_strict_extra(P.X, Rw);
   fe_copy(x, P.X);
   fe_copy(y, P.Y);
   return ok;

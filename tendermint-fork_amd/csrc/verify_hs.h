@@ -282,15 +282,11 @@ TMED_HD int sc_halfsize(uint32_t c[8], uint32_t dm[8], bool &dneg, const uint32_
   return W < 29 ? 29 : W;
 }
 
-// Phase 1b of the half-size path (after verify_prep's hash / S check / decode of A): strict
-// decode of R, the lattice step and e = d S mod L.  Writes the recoded scalars — cr, dr:
-// signed radix-16 (sc_recode16; dr words 5..7 are 0x88888888, i.e. zero digits, since
-// |d| < 2^150), er: signed radix-2^16 — R (affine; the identity when it does not decode)
-// and the window count; returns the R verdict.
-TMED_HD bool hs_prep_r(const uint32_t k[8], const uint32_t s[8], const uint32_t Rw[8], uint32_t cr[8],
-                       uint32_t dr[8], uint32_t er[8], bool &dneg, fe &Rx, fe &Ry, int &W) {
-  const bool rok = r_decode_strict(Rx, Ry, Rw);
-  if (!rok) { fe_0(Rx); fe_1(Ry); }
+// The scalar half of phase 1b: the lattice step and e = d S mod L.  Writes the recoded
+// scalars — cr, dr: signed radix-16 (sc_recode16; dr words 5..7 are 0x88888888, i.e. zero
+// digits, since |d| < 2^150), er: signed radix-2^16 — and the window count W.
+TMED_HD void hs_scalars(const uint32_t k[8], const uint32_t s[8], uint32_t cr[8], uint32_t dr[8], uint32_t er[8],
+                        bool &dneg, int &W) {
   uint32_t c[8], dm[8], e[8];
   W = sc_halfsize(c, dm, dneg, k);
   uint32_t zero[8];
@@ -310,6 +306,16 @@ TMED_HD bool hs_prep_r(const uint32_t k[8], const uint32_t s[8], const uint32_t 
   sc_recode16(cr, c);
   sc_recode16(dr, dm);
   sc_recode_b<16>(er, e);
+}
+
+// Phase 1b of the half-size path (after verify_prep's hash / S check / decode of A): strict
+// decode of R (affine; the identity when it does not decode) and hs_scalars; returns the R
+// verdict.
+TMED_HD bool hs_prep_r(const uint32_t k[8], const uint32_t s[8], const uint32_t Rw[8], uint32_t cr[8],
+                       uint32_t dr[8], uint32_t er[8], bool &dneg, fe &Rx, fe &Ry, int &W) {
+  const bool rok = r_decode_strict(Rx, Ry, Rw);
+  if (!rok) { fe_0(Rx); fe_1(Ry); }
+  hs_scalars(k, s, cr, dr, er, dneg, W);
   return rok;
 }
 

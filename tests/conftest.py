@@ -38,3 +38,33 @@ def engine():
     e = Engine(0)
     yield e
     e.close()
+
+
+def engine_with_env(**env):
+    """A second context created with TMED_* overrides (read by tmed_init only)."""
+    from tmed import Engine
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return Engine(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="session")
+def generic_engines():
+    """The generic path's two kernel pipelines on the same inputs: the latency kernels
+    (latency.hip, every batch up to kGLatMax) and the throughput kernels (TMED_GLAT_MAX=0)."""
+    es = {"latency": engine_with_env(TMED_GLAT_MAX=1 << 16), "throughput": engine_with_env(TMED_GLAT_MAX=0)}
+    yield es
+    for e in es.values():
+        e.close()
+
+
+@pytest.fixture(params=["latency", "throughput"])
+def generic_engine(request, generic_engines):
+    return generic_engines[request.param]

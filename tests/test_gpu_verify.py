@@ -11,7 +11,8 @@ from oracle import port
 pytestmark = pytest.mark.gpu
 
 
-def test_golden_vectors(engine, golden):
+def test_golden_vectors(generic_engine, golden):
+    engine = generic_engine
     pubs = [bytes.fromhex(v["pub"]) for v in golden]
     msgs = [bytes.fromhex(v["msg"]) for v in golden]
     sigs = [bytes.fromhex(v["sig"]) for v in golden]
@@ -56,8 +57,9 @@ def test_sign_kernel_privval_known_answer(engine):
     assert out.tolist() == [1]
 
 
-@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 257, 1000])
-def test_batch_sizes(engine, n):
+@pytest.mark.parametrize("n", [1, 2, 7, 8, 9, 63, 64, 65, 255, 257, 1000])
+def test_batch_sizes(generic_engine, n):
+    engine = generic_engine
     rng, seeds, msgs, offs = _random_batch(n, 100 + n)
     sigs, pubs = port.sign_batch(seeds, msgs, offs, 8)
     sigs[::3, 5] ^= 0x10
@@ -66,8 +68,10 @@ def test_batch_sizes(engine, n):
     assert (out == exp).all()
 
 
-def test_c5_adversarial_mix(engine):
-    """C5: 1% invalid / non-canonical / small-order edge cases mixed into a valid batch (seed 0x5EED)."""
+def test_c5_adversarial_mix(generic_engines):
+    """C5: 1% invalid / non-canonical / small-order edge cases mixed into a valid batch (seed 0x5EED),
+    through the throughput kernels (100k) and the latency kernels (the first 60k)."""
+    engine = generic_engines["throughput"]
     n = 100_000
     rng, seeds, msgs, offs = _random_batch(n, 0x5EED, (100, 130))
     sigs, pubs = engine.sign_arrays(seeds, msgs, offs.astype(np.uint32))
@@ -93,6 +97,9 @@ def test_c5_adversarial_mix(engine):
     exp = port.verify_batch(pubs, sigs, msgs, offs, 16)
     assert int((out != exp).sum()) == 0
     assert exp.sum() <= n - len(idx) + 16
+    m = 60_000
+    out = generic_engines["latency"].verify_arrays(pubs[:m], sigs[:m], msgs, offs[:m + 1].astype(np.uint32))
+    assert int((out != exp[:m]).sum()) == 0
 
 
 def test_full_size_property(engine):
