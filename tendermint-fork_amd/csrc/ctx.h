@@ -130,7 +130,8 @@ struct tmed_ctx {
   uint32_t lat_max = 24576;  // key-cached batches up to this size take the latency kernels (crossover ~32k,
                              // profiles/r01/session3/lat_sweep.jsonl); env TMED_LAT_MAX
   int4 *d_glat = nullptr;    // generic latency mode hand-off (kGLatHandBytes)
-  uint32_t glat_max = 4096;  // generic batches up to this size take the latency kernels; env TMED_GLAT_MAX
+  uint32_t glat_max = 24576;  // generic batches up to this size take the latency kernels (crossover ~32k,
+                              // profiles/r02/s6/sweep_glat*.jsonl); env TMED_GLAT_MAX
   bool timing = false;    // tmed_set_kernel_timing
   uint32_t last_hs_count = 0;  // signatures of the last half-size chunk in d_prep (tmed_window_stats)
   tmed::KernelTimer timer;
