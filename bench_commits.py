@@ -6,8 +6,10 @@
                 generic and key-cached paths, next to the CPU path (the port verifying the
                 same 175 tuples sequentially, 1 thread: the reference's loop).
   --config c3   light client: H headers x 175 validators, the set changing by one key per
-                height; each (h, h+2) pair = VerifyCommitLightTrusting(1/3) + VerifyCommitLight,
-                all pairs in one seam call (light/verifier.go:32-79).
+                height; direct: each (h, h+2) pair = VerifyCommitLightTrusting(1/3) +
+                VerifyCommitLight, all pairs in one seam call (light/verifier.go:32-79), median of
+                --runs calls with the host plan/verify/replay shares; bisection: targets 150
+                heights away, verifySkipping's pivots (light/client.go:706-773), one seam call per round.
   --config c4   blocksync replay: B blocks x V validators, VerifyCommitLight per block
                 (blockchain/v0/reactor.go:366-367), key-cached; with N ranks the blocks are
                 sharded and the per-rank int64 tallies all-reduced (RCCL; gloo on CPU).
@@ -86,15 +88,24 @@ def c1(eng, reps: int, cpu: bool):
     return res
 
 
-def c3(eng, headers: int, gap: int, use_keyset: bool):
-    import tmed.types as T
+def _host_threads():
+    """The seam's host worker count (commit.hip host_threads: TMED_HOST_THREADS, default 16,
+    capped at the machine's hardware threads)."""
+    want = int(os.environ.get("TMED_HOST_THREADS", "16"))
+    return {"seam_threads": min(want, os.cpu_count() or 1), "machine_hw_threads": os.cpu_count()}
+
+
+def _c3_world(eng, headers: int, reach: int, use_keyset: bool):
+    """Heights 0 .. headers + reach - 1: validator set h = pool keys [h, h + 175) (one key
+    replaced per height, equal powers 10), commit h signed by set h."""
     from tmed.workload import make_valset, pubkeys_of, seeds_from_tag, sign_commits
     nv = 175
-    pool_seeds = seeds_from_tag(b"tmed-c3-key", 0, headers + gap + nv)
+    nh = headers + reach
+    pool_seeds = seeds_from_tag(b"tmed-c3-key", 0, nh + nv)
     pool_pubs = pubkeys_of(eng, pool_seeds)
     ks = eng.keyset_load(pool_pubs) if use_keyset else 0
     sets, specs = [], []
-    for h in range(headers + gap):
+    for h in range(nh):
         vals, order = make_valset(pool_pubs[h:h + nv], [10] * nv)
         vals.keyset = ks
         vals.keyset_index = (order + h).astype(np.uint32)
@@ -103,7 +114,44 @@ def c3(eng, headers: int, gap: int, use_keyset: bool):
         specs.append((pool_seeds[h:h + nv][order], addrs, h + 1, 0, block_id(b"c3-%d" % (h + 1)), T2023 + h, None))
     t_sign = time.perf_counter()
     commits = sign_commits(eng, "test_chain_id", specs)
-    t_sign = time.perf_counter() - t_sign
+    return sets, commits, ks, time.perf_counter() - t_sign
+
+
+def _timed_runs(eng, pb, runs: int):
+    """`runs` timed seam calls of one prepared batch: (median s, min s, max s, median phase
+    shares plan / verify / replay)."""
+    from tmed.types import seam_phase_us
+    ts, ph = [], []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        pb.run(eng)
+        ts.append(time.perf_counter() - t0)
+        ph.append(seam_phase_us())
+    ph = np.median(np.array(ph), axis=0)
+    share = ph / max(ph.sum(), 1e-9)
+    return (float(np.median(ts)), float(min(ts)), float(max(ts)),
+            {"plan": round(float(share[0]), 3), "verify": round(float(share[1]), 3), "replay": round(float(share[2]), 3),
+             "plan_ms": round(float(ph[0]) / 1e3, 3), "verify_ms": round(float(ph[1]) / 1e3, 3),
+             "replay_ms": round(float(ph[2]) / 1e3, 3)})
+
+
+def c3(eng, headers: int, gap: int, use_keyset: bool, runs: int = 7, bisect_gap: int = 150):
+    """Light client (BASELINE C3), two workloads over the same synthetic chain:
+      direct:    each header h verified from trusted h - gap in one step (Trusting 1/3 + Light),
+                 all headers in one seam call, timed `runs` times (median, spread, phase shares);
+      bisection: each header h + bisect_gap from trusted h by light/client.go:706-773
+                 verifySkipping — Trusting fails at this distance (the sets share fewer than 1/3
+                 of their keys), the client pivots at 9/16 of the interval and retries; one seam
+                 call per round over all headers' pending Verify calls, until every header is done.
+    Every failing Trusting is checked for ErrNotEnoughVotingPowerSigned Got/Needed."""
+    import tmed.types as T
+    reach = max(gap, bisect_gap)
+    sets, commits, ks, t_sign = _c3_world(eng, headers, reach, use_keyset)
+    res = {"metric": "light-client headers/s (VerifyCommitLightTrusting + VerifyCommitLight per header)",
+           "unit": "headers/s", "host": _host_threads(),
+           "config": {"workload": "C3: %d headers x 175 validators, trust 1/3, set changes 1 key/height" % headers,
+                      "key_cache": bool(ks), "sign_s": round(t_sign, 2), "timed_runs": runs}}
+    # ---- direct (gap) ----
     reqs = []
     for h in range(headers):
         u = h + gap
@@ -111,18 +159,72 @@ def c3(eng, headers: int, gap: int, use_keyset: bool):
         reqs.append((T.MODE_LIGHT, sets[u], "test_chain_id", commits[u].block_id, u + 1, commits[u], 0, 0))
     pb = T.PreparedBatch(reqs)
     pb.run(eng)  # warm
-    t0 = time.perf_counter()
-    pb.run(eng)
-    dt = time.perf_counter() - t0
+    med, lo, hi, phases = _timed_runs(eng, pb, runs)
     codes = pb.codes()
     ver = int(pb.verified().sum())
+    res["value"] = round(headers / med, 1)
+    res["direct"] = {"gap": gap, "headers_per_s": round(headers / med, 1), "verifies_per_s": round(ver / med, 1),
+                     "seconds_median": round(med, 4), "seconds_min": round(lo, 4), "seconds_max": round(hi, 4),
+                     "verifies": ver, "all_ok": bool((codes == 0).all()), "phase_share": phases}
+    # ---- bisection (verifySkipping) ----
+    num, den = 9, 16  # light/client.go:31-32
+    total = 175 * 10
+    needed = total * 1 // 3
+    st = [{"verified": h, "cache": [h + bisect_gap], "depth": 0, "done": False} for h in range(headers)]
+    rounds, calls, ver_b, fails, bad_gn = 0, 0, 0, 0, 0
+    t_seam = 0.0
+    t0 = time.perf_counter()
+    while True:
+        act = [i for i in range(headers) if not st[i]["done"]]
+        if not act:
+            break
+        reqs = []
+        for i in act:
+            v, c = st[i]["verified"], st[i]["cache"][st[i]["depth"]]
+            reqs.append((T.MODE_LIGHT_TRUSTING, sets[v], "test_chain_id", None, 0, commits[c], 1, 3))
+            reqs.append((T.MODE_LIGHT, sets[c], "test_chain_id", commits[c].block_id, c + 1, commits[c], 0, 0))
+        pb = T.PreparedBatch(reqs)
+        ts = time.perf_counter()
+        pb.run(eng)
+        t_seam += time.perf_counter() - ts
+        rounds += 1
+        calls += len(act)
+        codes = pb.codes()
+        vers = pb.verified()
+        for j, i in enumerate(act):
+            s_ = st[i]
+            v, c = s_["verified"], s_["cache"][s_["depth"]]
+            ct, cl = int(codes[2 * j]), int(codes[2 * j + 1])
+            ver_b += int(vers[2 * j]) + (int(vers[2 * j + 1]) if ct == 0 else 0)
+            if ct == 0 and cl == 0:                    # Verify ok
+                if s_["depth"] == 0:
+                    s_["done"] = True
+                else:
+                    s_["verified"] = c
+                    s_["cache"] = s_["cache"][:s_["depth"]]
+                    s_["depth"] = 0
+            elif ct == 5:                              # ErrNewValSetCantBeTrusted
+                fails += 1
+                r = pb.res[2 * j]
+                if r.got != (175 - (c - v)) * 10 or r.needed != needed:
+                    bad_gn += 1
+                if s_["depth"] == len(s_["cache"]) - 1:
+                    pivot = v + (c - v) * num // den
+                    s_["cache"] += [pivot, pivot]      # appended twice, as the reference does
+                s_["depth"] += 1
+            else:
+                raise RuntimeError("header %d: verify %d -> %d failed (%d, %d)" % (i, v, c, ct, cl))
+    wall = time.perf_counter() - t0
+    # headers/s over the seam calls; the Python state machine and request packing of this
+    # harness (the light client's own host work, Go in the reference) is reported beside it
+    res["bisection"] = {"target_gap": bisect_gap, "headers_per_s": round(headers / t_seam, 1),
+                        "seam_seconds": round(t_seam, 4), "harness_seconds": round(wall - t_seam, 4),
+                        "rounds": rounds, "verify_calls": calls,
+                        "trusting_failures": fails, "got_needed_mismatches": bad_gn, "verifies": ver_b,
+                        "all_ok": bad_gn == 0 and fails > 0}
     if ks:
         eng.keyset_free(ks)
-    return {"metric": "light-client headers/s (VerifyCommitLightTrusting + VerifyCommitLight per header)",
-            "value": round(headers / dt, 1), "unit": "headers/s", "verifies_per_s": round(ver / dt, 1),
-            "verifies": ver, "all_ok": bool((codes == 0).all()), "seconds": round(dt, 4),
-            "config": {"workload": "C3: %d headers x 175 validators, trust 1/3, gap %d, set changes 1 key/height"
-                       % (headers, gap), "key_cache": bool(ks), "sign_s": round(t_sign, 2)}}
+    return res
 
 
 def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, batch: int):
@@ -193,6 +295,8 @@ def main():
     ap.add_argument("--reps", type=int, default=1000)
     ap.add_argument("--headers", type=int, default=10_000)
     ap.add_argument("--gap", type=int, default=2)
+    ap.add_argument("--bisect-gap", type=int, default=150, help="C3 bisection target distance (Trusting fails past 116)")
+    ap.add_argument("--runs", type=int, default=7, help="C3 timed repetitions (median reported)")
     ap.add_argument("--blocks", type=int, default=100_000)
     ap.add_argument("--window", type=int, default=1000, help="blocks generated and verified per seam call")
     ap.add_argument("--batch", type=int, default=128, help="blocks per device batch inside the seam")
@@ -210,7 +314,7 @@ def main():
         if cfg == "c1" and rank == 0:
             r = c1(eng, args.reps, not args.no_cpu)
         elif cfg == "c3" and rank == 0:
-            r = c3(eng, args.headers, args.gap, not args.no_keyset)
+            r = c3(eng, args.headers, args.gap, not args.no_keyset, args.runs, args.bisect_gap)
         elif cfg == "c4":
             r = c4(eng, args.blocks, args.validators, rank, world, coll, args.window, args.batch)
         else:

@@ -281,6 +281,13 @@ typedef int (*tmed_batch_verify_fn)(void *user, const uint8_t *pubkeys, const ui
 int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out,
                              tmed_batch_verify_fn verify, void *user);
 
+/*
+ * Diagnostics: wall time in microseconds of the three phases of the calling thread's last
+ * tmed_verify_commits / tmed_verify_commits_with call — [0] host plan (prechecks, candidate
+ * collection), [1] verify (sign-bytes, staging, device, copy back), [2] host replay.
+ */
+int tmed_seam_phase_us(double out_us[3]);
+
 /* ------------------------------------------------ Merkle hashing (f3) */
 
 /*

@@ -597,8 +597,14 @@ static int seam_replay(const tmed_commit_request *reqs, size_t n, tmed_commit_re
   return TMED_OK;
 }
 
+// Wall time of the three phases of the calling thread's last run_seam (tmed_seam_phase_us).
+static thread_local double g_seam_us[3] = {0, 0, 0};
+
 static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, const BatchVerifier &verify) {
   if (n && (!reqs || !out)) return TMED_EINVAL;
+  using clock = std::chrono::steady_clock;
+  auto us = [](clock::time_point a, clock::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+  const auto t0 = clock::now();
   PhaseClock clk;
   Plans plans;
   std::vector<Cand> cands;
@@ -606,6 +612,7 @@ static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_resul
   int rc = seam_plan(reqs, n, out, plans, cands, cache);
   if (rc != TMED_OK) return rc;
   clk.lap("plan");
+  const auto t1 = clock::now();
   // ---- one device batch for every candidate of every request
   const size_t m = cands.size();
   std::vector<uint8_t> valid(m, 0);
@@ -614,10 +621,21 @@ static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_resul
     if (rc != TMED_OK) return rc;
   }
   clk.lap("verify");
+  const auto t2 = clock::now();
   rc = seam_replay(reqs, n, out, plans, valid.data());
   clk.lap("replay");
   clk.emit("seam", n, m);
+  const auto t3 = clock::now();
+  g_seam_us[0] = us(t0, t1);
+  g_seam_us[1] = us(t1, t2);
+  g_seam_us[2] = us(t2, t3);
   return rc;
+}
+
+extern "C" int tmed_seam_phase_us(double out_us[3]) {
+  if (!out_us) return TMED_EINVAL;
+  for (int k = 0; k < 3; k++) out_us[k] = g_seam_us[k];
+  return TMED_OK;
 }
 
 extern "C" int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out,

@@ -91,5 +91,5 @@ EXPORTED_SYMBOLS = [
     "tmed_keyset_load", "tmed_keyset_free", "tmed_verify_batch_keyset", "tmed_verify_batch_keyset_device",
     "tmed_set_kernel_timing", "tmed_kernel_times", "tmed_blocksync_verify",
     "tmed_merkle_roots", "tmed_valset_hashes", "tmed_header_hashes", "tmed_partset_roots",
-    "tmed_verify_commits_multi", "tmed_blocksync_verify_multi", "tmed_window_stats",
+    "tmed_verify_commits_multi", "tmed_blocksync_verify_multi", "tmed_window_stats", "tmed_seam_phase_us",
 ]

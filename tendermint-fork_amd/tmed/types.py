@@ -278,6 +278,8 @@ def _bind():
         l.tmed_blocksync_verify_multi.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t,
                                                   ctypes.POINTER(_BlocksyncWindowC), ctypes.c_uint32,
                                                   ctypes.POINTER(_ResultC)]
+        l.tmed_seam_phase_us.restype = ctypes.c_int
+        l.tmed_seam_phase_us.argtypes = [ctypes.POINTER(ctypes.c_double)]
     return l
 
 
@@ -395,6 +397,16 @@ class PreparedBatch:
         for q, (mode, vals, chain_id, block_id, height, commit, num, den) in enumerate(self.requests):
             out.append(_to_error(self.res[q].code, self.res[q], vals, block_id, commit))
         return out
+
+
+def seam_phase_us():
+    """(plan, verify, replay) wall microseconds of this thread's last seam call (tmed_seam_phase_us)."""
+    l = _bind()
+    out = (ctypes.c_double * 3)()
+    rc = l.tmed_seam_phase_us(out)
+    if rc != TMED_OK:
+        raise TmedError(rc, "tmed_seam_phase_us")
+    return tuple(out)
 
 
 def verify_commits(engine, requests: Sequence[tuple], verifier=None, stats: Optional[list] = None):
