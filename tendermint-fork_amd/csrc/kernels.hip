@@ -336,18 +336,26 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_hs_kernel(
 __global__ __launch_bounds__(kThreadsPerBlock) void window_stats_kernel(const int4 *__restrict__ prep2, uint32_t stride,
                                                                        uint32_t count, uint32_t *__restrict__ lane_hist,
                                                                        uint32_t *__restrict__ wave_hist) {
+  __shared__ uint32_t lh[65], wh[65];  // block-local histograms, one global atomic per bin per block
+  for (uint32_t b = threadIdx.x; b < 65; b += blockDim.x) lh[b] = wh[b] = 0;
+  __syncthreads();
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = slot < count;
   int W = active ? (prep2[(size_t)10 * stride + slot].y >> 8) : 0;  // word 41
   if (W < 0 || W > 64) W = 64;
-  if (active) atomicAdd(&lane_hist[W], 1u);
+  if (active) atomicAdd(&lh[W], 1u);
   int m = W;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const int x = __shfl_xor(m, o);
     m = x > m ? x : m;
   }
-  if ((threadIdx.x & 63u) == 0 && slot < count) atomicAdd(&wave_hist[m], 1u);
+  if ((threadIdx.x & 63u) == 0 && slot < count) atomicAdd(&wh[m], 1u);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < 65; b += blockDim.x) {
+    if (lh[b]) atomicAdd(&lane_hist[b], lh[b]);
+    if (wh[b]) atomicAdd(&wave_hist[b], wh[b]);
+  }
 }
 
 hipError_t launch_window_stats(const int4 *prep, uint32_t stride, uint32_t count, uint32_t *d_hist,

@@ -21,7 +21,7 @@ for s in $STEPS; do
       echo "bench rc=$rc" | tee -a $OUT/bench.log; tail -1 $OUT/bench.log ;;
     prof)
       cd /tmp && export TMPDIR=/tmp
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1; rc=$?
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-c1 --no-keyset > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1; rc=$?
       cd $GRAFT_REPO_ROOT; echo "prof rc=$rc" | tee -a $OUT/prof.log ;;
     variants)
       rc=0
@@ -48,11 +48,11 @@ for s in $STEPS; do
     pmc)
       cd /tmp && export TMPDIR=/tmp
       rc=0
-      PMC_SETS=${PMC_SETS:-"FETCH_SIZE|WRITE_SIZE|SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE|SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES"}
+      PMC_SETS=${PMC_SETS:-"FETCH_SIZE|WRITE_SIZE|SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE|SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"}
       IFS='|' read -ra SETS <<< "$PMC_SETS"
       for ctr in "${SETS[@]}"; do
         tag=$(echo $ctr | tr ' ' '_')
-        timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$OUT/pmc_$tag -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-peak > $GRAFT_REPO_ROOT/$OUT/pmc_$tag.log 2>&1; rc=$?
+        timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$OUT/pmc_$tag -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-peak --no-c1 --no-keyset > $GRAFT_REPO_ROOT/$OUT/pmc_$tag.log 2>&1; rc=$?
         echo "pmc $ctr rc=$rc" | tee -a $GRAFT_REPO_ROOT/$OUT/pmc.log
         if fatal $rc; then break; fi
       done

@@ -46,6 +46,14 @@ def main():
                 continue
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
             grid[k].append(int(r["Grid_Size"]))
+    # dispatch durations from the kernel traces of the same runs (effective clock)
+    dur = collections.defaultdict(list)
+    for a in srcs:
+        for f in (glob.glob(os.path.join(a, "**", "*kernel_trace.csv"), recursive=True) if os.path.isdir(a) else []):
+            for r in csv.DictReader(open(f)):
+                k = short(r["Kernel_Name"])
+                if k:
+                    dur[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     res = {}
     for k, cs in acc.items():
         d = {c: sum(v) / len(v) for c, v in cs.items()}
@@ -60,11 +68,23 @@ def main():
             d["hbm_bytes_per_sig"] = (fb + wb) / d["grid_mean"]
         if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d:
             d["valu_insts_per_wave"] = d["SQ_INSTS_VALU"] / d["SQ_WAVES"]
+        if dur[k]:
+            d["dispatch_ms_mean"] = sum(dur[k]) / len(dur[k]) / 1e6
+            if "GRBM_GUI_ACTIVE" in d:  # GUI-active cycles summed over the 8 XCDs
+                d["effective_clock_ghz"] = d["GRBM_GUI_ACTIVE"] / 8 / (d["dispatch_ms_mean"] * 1e6)
+        if "SQ_WAVE_CYCLES" in d and "SQ_ACTIVE_INST_ANY" in d:  # the wave-state partition
+            wc = d["SQ_WAVE_CYCLES"]
+            d["active_inst_any_frac"] = d["SQ_ACTIVE_INST_ANY"] / wc
+            d["wait_inst_any_frac"] = d.get("SQ_WAIT_INST_ANY", 0) / wc
+            d["wait_any_frac"] = d.get("SQ_WAIT_ANY", 0) / wc
+            d["valu_active_frac"] = d.get("SQ_ACTIVE_INST_VALU", 0) / wc
         res[k] = d
     with open(out_path, "w") as fh:
         json.dump(res, fh, indent=1, sort_keys=True)
     for k, d in res.items():
-        print(k, {x: round(d[x], 1) for x in ("hbm_bytes_per_sig", "valu_insts_per_wave", "grid_mean") if x in d})
+        print(k, {x: round(d[x], 3) for x in ("hbm_bytes_per_sig", "valu_insts_per_wave", "dispatch_ms_mean",
+                                              "effective_clock_ghz", "active_inst_any_frac", "wait_inst_any_frac",
+                                              "wait_any_frac") if x in d})
 
 
 if __name__ == "__main__":
