@@ -24,8 +24,8 @@ struct KernelTimer {
 
 constexpr uint32_t kThreadsPerBlock = 256;
 // Variable-base table slab: lane slots (grid-stride loop bounds the grid to
-// slab_slots / kThreadsPerBlock blocks).  9 entries x 160 B per slot.
-constexpr uint32_t kSlabSlotBytes = 9 * 128;  // 9 cached points in fe_pack256 form
+// slab_slots / kThreadsPerBlock blocks).
+constexpr uint32_t kSlabSlotBytes = 8 * 128;  // cached j*P, j = 1..8, in fe_pack256 form (j = 0: one shared row)
 // The half-size path (main variant 6, the default) keeps two per-lane tables (-A and
 // -sign(d) R): its slab has two slot regions; the full-length fallback (variant 5) one.
 inline uint32_t slab_tables(int main_waves) { return main_waves == 5 ? 1u : 2u; }

@@ -8,7 +8,7 @@
 // Memory layout
 //   pub   n x 32 B, sig n x 64 B (16-B aligned rows -> dwordx4 loads)
 //   msgs  concatenated bytes, off[n+1] u32 (or fixed 256-B vote slots)
-//   slab  per-lane variable-base tables: 9 cached points x 128 B (fe_pack256), lane-major [slot][entry][chunk]
+//   slab  per-lane variable-base tables: 8 cached points x 128 B (fe_pack256), lane-major [slot][entry][chunk]
 //   b16   32769 niels multiples of B in 128-B rows in HBM (4.2 MB; the full-length fallback, variant 5)
 //   combs key-set combs [key][window][entry] and the shared combs of B (radix 256, radix 2^16)
 #include "kernels.h"
@@ -18,31 +18,41 @@
 
 namespace tmed {
 
-// Per-lane table in the HBM slab, lane-major [slot][entry][chunk]: each lane's entry is one
+// Per-lane table in the HBM slab, lane-major [slot][entry 1..8][chunk]: each lane's entry is one
 // aligned 128-B line (the four coordinates in fe_pack256 form), so a divergent lookup reads
 // exactly one line.  The slab does not fit L2/MALL at full occupancy; the 160-B int32 form
 // read 2.25 lines per lookup, and its traffic cost ~10 % of the clock (profiles/r02/s4).
+// Entry 0 (the identity, cached form (1, 1, 1, 0)) is not stored per lane: every lane reads this
+// one row (an L2 hit), so the slab holds entries 1..8.
+__device__ const int4 kIdentityRow[8] = {{1, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}, {0, 0, 0, 0},
+                                          {1, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+
 struct SlabTab {
   int4 *base;
   uint32_t slot;
 
-  __device__ __forceinline__ size_t idx(int j, int q) const { return ((size_t)slot * 9 + j) * 8 + q; }
+  __device__ __forceinline__ const int4 *row(int j) const {
+    return j == 0 ? kIdentityRow : base + ((size_t)slot * 8 + (j - 1)) * 8;
+  }
 
   __device__ __forceinline__ void store(int j, const ge_cached &c) const {
+    if (j == 0) return;
+    int4 *r = base + ((size_t)slot * 8 + (j - 1)) * 8;
     const fe *fs[4] = {&c.YpX, &c.YmX, &c.Z, &c.T2d};
 #pragma unroll
     for (int f = 0; f < 4; f++) {
       uint32_t w[8];
       fe_pack256(w, *fs[f]);
-      base[idx(j, 2 * f)] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
-      base[idx(j, 2 * f + 1)] = make_int4((int)w[4], (int)w[5], (int)w[6], (int)w[7]);
+      r[2 * f] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+      r[2 * f + 1] = make_int4((int)w[4], (int)w[5], (int)w[6], (int)w[7]);
     }
   }
   __device__ __forceinline__ void load(int j, ge_cached &c) const {
     fe *fs[4] = {&c.YpX, &c.YmX, &c.Z, &c.T2d};
+    const int4 *r = row(j);
     int4 v[8];
 #pragma unroll
-    for (int q = 0; q < 8; q++) v[q] = base[idx(j, q)];
+    for (int q = 0; q < 8; q++) v[q] = r[q];
 #pragma unroll
     for (int f = 0; f < 4; f++) {
       const uint32_t w[8] = {(uint32_t)v[2 * f].x, (uint32_t)v[2 * f].y, (uint32_t)v[2 * f].z,
@@ -322,7 +332,7 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_hs_kernel(
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const HsDigitsDev ds{prep2, stride, slot};
   SlabTab ta{slab, slot};
-  SlabTab tr{slab + (size_t)stride * 72, slot};
+  SlabTab tr{slab + (size_t)stride * 64, slot};
   B16Pf bl{comb16, sbl[wv], lane};
   B16Pf bh{comb16 + (size_t)8 * kB16Entries * kCombEntryInt4, sbh[wv], lane};
   const bool id = verify_main_hs(ds, (flags & 2) != 0, er, W, A, Rx, Ry, ta, tr, bl, bh);
