@@ -63,8 +63,10 @@ if MAIN_VARIANT == 6:
     # and T = XY of A and R; no finish.  Outside the main kernel: decode of A and strict decode
     # of R, the mod-L work (Barrett + |d| S).  The lattice step (fp64 quotient estimates,
     # ~130 Euclid steps) is not counted in mads.
+    # tables by build_table_affine: 2d*xy (1 M) + 7 x (mixed add 3 M + p1p1->p3 4 M + 2dT 1 M)
+    MADS_TABLE_HS = 57 * MUL
     HS_W = 33
-    MADS_MAIN = (HS_W - 1) * (16 * SQ + 13 * MUL) + HS_W * 15 * MUL + 8 * 14 * MUL + 2 * MADS_TABLE + 2 * MUL
+    MADS_MAIN = (HS_W - 1) * (16 * SQ + 13 * MUL) + HS_W * 15 * MUL + 8 * 14 * MUL + 2 * MADS_TABLE_HS + 2 * MUL
     MADS_PER_VERIFY_GENERIC = MADS_MAIN + 2 * MADS_DECODE + MADS_SCALAR + 64 + 188
     MAIN_KERNEL = "verify_main_hs_kernel"
 # key-cached main kernel (C2 variant): 32 A-comb + 16 radix-2^16 B-comb mixed additions (3M),
@@ -107,7 +109,7 @@ def spawn_ranks(n: int) -> int:
 
 def mads_main_hs(w: float) -> float:
     """v_mad_i64_i32 of verify_main_hs_kernel per signature at a wave loop length of w windows."""
-    return (w - 1) * (16 * SQ + 13 * MUL) + w * 15 * MUL + 8 * 14 * MUL + 2 * MADS_TABLE + 2 * MUL
+    return (w - 1) * (16 * SQ + 13 * MUL) + w * 15 * MUL + 8 * 14 * MUL + 2 * 57 * MUL + 2 * MUL
 
 
 def window_summary(eng):
