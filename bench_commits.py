@@ -118,8 +118,10 @@ def _c3_world(eng, headers: int, reach: int, use_keyset: bool):
 
 
 def _timed_runs(eng, pb, runs: int):
-    """`runs` timed seam calls of one prepared batch: (median s, min s, max s, median phase
-    shares plan / verify / replay)."""
+    """`runs` timed seam calls of one prepared batch: (median s, min s, max s, the median host
+    phase times of tmed_seam_phase_us as fractions of the median call).  A large call is
+    pipelined by the seam: then plan = host plan + staging and replay = host scatter + replay
+    (both overlapping device work) and verify = the time the host sat waiting for the device."""
     from tmed.types import seam_phase_us
     ts, ph = [], []
     for _ in range(runs):
@@ -128,11 +130,12 @@ def _timed_runs(eng, pb, runs: int):
         ts.append(time.perf_counter() - t0)
         ph.append(seam_phase_us())
     ph = np.median(np.array(ph), axis=0)
-    share = ph / max(ph.sum(), 1e-9)
-    return (float(np.median(ts)), float(min(ts)), float(max(ts)),
-            {"plan": round(float(share[0]), 3), "verify": round(float(share[1]), 3), "replay": round(float(share[2]), 3),
-             "plan_ms": round(float(ph[0]) / 1e3, 3), "verify_ms": round(float(ph[1]) / 1e3, 3),
-             "replay_ms": round(float(ph[2]) / 1e3, 3)})
+    med = float(np.median(ts))
+    frac = ph / 1e6 / med
+    return (med, float(min(ts)), float(max(ts)),
+            {"plan_host_ms": round(float(ph[0]) / 1e3, 3), "wait_or_verify_ms": round(float(ph[1]) / 1e3, 3),
+             "replay_host_ms": round(float(ph[2]) / 1e3, 3), "plan_frac": round(float(frac[0]), 3),
+             "wait_or_verify_frac": round(float(frac[1]), 3), "replay_frac": round(float(frac[2]), 3)})
 
 
 def c3(eng, headers: int, gap: int, use_keyset: bool, runs: int = 7, bisect_gap: int = 150):

@@ -283,8 +283,11 @@ int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t n, tmed_com
 
 /*
  * Diagnostics: wall time in microseconds of the three phases of the calling thread's last
- * tmed_verify_commits / tmed_verify_commits_with call — [0] host plan (prechecks, candidate
- * collection), [1] verify (sign-bytes, staging, device, copy back), [2] host replay.
+ * tmed_verify_commits / tmed_verify_commits_with / tmed_blocksync_verify call — [0] host plan
+ * (prechecks, candidate collection), [1] verify (sign-bytes, staging, device, copy back),
+ * [2] host replay.  For a call the seam pipelines (large batches: two vote slots), [0] is the
+ * host plan + staging time, [1] the time the host is blocked waiting for the device and [2]
+ * the host scatter + replay time; [0] and [2] overlap device work there.
  */
 int tmed_seam_phase_us(double out_us[3]);
 

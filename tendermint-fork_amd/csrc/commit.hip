@@ -855,16 +855,25 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
                          tmed_commit_result *out) {
   BsBatch slots[2];
   int rc = TMED_OK;
+  // tmed_seam_phase_us for a pipelined call: host plan + staging, host time blocked on the
+  // device (votes_collect), host scatter + replay — the first and last overlap device work.
+  using clock = std::chrono::steady_clock;
+  auto us = [](clock::time_point a, clock::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+  double ph[3] = {0, 0, 0};
   auto finish = [&](BsBatch &b) -> int {
     if (b.n == 0) return TMED_OK;
     const size_t m = b.cands.size();
     if (b.device) {
       b.bits.resize(m);
+      const auto t0 = clock::now();
       int r = tmed::votes_collect(ctx, b.st, b.bits.data());
+      ph[1] += us(t0, clock::now());
       if (r != TMED_OK) return r;
-      scatter_bits(reqs + b.lo, b.cands, nullptr, (uint32_t)m, b.bits.data(), b.valid.data());
     }
+    const auto t1 = clock::now();
+    if (b.device) scatter_bits(reqs + b.lo, b.cands, nullptr, (uint32_t)m, b.bits.data(), b.valid.data());
     int r = seam_replay(reqs + b.lo, b.n, out + b.lo, b.plans, b.valid.data());
+    ph[2] += us(t1, clock::now());
     b.n = 0;
     b.device = false;
     return r;
@@ -878,6 +887,7 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
     b.lo = lo;
     b.n = std::min(bsz, nb - lo);
     const tmed_commit_request *rq = reqs + lo;
+    const auto tp = clock::now();
     rc = seam_plan(rq, b.n, out + lo, b.plans, b.cands, b.cache);
     clk.lap("plan");
     const size_t m = b.cands.size();
@@ -892,6 +902,7 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
         if (rc == TMED_OK) rc = tmed::votes_enqueue(ctx, b.st);
         clk.lap("enqueue");
         b.device = rc == TMED_OK;
+        ph[0] += us(tp, clock::now());
       } else {  // oversize template: host-assembled messages, synchronous (drain the pipeline first)
         rc = finish(prev);
         lk.unlock();
@@ -908,6 +919,7 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
   for (BsBatch &b : slots)
     if (rc == TMED_OK) rc = finish(b);
   if (rc != TMED_OK) (void)hipStreamSynchronize(ctx->stream);
+  for (int k = 0; k < 3; k++) g_seam_us[k] = ph[k];
   return rc;
 }
 
