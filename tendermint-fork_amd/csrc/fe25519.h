@@ -40,6 +40,8 @@ struct fe { int32_t v[10]; };
 TMED_HD int32_t mul19(int32_t x) { return (int32_t)(19u * (uint32_t)x); }
 TMED_HD int32_t mul38(int32_t x) { return (int32_t)(38u * (uint32_t)x); }
 
+
+
 TMED_HD void fe_0(fe &h) {
 #pragma unroll
   for (int i = 0; i < 10; i++) h.v[i] = 0;
@@ -140,7 +142,7 @@ struct fe_premul {
       x2[i] = (int32_t)(2u * u);
       x4[i] = (int32_t)(4u * u);
       x19[i] = mul19(f.v[i]);
-      x38[i] = (int32_t)((uint32_t)x19[i] << 1);  // a shift, not a second v_mul_lo_u32
+      x38[i] = (int32_t)((uint32_t)x19[i] << 1);  // LLVM folds this back into a v_mul_lo_u32 by 38
     }
   }
 };

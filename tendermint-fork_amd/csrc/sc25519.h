@@ -14,6 +14,33 @@
 
 namespace tmed {
 
+// 32-bit add / subtract with carry (device: the carry-chain builtins, which become one
+// v_addc / v_subb each; the 64-bit spelling costs a sign extension and register moves per word).
+TMED_HD uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t &cout) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  unsigned int co;
+  const uint32_t r = __builtin_addc(a, b, cin, &co);
+  cout = co;
+  return r;
+#else
+  const uint64_t t = (uint64_t)a + b + cin;
+  cout = (uint32_t)(t >> 32);
+  return (uint32_t)t;
+#endif
+}
+TMED_HD uint32_t subb32(uint32_t a, uint32_t b, uint32_t bin, uint32_t &bout) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  unsigned int bo;
+  const uint32_t r = __builtin_subc(a, b, bin, &bo);
+  bout = bo;
+  return r;
+#else
+  const uint64_t d = (uint64_t)a - b - bin;
+  bout = (uint32_t)(d >> 63);
+  return (uint32_t)d;
+#endif
+}
+
 TMED_HD void sc_const_L(uint32_t l[8]) {
   const uint32_t c[8] = {0x5cf5d3edu, 0x5812631au, 0xa2f79cd6u, 0x14def9deu, 0u, 0u, 0u, 0x10000000u};
 #pragma unroll
@@ -26,54 +53,49 @@ TMED_HD void sc_reduce512(uint32_t r[8], const uint32_t x[16]) {
                           0xffffffffu, 0xffffffffu, 0xffffffffu, 0x0000000fu};
   uint32_t L[8];
   sc_const_L(L);
+  // prod = x * mu, row by row (x[i] * mu into prod[i .. i+9]; prod[i+9] is still zero when
+  // row i starts); two carry chains per row as in sc_muladd.
   uint32_t prod[25];
 #pragma unroll
   for (int i = 0; i < 25; i++) prod[i] = 0;
 #pragma unroll
   for (int i = 0; i < 16; i++) {
-    uint64_t c = 0;
+    uint32_t c1 = 0, c2 = 0, hi = 0;
 #pragma unroll
     for (int j = 0; j < 9; j++) {
-      const uint64_t t = (uint64_t)x[i] * mu[j] + prod[i + j] + c;
-      prod[i + j] = (uint32_t)t;
-      c = t >> 32;
+      const uint64_t p = (uint64_t)x[i] * mu[j];
+      const uint32_t u = addc32(prod[i + j], (uint32_t)p, c1, c1);
+      prod[i + j] = addc32(u, hi, c2, c2);
+      hi = (uint32_t)(p >> 32);
     }
-    prod[i + 9] = (uint32_t)c;
+    prod[i + 9] = hi + c1 + c2;
   }
-  // q = prod[16..24]; ql = low 9 words of q*L
+  // q = prod[16..24]; ql = q * L mod 2^288 (the words past 8 are not needed)
   uint32_t ql[9];
 #pragma unroll
   for (int i = 0; i < 9; i++) ql[i] = 0;
 #pragma unroll
   for (int i = 0; i < 9; i++) {
-    uint64_t c = 0;
+    uint32_t c1 = 0, c2 = 0, hi = 0;
 #pragma unroll
     for (int j = 0; j < 8; j++) {
       if (i + j < 9) {
-        const uint64_t t = (uint64_t)prod[16 + i] * L[j] + ql[i + j] + c;
-        ql[i + j] = (uint32_t)t;
-        c = t >> 32;
+        const uint64_t p = (uint64_t)prod[16 + i] * L[j];
+        const uint32_t u = addc32(ql[i + j], (uint32_t)p, c1, c1);
+        ql[i + j] = addc32(u, hi, c2, c2);
+        hi = (uint32_t)(p >> 32);
       }
     }
-    if (i + 8 < 9) ql[i + 8] = (uint32_t)c;
+    if (i == 0) ql[8] = hi + c1 + c2;  // rows i >= 1 carry past word 8 only
   }
-  uint32_t rr[9];
+  uint32_t rr[9], t[9];
   uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 9; i++) {
-    const uint64_t d = (uint64_t)x[i] - ql[i] - borrow;
-    rr[i] = (uint32_t)d;
-    borrow = (uint32_t)(d >> 63);
-  }
+  for (int i = 0; i < 9; i++) rr[i] = subb32(x[i], ql[i], borrow, borrow);
   // conditional subtract L (rr < 2L)
-  uint32_t t[9];
   borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 9; i++) {
-    const uint64_t d = (uint64_t)rr[i] - (i < 8 ? L[i] : 0u) - borrow;
-    t[i] = (uint32_t)d;
-    borrow = (uint32_t)(d >> 63);
-  }
+  for (int i = 0; i < 9; i++) t[i] = subb32(rr[i], i < 8 ? L[i] : 0u, borrow, borrow);
 #pragma unroll
   for (int i = 0; i < 8; i++) r[i] = borrow ? rr[i] : t[i];
 }
@@ -96,21 +118,19 @@ TMED_HD void sc_muladd(uint32_t r[8], const uint32_t a[8], const uint32_t b[8], 
   uint32_t x[16];
 #pragma unroll
   for (int i = 0; i < 16; i++) x[i] = i < 8 ? c[i] : 0u;
+  // row i adds a[i] * b into x[i .. i+8]; x[i+8] is still zero when row i starts, so the row's
+  // carry-out is just stored.  Two carry chains: low halves of a[i] b[j], high halves of a[i] b[j-1].
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    uint64_t cc = 0;
+    uint32_t c1 = 0, c2 = 0, hi = 0;
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-      const uint64_t t = (uint64_t)a[i] * b[j] + x[i + j] + cc;
-      x[i + j] = (uint32_t)t;
-      cc = t >> 32;
+      const uint64_t p = (uint64_t)a[i] * b[j];
+      const uint32_t u = addc32(x[i + j], (uint32_t)p, c1, c1);
+      x[i + j] = addc32(u, hi, c2, c2);
+      hi = (uint32_t)(p >> 32);
     }
-#pragma unroll
-    for (int k = i + 8; k < 16; k++) {
-      const uint64_t t = (uint64_t)x[k] + cc;
-      x[k] = (uint32_t)t;
-      cc = t >> 32;
-    }
+    x[i + 8] = hi + c1 + c2;  // < 2^32: the row sum fits in nine words
   }
   sc_reduce512(r, x);
 }

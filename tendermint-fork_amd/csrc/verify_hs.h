@@ -59,33 +59,6 @@ TMED_HD double words_to_double(const uint32_t *x, int n) {
   return r;
 }
 
-// 32-bit add / subtract with carry (device: the carry-chain builtins, which become one
-// v_addc / v_subb each; the 64-bit spelling costs a sign extension and register moves per word).
-TMED_HD uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t &cout) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  unsigned int co;
-  const uint32_t r = __builtin_addc(a, b, cin, &co);
-  cout = co;
-  return r;
-#else
-  const uint64_t t = (uint64_t)a + b + cin;
-  cout = (uint32_t)(t >> 32);
-  return (uint32_t)t;
-#endif
-}
-TMED_HD uint32_t subb32(uint32_t a, uint32_t b, uint32_t bin, uint32_t &bout) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  unsigned int bo;
-  const uint32_t r = __builtin_subc(a, b, bin, &bo);
-  bout = bo;
-  return r;
-#else
-  const uint64_t d = (uint64_t)a - b - bin;
-  bout = (uint32_t)(d >> 63);
-  return (uint32_t)d;
-#endif
-}
-
 // r = a - q*b (8 words); returns true if the result went negative (wrapped mod 2^256).
 // Two borrow chains: the low halves of q*b[i] and the high halves of q*b[i-1].
 TMED_HD bool words8_submul(uint32_t r[8], const uint32_t a[8], uint32_t q, const uint32_t b[8]) {
