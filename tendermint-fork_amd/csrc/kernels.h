@@ -64,8 +64,11 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
 hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t *off, uint32_t n, uint8_t *sig_out,
                        uint8_t *pub_out, const int4 *bcomb, hipStream_t stream);
 
-// prep hand-off bytes per signature slot (k, s, A.x, A.y, ok)
-constexpr uint32_t kPrepSlotBytes = 352;  // 10 int4 (k, s, A) + 11 int4 (the half-size hand-off), padded
+// prep hand-off bytes per signature slot: 10 int4 (k, s, A, ok) + 16 int4 (the half-size hand-off,
+// placed in window-count order: kernels.hip verify_prep_r_kernel).  The allocation carries
+// kPrepTailBytes more for the two placement counters of the half-size path.
+constexpr uint32_t kPrepSlotBytes = 416;
+constexpr uint32_t kPrepTailBytes = 256;
 
 // ---- fixed-base combs (key cache) -------------------------------
 // Signed radix-256 comb of a point P: entry [w][j] = j * 256^w * P (niels, affine),

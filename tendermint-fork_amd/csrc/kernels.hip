@@ -12,6 +12,9 @@
 //   b16   32769 niels multiples of B in 128-B rows in HBM (4.2 MB; the full-length fallback, variant 5)
 //   combs key-set combs [key][window][entry] and the shared combs of B (radix 256, radix 2^16)
 #include "kernels.h"
+#ifndef TMED_SLAB_PF
+#define TMED_SLAB_PF 0  // A/B knob: where the per-lane table rows are loaded (verify_hs.h hs_straus)
+#endif
 #include "verify_core.h"
 #include "verify_hs.h"
 #include "kernel_util.h"
@@ -61,9 +64,29 @@ struct SlabTab {
       fe_unpack256(*fs[f], w);
     }
   }
+#if TMED_SLAB_PF
+  // prefetch issues the row's eight 16-B loads into registers; take unpacks them
+  int4 pv[8];
+  __device__ __forceinline__ void prefetch(int j) {
+    const int4 *r = row(j);
+#pragma unroll
+    for (int q = 0; q < 8; q++) pv[q] = r[q];
+  }
+  __device__ __forceinline__ void take(ge_cached &c) const {
+    fe *fs[4] = {&c.YpX, &c.YmX, &c.Z, &c.T2d};
+#pragma unroll
+    for (int f = 0; f < 4; f++) {
+      const uint32_t w[8] = {(uint32_t)pv[2 * f].x, (uint32_t)pv[2 * f].y, (uint32_t)pv[2 * f].z,
+                             (uint32_t)pv[2 * f].w, (uint32_t)pv[2 * f + 1].x, (uint32_t)pv[2 * f + 1].y,
+                             (uint32_t)pv[2 * f + 1].z, (uint32_t)pv[2 * f + 1].w};
+      fe_unpack256(*fs[f], w);
+    }
+  }
+#else
   int pf = 0;
   __device__ __forceinline__ void prefetch(int j) { pf = j; }
   __device__ __forceinline__ void take(ge_cached &c) const { load(pf, c); }
+#endif
 };
 
 typedef __attribute__((address_space(1))) void global_void;
@@ -138,8 +161,9 @@ __device__ __forceinline__ bool prep_load(const int4 *prep, uint32_t stride, uin
 // of the chunk [base, base + count)).
 __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_prep_kernel(
     const uint8_t *__restrict__ pub, const uint8_t *__restrict__ sig, MsgSrc ms, uint32_t base, uint32_t count,
-    int4 *__restrict__ prep, uint32_t stride) {
+    int4 *__restrict__ prep, uint32_t stride, uint32_t *__restrict__ place) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  if (place && slot == 0) place[0] = place[1] = 0;  // the half-size placement counters (verify_prep_r_kernel)
   if (slot >= count) return;
   const uint32_t i = base + slot;
   uint32_t pw[8], sw[16], k[8], s[8];
@@ -233,18 +257,27 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_kernel(
 
 // ---- half-size path (verify_hs.h; main variant 6, the default) -----------------------
 // verify_prep_kernel writes k, s, A, ok to the first prep region (10 int4 per slot); the
-// R kernel adds, in the second region (kPrepHsInt4 int4 per slot, [q][slot]): recoded c
+// R kernel writes the second region (kPrepHsInt4 int4 per position, [q][position]): recoded c
 // (words 0-7), recoded |d| (8-12), recoded e (13-20), R.x (21-30), R.y (31-40), flags (41:
-// bit 0 ok, bit 1 d < 0, bits 8.. window count).
-constexpr int kPrepHsInt4 = 11;
+// bit 0 ok, bit 1 d < 0, bits 8.. window count W), the signature's slot (42), A.x (44-53),
+// A.y (54-63) — everything the main kernel reads.
+//
+// Placement by window count: the main kernel runs every lane of a wave over the wave's largest
+// W, and W is 32 or 33 for almost every signature (a few lanes 34+).  The R kernel therefore
+// writes signatures with W <= 32 from the front of the region and the others from the back (one
+// atomic per wave and group on place[0] / place[1], the lanes of a group at consecutive
+// positions, so the stores stay coalesced): the waves of the front part run 32 windows instead
+// of the unsorted wave maximum (~33.3 on average, tmed_window_stats), ~2 % of the main kernel.
+constexpr int kPrepHsInt4 = 16;
+constexpr int kHsWSmall = 32;
 static_assert((kPrepInt4 + kPrepHsInt4) * 16 <= kPrepSlotBytes, "prep slot too small for the half-size hand-off");
 
 __global__ __launch_bounds__(kThreadsPerBlock) void verify_prep_r_kernel(
     const uint8_t *__restrict__ sig, uint32_t base, uint32_t count, const int4 *__restrict__ prep,
-    int4 *__restrict__ prep2, uint32_t stride) {
+    int4 *__restrict__ prep2, uint32_t stride, uint32_t *__restrict__ place) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   if (slot >= count) return;
-  int32_t w[44];
+  int32_t w[64];
 #pragma unroll
   for (int q = 0; q < 4; q++) {  // k (words 0-7), s (8-15)
     const int4 v = prep[(size_t)q * stride + slot];
@@ -266,10 +299,32 @@ __global__ __launch_bounds__(kThreadsPerBlock) void verify_prep_r_kernel(
 #pragma unroll
   for (int j = 0; j < 10; j++) { w[21 + j] = Rx.v[j]; w[31 + j] = Ry.v[j]; }
   w[41] = ((ok && rok) ? 1 : 0) | (dneg ? 2 : 0) | (W << 8);
-  w[42] = w[43] = 0;
+  w[42] = (int32_t)slot;
+  w[43] = 0;
+#pragma unroll
+  for (int q = 4; q < 9; q++) {  // A.x, A.y: words 16..35 of the first region
+    const int4 v = prep[(size_t)q * stride + slot];
+    w[28 + 4 * q] = v.x; w[29 + 4 * q] = v.y; w[30 + 4 * q] = v.z; w[31 + 4 * q] = v.w;
+  }
+  // position: W <= kHsWSmall from the front, the rest from the back (count - 1 downwards)
+  const bool small = W <= kHsWSmall;
+  const uint64_t act = __ballot(1), sm = __ballot(small);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint32_t fs = 0, fl = 0;
+  if (lane == (uint32_t)__builtin_ctzll(act)) {  // the wave's first active lane takes both ranges
+    const uint32_t ns = (uint32_t)__builtin_popcountll(sm), nl = (uint32_t)__builtin_popcountll(act & ~sm);
+    if (ns) fs = atomicAdd(&place[0], ns);
+    if (nl) fl = atomicAdd(&place[1], nl);
+  }
+  const int leader = __builtin_ctzll(act);
+  fs = (uint32_t)__shfl((int)fs, leader);
+  fl = (uint32_t)__shfl((int)fl, leader);
+  const uint32_t pos = small ? fs + (uint32_t)__builtin_popcountll(sm & below)
+                             : count - 1u - (fl + (uint32_t)__builtin_popcountll(act & ~sm & below));
 #pragma unroll
   for (int q = 0; q < kPrepHsInt4; q++)
-    prep2[(size_t)q * stride + slot] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    prep2[(size_t)q * stride + pos] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 
 // Digits of the recoded c / |d| straight from the hand-off (one dword per eight windows).
@@ -293,11 +348,11 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_hs_kernel(
     int4 *__restrict__ slab, const int4 *__restrict__ comb16, uint8_t *__restrict__ out) {
   __shared__ int4 sbl[kThreadsPerBlock / 64][8 * 64];
   __shared__ int4 sbh[kThreadsPerBlock / 64][8 * 64];
-  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // position in the placed hand-off
   const bool active = slot < count;
-  int32_t w[44];
+  int32_t w[64];
 #pragma unroll
-  for (int q = 3; q < kPrepHsInt4; q++) {  // e, R, flags (words 12..43)
+  for (int q = 3; q < kPrepHsInt4; q++) {  // e, R, flags, the signature's slot, A (words 12..63)
     const int4 v = active ? prep2[(size_t)q * stride + slot] : make_int4(0, 0, 0, 0);
     w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
   }
@@ -307,15 +362,9 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_hs_kernel(
   fe Rx, Ry;
 #pragma unroll
   for (int j = 0; j < 10; j++) { Rx.v[j] = w[21 + j]; Ry.v[j] = w[31 + j]; }
-  int32_t a[20];
-#pragma unroll
-  for (int q = 4; q < 9; q++) {  // A.x, A.y: words 16..35 of the first region
-    const int4 v = active ? prep[(size_t)q * stride + slot] : make_int4(0, 0, 0, 0);
-    a[4 * q - 16] = v.x; a[4 * q - 15] = v.y; a[4 * q - 14] = v.z; a[4 * q - 13] = v.w;
-  }
   ge_p3 A;
 #pragma unroll
-  for (int j = 0; j < 10; j++) { A.X.v[j] = a[j]; A.Y.v[j] = a[10 + j]; }
+  for (int j = 0; j < 10; j++) { A.X.v[j] = w[44 + j]; A.Y.v[j] = w[54 + j]; }
   if (!active) { fe_1(A.Y); fe_1(Ry); }
   fe_1(A.Z);
   fe_mul(A.T, A.X, A.Y);
@@ -336,7 +385,7 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_hs_kernel(
   B16Pf bl{comb16, sbl[wv], lane};
   B16Pf bh{comb16 + (size_t)8 * kB16Entries * kCombEntryInt4, sbh[wv], lane};
   const bool id = verify_main_hs(ds, (flags & 2) != 0, er, W, A, Rx, Ry, ta, tr, bl, bh);
-  if (active) out[base + slot] = ((flags & 1) && id) ? 1 : 0;
+  if (active) out[base + (uint32_t)w[42]] = ((flags & 1) && id) ? 1 : 0;
 }
 
 // Diagnostics (tmed_window_stats): the lattice step's window count W of every lane of the last
@@ -497,6 +546,8 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
   if (chunk == 0 || chunk > slab_stride) chunk = slab_stride;
   if (chunk % kThreadsPerBlock != 0 || slab_stride % kThreadsPerBlock != 0) return hipErrorInvalidValue;
   const bool hs = main_waves != 5;
+  // placement counters of the half-size hand-off: the tail of the prep allocation (kPrepTailBytes)
+  uint32_t *place = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(prep) + (size_t)slab_stride * kPrepSlotBytes);
   if (timer) timer->mark(stream, -1);
   for (uint32_t fbase = 0; fbase < n; fbase += kFinCap) {
     const uint32_t m = (n - fbase) < kFinCap ? (n - fbase) : kFinCap;
@@ -505,12 +556,12 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
       const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
 
       hipLaunchKernelGGL(verify_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, pub, sig, ms, base,
-                         count, prep, slab_stride);
+                         count, prep, slab_stride, hs ? place : nullptr);
       if (timer) timer->mark(stream, 0);
       if (hs) {  // default: half-size scalars (verify_hs.h): R decode + lattice, main; no finish
         int4 *prep2 = prep + (size_t)kPrepInt4 * slab_stride;
         hipLaunchKernelGGL(verify_prep_r_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base, count,
-                           prep, prep2, slab_stride);
+                           prep, prep2, slab_stride, place);
         if (timer) timer->mark(stream, 0);
         hipLaunchKernelGGL(verify_main_hs_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base, count, prep,
                            prep2, slab_stride, slab, btab.comb16, out);

@@ -327,7 +327,12 @@ __global__ __launch_bounds__(64) void verify_glat_main_kernel(const int4 *__rest
 #pragma unroll 1
       for (int k = 0; k < 4; k++) quad_dbl(acc, K);
     }
-    const int dg = (int)((cw >> (4 * (nw & 7))) & 15u) - 8;
+    int dg = (int)((cw >> (4 * (nw & 7))) & 15u) - 8;
+    if (nw == W - 1 && W < 64) {  // top window: the recoding's carry into nibble W (hs_top_digit)
+      const uint32_t wn = dbase + (uint32_t)(W >> 3);
+      const uint32_t cn = (W & 7) ? cw : reinterpret_cast<const uint32_t *>(sc + (size_t)(wn >> 2) * cap + i)[wn & 3];
+      dg = hs_top_digit(cw, cn, W);
+    }
     tab.take(c, dg, K);
     quad_add(acc, c, K);
     if ((nw & 3) == 0 && nw <= 28) {

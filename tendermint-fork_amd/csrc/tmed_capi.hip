@@ -80,7 +80,7 @@ int tmed_init(int device, tmed_ctx **out) {
   if (c->glat_max > kGLatMax) c->glat_max = kGLatMax;
   if (e == hipSuccess)
     e = hipMalloc((void **)&c->d_slab, (size_t)c->slab_slots * kSlabSlotBytes * slab_tables(c->main_waves));
-  if (e == hipSuccess) e = hipMalloc((void **)&c->d_prep, (size_t)c->slab_slots * kPrepSlotBytes);
+  if (e == hipSuccess) e = hipMalloc((void **)&c->d_prep, (size_t)c->slab_slots * kPrepSlotBytes + kPrepTailBytes);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_fin, kFinBytes);          // 128 MB: projective R'
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_fin_pre, kFinPreBytes);   // 48 MB: prefix products
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_glat, kGLatHandBytes);     // 20 MB: latency-mode hand-off

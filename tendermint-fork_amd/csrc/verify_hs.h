@@ -35,6 +35,10 @@
 
 #include "verify_core.h"
 
+#ifndef TMED_SLAB_PF
+#define TMED_SLAB_PF 0
+#endif
+
 namespace tmed {
 
 // N = 8L (little-endian words).
@@ -251,8 +255,21 @@ TMED_HD int sc_halfsize(uint32_t c[8], uint32_t dm[8], bool &dneg, const uint32_
     return 64;
   }
   const int bits = bc > bd ? bc : bd;
-  int W = (bits + 2 + 3) / 4;  // |x| < 2^(4W-2): no carry out of the W recoded nibbles
+  // |x| < 2^(4W-1): the recoding's carry out of nibble W-1 is folded into the top digit
+  // (hs_top_digit, digits -8..8), so 4W-1 bits suffice — one window less on a quarter of the lanes
+  const int W = bits / 4 + 1;
   return W < 29 ? 29 : W;
+}
+
+// Top digit (window W-1) of a W-window signed radix-16 recoding (sc_recode16) of x < 2^(4W-1):
+// nibble W-1 minus 8, plus 16 times the carry the recoding moved into nibble W (that nibble is
+// 8 or 9; every nibble above it is 8).  In [0, 8]: the tables hold j*P for j = 1..8.  w_top is
+// the recoded word holding nibble W-1, w_next the one holding nibble W (W < 64; at W = 64 the
+// (k, 1) fallback has x < 2^253 and no carry).
+TMED_HD int hs_top_digit(uint32_t w_top, uint32_t w_next, int W) {
+  const int n = W - 1;
+  const int d = (int)((w_top >> (4 * (n & 7))) & 15u) - 8;
+  return W < 64 ? d + 16 * (int)((w_next >> (4 * (W & 7))) & 1u) : d;
 }
 
 // The scalar half of phase 1b: the lattice step and e = d S mod L.  Writes the recoded
@@ -316,7 +333,8 @@ TMED_HD void words4_shl16(uint32_t x[4]) {
 
 // Q = [e]B + [c](-A) + [|d|](-sign(d) R) over W radix-16 windows (Straus, most significant
 // first).  DS: cword(w) / dword(w), word w (0..7) of the recoded c / |d| — read once per
-// eight windows, before the doublings that hide the read.  TA / TR: per-lane cached tables
+// eight windows, before the doublings that hide the read; the top window's digit also takes
+// the recoding's carry from nibble W (hs_top_digit).  TA / TR: per-lane cached tables
 // of j*(-A) and j*(-sign(d) R), j = 0..8 (build_table_affine), prefetch(j) / take(ge_cached&).
 // BL / BH: niels tables of j*B and j*2^128*B, j = 0..32768, prefetch(j) / take(ge_niels&);
 // the 16-bit digits of e (er, recoded) are added at windows 28, 24, ..., 0 (16 doublings
@@ -343,23 +361,29 @@ TMED_HD void hs_straus(ge_p2 &out, const DS &ds, const uint32_t er[8], int W, TA
       dw = ds.dword(n >> 3);
     }
     const int sh = 4 * (n & 7);
-    const int dc = (int)((cw >> sh) & 15u) - 8, dd = (int)((dw >> sh) & 15u) - 8;
+    int dc = (int)((cw >> sh) & 15u) - 8, dd = (int)((dw >> sh) & 15u) - 8;
     if (n == W - 1) {
+      dc = hs_top_digit(cw, (W & 7) ? cw : ds.cword(W >> 3), W);
+      dd = hs_top_digit(dw, (W & 7) ? dw : ds.dword(W >> 3), W);
       ge_p3_0(r);
+      if (TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc);
     } else {
 #pragma unroll 1
       for (int k = 0; k < 3; k++) {
         ge_p2_dbl(t, q);
         ge_p1p1_to_p2(q, t);
       }
+      if (TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc);  // the row load overlaps the last doubling
+      if (TMED_SLAB_PF == 2) tr.prefetch(dd < 0 ? -dd : dd);
       ge_p2_dbl(t, q);
       ge_p1p1_to_p3(r, t);
     }
-    ta.prefetch(dc < 0 ? -dc : dc);
+    if (!TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc);
     ta.take(ca);
+    if (TMED_SLAB_PF == 1 || (TMED_SLAB_PF == 2 && n == W - 1)) tr.prefetch(dd < 0 ? -dd : dd);  // overlaps the A addition
     ge_add_cached(t, r, ca, dc < 0);
     ge_p1p1_to_p3(r, t);
-    tr.prefetch(dd < 0 ? -dd : dd);
+    if (!TMED_SLAB_PF) tr.prefetch(dd < 0 ? -dd : dd);
     tr.take(ca);
     ge_add_cached(t, r, ca, dd < 0);
     if ((n & 3) == 0 && n <= 28) {

@@ -148,8 +148,10 @@ static const std::vector<ge_niels> &b16hi_tab() {
   return t;
 }
 
-void hostsim_verify_batch_hs(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
-                             size_t n, uint8_t *out, int32_t *wins) {
+// wmin (optional): run signature i's Straus over max(W_i, wmin[i]) windows — the device runs every
+// lane of a wave over the wave's largest W, so a lane's top windows may lie above its own W.
+void hostsim_verify_batch_hs_w(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
+                               size_t n, uint8_t *out, int32_t *wins, const int32_t *wmin) {
   const ge_niels *lo = b16tab().data();
   const ge_niels *hi = b16hi_tab().data();
 #pragma omp parallel for schedule(dynamic, 16)
@@ -166,10 +168,16 @@ void hostsim_verify_batch_hs(const uint8_t *pub, const uint8_t *sig, const uint8
     int W;
     HsDigits dg;
     const bool ok = verify_prep_hs(pw, sw, msgs + off[i], off[i + 1] - off[i], dg, er, dneg, A, Rx, Ry, W);
-    const bool id = verify_main_hs(dg, dneg, er, W, A, Rx, Ry, ta, tr, bl, bh);
+    const int Wrun = (wmin && wmin[i] > W) ? (wmin[i] > 64 ? 64 : wmin[i]) : W;
+    const bool id = verify_main_hs(dg, dneg, er, Wrun, A, Rx, Ry, ta, tr, bl, bh);
     out[i] = ok && id ? 1 : 0;
     if (wins) wins[i] = W;
   }
+}
+
+void hostsim_verify_batch_hs(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
+                             size_t n, uint8_t *out, int32_t *wins) {
+  hostsim_verify_batch_hs_w(pub, sig, msgs, off, n, out, wins, nullptr);
 }
 
 // The lattice step alone: c, |d| (32-byte LE each), dneg, window count.

@@ -183,7 +183,8 @@ def test_comb_path_hostsim(hostsim, golden, fn):
 
 def test_halfsize_lattice(hostsim):
     """verify_hs.h sc_halfsize: c = d k (mod 8L), d odd, both within the window count's range
-    (|x| < 2^(4W-2)); W = 64 only for the (k, 1) fallback; typical W is 32..34."""
+    (|x| < 2^(4W-1), the top digit taking the recoding's carry); W = 64 only for the (k, 1)
+    fallback; typical W is 32..33."""
     L = E.L
     rng = random.Random(3)
     ks = [0, 1, 2, 3, 8, 16, L - 1, L - 2, 2**127, 2**128 - 1, 2**128, 2**200, 2**252 - 1, 5 * 2**128 + 3]
@@ -198,12 +199,12 @@ def test_halfsize_lattice(hostsim):
             di = -di
         assert (ci - di * k) % (8 * L) == 0, k
         assert di % 2 == 1 and 0 < abs(di) < L, k
-        assert 29 <= W <= 64 and max(ci.bit_length(), abs(di).bit_length()) <= 4 * W - 2, (k, W)
+        assert 29 <= W <= 64 and max(ci.bit_length(), abs(di).bit_length()) <= 4 * W - 1, (k, W)
         if W == 64:
             assert (ci, di) == (k, 1)
         ws.append(W)
     rand = ws[14:]
-    assert max(rand) <= 36 and sum(rand) / len(rand) < 33.2
+    assert max(rand) <= 36 and sum(rand) / len(rand) < 32.8
 
 
 def test_halfsize_torsion_keys(hostsim):
@@ -269,3 +270,30 @@ def test_halfsize_fast_euclid_equals_reference_loop(hostsim):
             W = fn(k.to_bytes(32, "little"), c, d, ctypes.byref(neg))
             out.append((W, c.raw, d.raw, neg.value))
         assert out[0] == out[1], k
+
+
+def test_halfsize_top_digit_and_wave_max(hostsim):
+    """Random signatures through the half-size path (host build of verify_hs.h): with each lane's
+    own W (the top digit carries the recoding's overflow, digits up to 8) and with W raised above
+    it, as in a wave whose largest W exceeds the lane's; one flipped bit of S or of the message
+    makes each invalid.  Decisions equal the oracle's C port."""
+    rng = np.random.default_rng(17)
+    n = 1536
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    offs = (np.arange(n + 1) * 110).astype(np.uint32)
+    msgs = rng.integers(0, 256, int(offs[-1]) + 1, dtype=np.uint8)
+    sig = np.zeros((n, 64), np.uint8)
+    pub = np.zeros((n, 32), np.uint8)
+    hostsim.hostsim_sign_batch(_p(seeds), _p(msgs), _p(offs), ctypes.c_size_t(n), _p(sig), _p(pub))
+    sig[1::5, 40] ^= 4        # S changed
+    msgs[offs[3:n:7]] ^= 1    # message changed
+    exp = port.verify_batch(pub, sig, msgs, offs.astype(np.uint64), 8)
+    assert 0 < exp.sum() < n
+    wins = np.zeros(n, np.int32)
+    for extra in (None, 1, 3):
+        out = np.zeros(n, np.uint8)
+        wmin = None if extra is None else _p(wins + extra)
+        hostsim.hostsim_verify_batch_hs_w(_p(pub), _p(sig), _p(msgs), _p(offs), ctypes.c_size_t(n), _p(out),
+                                          _p(wins) if extra is None else None, wmin)
+        assert (out == exp).all(), (extra, np.nonzero(out != exp)[0][:8])
+    assert wins.min() >= 29 and (wins == 32).sum() > n // 4, np.bincount(wins)
