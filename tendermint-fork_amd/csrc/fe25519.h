@@ -10,11 +10,14 @@
 // odd-odd factor) never overflows int64, so no carry handling is needed inside
 // a multiplication — only one carry pass per result.
 //
-// Magnitude discipline (checked by tests/test_kernel_host.py on the host build):
-//   "carried" value: |limb| <= ~1.01 * 2^25 (even) / 2^24 (odd)  — every mul/sq output
+// Magnitude discipline (checked by tools/gen_fe_asm.py check_bounds and by
+// tests/test_kernel_host.py on the host build):
+//   "carried" value — every mul/sq output: even limbs in [-2^25, 2^25) (rounded carries),
+//     odd limbs in [0, 2^25) (floored carries; limb 1 in [-2^16, 2^25 + 2^16)); fe_carry /
+//     fe_from_words give odd limbs in [-2^24, 2^24], inside the same bound
 //   mul/sq inputs may be sums/differences of up to THREE carried values
-//   (19 * 3.03 * 2^25 < 2^31 keeps the pre-multiplied operand in int32; the
-//   column sum stays below 2^61.2).
+//   (19 * 3 * (2^25 + 2^16) < 2^31 keeps the pre-multiplied operand in int32; the
+//   column sum stays below 2^61.3).
 //
 // All functions are __host__ __device__ so that the identical code can be
 // exercised on the CPU by the test-only host build (tests/, never the product).
@@ -39,6 +42,21 @@ struct fe { int32_t v[10]; };
 // form would cost twice as much.)
 TMED_HD int32_t mul19(int32_t x) { return (int32_t)(19u * (uint32_t)x); }
 TMED_HD int32_t mul38(int32_t x) { return (int32_t)(38u * (uint32_t)x); }
+// 2x as one v_add_u32 (LLVM selects v_lshlrev_b32 for x << 1, which issues at half the rate of
+// v_add_u32 on gfx950: profiles/r02/micro/issue_probe.jsonl).
+TMED_HD int32_t dbl32(int32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  int32_t r;
+  asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(x));
+  return r;
+#else
+  return (int32_t)(2u * (uint32_t)x);
+#endif
+}
+
+#ifndef TMED_FE_FUSED
+#define TMED_FE_FUSED 1  // A/B knob: 0 = column sums + separate carry pass (round 2 first half)
+#endif
 
 
 
@@ -113,17 +131,42 @@ TMED_HD void fe_carry(fe &h, const fe &f) {
   fe_carry64(h, t);
 }
 
+// Fused carry (fe_mul_fused / fe_sq1_fused / fe_sq2_fused, tools/gen_fe_asm.py): the carry
+// chain runs inside the column schedule.  Even columns round (their bias 2^25 arrives with the
+// carry from below), odd columns floor: column 0 starts from 2^25, columns 1, 3, 5, 7 from 2^50
+// (the bias of the next even column, pre-shifted by 25 — a multiple of 2^25, so the odd limb is
+// unchanged and the odd carry brings exactly +2^25), column 9 from 0; even columns 2..8 start
+// FROM the odd carry below (the first mad's addend: no add), odd columns take the even carry
+// below with one 64-bit add.  Against fe_carry64: 5 instead of 10 64-bit adds, 9 instead of 11
+// 64-bit shifts before the wrap, and only the even limbs lose a bias.  Here: the x19 wrap of
+// column 9 into the biased column 0, its small carry into limb 1, and the limbs.
+TMED_HD void fe_fused_fin(fe &h, const int64_t H[10]) {
+  const int64_t c9 = H[9] >> 25;
+  const int64_t h0 = (int64_t)((uint32_t)H[0] & 0x3ffffffu) + c9 * 19;
+  const int32_t c0 = (int32_t)(h0 >> 26);  // |c0| < 2^16
+  h.v[0] = (int32_t)((uint32_t)h0 & 0x3ffffffu) - (1 << 25);
+  h.v[1] = (int32_t)((uint32_t)H[1] & 0x1ffffffu) + c0;
+#pragma unroll
+  for (int k = 2; k < 10; k++)
+    h.v[k] = (k & 1) ? (int32_t)((uint32_t)H[k] & 0x1ffffffu) : (int32_t)((uint32_t)H[k] & 0x3ffffffu) - (1 << 25);
+}
+
 // h = f * g  (100 v_mad_i64_i32; operand pairs (i, j) carry x2 when both are odd and x19 on g_j
-// when i + j >= 10 — fe_mul_cols)
+// when i + j >= 10 — fe_mul_cols / fe_mul_fused)
 TMED_HD void fe_mul(fe &h, const fe &f, const fe &g) {
   int32_t g19[10], f2[10];
 #pragma unroll
   for (int j = 0; j < 10; j++) g19[j] = mul19(g.v[j]);
 #pragma unroll
-  for (int i = 0; i < 10; i++) f2[i] = (int32_t)(2u * (uint32_t)f.v[i]);
+  for (int i = 0; i < 10; i++) f2[i] = dbl32(f.v[i]);
   int64_t acc[10];
+#if TMED_FE_FUSED
+  fe_mul_fused(acc, f.v, f2, g.v, g19);
+  fe_fused_fin(h, acc);
+#else
   fe_mul_cols(acc, f.v, f2, g.v, g19);
   fe_carry64(h, acc);
+#endif
 }
 
 // Column sums of D f^2, D = 1 (square) or 2 (the doubling's 2 Z^2): 55 products.  Pair (i, j),
@@ -132,17 +175,18 @@ TMED_HD void fe_mul(fe &h, const fe &f, const fe &g) {
 // tools/gen_fe_asm.py sq_products): the 19 on the odd-index operand where there is one, with a
 // factor 2 only on an odd (25-bit) limb, so every operand stays inside int32 for inputs up to
 // three carried values (D = 1) or one (D = 2).
+// (The fused squarings put the 19 on the higher index of a wrapped pair and never x38 on a
+// 3-sum: fe_sq1_fused needs x2 of every limb, x4 of limbs 1, 3, 5, 7 and x19 of 5..9.)
 struct fe_premul {
   int32_t x[10], x2[10], x4[10], x19[10], x38[10];
   TMED_HDM explicit fe_premul(const fe &f) {
 #pragma unroll
     for (int i = 0; i < 10; i++) {
-      const uint32_t u = (uint32_t)f.v[i];
       x[i] = f.v[i];
-      x2[i] = (int32_t)(2u * u);
-      x4[i] = (int32_t)(4u * u);
+      x2[i] = dbl32(f.v[i]);
+      x4[i] = dbl32(x2[i]);
       x19[i] = mul19(f.v[i]);
-      x38[i] = (int32_t)((uint32_t)x19[i] << 1);  // LLVM folds this back into a v_mul_lo_u32 by 38
+      x38[i] = mul38(f.v[i]);
     }
   }
 };
@@ -150,16 +194,26 @@ struct fe_premul {
 TMED_HD void fe_sq(fe &h, const fe &f) {
   const fe_premul p(f);
   int64_t acc[10];
+#if TMED_FE_FUSED
+  fe_sq1_fused(acc, p.x, p.x2, p.x4, p.x19, p.x38);
+  fe_fused_fin(h, acc);
+#else
   fe_sq1_cols(acc, p.x, p.x2, p.x4, p.x19, p.x38);
   fe_carry64(h, acc);
+#endif
 }
 
 // h = 2 f^2 (f carried)
 TMED_HD void fe_sq2(fe &h, const fe &f) {
   const fe_premul p(f);
   int64_t acc[10];
+#if TMED_FE_FUSED
+  fe_sq2_fused(acc, p.x, p.x2, p.x4, p.x19, p.x38);
+  fe_fused_fin(h, acc);
+#else
   fe_sq2_cols(acc, p.x, p.x2, p.x4, p.x19, p.x38);
   fe_carry64(h, acc);
+#endif
 }
 
 TMED_HD void fe_sqn(fe &h, const fe &f, int n) {

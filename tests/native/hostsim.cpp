@@ -377,6 +377,20 @@ void hostsim_fe_op(int op, const uint8_t *a, const uint8_t *b, uint8_t *out) {
   to_bytes(out, wo);
 }
 
+// mul / sq / sq2 on raw limbs (signed 32-bit; the caller keeps them inside the documented input
+// bounds), the product's limbs and its canonical encoding out.
+void hostsim_fe_raw(int op, const int32_t *a, const int32_t *b, int32_t *out_limbs, uint8_t *out) {
+  fe fa, fb, fo;
+  for (int i = 0; i < 10; i++) { fa.v[i] = a[i]; fb.v[i] = b[i]; }
+  if (op == 0) fe_mul(fo, fa, fb);
+  else if (op == 1) fe_sq(fo, fa);
+  else fe_sq2(fo, fa);
+  for (int i = 0; i < 10; i++) out_limbs[i] = fo.v[i];
+  uint32_t wo[8];
+  fe_to_words(wo, fo);
+  to_bytes(out, wo);
+}
+
 // fe_pack256 / fe_unpack256 on raw limbs (the main kernel's table storage form): unpacked limbs
 // out, and the product of the unpacked value with the carried g (32-byte LE) as a canonical encoding.
 void hostsim_pack256(const int32_t *limbs, const uint8_t *g, int32_t *out_limbs, uint8_t *prod) {

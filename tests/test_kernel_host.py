@@ -297,3 +297,51 @@ def test_halfsize_top_digit_and_wave_max(hostsim):
                                           _p(wins) if extra is None else None, wmin)
         assert (out == exp).all(), (extra, np.nonzero(out != exp)[0][:8])
     assert wins.min() >= 29 and (wins == 32).sum() > n // 4, np.bincount(wins)
+
+
+def test_fused_carry_at_the_limb_extremes(hostsim):
+    """fe_mul / fe_sq (3-sum inputs) and fe_sq2 (carried input) at the ends of the carried limb
+    ranges (fe25519.h: even limbs [-2^25, 2^25), odd [0, 2^25), limb 1 [-2^16, 2^25 + 2^16), and
+    fe_carry's odd [-2^24, 2^24]): the result is the product mod p and its limbs are carried."""
+    P = E.P
+    off = [0, 26, 51, 77, 102, 128, 153, 179, 204, 230]
+    lo = [-(2**25) if i % 2 == 0 else -(2**24) for i in range(10)]
+    hi = [2**25 - 1 if i % 2 == 0 else 2**25 - 1 for i in range(10)]
+    lo[1], hi[1] = -(2**24) - 2**16, 2**25 + 2**16
+    rng = random.Random(23)
+
+    def val(c):
+        return sum(x << o for x, o in zip(c, off))
+
+    def carried():
+        r = rng.random()
+        if r < 0.3:
+            return [lo[i] if rng.random() < 0.5 else hi[i] for i in range(10)]
+        return [rng.randint(lo[i], hi[i]) for i in range(10)]
+
+    def nsum(n):
+        cs = [carried() for _ in range(n)]
+        return [sum(c[i] for c in cs) for i in range(10)]
+
+    cases = [([3 * hi[i] for i in range(10)], [3 * hi[i] for i in range(10)]),
+             ([3 * lo[i] for i in range(10)], [3 * lo[i] for i in range(10)]),
+             ([3 * hi[i] for i in range(10)], [3 * lo[i] for i in range(10)])]
+    cases += [(nsum(3), nsum(3)) for _ in range(600)] + [(nsum(1), nsum(2)) for _ in range(300)]
+    out = (ctypes.c_int32 * 10)()
+    enc = ctypes.create_string_buffer(32)
+    A = lambda c: (ctypes.c_int32 * 10)(*c)
+    for a, b in cases:
+        for op, exp, inputs_ok in ((0, val(a) * val(b), True), (1, val(a) ** 2, True),
+                                   (2, 2 * val(a) ** 2, all(lo[i] <= a[i] <= hi[i] for i in range(10)))):
+            if not inputs_ok:
+                continue
+            hostsim.hostsim_fe_raw(op, A(a), A(b), out, enc)
+            assert int.from_bytes(enc.raw, "little") == exp % P, (op, a, b)
+            u = list(out)
+            for i in range(10):
+                assert lo[i] <= u[i] <= hi[i] or (i % 2 == 1 and 0 <= u[i] < 2**25), (op, i, u[i])
+    # fe_sq2 on carried inputs at the extremes
+    for _ in range(400):
+        a = carried()
+        hostsim.hostsim_fe_raw(2, A(a), A(a), out, enc)
+        assert int.from_bytes(enc.raw, "little") == 2 * val(a) ** 2 % P

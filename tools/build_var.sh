@@ -9,6 +9,6 @@ make -s >/dev/null
 mkdir -p lib_var/$name /tmp/tmed_var_$name
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -Wno-unused-value "$@" \
   -c csrc/kernels.hip -o /tmp/tmed_var_$name/kernels.o
-objs="lib/tmed_capi.o lib/signbytes.o lib/microbench.o lib/commit.o lib/keyset.o lib/merkle.o"
+objs="lib/latency.o lib/tmed_capi.o lib/signbytes.o lib/microbench.o lib/commit.o lib/keyset.o lib/merkle.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC /tmp/tmed_var_$name/kernels.o $objs -o lib_var/$name/libtmed25519_hip.so
 echo "built lib_var/$name"
