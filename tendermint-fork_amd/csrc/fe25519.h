@@ -55,7 +55,8 @@ TMED_HD int32_t dbl32(int32_t x) {
 }
 
 #ifndef TMED_FE_FUSED
-#define TMED_FE_FUSED 1  // A/B knob: 0 = column sums + separate carry pass (round 2 first half)
+#define TMED_FE_FUSED 2  // A/B knob: 0 = column sums + separate carry pass, 1 = fused carry one product
+                         // at a time, 2 = independent pairs in one schedule (fe_mul_x2 / fe_sq_x2)
 #endif
 
 
@@ -213,6 +214,60 @@ TMED_HD void fe_sq2(fe &h, const fe &f) {
 #else
   fe_sq2_cols(acc, p.x, p.x2, p.x4, p.x19, p.x38);
   fe_carry64(h, acc);
+#endif
+}
+
+// Two independent products / squares in one schedule (fe_mul_fused_x2, fe_sq1_fused_x2,
+// fe_sq2_sq1_fused): each chain's dependent instructions are >= 3 slots apart, where one product at
+// a time leaves them 2 apart (~5 % per mad: profiles/r02/micro/mad_dep_probe.jsonl).  Outputs may
+// alias inputs (everything is read before anything is written).
+TMED_HD void fe_mul_x2(fe &h0, const fe &f0, const fe &g0, fe &h1, const fe &f1, const fe &g1) {
+#if TMED_FE_FUSED >= 2
+  int32_t a19[10], a2[10], b19[10], b2[10];
+#pragma unroll
+  for (int j = 0; j < 10; j++) { a19[j] = mul19(g0.v[j]); b19[j] = mul19(g1.v[j]); }
+#pragma unroll
+  for (int i = 0; i < 10; i++) { a2[i] = dbl32(f0.v[i]); b2[i] = dbl32(f1.v[i]); }
+  int64_t H0[10], H1[10];
+  fe_mul_fused_x2(H0, H1, f0.v, a2, g0.v, a19, f1.v, b2, g1.v, b19);
+  fe_fused_fin(h0, H0);
+  fe_fused_fin(h1, H1);
+#else
+  fe t;
+  fe_mul(t, f0, g0);
+  fe_mul(h1, f1, g1);
+  fe_copy(h0, t);
+#endif
+}
+
+TMED_HD void fe_sq_x2(fe &h0, const fe &f0, fe &h1, const fe &f1) {
+#if TMED_FE_FUSED >= 2
+  const fe_premul a(f0), b(f1);
+  int64_t H0[10], H1[10];
+  fe_sq1_fused_x2(H0, H1, a.x, a.x2, a.x4, a.x19, a.x38, b.x, b.x2, b.x4, b.x19, b.x38);
+  fe_fused_fin(h0, H0);
+  fe_fused_fin(h1, H1);
+#else
+  fe t;
+  fe_sq(t, f0);
+  fe_sq(h1, f1);
+  fe_copy(h0, t);
+#endif
+}
+
+// h0 = 2 f0^2 (f0 carried), h1 = f1^2
+TMED_HD void fe_sq2_sq(fe &h0, const fe &f0, fe &h1, const fe &f1) {
+#if TMED_FE_FUSED >= 2
+  const fe_premul a(f0), b(f1);
+  int64_t H0[10], H1[10];
+  fe_sq2_sq1_fused(H0, H1, a.x, a.x2, a.x4, a.x19, a.x38, b.x, b.x2, b.x4, b.x19, b.x38);
+  fe_fused_fin(h0, H0);
+  fe_fused_fin(h1, H1);
+#else
+  fe t;
+  fe_sq2(t, f0);
+  fe_sq(h1, f1);
+  fe_copy(h0, t);
 #endif
 }
 

@@ -17,6 +17,14 @@
 #pragma once
 #include "fe25519.h"
 
+#ifndef TMED_CONV_X2
+#define TMED_CONV_X2 3  // A/B knob: paired products in p1p1 -> p2 (bit 0), p1p1 -> p3 (bit 1: one pair,
+                        // bit 2: two pairs — spills in verify_main_hs_kernel)
+#endif
+#ifndef TMED_ADD_X2
+#define TMED_ADD_X2 1  // A/B knob: paired products also in the additions (0: one at a time)
+#endif
+
 namespace tmed {
 
 struct ge_p2 { fe X, Y, Z; };
@@ -31,15 +39,28 @@ TMED_HD void ge_cached_0(ge_cached &h) { fe_1(h.YpX); fe_1(h.YmX); fe_1(h.Z); fe
 TMED_HD void ge_niels_0(ge_niels &h) { fe_1(h.YpX); fe_1(h.YmX); fe_0(h.XY2d); }
 
 TMED_HD void ge_p1p1_to_p2(ge_p2 &r, const ge_p1p1 &p) {
+#if TMED_CONV_X2 & 1
+  fe_mul_x2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
+#else
   fe_mul(r.X, p.X, p.T);
   fe_mul(r.Y, p.Y, p.Z);
+#endif
   fe_mul(r.Z, p.Z, p.T);
 }
 TMED_HD void ge_p1p1_to_p3(ge_p3 &r, const ge_p1p1 &p) {
+#if TMED_CONV_X2 & 4
+  fe_mul_x2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
+  fe_mul_x2(r.Z, p.Z, p.T, r.T, p.X, p.Y);
+#elif TMED_CONV_X2 & 2
+  fe_mul_x2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
+  fe_mul(r.Z, p.Z, p.T);
+  fe_mul(r.T, p.X, p.Y);
+#else
   fe_mul(r.X, p.X, p.T);
   fe_mul(r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.Z, p.T);
   fe_mul(r.T, p.X, p.Y);
+#endif
 }
 TMED_HD void ge_p3_to_p2(ge_p2 &r, const ge_p3 &p) { fe_copy(r.X, p.X); fe_copy(r.Y, p.Y); fe_copy(r.Z, p.Z); }
 TMED_HD void ge_p3_to_cached(ge_cached &r, const ge_p3 &p) {
@@ -53,11 +74,9 @@ TMED_HD void ge_p3_to_cached(ge_cached &r, const ge_p3 &p) {
 // r = 2p.  4 squarings; outputs are <= 3-sums (see fe25519.h).
 TMED_HD void ge_p2_dbl(ge_p1p1 &r, const ge_p2 &p) {
   fe xx, yy, b, a, t;
-  fe_sq(xx, p.X);
-  fe_sq(yy, p.Y);
-  fe_sq2(b, p.Z);
+  fe_sq_x2(xx, p.X, yy, p.Y);
   fe_add(t, p.X, p.Y);
-  fe_sq(a, t);
+  fe_sq2_sq(b, p.Z, a, t);
   fe_add(r.Y, yy, xx);
   fe_sub(r.Z, yy, xx);
   fe_sub(r.X, a, r.Y);
@@ -66,14 +85,22 @@ TMED_HD void ge_p2_dbl(ge_p1p1 &r, const ge_p2 &p) {
 
 // r = p + (neg ? -q : q)   with q cached.  -q = (Y-X, Y+X, Z, -2dT).
 TMED_HD void ge_add_cached(ge_p1p1 &r, const ge_p3 &p, const ge_cached &q, bool neg) {
-  fe a, b, c, d, t, qp, qm;
+  fe a, b, c, d, t, t2, qp, qm;
   fe_select(qp, q.YpX, q.YmX, neg);
   fe_select(qm, q.YmX, q.YpX, neg);
-  fe_add(t, p.Y, p.X); fe_mul(a, t, qp);
-  fe_sub(t, p.Y, p.X); fe_mul(b, t, qm);
+  fe_add(t, p.Y, p.X);
+  fe_sub(t2, p.Y, p.X);
+#if TMED_ADD_X2
+  fe_mul_x2(a, t, qp, b, t2, qm);
+  fe_mul_x2(c, q.T2d, p.T, d, p.Z, q.Z);
+#else
+  fe_mul(a, t, qp);
+  fe_mul(b, t2, qm);
   fe_mul(c, q.T2d, p.T);
+  fe_mul(d, p.Z, q.Z);
+#endif
   fe_neg(t, c); fe_select(c, c, t, neg);
-  fe_mul(d, p.Z, q.Z); fe_add(d, d, d);
+  fe_add(d, d, d);
   fe_sub(r.X, a, b);
   fe_add(r.Y, a, b);
   fe_add(r.Z, d, c);
@@ -82,11 +109,17 @@ TMED_HD void ge_add_cached(ge_p1p1 &r, const ge_p3 &p, const ge_cached &q, bool 
 
 // r = p + (neg ? -q : q)   with q niels (affine, Z = 1).
 TMED_HD void ge_madd_niels(ge_p1p1 &r, const ge_p3 &p, const ge_niels &q, bool neg) {
-  fe a, b, c, d, t, qp, qm;
+  fe a, b, c, d, t, t2, qp, qm;
   fe_select(qp, q.YpX, q.YmX, neg);
   fe_select(qm, q.YmX, q.YpX, neg);
-  fe_add(t, p.Y, p.X); fe_mul(a, t, qp);
-  fe_sub(t, p.Y, p.X); fe_mul(b, t, qm);
+  fe_add(t, p.Y, p.X);
+  fe_sub(t2, p.Y, p.X);
+#if TMED_ADD_X2
+  fe_mul_x2(a, t, qp, b, t2, qm);
+#else
+  fe_mul(a, t, qp);
+  fe_mul(b, t2, qm);
+#endif
   fe_mul(c, q.XY2d, p.T);
   fe_neg(t, c); fe_select(c, c, t, neg);
   fe_add(d, p.Z, p.Z);

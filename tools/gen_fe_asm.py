@@ -304,6 +304,76 @@ def emit_fused(fn_sig, cols, inputs, doc):
        ",\n        ".join(", ".join(ins[i:i + 6]) for i in range(0, len(ins), 6)), "\n".join(host))
 
 
+def emit_fused_multi(fn_sig, ops, doc, min_dist=3):
+    """Several independent fused sums in ONE schedule (ops: [(cols, inputs, prefix)]): with two
+    chains interleaved every dependent pair of instructions is >= 3 slots apart (the
+    dependent-mad probe: distance <= 2 costs ~5 % per mad, >= 3 nothing)."""
+    nodes, deps = [], {}
+    for o, (cols, _, _) in enumerate(ops):
+        n1, d1 = fused_nodes(cols)
+        tag = lambda n: (o,) + n
+        nodes += [tag(n) for n in n1]
+        for n, d in d1.items():
+            deps[tag(n)] = [tag(x) for x in d]
+    order = list_schedule(nodes, deps, min_dist)
+    outs, ins, idx = [], [], {}
+    for o, (cols, inputs, pre) in enumerate(ops):
+        outs += ['"=&v"(H%d[%d])' % (o, k) for k in range(10)] + ['"=&v"(t%d_0)' % o, '"=&v"(t%d_1)' % o]
+    nout = len(outs)
+    for o, (cols, inputs, pre) in enumerate(ops):
+        for op in inputs:
+            idx[(o, op)] = nout + len(ins)
+            ins.append('"v"(%s%s[%d])' % (pre, op[0], op[1]))
+    i_b0 = nout + len(ins); ins.append('"s"(b0)')
+    i_b50 = nout + len(ins); ins.append('"s"(b50)')
+    H = lambda o, k: "%%%d" % (12 * o + k)
+    T = lambda o, k: "%%%d" % (12 * o + 10 + (k % 2))
+    lines, host = [], []
+    for n in order:
+        o, kind = n[0], n[1]
+        cols, inputs, pre = ops[o]
+        if kind == "m":
+            k, r = n[2], n[3]
+            a, b = cols[k][r]
+            if r > 0:
+                add, hadd = H(o, k), "H%d[%d]" % (o, k)
+            elif k == 0:
+                add, hadd = "%%%d" % i_b0, "b0"
+            elif k % 2 == 1:
+                add, hadd = ("%%%d" % i_b50, "b50") if k < 9 else ("0", "0")
+            else:
+                add, hadd = T(o, k - 1), "t%d_%d" % (o, (k - 1) % 2)
+            lines.append("v_mad_i64_i32 %s, vcc, %%%d, %%%d, %s" % (H(o, k), idx[(o, a)], idx[(o, b)], add))
+            host.append("  H%d[%d] = %s + (int64_t)%s%s[%d] * (int64_t)%s%s[%d];"
+                        % (o, k, hadd, pre, a[0], a[1], pre, b[0], b[1]))
+        elif kind == "c":
+            k = n[2]
+            lines.append("v_ashrrev_i64 %s, %d, %s" % (T(o, k), S[k], H(o, k)))
+            host.append("  t%d_%d = H%d[%d] >> %d;" % (o, k % 2, o, k, S[k]))
+        else:
+            k = n[2]
+            lines.append("v_lshl_add_u64 %s, %s, 0, %s" % (H(o, k), T(o, k - 1), H(o, k)))
+            host.append("  H%d[%d] += t%d_%d;" % (o, k, o, (k - 1) % 2))
+    asm = "\n".join('      "%s\\n"' % l for l in lines)
+    temps = ", ".join("t%d_0, t%d_1" % (o, o) for o in range(len(ops)))
+    return """%s
+%s {
+  const int64_t b0 = (int64_t)1 << 25, b50 = (int64_t)1 << 50;  // column constants (fe_fused_fin)
+  int64_t %s;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm(
+%s
+      : %s
+      : %s
+      : "vcc");
+#else
+%s
+#endif
+}
+""" % (doc, fn_sig, temps, asm, ",\n        ".join(", ".join(outs[i:i + 6]) for i in range(0, len(outs), 6)),
+       ",\n        ".join(", ".join(ins[i:i + 6]) for i in range(0, len(ins), 6)), "\n".join(host))
+
+
 def used_inputs(cols, sortkey):
     used = []
     for k in range(10):
@@ -368,6 +438,28 @@ def main():
                                 "// %s (inputs up to %d-sums of carried values): 55 mads, 9 carries, 5 adds; premuls used: %s"
                                 % ("f^2" if D == 1 else "2 f^2", nsum,
                                    " ".join("%s[%d]" % o for o in used if o[0] != "x"))))
+    parts.append('''
+// ---- pairs of independent fused sums in one schedule (the point formulas' independent
+// multiplications and squarings): dependent instructions >= 3 slots apart.''')
+    mcols = mul_products()
+    mins = [("f", i) for i in range(10)] + [("f2", i) for i in (1, 3, 5, 7, 9)] + \
+           [("g", j) for j in range(10)] + [("g19", j) for j in range(1, 10)]
+    parts.append(emit_fused_multi(
+        "TMED_HD void fe_mul_fused_x2(int64_t H0[10], int64_t H1[10], const int32_t a_f[10], const int32_t a_f2[10], "
+        "const int32_t a_g[10], const int32_t a_g19[10], const int32_t b_f[10], const int32_t b_f2[10], "
+        "const int32_t b_g[10], const int32_t b_g19[10])", [(mcols, mins, "a_"), (mcols, mins, "b_")],
+        "// two independent products f * g"))
+    sortk = lambda o: (["x", "x2", "x4", "x19", "x38"].index(o[0]), o[1])
+    s1 = sq_products_fused(1, 3)
+    s2 = sq_products_fused(2, 1)
+    psig = "const int32_t %s_x[10], const int32_t %s_x2[10], const int32_t %s_x4[10], const int32_t %s_x19[10], " \
+           "const int32_t %s_x38[10]"
+    parts.append(emit_fused_multi(
+        "TMED_HD void fe_sq1_fused_x2(int64_t H0[10], int64_t H1[10], %s, %s)" % (psig % (("a",) * 5), psig % (("b",) * 5)),
+        [(s1, used_inputs(s1, sortk), "a_"), (s1, used_inputs(s1, sortk), "b_")], "// two independent squares"))
+    parts.append(emit_fused_multi(
+        "TMED_HD void fe_sq2_sq1_fused(int64_t H0[10], int64_t H1[10], %s, %s)" % (psig % (("a",) * 5), psig % (("b",) * 5)),
+        [(s2, used_inputs(s2, sortk), "a_"), (s1, used_inputs(s1, sortk), "b_")], "// 2 a^2 (a carried) and b^2"))
     with open(OUT, "w") as fh:
         fh.write("\n".join(parts))
     print("wrote", OUT)
