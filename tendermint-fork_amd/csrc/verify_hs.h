@@ -36,7 +36,7 @@
 #include "verify_core.h"
 
 #ifndef TMED_SLAB_PF
-#define TMED_SLAB_PF 0
+#define TMED_SLAB_PF 1  // the default of kernels.hip (host builds follow the same order)
 #endif
 
 namespace tmed {
