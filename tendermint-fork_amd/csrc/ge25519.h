@@ -84,6 +84,29 @@ TMED_HD void ge_p2_dbl(ge_p1p1 &r, const ge_p2 &p) {
 }
 
 // r = p + (neg ? -q : q)   with q cached.  -q = (Y-X, Y+X, Z, -2dT).
+// r = p + (neg ? -q : q), with q's Y+X / Y-X already exchanged when neg (the per-lane tables
+// swap them through the load addresses): only 2dT's sign is left.
+TMED_HD void ge_add_cached_pre(ge_p1p1 &r, const ge_p3 &p, const ge_cached &q, bool neg) {
+  fe a, b, c, d, t, t2;
+  fe_add(t, p.Y, p.X);
+  fe_sub(t2, p.Y, p.X);
+#if TMED_ADD_X2
+  fe_mul_x2(a, t, q.YpX, b, t2, q.YmX);
+  fe_mul_x2(c, q.T2d, p.T, d, p.Z, q.Z);
+#else
+  fe_mul(a, t, q.YpX);
+  fe_mul(b, t2, q.YmX);
+  fe_mul(c, q.T2d, p.T);
+  fe_mul(d, p.Z, q.Z);
+#endif
+  fe_neg(t, c); fe_select(c, c, t, neg);
+  fe_add(d, d, d);
+  fe_sub(r.X, a, b);
+  fe_add(r.Y, a, b);
+  fe_add(r.Z, d, c);
+  fe_sub(r.T, d, c);
+}
+
 TMED_HD void ge_add_cached(ge_p1p1 &r, const ge_p3 &p, const ge_cached &q, bool neg) {
   fe a, b, c, d, t, t2, qp, qm;
   fe_select(qp, q.YpX, q.YmX, neg);

@@ -66,12 +66,14 @@ struct SlabTab {
     }
   }
 #if TMED_SLAB_PF
-  // prefetch issues the row's eight 16-B loads into registers; take unpacks them
+  // prefetch issues the row's eight 16-B loads into registers (swap: Y+X and Y-X exchanged by
+  // the load addresses — a negative digit's entry, ge_add_cached_pre); take unpacks them
   int4 pv[8];
-  __device__ __forceinline__ void prefetch(int j) {
+  __device__ __forceinline__ void prefetch(int j, bool swap = false) {
     const int4 *r = row(j);
+    const int sx = swap ? 2 : 0;
 #pragma unroll
-    for (int q = 0; q < 8; q++) pv[q] = r[q];
+    for (int q = 0; q < 8; q++) pv[q] = r[q < 4 ? (q ^ sx) : q];
   }
   __device__ __forceinline__ void take(ge_cached &c) const {
     fe *fs[4] = {&c.YpX, &c.YmX, &c.Z, &c.T2d};
@@ -85,8 +87,16 @@ struct SlabTab {
   }
 #else
   int pf = 0;
-  __device__ __forceinline__ void prefetch(int j) { pf = j; }
-  __device__ __forceinline__ void take(ge_cached &c) const { load(pf, c); }
+  bool sw = false;
+  __device__ __forceinline__ void prefetch(int j, bool swap = false) { pf = j; sw = swap; }
+  __device__ __forceinline__ void take(ge_cached &c) const {
+    ge_cached t;
+    load(pf, t);
+    fe_select(c.YpX, t.YpX, t.YmX, sw);
+    fe_select(c.YmX, t.YmX, t.YpX, sw);
+    fe_copy(c.Z, t.Z);
+    fe_copy(c.T2d, t.T2d);
+  }
 #endif
 };
 

@@ -335,7 +335,8 @@ TMED_HD void words4_shl16(uint32_t x[4]) {
 // first).  DS: cword(w) / dword(w), word w (0..7) of the recoded c / |d| — read once per
 // eight windows, before the doublings that hide the read; the top window's digit also takes
 // the recoding's carry from nibble W (hs_top_digit).  TA / TR: per-lane cached tables
-// of j*(-A) and j*(-sign(d) R), j = 0..8 (build_table_affine), prefetch(j) / take(ge_cached&).
+// of j*(-A) and j*(-sign(d) R), j = 0..8 (build_table_affine), prefetch(j, neg) / take(ge_cached&):
+// for neg the entry comes back with Y+X and Y-X exchanged (ge_add_cached_pre).
 // BL / BH: niels tables of j*B and j*2^128*B, j = 0..32768, prefetch(j) / take(ge_niels&);
 // the 16-bit digits of e (er, recoded) are added at windows 28, 24, ..., 0 (16 doublings
 // apart): low-table digit m and high-table digit m + 8 at window 4m, each entry prefetched
@@ -366,26 +367,26 @@ TMED_HD void hs_straus(ge_p2 &out, const DS &ds, const uint32_t er[8], int W, TA
       dc = hs_top_digit(cw, (W & 7) ? cw : ds.cword(W >> 3), W);
       dd = hs_top_digit(dw, (W & 7) ? dw : ds.dword(W >> 3), W);
       ge_p3_0(r);
-      if (TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc);
+      if (TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc, dc < 0);
     } else {
 #pragma unroll 1
       for (int k = 0; k < 3; k++) {
         ge_p2_dbl(t, q);
         ge_p1p1_to_p2(q, t);
       }
-      if (TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc);  // the row load overlaps the last doubling
-      if (TMED_SLAB_PF == 2) tr.prefetch(dd < 0 ? -dd : dd);
+      if (TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc, dc < 0);  // the row load overlaps the last doubling
+      if (TMED_SLAB_PF == 2) tr.prefetch(dd < 0 ? -dd : dd, dd < 0);
       ge_p2_dbl(t, q);
       ge_p1p1_to_p3(r, t);
     }
-    if (!TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc);
+    if (!TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc, dc < 0);
     ta.take(ca);
-    if (TMED_SLAB_PF == 1 || (TMED_SLAB_PF == 2 && n == W - 1)) tr.prefetch(dd < 0 ? -dd : dd);  // overlaps the A addition
-    ge_add_cached(t, r, ca, dc < 0);
+    if (TMED_SLAB_PF == 1 || (TMED_SLAB_PF == 2 && n == W - 1)) tr.prefetch(dd < 0 ? -dd : dd, dd < 0);  // overlaps the A addition
+    ge_add_cached_pre(t, r, ca, dc < 0);
     ge_p1p1_to_p3(r, t);
-    if (!TMED_SLAB_PF) tr.prefetch(dd < 0 ? -dd : dd);
+    if (!TMED_SLAB_PF) tr.prefetch(dd < 0 ? -dd : dd, dd < 0);
     tr.take(ca);
-    ge_add_cached(t, r, ca, dd < 0);
+    ge_add_cached_pre(t, r, ca, dd < 0);
     if ((n & 3) == 0 && n <= 28) {
       const int dl = (int)(el[3] >> 16) - 32768, dh = (int)(eh[3] >> 16) - 32768;
       words4_shl16(el);

@@ -20,8 +20,12 @@ struct HostTab {
   void store(int j, const ge_cached &c) { e[j] = c; }
   void load(int j, ge_cached &c) const { c = e[j]; }
   int pf = 0;
-  void prefetch(int j) { pf = j; }
-  void take(ge_cached &c) const { c = e[pf]; }
+  bool sw = false;
+  void prefetch(int j, bool swap = false) { pf = j; sw = swap; }
+  void take(ge_cached &c) const {
+    c = e[pf];
+    if (sw) { const fe t = c.YpX; c.YpX = c.YmX; c.YmX = t; }
+  }
 };
 struct HostBTab {
   ge_niels e[129];
