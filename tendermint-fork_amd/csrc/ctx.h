@@ -91,7 +91,10 @@ struct VoteStage {
   uint32_t *tidx = nullptr;
   int64_t *sec = nullptr;
   int32_t *nan = nullptr;
+  bool zc = false;  // the kernels read the pinned staging buffer directly (votes_enqueue)
 };
+// staged-vote batches up to this size skip the copies (kernels read / write pinned host memory)
+constexpr size_t kVoteZeroCopyMax = 256u << 10;
 int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st, int slot = 0);
 int votes_enqueue(tmed_ctx *c, VoteStage &st);
 int votes_collect(tmed_ctx *c, const VoteStage &st, uint8_t *out);
@@ -172,13 +175,17 @@ inline uint32_t last_chunk_count(uint32_t n, uint32_t chunk) {
 }
 // A generic (uncached-key) batch on stream s: the latency kernels (latency.hip) up to
 // c->glat_max signatures, the throughput pipeline above.  Inside a scratch_acquire/release pair.
+// va: assemble the vote sign-bytes inside the latency kernels (only when n <= glat_max, where
+// generic_uses_glat says they run; the caller then skips assemble_votes).
+inline bool generic_uses_glat(const tmed_ctx *c, uint32_t n) { return n <= c->glat_max; }
 inline hipError_t generic_verify(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs,
                                  const uint32_t *off, uint32_t n, uint8_t *out, hipStream_t s, bool msg_slots,
-                                 KernelTimer *timer) {
-  if (n <= c->glat_max) {
+                                 KernelTimer *timer, const VoteAsm *va = nullptr) {
+  if (generic_uses_glat(c, n)) {
     c->last_hs_count = 0;  // no half-size hand-off in d_prep (tmed_window_stats)
-    return launch_verify_glat(pub, sig, msgs, off, n, out, c->d_bcomb16, c->d_glat, s, msg_slots, timer);
+    return launch_verify_glat(pub, sig, msgs, off, n, out, c->d_bcomb16, c->d_glat, s, msg_slots, timer, va);
   }
+  if (va) return hipErrorInvalidValue;
   hipError_t e = launch_verify(pub, sig, msgs, off, n, out, c->d_slab, c->slab_slots, BTabs{c->d_b16, c->d_bcomb16},
                                c->d_prep, c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves, msg_slots, timer);
   c->last_hs_count = (e != hipSuccess || c->main_waves == 5) ? 0 : last_chunk_count(n, c->chunk);

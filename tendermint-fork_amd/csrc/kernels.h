@@ -110,9 +110,20 @@ hipError_t launch_verify_keyset_lat(const uint32_t *val_idx, const uint8_t *key_
 // 8 lanes per signature (two quads, 4-way point formulas).  hand: kGLatHandBytes of scratch.
 constexpr uint32_t kGLatMax = 1u << 16;
 constexpr size_t kGLatHandBytes = (size_t)kGLatMax * (6 * 2 + 7) * 16;
+// Per-vote inputs of the device sign-bytes assembly (votes_dev.h; device or pinned-host pointers).
+struct VoteAsm {
+  const uint8_t *tmpl;
+  const uint32_t *tmpl_idx;
+  const uint8_t *flags;
+  const int64_t *ts_sec;
+  const int32_t *ts_nanos;
+};
+
+// va (vote slots only): the hash lanes assemble their vote's sign-bytes into its slot of msgs
+// first (no separate assemble_votes launch in front of the latency kernels).
 hipError_t launch_verify_glat(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                               uint32_t n, uint8_t *out, const int4 *comb16, int4 *hand, hipStream_t stream,
-                              bool msg_slots = false, KernelTimer *timer = nullptr);
+                              bool msg_slots = false, KernelTimer *timer = nullptr, const VoteAsm *va = nullptr);
 
 // f1: on-device CanonicalVote assembly.  Templates are kVoteTmplBytes records
 // ([pre_len, bid_len, cid_len, 0] + bytes); message i is written to out + i * kVoteSlot

@@ -19,6 +19,7 @@
 #include "verify_core.h"
 #include "verify_hs.h"
 #include "kernel_util.h"
+#include "votes_dev.h"
 
 namespace tmed {
 
@@ -189,48 +190,14 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_prep_kernel(
 }
 
 // ---- f1: CanonicalVote sign-bytes assembled on the device ----------
-// Per commit a template (signbytes.hip VoteEncoder): [pre_len, bid_len, cid_len, 0] then the
-// pre bytes (type/height/round), the complete BlockID field (tag 0x22 + len + body) and the
-// complete chain-id field (tag 0x32 + len + bytes).  Per vote only the flag and the
-// timestamp vary (types/block.go:784-810): the message is
-//   uvarint(body) || pre || [BlockID field if flag == Commit] || 0x2a len {0x08 sec}{0x10 nanos} || chain
-__device__ __forceinline__ int uvarint_len_dev(uint64_t v) {
-  int n = 1;
-  while (v >= 0x80) { v >>= 7; n++; }
-  return n;
-}
-__device__ __forceinline__ uint32_t put_uvarint_dev(uint8_t *p, uint32_t pos, uint64_t v) {
-  while (v >= 0x80) { p[pos++] = (uint8_t)(v | 0x80); v >>= 7; }
-  p[pos++] = (uint8_t)v;
-  return pos;
-}
-
-__global__ __launch_bounds__(kThreadsPerBlock) void assemble_votes_kernel(
-    const uint8_t *__restrict__ tmpl, const uint32_t *__restrict__ tmpl_idx, const uint8_t *__restrict__ flags,
-    const int64_t *__restrict__ ts_sec, const int32_t *__restrict__ ts_nanos, uint32_t n, uint8_t *__restrict__ out,
-    uint32_t *__restrict__ out_len) {
+// (votes_dev.h assemble_vote; this kernel serves the throughput and key-cached paths, the
+// generic latency kernels assemble in their hash lanes.)
+__global__ __launch_bounds__(kThreadsPerBlock) void assemble_votes_kernel(VoteAsm va, uint32_t n, uint8_t *__restrict__ out,
+                                                                        uint32_t *__restrict__ out_len) {
+  __shared__ int4 tl[kThreadsPerBlock][kVoteTmplBytes / 16];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint8_t *t = tmpl + (size_t)tmpl_idx[i] * kVoteTmplBytes;
-  const uint32_t pre_len = t[0], bid_len = t[1], cid_len = t[2];
-  const bool with_bid = flags[i] == 2;
-  const uint64_t s = (uint64_t)ts_sec[i], ns = (uint64_t)(int64_t)ts_nanos[i];
-  const uint32_t ts_body = (s ? 1 + uvarint_len_dev(s) : 0) + (ns ? 1 + uvarint_len_dev(ns) : 0);
-  const uint32_t body = pre_len + (with_bid ? bid_len : 0) + 1 + uvarint_len_dev(ts_body) + ts_body + cid_len;
-  uint8_t *o = out + (size_t)i * kVoteSlot;
-  uint32_t p = put_uvarint_dev(o, 0, body);
-  const uint8_t *src = t + 4;
-  for (uint32_t j = 0; j < pre_len; j++) o[p++] = src[j];
-  src += pre_len;
-  if (with_bid)
-    for (uint32_t j = 0; j < bid_len; j++) o[p++] = src[j];
-  src += bid_len;
-  o[p++] = 0x2a;
-  p = put_uvarint_dev(o, p, ts_body);
-  if (s) { o[p++] = 0x08; p = put_uvarint_dev(o, p, s); }
-  if (ns) { o[p++] = 0x10; p = put_uvarint_dev(o, p, ns); }
-  for (uint32_t j = 0; j < cid_len; j++) o[p++] = src[j];
-  out_len[i] = p;
+  assemble_vote(va, i, out, out_len, tl[threadIdx.x]);
 }
 
 // Projective R' of signature slot (X, Y, Z: 30 limbs + 2 pad = 8 int4), stored [q][slot].
@@ -971,7 +938,7 @@ hipError_t launch_assemble_votes(const uint8_t *tmpl, const uint32_t *tmpl_idx, 
                                  uint32_t *out_len, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(assemble_votes_kernel, dim3((n + kThreadsPerBlock - 1) / kThreadsPerBlock),
-                     dim3(kThreadsPerBlock), 0, stream, tmpl, tmpl_idx, flags, ts_sec, ts_nanos, n, out, out_len);
+                     dim3(kThreadsPerBlock), 0, stream, VoteAsm{tmpl, tmpl_idx, flags, ts_sec, ts_nanos}, n, out, out_len);
   return hipGetLastError();
 }
 

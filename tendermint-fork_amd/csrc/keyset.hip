@@ -104,8 +104,23 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   // before (the other slot; this slot's previous batch was collected before it was
   // restaged).  A small one (a single commit) stays on the kernel stream: the cross-stream
   // event would cost more latency than the copy.
+  // A batch of up to kVoteZeroCopyMax staged bytes (a single commit: C1) is not copied at all:
+  // the kernels read the pinned staging buffer over the bus and write the decisions into the
+  // pinned result buffer, which saves the copy-in and copy-out latencies (~15 us of a 100-us
+  // commit).  TMED_VOTES_ZC=0 turns it off.
+  static const bool zc_on = [] {
+    const char *v = getenv("TMED_VOTES_ZC");
+    return !(v && v[0] == '0');
+  }();
+  st.zc = zc_on && st.total <= kVoteZeroCopyMax;
+  uint8_t *out_dev = (uint8_t *)vs.d_out.p;
   hipError_t e = hipSuccess;
-  if (st.total >= (1u << 20)) {
+  if (st.zc) {
+    void *dh = nullptr, *dout = nullptr;
+    e = hipHostGetDevicePointer(&dh, vs.h_votes.p, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&dout, vs.h_out.p, 0);
+    if (e == hipSuccess) { d = (uint8_t *)dh; out_dev = (uint8_t *)dout; }
+  } else if (st.total >= (1u << 20)) {
     e = hipMemcpyAsync(d, vs.h_votes.p, st.total, hipMemcpyHostToDevice, c->copy_stream);
     if (e == hipSuccess) e = hipEventRecord(vs.copied, c->copy_stream);
     if (e == hipSuccess) e = hipStreamWaitEvent(s, vs.copied, 0);
@@ -114,21 +129,24 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   }
   if (e == hipSuccess) e = scratch_acquire(c, s);
   if (e == hipSuccess) e = hipEventRecord(vs.ev0, s);
-  if (e == hipSuccess)
-    e = launch_assemble_votes(d + st.o_tmpl, (const uint32_t *)(d + st.o_tidx), d + st.o_flag,
-                              (const int64_t *)(d + st.o_sec), (const int32_t *)(d + st.o_nan), m,
-                              (uint8_t *)vs.d_vmsg.p, (uint32_t *)vs.d_off.p, s);
+  // the generic latency kernels assemble the sign-bytes in their hash lanes (no launch in front)
+  const VoteAsm va{d + st.o_tmpl, (const uint32_t *)(d + st.o_tidx), d + st.o_flag, (const int64_t *)(d + st.o_sec),
+                   (const int32_t *)(d + st.o_nan)};
+  const bool fused = !st.ks && generic_uses_glat(c, m);
+  if (e == hipSuccess && !fused)
+    e = launch_assemble_votes(va.tmpl, va.tmpl_idx, va.flags, va.ts_sec, va.ts_nanos, m, (uint8_t *)vs.d_vmsg.p,
+                              (uint32_t *)vs.d_off.p, s);
   if (e == hipSuccess) {
     if (st.ks)
       e = keyset_verify(c, *st.ks, (const uint32_t *)(d + st.o_key), d + st.o_sig, (const uint8_t *)vs.d_vmsg.p,
-                        (const uint32_t *)vs.d_off.p, m, (uint8_t *)vs.d_out.p, s, /*msg_slots=*/true);
+                        (const uint32_t *)vs.d_off.p, m, out_dev, s, /*msg_slots=*/true);
     else
       e = generic_verify(c, d + st.o_key, d + st.o_sig, (const uint8_t *)vs.d_vmsg.p, (const uint32_t *)vs.d_off.p, m,
-                         (uint8_t *)vs.d_out.p, s, /*msg_slots=*/true, nullptr);
+                         out_dev, s, /*msg_slots=*/true, nullptr, fused ? &va : nullptr);
   }
   if (e == hipSuccess) e = hipEventRecord(vs.ev1, s);
   if (e == hipSuccess) e = scratch_release(c, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(vs.h_out.p, vs.d_out.p, m, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess && !st.zc) e = hipMemcpyAsync(vs.h_out.p, vs.d_out.p, m, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipEventRecord(vs.done, s);
   return map_err(e);
 }

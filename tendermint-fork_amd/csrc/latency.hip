@@ -25,6 +25,7 @@
 //     the B entries come from the radix-2^16 comb.  Quad 1's sum is moved onto quad 0 (DPP
 //     row shift), added, and the identity test is projective.
 #include "kernel_util.h"
+#include "votes_dev.h"
 #include "kernels.h"
 #include "verify_core.h"
 #include "verify_hs.h"
@@ -209,7 +210,9 @@ constexpr int kScInt4 = 7;
 
 __global__ __launch_bounds__(64) void verify_glat_prep_kernel(const uint8_t *__restrict__ pub,
                                                               const uint8_t *__restrict__ sig, MsgSrc ms, uint32_t n,
-                                                              uint32_t nD, int4 *__restrict__ hand, uint32_t cap) {
+                                                              uint32_t nD, int4 *__restrict__ hand, uint32_t cap,
+                                                              VoteAsm va, int assemble) {
+  __shared__ int4 tl[64][kVoteTmplBytes / 16];  // the hash lanes' vote templates (assemble_vote)
   const uint32_t t = threadIdx.x;
   if (blockIdx.x < nD) {  // decode role: point p = A_p (p < n) or R_{p-n}
     const uint32_t p = blockIdx.x * 64 + t;
@@ -241,6 +244,7 @@ __global__ __launch_bounds__(64) void verify_glat_prep_kernel(const uint8_t *__r
   }
   const uint32_t i = (blockIdx.x - nD) * 64 + t;  // scalar role
   if (i >= n) return;
+  if (assemble) assemble_vote(va, i, const_cast<uint8_t *>(ms.msgs), const_cast<uint32_t *>(ms.off), tl[t]);
   uint32_t pw[8], sw[16], k[8], s[8], cr[8], dr[8], er[8];
   load_row_words(pw, pub + 32 * (size_t)i, 2);
   load_row_words(sw, sig + 64 * (size_t)i, 4);
@@ -363,14 +367,15 @@ __global__ __launch_bounds__(64) void verify_glat_main_kernel(const int4 *__rest
 
 hipError_t launch_verify_glat(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                               uint32_t n, uint8_t *out, const int4 *comb16, int4 *hand, hipStream_t stream,
-                              bool msg_slots, KernelTimer *timer) {
+                              bool msg_slots, KernelTimer *timer, const VoteAsm *va) {
   if (n == 0) return hipSuccess;
   if (n > kGLatMax) return hipErrorInvalidValue;  // the hand-off is sized for kGLatMax signatures
   const MsgSrc ms{msgs, off, msg_slots};
   const uint32_t nD = (2 * n + 63) / 64, nH = (n + 63) / 64;
   if (timer) timer->mark(stream, -1);
+  if (va && !msg_slots) return hipErrorInvalidValue;
   hipLaunchKernelGGL(verify_glat_prep_kernel, dim3(nD + nH), dim3(64), 0, stream, pub, sig, ms, n, nD, hand,
-                     kGLatMax);
+                     kGLatMax, va ? *va : VoteAsm{}, va ? 1 : 0);
   if (timer) timer->mark(stream, 0);
   hipLaunchKernelGGL(verify_glat_main_kernel, dim3((n + 7) / 8), dim3(64), 0, stream, hand, n, kGLatMax, comb16, out);
   if (timer) timer->mark(stream, 1);
