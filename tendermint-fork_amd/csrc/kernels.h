@@ -101,10 +101,13 @@ hipError_t launch_window_stats(const int4 *prep, uint32_t stride, uint32_t count
 // comb sum, strict decode of R on other lanes instead of the inversion; two launches.
 // fin as above; dec: kLatDecInt4 x n int4 (fits the fin_pre buffer for n <= kLatMax).
 constexpr uint32_t kLatMax = 1u << 16;
+struct VoteAsm;
+// va (vote slots only): every lane of a signature's group assembles the vote's sign-bytes into
+// its slot first (identical bytes; no separate assemble_votes launch in front).
 hipError_t launch_verify_keyset_lat(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
                                     const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                     const uint32_t *off, uint32_t n, uint8_t *out, int4 *fin, int4 *dec,
-                                    hipStream_t stream, bool msg_slots = false);
+                                    hipStream_t stream, bool msg_slots = false, const VoteAsm *va = nullptr);
 
 // Latency mode of the generic path (latency.hip; n <= kGLatMax): decode / hash roles, then
 // 8 lanes per signature (two quads, 4-way point formulas).  hand: kGLatHandBytes of scratch.

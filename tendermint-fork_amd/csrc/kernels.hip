@@ -805,7 +805,9 @@ __device__ __forceinline__ void shfl_down_fe(fe &o, const fe &f, int L) {
 __global__ __launch_bounds__(64) void verify_keyset_lat_kernel(
     const uint32_t *__restrict__ val_idx, const uint8_t *__restrict__ key_pub, const uint8_t *__restrict__ key_ok,
     const int4 *__restrict__ acomb, const int4 *__restrict__ bcomb, const uint8_t *__restrict__ sig, MsgSrc ms,
-    uint32_t m, uint32_t nR, int4 *__restrict__ fin, int4 *__restrict__ dec, uint8_t *__restrict__ out) {
+    uint32_t m, uint32_t nR, int4 *__restrict__ fin, int4 *__restrict__ dec, uint8_t *__restrict__ out, VoteAsm va,
+    int assemble) {
+  __shared__ int4 tl[64][kVoteTmplBytes / 16];  // the comb lanes' vote templates (assemble_vote)
   if (blockIdx.x < nR) {
     const uint32_t i = blockIdx.x * 64 + threadIdx.x;
     if (i >= m) return;
@@ -825,6 +827,7 @@ __global__ __launch_bounds__(64) void verify_keyset_lat_kernel(
   const uint32_t g = (blockIdx.x - nR) * (64 / kLatLanes) + (threadIdx.x / kLatLanes);
   const int r = (int)(threadIdx.x % kLatLanes);
   if (g >= m) return;  // whole 8-lane groups leave together: the shuffles stay inside live groups
+  if (assemble) assemble_vote(va, g, const_cast<uint8_t *>(ms.msgs), const_cast<uint32_t *>(ms.off), tl[threadIdx.x]);
   const uint32_t v = val_idx[g];
   uint32_t pw[8], sw[16], k[8], s[8], kr[8], sr[8];
   load_row_words(pw, key_pub + 32 * (size_t)v, 2);
@@ -881,13 +884,14 @@ __global__ __launch_bounds__(kThreadsPerBlock) void verify_lat_finish_kernel(con
 hipError_t launch_verify_keyset_lat(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
                                     const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                     const uint32_t *off, uint32_t n, uint8_t *out, int4 *fin, int4 *dec,
-                                    hipStream_t stream, bool msg_slots) {
+                                    hipStream_t stream, bool msg_slots, const VoteAsm *va) {
   if (n == 0) return hipSuccess;
   if (n > kLatMax) return hipErrorInvalidValue;  // fin / dec are sized for kLatMax signatures
+  if (va && !msg_slots) return hipErrorInvalidValue;
   const MsgSrc ms{msgs, off, msg_slots};
   const uint32_t nR = (n + 63) / 64, nC = (n + 64 / kLatLanes - 1) / (64 / kLatLanes);
   hipLaunchKernelGGL(verify_keyset_lat_kernel, dim3(nR + nC), dim3(64), 0, stream, val_idx, key_pub, key_ok, acomb,
-                     bcomb, sig, ms, n, nR, fin, dec, out);
+                     bcomb, sig, ms, n, nR, fin, dec, out, va ? *va : VoteAsm{}, va ? 1 : 0);
   hipLaunchKernelGGL(verify_lat_finish_kernel, dim3((n + kThreadsPerBlock - 1) / kThreadsPerBlock),
                      dim3(kThreadsPerBlock), 0, stream, fin, dec, n, out);
   return hipGetLastError();

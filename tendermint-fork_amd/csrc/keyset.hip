@@ -38,11 +38,12 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // commit), the throughput kernels (prep / comb main / batched finish) above c->lat_max.
 static hipError_t keyset_verify(tmed_ctx *c, const Keyset &k, const uint32_t *d_idx, const uint8_t *d_sig,
                                 const uint8_t *d_msgs, const uint32_t *d_off, uint32_t n, uint8_t *d_out,
-                                hipStream_t s, bool msg_slots) {
+                                hipStream_t s, bool msg_slots, const VoteAsm *va = nullptr) {
   c->last_hs_count = 0;  // d_prep now holds another path's hand-off (tmed_window_stats)
   if (n <= c->lat_max)
     return launch_verify_keyset_lat(d_idx, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb, d_sig, d_msgs, d_off, n, d_out,
-                                    c->d_fin, c->d_fin_pre, s, msg_slots);
+                                    c->d_fin, c->d_fin_pre, s, msg_slots, va);
+  if (va) return hipErrorInvalidValue;
   return launch_verify_keyset(d_idx, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb16, d_sig, d_msgs, d_off, n, d_out, c->d_prep,
                               c->slab_slots, c->d_fin, c->d_fin_pre, s, msg_slots,
                               (c->timing && !msg_slots) ? &c->timer : nullptr);
@@ -129,17 +130,18 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   }
   if (e == hipSuccess) e = scratch_acquire(c, s);
   if (e == hipSuccess) e = hipEventRecord(vs.ev0, s);
-  // the generic latency kernels assemble the sign-bytes in their hash lanes (no launch in front)
+  // the latency kernels (generic and key-cached) assemble the sign-bytes in their hash lanes (no
+  // launch in front)
   const VoteAsm va{d + st.o_tmpl, (const uint32_t *)(d + st.o_tidx), d + st.o_flag, (const int64_t *)(d + st.o_sec),
                    (const int32_t *)(d + st.o_nan)};
-  const bool fused = !st.ks && generic_uses_glat(c, m);
+  const bool fused = st.ks ? m <= c->lat_max : generic_uses_glat(c, m);
   if (e == hipSuccess && !fused)
     e = launch_assemble_votes(va.tmpl, va.tmpl_idx, va.flags, va.ts_sec, va.ts_nanos, m, (uint8_t *)vs.d_vmsg.p,
                               (uint32_t *)vs.d_off.p, s);
   if (e == hipSuccess) {
     if (st.ks)
       e = keyset_verify(c, *st.ks, (const uint32_t *)(d + st.o_key), d + st.o_sig, (const uint8_t *)vs.d_vmsg.p,
-                        (const uint32_t *)vs.d_off.p, m, out_dev, s, /*msg_slots=*/true);
+                        (const uint32_t *)vs.d_off.p, m, out_dev, s, /*msg_slots=*/true, fused ? &va : nullptr);
     else
       e = generic_verify(c, d + st.o_key, d + st.o_sig, (const uint8_t *)vs.d_vmsg.p, (const uint32_t *)vs.d_off.p, m,
                          out_dev, s, /*msg_slots=*/true, nullptr, fused ? &va : nullptr);
