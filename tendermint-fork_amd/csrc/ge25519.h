@@ -17,14 +17,6 @@
 #pragma once
 #include "fe25519.h"
 
-#ifndef TMED_CONV_X2
-#define TMED_CONV_X2 3  // A/B knob: paired products in p1p1 -> p2 (bit 0), p1p1 -> p3 (bit 1: one pair,
-                        // bit 2: two pairs — spills in verify_main_hs_kernel)
-#endif
-#ifndef TMED_ADD_X2
-#define TMED_ADD_X2 1  // A/B knob: paired products also in the additions (0: one at a time)
-#endif
-
 namespace tmed {
 
 struct ge_p2 { fe X, Y, Z; };
@@ -38,29 +30,16 @@ TMED_HD void ge_p3_0(ge_p3 &h) { fe_0(h.X); fe_1(h.Y); fe_1(h.Z); fe_0(h.T); }
 TMED_HD void ge_cached_0(ge_cached &h) { fe_1(h.YpX); fe_1(h.YmX); fe_1(h.Z); fe_0(h.T2d); }
 TMED_HD void ge_niels_0(ge_niels &h) { fe_1(h.YpX); fe_1(h.YmX); fe_0(h.XY2d); }
 
+// (Independent products in pairs, fe_mul_x2; p1p1 -> p3 pairs only X, Y: a second pair spilled
+// in verify_main_hs_kernel.)
 TMED_HD void ge_p1p1_to_p2(ge_p2 &r, const ge_p1p1 &p) {
-#if TMED_CONV_X2 & 1
   fe_mul_x2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
-#else
-  fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
-#endif
   fe_mul(r.Z, p.Z, p.T);
 }
 TMED_HD void ge_p1p1_to_p3(ge_p3 &r, const ge_p1p1 &p) {
-#if TMED_CONV_X2 & 4
-  fe_mul_x2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
-  fe_mul_x2(r.Z, p.Z, p.T, r.T, p.X, p.Y);
-#elif TMED_CONV_X2 & 2
   fe_mul_x2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.Z, p.T);
   fe_mul(r.T, p.X, p.Y);
-#else
-  fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
-  fe_mul(r.Z, p.Z, p.T);
-  fe_mul(r.T, p.X, p.Y);
-#endif
 }
 TMED_HD void ge_p3_to_p2(ge_p2 &r, const ge_p3 &p) { fe_copy(r.X, p.X); fe_copy(r.Y, p.Y); fe_copy(r.Z, p.Z); }
 TMED_HD void ge_p3_to_cached(ge_cached &r, const ge_p3 &p) {
@@ -90,15 +69,8 @@ TMED_HD void ge_add_cached_pre(ge_p1p1 &r, const ge_p3 &p, const ge_cached &q, b
   fe a, b, c, d, t, t2;
   fe_add(t, p.Y, p.X);
   fe_sub(t2, p.Y, p.X);
-#if TMED_ADD_X2
   fe_mul_x2(a, t, q.YpX, b, t2, q.YmX);
   fe_mul_x2(c, q.T2d, p.T, d, p.Z, q.Z);
-#else
-  fe_mul(a, t, q.YpX);
-  fe_mul(b, t2, q.YmX);
-  fe_mul(c, q.T2d, p.T);
-  fe_mul(d, p.Z, q.Z);
-#endif
   fe_neg(t, c); fe_select(c, c, t, neg);
   fe_add(d, d, d);
   fe_sub(r.X, a, b);
@@ -113,15 +85,8 @@ TMED_HD void ge_add_cached(ge_p1p1 &r, const ge_p3 &p, const ge_cached &q, bool 
   fe_select(qm, q.YmX, q.YpX, neg);
   fe_add(t, p.Y, p.X);
   fe_sub(t2, p.Y, p.X);
-#if TMED_ADD_X2
   fe_mul_x2(a, t, qp, b, t2, qm);
   fe_mul_x2(c, q.T2d, p.T, d, p.Z, q.Z);
-#else
-  fe_mul(a, t, qp);
-  fe_mul(b, t2, qm);
-  fe_mul(c, q.T2d, p.T);
-  fe_mul(d, p.Z, q.Z);
-#endif
   fe_neg(t, c); fe_select(c, c, t, neg);
   fe_add(d, d, d);
   fe_sub(r.X, a, b);
@@ -137,12 +102,7 @@ TMED_HD void ge_madd_niels(ge_p1p1 &r, const ge_p3 &p, const ge_niels &q, bool n
   fe_select(qm, q.YmX, q.YpX, neg);
   fe_add(t, p.Y, p.X);
   fe_sub(t2, p.Y, p.X);
-#if TMED_ADD_X2
   fe_mul_x2(a, t, qp, b, t2, qm);
-#else
-  fe_mul(a, t, qp);
-  fe_mul(b, t2, qm);
-#endif
   fe_mul(c, q.XY2d, p.T);
   fe_neg(t, c); fe_select(c, c, t, neg);
   fe_add(d, p.Z, p.Z);

@@ -13,8 +13,8 @@
 //   combs key-set combs [key][window][entry] and the shared combs of B (radix 256, radix 2^16)
 #include "kernels.h"
 #ifndef TMED_SLAB_PF
-#define TMED_SLAB_PF 1  // A/B knob: where the per-lane table rows are loaded (verify_hs.h hs_straus;
-                        // 1: the -A row before the last doubling, the R row before the -A addition)
+#define TMED_SLAB_PF 1  // per-lane table rows loaded ahead (verify_hs.h hs_straus): the -A row before
+                        // the last doubling, the R row before the -A addition (0: right before use)
 #endif
 #include "verify_core.h"
 #include "verify_hs.h"

@@ -375,13 +375,12 @@ TMED_HD void hs_straus(ge_p2 &out, const DS &ds, const uint32_t er[8], int W, TA
         ge_p1p1_to_p2(q, t);
       }
       if (TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc, dc < 0);  // the row load overlaps the last doubling
-      if (TMED_SLAB_PF == 2) tr.prefetch(dd < 0 ? -dd : dd, dd < 0);
       ge_p2_dbl(t, q);
       ge_p1p1_to_p3(r, t);
     }
     if (!TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc, dc < 0);
     ta.take(ca);
-    if (TMED_SLAB_PF == 1 || (TMED_SLAB_PF == 2 && n == W - 1)) tr.prefetch(dd < 0 ? -dd : dd, dd < 0);  // overlaps the A addition
+    if (TMED_SLAB_PF) tr.prefetch(dd < 0 ? -dd : dd, dd < 0);  // the row load overlaps the A addition
     ge_add_cached_pre(t, r, ca, dc < 0);
     ge_p1p1_to_p3(r, t);
     if (!TMED_SLAB_PF) tr.prefetch(dd < 0 ? -dd : dd, dd < 0);

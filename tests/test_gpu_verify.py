@@ -121,6 +121,14 @@ def test_full_size_property(engine):
     engine.verify_device(d_pub, d_sig, d_msg, d_off, d_out, n)
     torch.cuda.synchronize()
     assert int(d_out.sum().item()) == n
+    # the half-size hand-off is placed by window count (kernels.hip verify_prep_r_kernel): the
+    # waves' loop length stays within ~0.1 window of the lanes' own mean (unplaced: ~0.7 above)
+    lh, wh = engine.window_stats()
+    ws = np.arange(65)
+    assert int(lh.sum()) == n and int(wh.sum()) == n // 64 and int(lh[64]) == 0
+    lane_mean, wave_mean = float((lh * ws).sum()) / n, float((wh * ws).sum()) / (n // 64)
+    assert 32.0 < lane_mean < 33.0 and wave_mean - lane_mean < 0.3, (lane_mean, wave_mean)
+    assert int(wh[32]) > n // 64 // 4
     d_sig[:, 40] ^= 1
     engine.verify_device(d_pub, d_sig, d_msg, d_off, d_out, n)
     torch.cuda.synchronize()
