@@ -171,7 +171,10 @@ __device__ __forceinline__ bool prep_load(const int4 *prep, uint32_t stride, uin
 
 // Phase 1: SHA-512(R||A||M) mod L, S < L, A = Point.SetBytes(pub)  (one lane per signature
 // of the chunk [base, base + count)).
-__global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_prep_kernel(
+#ifndef TMED_PREP_WAVES
+#define TMED_PREP_WAVES 3  // 168 VGPRs, 59 spilled: -20 us per 2^20 against 2 waves (kernel-trace A/B)
+#endif
+__global__ __launch_bounds__(kThreadsPerBlock, TMED_PREP_WAVES) void verify_prep_kernel(
     const uint8_t *__restrict__ pub, const uint8_t *__restrict__ sig, MsgSrc ms, uint32_t base, uint32_t count,
     int4 *__restrict__ prep, uint32_t stride, uint32_t *__restrict__ place) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
@@ -250,7 +253,10 @@ constexpr int kPrepHsInt4 = 16;
 constexpr int kHsWSmall = 32;
 static_assert((kPrepInt4 + kPrepHsInt4) * 16 <= kPrepSlotBytes, "prep slot too small for the half-size hand-off");
 
-__global__ __launch_bounds__(kThreadsPerBlock) void verify_prep_r_kernel(
+#ifndef TMED_PREP_R_WAVES
+#define TMED_PREP_R_WAVES 3  // 168 VGPRs, 20 spilled: -0.06 ms per 2^20 against 2 waves (the Euclid loop hides its memory waits)
+#endif
+__global__ __launch_bounds__(kThreadsPerBlock, TMED_PREP_R_WAVES) void verify_prep_r_kernel(
     const uint8_t *__restrict__ sig, uint32_t base, uint32_t count, const int4 *__restrict__ prep,
     int4 *__restrict__ prep2, uint32_t stride, uint32_t *__restrict__ place) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
