@@ -124,10 +124,13 @@ struct Plan {
   bool decided = false;
   int64_t needed = 0;
   int32_t panic_idx = -1;         // the loop panics on reaching this signature (TMED_COMMIT_PANIC)
-  int32_t *bit_of_sig = nullptr;  // sig idx -> candidate slot in its planning part (-1 = not sent)
+  int32_t *bit_of_sig = nullptr;  // sig idx -> candidate slot in its planning part (-1 = not sent,
+                                  // kNoValidator = Trusting: the address is not in the set)
   size_t cand_off = 0;            // + the part's offset in the merged candidate list
-  const AddrIndex *addr_index = nullptr;  // Trusting only (shared by requests on the same valset)
+  // Trusting: the double vote the loop stops at (sig idx, validator, first sig idx), -1 = none
+  int32_t dv_idx = -1, dv_val = -1, dv_first = -1;
 };
+constexpr int32_t kNoValidator = -2;
 
 // Growable array without value-initialisation (every element is written before use).
 template <class T>
@@ -229,14 +232,21 @@ struct CandBatch {
 using BatchVerifier =
     std::function<int(const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands, uint8_t *valid)>;
 
-// Per-request CanonicalVote encoders for the requests that have candidates.
+// Per-request CanonicalVote encoders for the requests that have candidates; then(q, enc)
+// runs right after request q's encoder is built (false = failure).  Candidates are in request
+// order, so the first candidate of each request marks it used (one writer per request).
+template <class Then>
 static int init_encoders(const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands,
-                         std::vector<tmed::VoteEncoder> &enc, std::vector<uint8_t> &used) {
+                         std::vector<tmed::VoteEncoder> &enc, std::vector<uint8_t> &used, Then &&then) {
   enc.assign(n, tmed::VoteEncoder());
   used.assign(n, 0);
-  for (const Cand &cd : cands) used[cd.req] = 1;
+  const size_t m = cands.size();
+  parallel_ranges(m, host_threads(m), [&](size_t lo, size_t hi, unsigned) {
+    for (size_t k = lo; k < hi; k++)
+      if (k == 0 || cands[k].req != cands[k - 1].req) used[cands[k].req] = 1;
+  });
   std::atomic<int> bad{0};
-  parallel_ranges(n, n >= 64 ? host_threads(cands.size()) : 1, [&](size_t lo, size_t hi, unsigned) {
+  parallel_ranges(n, n >= 64 ? host_threads(m) : 1, [&](size_t lo, size_t hi, unsigned) {
   for (size_t q = lo; q < hi; q++) {
     if (!used[q]) continue;
     const tmed_commit &c = *reqs[q].commit;
@@ -250,7 +260,7 @@ static int init_encoders(const tmed_commit_request *reqs, size_t n, const std::v
     t.psh_total = c.block_id.psh_total;
     t.psh_hash = c.block_id.psh_hash;
     t.psh_hash_len = c.block_id.psh_hash_len;
-    if (enc[q].init(&t) != TMED_OK) bad = 1;
+    if (enc[q].init(&t) != TMED_OK || !then(q, enc[q])) bad = 1;
   }
   });
   return bad ? TMED_EINVAL : TMED_OK;
@@ -260,7 +270,7 @@ static int init_encoders(const tmed_commit_request *reqs, size_t n, const std::v
 static int build_cand_batch(const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands,
                             CandBatch &cb) {
   std::vector<uint8_t> used;
-  int rc = init_encoders(reqs, n, cands, cb.enc, used);
+  int rc = init_encoders(reqs, n, cands, cb.enc, used, [](size_t, const tmed::VoteEncoder &) { return true; });
   if (rc != TMED_OK) return rc;
   const size_t m = cands.size();
   cb.m = m;
@@ -294,30 +304,23 @@ static int build_cand_batch(const tmed_commit_request *reqs, size_t n, const std
 
 // ---- planning: prechecks + candidate selection, parallel over requests ----------------
 
-// Address indexes for every LightTrusting valset of the call (built once, read-only after).
-using AddrCache = std::unordered_map<const tmed_valset *, std::unique_ptr<AddrIndex>>;
-
-
-static void build_addr_cache(const tmed_commit_request *reqs, size_t n, AddrCache &cache) {
-  std::vector<std::pair<const tmed_valset *, AddrIndex *>> todo;
-  size_t work = 0;
-  for (size_t q = 0; q < n; q++) {
-    const tmed_commit_request &r = reqs[q];
-    if (r.mode != TMED_MODE_LIGHT_TRUSTING || !r.vals) continue;
-    auto &slot = cache[r.vals];
-    if (slot) continue;
-    slot.reset(new AddrIndex());
-    todo.emplace_back(r.vals, slot.get());
-    work += r.vals->n;
+// Address index of the Trusting set being planned, owned by one planning thread: rebuilt
+// when that thread moves to a request on another set (within one seam call only, so a
+// caller may rewrite its buffers between calls).  The plan records every lookup result the
+// replay needs (the candidate's validator, kNoValidator, the double vote), so the index is
+// never read after planning.
+struct AddrScratch {
+  AddrIndex ix;
+  const tmed_valset *of = nullptr;
+  const AddrIndex &get(const tmed_valset &vs) {
+    if (of != &vs) { ix.build(vs.addresses, vs.n); of = &vs; }
+    return ix;
   }
-  parallel_ranges(todo.size(), host_threads(work), [&](size_t lo, size_t hi, unsigned) {
-    for (size_t t = lo; t < hi; t++) todo[t].second->build(todo[t].first->addresses, todo[t].first->n);
-  });
-}
+};
 
 // Plan one request; candidates are appended to `cands` and bit_of_sig holds their index there.
 static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_result &o, Plan &pl,
-                        std::vector<Cand> &cands, const AddrCache &cache) {
+                        std::vector<Cand> &cands, AddrScratch &addr) {
   const tmed_commit_request &r = reqs[q];
   memset(&o, 0, sizeof o);
   int rc = check_request(r);
@@ -365,15 +368,18 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
     int64_t prod;
     if (safe_mul(vs.total_power, r.trust_num, &prod)) { o.code = TMED_COMMIT_OVERFLOW; pl.decided = true; return TMED_OK; }
     pl.needed = prod / r.trust_den;  // Go int64 division truncates toward zero, as C++ does
-    pl.addr_index = cache.at(r.vals).get();
+    const AddrIndex &ix = addr.get(vs);
     thread_local SeenMarks seen;
     seen.reset(vs.n);
     int64_t tally = 0;
     for (size_t i = 0; i < c.n_sigs; i++) {
       if (c.flags[i] != kCommit) continue;
-      const int32_t v = lookup_address(*pl.addr_index, c, i);
-      if (v < 0) continue;
-      if (seen.get(v) >= 0) break;  // the loop returns the double-vote error here
+      const int32_t v = lookup_address(ix, c, i);
+      if (v < 0) { pl.bit_of_sig[i] = kNoValidator; continue; }
+      if (seen.get(v) >= 0) {  // the loop returns the double-vote error here
+        pl.dv_idx = (int32_t)i; pl.dv_val = v; pl.dv_first = seen.get(v);
+        break;
+      }
       seen.set(v, (int32_t)i);
       if (!bid_ok) { pl.panic_idx = (int32_t)i; break; }
       pl.bit_of_sig[i] = (int32_t)cands.size();
@@ -463,7 +469,7 @@ static size_t total_sigs(const tmed_commit_request *reqs, size_t n) {
 
 // Candidates of requests [0, n) in request order (identical to a serial plan).
 static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, Plans &ps,
-                     std::vector<Cand> &cands, AddrCache &cache) {
+                     std::vector<Cand> &cands) {
   PhaseClock clk;
   std::vector<Plan> &plans = ps.v;
   plans.assign(n, Plan());
@@ -480,12 +486,11 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
     nbits += reqs[q].commit->n_sigs;
   }
   clk.lap("check");
-  build_addr_cache(reqs, n, cache);
-  clk.lap("addr_cache");
   const unsigned nt = host_threads(total_sigs(reqs, n));
   if (nt <= 1) {
+    AddrScratch addr;
     for (size_t q = 0; q < n; q++) {
-      int rc = plan_request(reqs, q, out[q], plans[q], cands, cache);
+      int rc = plan_request(reqs, q, out[q], plans[q], cands, addr);
       if (rc != TMED_OK) return rc;
     }
     return TMED_OK;
@@ -500,7 +505,10 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
     size_t cap = 0;
     for (size_t q = lo; q < hi; q++) cap += reqs[q].commit->n_sigs;
     part[t].reserve(cap);
-    for (size_t q = lo; q < hi && rcs[t] == TMED_OK; q++) rcs[t] = plan_request(reqs, q, out[q], plans[q], part[t], cache);
+    AddrScratch addr;
+    for (size_t q = lo; q < hi && rcs[t] == TMED_OK; q++) {
+      rcs[t] = plan_request(reqs, q, out[q], plans[q], part[t], addr);
+    }
   });
   for (int rc : rcs)
     if (rc != TMED_OK) return rc;
@@ -521,7 +529,8 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
 
 // ---- replay of every reference loop over the validity bits (parallel over requests) ----
 
-static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, const Plan &pl, const uint8_t *valid) {
+static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, const Plan &pl, const Cand *cands,
+                          const uint8_t *valid) {
   const tmed_valset &vs = *r.vals;
   const tmed_commit &c = *r.commit;
   auto bit = [&](size_t i, bool *ok) -> bool {
@@ -560,20 +569,16 @@ static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, c
     }
     if (o.code < 0 && ok) { o.code = TMED_COMMIT_NOT_ENOUGH_POWER; o.got = tally; o.needed = pl.needed; }
   } else {
-    thread_local SeenMarks seen;
-    seen.reset(vs.n);
+    // the plan resolved every address up to where its loop stopped, and the replay stops no later
     for (size_t i = 0; i < c.n_sigs && o.code < 0; i++) {
-      if (c.flags[i] != kCommit) continue;
-      const int32_t v = lookup_address(*pl.addr_index, c, i);
-      if (v < 0) continue;
-      if (seen.get(v) >= 0) {
-        o.code = TMED_COMMIT_DOUBLE_VOTE; o.val_idx = v; o.idx_first = seen.get(v); o.idx = (int32_t)i;
+      if (c.flags[i] != kCommit || pl.bit_of_sig[i] == kNoValidator) continue;
+      if ((int32_t)i == pl.dv_idx) {
+        o.code = TMED_COMMIT_DOUBLE_VOTE; o.val_idx = pl.dv_val; o.idx_first = pl.dv_first; o.idx = (int32_t)i;
         break;
       }
-      seen.set(v, (int32_t)i);
       if (panics(i)) break;
       if (!bit(i, &ok)) { if (ok) { o.code = TMED_COMMIT_WRONG_SIGNATURE; o.idx = (int32_t)i; } break; }
-      tally += vs.powers[v];
+      tally += vs.powers[cands[pl.cand_off + (size_t)pl.bit_of_sig[i]].val_idx];
       if (tally > pl.needed) o.code = TMED_COMMIT_OK;
     }
     if (o.code < 0 && ok) { o.code = TMED_COMMIT_NOT_ENOUGH_POWER; o.got = tally; o.needed = pl.needed; }
@@ -582,14 +587,14 @@ static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, c
 }
 
 static int seam_replay(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out,
-                       const Plans &ps, const uint8_t *valid) {
+                       const Plans &ps, const std::vector<Cand> &cands, const uint8_t *valid) {
   const std::vector<Plan> &plans = ps.v;
   const unsigned nt = host_threads(total_sigs(reqs, n));
   std::vector<int> rcs(std::max(1u, nt), TMED_OK);
   parallel_ranges(n, nt, [&](size_t lo, size_t hi, unsigned t) {
     for (size_t q = lo; q < hi; q++) {
       if (plans[q].decided) continue;
-      if (replay_request(reqs[q], out[q], plans[q], valid) != TMED_OK) rcs[t] = TMED_EINVAL;
+      if (replay_request(reqs[q], out[q], plans[q], cands.data(), valid) != TMED_OK) rcs[t] = TMED_EINVAL;
     }
   });
   for (int rc : rcs)
@@ -608,8 +613,7 @@ static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_resul
   PhaseClock clk;
   Plans plans;
   std::vector<Cand> cands;
-  AddrCache cache;
-  int rc = seam_plan(reqs, n, out, plans, cands, cache);
+  int rc = seam_plan(reqs, n, out, plans, cands);
   if (rc != TMED_OK) return rc;
   clk.lap("plan");
   const auto t1 = clock::now();
@@ -622,7 +626,7 @@ static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_resul
   }
   clk.lap("verify");
   const auto t2 = clock::now();
-  rc = seam_replay(reqs, n, out, plans, valid.data());
+  rc = seam_replay(reqs, n, out, plans, cands, valid.data());
   clk.lap("replay");
   clk.emit("seam", n, m);
   const auto t3 = clock::now();
@@ -747,14 +751,15 @@ static int device_templates(const tmed_commit_request *reqs, size_t n, const std
                             std::vector<uint8_t> &tmpl, bool *fits) {
   std::vector<tmed::VoteEncoder> enc;
   std::vector<uint8_t> used;
-  int rc = init_encoders(reqs, n, cands, enc, used);
-  if (rc != TMED_OK) return rc;
-  tmpl.assign(n * tmed::kVoteTmplBytes, 0);
+  tmpl.resize(n * tmed::kVoteTmplBytes);  // rows of requests without candidates are never read
   std::atomic<bool> ok{true};
-  parallel_ranges(n, n >= 64 ? host_threads(cands.size()) : 1, [&](size_t lo, size_t hi, unsigned) {
-    for (size_t q = lo; q < hi; q++)
-      if (used[q] && !enc[q].device_template(&tmpl[q * tmed::kVoteTmplBytes], tmed::kVoteTmplBytes)) ok = false;
+  int rc = init_encoders(reqs, n, cands, enc, used, [&](size_t q, const tmed::VoteEncoder &e) {
+    uint8_t *row = &tmpl[q * tmed::kVoteTmplBytes];
+    memset(row, 0, tmed::kVoteTmplBytes);
+    if (!e.device_template(row, tmed::kVoteTmplBytes)) ok = false;
+    return true;
   });
+  if (rc != TMED_OK) return rc;
   *fits = ok;
   return TMED_OK;
 }
@@ -840,7 +845,6 @@ struct BsBatch {
   size_t lo = 0, n = 0;
   Plans plans;
   std::vector<Cand> cands;
-  AddrCache cache;
   std::vector<uint8_t> tmpl, bits, valid;
   tmed::VoteStage st;
   bool device = false;  // queued on a vote slot (else verified synchronously / nothing to verify)
@@ -872,7 +876,7 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
     }
     const auto t1 = clock::now();
     if (b.device) scatter_bits(reqs + b.lo, b.cands, nullptr, (uint32_t)m, b.bits.data(), b.valid.data());
-    int r = seam_replay(reqs + b.lo, b.n, out + b.lo, b.plans, b.valid.data());
+    int r = seam_replay(reqs + b.lo, b.n, out + b.lo, b.plans, b.cands, b.valid.data());
     ph[2] += us(t1, clock::now());
     b.n = 0;
     b.device = false;
@@ -888,7 +892,7 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
     b.n = std::min(bsz, nb - lo);
     const tmed_commit_request *rq = reqs + lo;
     const auto tp = clock::now();
-    rc = seam_plan(rq, b.n, out + lo, b.plans, b.cands, b.cache);
+    rc = seam_plan(rq, b.n, out + lo, b.plans, b.cands);
     clk.lap("plan");
     const size_t m = b.cands.size();
     b.valid.assign(m, 0);
