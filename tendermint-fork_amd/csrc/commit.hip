@@ -537,7 +537,8 @@ static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, c
     const int32_t k = pl.bit_of_sig[i];
     if (k < 0) { *ok = false; return false; }
     o.verified++;
-    return valid[pl.cand_off + (size_t)k] != 0;
+    // a signature of any length but 64 is false (ed25519.go:150-152), whatever the verifier said
+    return valid[pl.cand_off + (size_t)k] != 0 && (!c.sig_lens || c.sig_lens[i] == 64);
   };
   auto panics = [&](size_t i) -> bool {
     if ((int32_t)i != pl.panic_idx) return false;
@@ -875,8 +876,9 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
       if (r != TMED_OK) return r;
     }
     const auto t1 = clock::now();
-    if (b.device) scatter_bits(reqs + b.lo, b.cands, nullptr, (uint32_t)m, b.bits.data(), b.valid.data());
-    int r = seam_replay(reqs + b.lo, b.n, out + b.lo, b.plans, b.cands, b.valid.data());
+    // the device bits are in candidate order: replay reads them directly (it applies the
+    // signature-length rule itself)
+    int r = seam_replay(reqs + b.lo, b.n, out + b.lo, b.plans, b.cands, b.device ? b.bits.data() : b.valid.data());
     ph[2] += us(t1, clock::now());
     b.n = 0;
     b.device = false;
@@ -895,7 +897,6 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
     rc = seam_plan(rq, b.n, out + lo, b.plans, b.cands);
     clk.lap("plan");
     const size_t m = b.cands.size();
-    b.valid.assign(m, 0);
     bool fits = true;
     if (rc == TMED_OK && m) rc = device_templates(rq, b.n, b.cands, b.tmpl, &fits);
     clk.lap("templates");
@@ -910,6 +911,7 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
       } else {  // oversize template: host-assembled messages, synchronous (drain the pipeline first)
         rc = finish(prev);
         lk.unlock();
+        b.valid.assign(m, 0);
         if (rc == TMED_OK) rc = ctx_verify_host_msgs(ctx, rq, b.n, b.cands, b.valid.data());
         lk.lock();
       }
