@@ -97,7 +97,10 @@ int tmed_sign_batch_device(tmed_ctx *ctx, const uint8_t *d_seeds, const uint8_t 
  */
 int tmed_window_stats(tmed_ctx *ctx, uint32_t lane_hist[65], uint32_t wave_hist[65]);
 
-/* Device time (ms) of the last verify/sign launch on this context (HIP events). */
+/* Device time (ms) of the last verify/sign launch on this context (HIP events).  A commit batch
+ * small enough for the zero-copy latency mode (a single commit), or a tmed_verify_batch of at most
+ * 1024 signatures, reports 0 unless kernel timing is on (tmed_set_kernel_timing): its events would
+ * add ~8 us to the call. */
 float tmed_last_kernel_ms(tmed_ctx *ctx);
 
 /*

@@ -92,9 +92,12 @@ struct VoteStage {
   int64_t *sec = nullptr;
   int32_t *nan = nullptr;
   bool zc = false;  // the kernels read the pinned staging buffer directly (votes_enqueue)
+  bool timed = true;  // kernel-time events recorded (tmed_last_kernel_ms)
 };
 // staged-vote batches up to this size skip the copies (kernels read / write pinned host memory)
 constexpr size_t kVoteZeroCopyMax = 256u << 10;
+// Raw host batches of at most this many signatures record no kernel-time events by default.
+constexpr size_t kLatencyUntimedMax = 1024;
 int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st, int slot = 0);
 int votes_enqueue(tmed_ctx *c, VoteStage &st);
 int votes_collect(tmed_ctx *c, const VoteStage &st, uint8_t *out);

@@ -129,7 +129,10 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
     e = hipMemcpyAsync(d, vs.h_votes.p, st.total, hipMemcpyHostToDevice, s);
   }
   if (e == hipSuccess) e = scratch_acquire(c, s);
-  if (e == hipSuccess) e = hipEventRecord(vs.ev0, s);
+  // Timing events cost ~8 us of a single commit's latency (C1 generic 249 -> 239 us, keyed
+  // 97 -> 88 us): a zero-copy batch records them only under tmed_set_kernel_timing.
+  st.timed = !st.zc || c->timing;
+  if (e == hipSuccess && st.timed) e = hipEventRecord(vs.ev0, s);
   // the latency kernels (generic and key-cached) assemble the sign-bytes in their hash lanes (no
   // launch in front)
   const VoteAsm va{d + st.o_tmpl, (const uint32_t *)(d + st.o_tidx), d + st.o_flag, (const int64_t *)(d + st.o_sec),
@@ -146,7 +149,7 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
       e = generic_verify(c, d + st.o_key, d + st.o_sig, (const uint8_t *)vs.d_vmsg.p, (const uint32_t *)vs.d_off.p, m,
                          out_dev, s, /*msg_slots=*/true, nullptr, fused ? &va : nullptr);
   }
-  if (e == hipSuccess) e = hipEventRecord(vs.ev1, s);
+  if (e == hipSuccess && st.timed) e = hipEventRecord(vs.ev1, s);
   if (e == hipSuccess) e = scratch_release(c, s);
   if (e == hipSuccess && !st.zc) e = hipMemcpyAsync(vs.h_out.p, vs.d_out.p, m, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipEventRecord(vs.done, s);
@@ -157,7 +160,8 @@ int votes_collect(tmed_ctx *c, const VoteStage &st, uint8_t *out) {
   VoteSlot &vs = c->vslot[st.slot];
   hipError_t e = hipEventSynchronize(vs.done);  // this slot only: a later batch may be queued behind it
   if (e != hipSuccess) return map_err(e);
-  (void)hipEventElapsedTime(&c->last_ms, vs.ev0, vs.ev1);
+  c->last_ms = 0.f;
+  if (st.timed) (void)hipEventElapsedTime(&c->last_ms, vs.ev0, vs.ev1);
   memcpy(out, vs.h_out.p, st.m);
   return TMED_OK;
 }
