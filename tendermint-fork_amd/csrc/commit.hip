@@ -707,7 +707,10 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
   int rc = tmed::votes_stage(ctx, keyset, m, n, st, slot);
   if (rc != TMED_OK) return rc;
   memcpy(st.tmpl, tmpl, n * tmed::kVoteTmplBytes);
+  std::atomic<bool> key_ok{true};
+  const uint32_t nkeys = keyed ? (uint32_t)st.ks->n : 0u;
   auto fill = [&](size_t lo, size_t hi, unsigned) {
+    bool ok = true;
     for (size_t j = lo; j < hi; j++) {
       const Cand &cd = cands[ix ? ix[j] : j];
       const tmed_commit_request &r = reqs[cd.req];
@@ -715,6 +718,7 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
       const size_t i = (size_t)cd.sig_idx;
       if (keyed) {
         const uint32_t v = r.vals->keyset_index ? r.vals->keyset_index[cd.val_idx] : (uint32_t)cd.val_idx;
+        ok = ok && v < nkeys;
         memcpy(st.key + j * 4, &v, 4);
       } else {
         memcpy(st.key + j * 32, r.vals->pubkeys + 32 * (size_t)cd.val_idx, 32);
@@ -728,8 +732,11 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
       st.sec[j] = c.ts_seconds[i];
       st.nan[j] = c.ts_nanos[i];
     }
+    if (!ok) key_ok = false;
   };
   parallel_ranges(m, host_threads(m), fill);
+  if (!key_ok) return TMED_EINVAL;  // a key-set index past the key set (votes_enqueue's check)
+  st.keys_checked = keyed;
   return TMED_OK;
 }
 

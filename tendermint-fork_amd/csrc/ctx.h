@@ -93,6 +93,7 @@ struct VoteStage {
   int32_t *nan = nullptr;
   bool zc = false;  // the kernels read the pinned staging buffer directly (votes_enqueue)
   bool timed = true;  // kernel-time events recorded (tmed_last_kernel_ms)
+  bool keys_checked = false;  // every key-set index < the key set's size (checked while staging)
 };
 // staged-vote batches up to this size skip the copies (kernels read / write pinned host memory)
 constexpr size_t kVoteZeroCopyMax = 256u << 10;

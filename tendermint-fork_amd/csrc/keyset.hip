@@ -54,6 +54,7 @@ int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteSta
   st.m = m;
   st.n_tmpl = n_tmpl;
   st.ks = nullptr;
+  st.keys_checked = false;
   if (keyset) {
     auto it = c->keysets.find(keyset);
     if (it == c->keysets.end()) return TMED_ENOKEYSET;
@@ -94,7 +95,7 @@ int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteSta
 
 int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   const uint32_t m = st.m;
-  if (st.ks)
+  if (st.ks && !st.keys_checked)
     for (uint32_t j = 0; j < m; j++)
       if (((const uint32_t *)st.key)[j] >= st.ks->n) return TMED_EINVAL;
   VoteSlot &vs = c->vslot[st.slot];

@@ -181,6 +181,30 @@ def test_keyset_seam_and_packed_commits(engine):
         engine.keyset_free(ks)
 
 
+def test_keyset_index_past_the_key_set_is_einval(engine):
+    """A key-set index past the key set fails the whole seam call with TMED_EINVAL (checked while
+    the candidates are staged), before anything runs on the device."""
+    import numpy as np
+    from oracle.fixtures import make_block_id, make_commit, make_valset, seed_of
+    from commit_cases import to_product
+    vs, seeds = make_valset([seed_of("kx", i) for i in range(6)], [10] * 6)
+    bid = make_block_id("kx")
+    cm = make_commit(vs, seeds, "kx", 7, 0, bid)
+    pv, pc = to_product(vs, cm)
+    pubs = np.array([np.frombuffer(v.pub_key, np.uint8) for v in pv.validators])
+    ks = engine.keyset_load(pubs)
+    pv.keyset = ks
+    pv.keyset_index = np.arange(len(pubs), dtype=np.uint32)
+    pv.keyset_index[3] = len(pubs)  # one past the end
+    try:
+        with pytest.raises(T.TmedError):
+            T.verify_commits(engine, [(T.MODE_COMMIT, pv, "kx", pbid(bid), cm.height, pc, 0, 0)])
+        pv.keyset_index[3] = 3
+        assert T.verify_commits(engine, [(T.MODE_COMMIT, pv, "kx", pbid(bid), cm.height, pc, 0, 0)]) == [None]
+    finally:
+        engine.keyset_free(ks)
+
+
 @pytest.mark.parametrize("batch,chain", [(1, "bs-chain"), (3, "bs-chain"), (256, "bs-chain"), (3, "c" * 200)])
 @pytest.mark.parametrize("keyed", [False, True])
 def test_blocksync_window_matches_light_loops(engine, batch, chain, keyed):
