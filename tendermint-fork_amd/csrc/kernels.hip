@@ -181,6 +181,46 @@ __global__ __launch_bounds__(kThreadsPerBlock, TMED_PREP_WAVES) void verify_prep
   if (place && slot == 0) place[0] = place[1] = 0;  // the half-size placement counters (verify_prep_r_kernel)
   if (slot >= count) return;
   const uint32_t i = base + slot;
+#ifndef TMED_PREP_SHA_FIRST
+#define TMED_PREP_SHA_FIRST 1
+#endif
+#if TMED_PREP_SHA_FIRST
+  // verify_prep's steps with the hash first and k, s handed over at once, so the decode of A
+  // runs with only the key's words live (s keeps S when only A fails to decode: the verdict
+  // is false either way and S < L after the S checks).
+  uint32_t pw[8];
+  bool sok;
+  {
+    uint32_t sw[16], k[8], h[16];
+    load_row_words(pw, pub + 32 * (size_t)i, 2);
+    load_row_words(sw, sig + 64 * (size_t)i, 4);
+    const uint8_t *m;
+    uint32_t mlen;
+    ms.get(i, m, mlen);
+    sok = (sw[15] & 0xE0000000u) == 0 && sc_is_canonical(sw + 8);
+    sha512_stream(h, sw, pw, 64, m, mlen);
+    sc_reduce512(k, h);
+#pragma unroll
+    for (int q = 0; q < 2; q++)
+      prep[(size_t)q * stride + slot] = make_int4((int)k[4 * q], (int)k[4 * q + 1], (int)k[4 * q + 2], (int)k[4 * q + 3]);
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const uint32_t *S = sw + 8 + 4 * q;
+      prep[(size_t)(2 + q) * stride + slot] = sok ? make_int4((int)S[0], (int)S[1], (int)S[2], (int)S[3])
+                                                  : make_int4(0, 0, 0, 0);
+    }
+  }
+  ge_p3 A;
+  const bool ok = ge_frombytes_go(A, pw) && sok;  // Point.SetBytes (identity on failure)
+  int32_t w[24];
+#pragma unroll
+  for (int j = 0; j < 10; j++) { w[j] = A.X.v[j]; w[10 + j] = A.Y.v[j]; }
+  w[20] = ok ? 1 : 0;
+  w[21] = w[22] = w[23] = 0;
+#pragma unroll
+  for (int q = 0; q < 6; q++)  // words 16..39: A.x, A.y, ok
+    prep[(size_t)(4 + q) * stride + slot] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+#else
   uint32_t pw[8], sw[16], k[8], s[8];
   load_row_words(pw, pub + 32 * (size_t)i, 2);
   load_row_words(sw, sig + 64 * (size_t)i, 4);
@@ -190,6 +230,7 @@ __global__ __launch_bounds__(kThreadsPerBlock, TMED_PREP_WAVES) void verify_prep
   ge_p3 A;
   const bool ok = verify_prep(pw, sw, m, mlen, k, s, A);
   prep_store(prep, stride, slot, k, s, A, ok);
+#endif
 }
 
 // ---- f1: CanonicalVote sign-bytes assembled on the device ----------
