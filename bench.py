@@ -78,7 +78,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
                     help="GPUs of this node; without a torchrun environment bench.py starts N ranks itself")
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)  # ~2 s timed: long enough for an smi busy sample
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--sigs", type=int, default=1 << 20, help="signatures per GPU (C2: 2^20)")
     ap.add_argument("--cpu-sample", type=int, default=150_000, help="signatures timed on the 1-thread CPU baseline")
