@@ -88,6 +88,9 @@ def parse():
     ap.add_argument("--no-c1", action="store_true", help="skip the VerifyCommit p50 @175 validators leg")
     ap.add_argument("--no-keyset", action="store_true", help="skip the 10k-reused-key C2 variant")
     ap.add_argument("--c1-reps", type=int, default=1000)
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 adversarial-mix leg")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 one-GPU-shard blocksync leg")
+    ap.add_argument("--c4-blocks", type=int, default=12_500, help="C4 shard: blocks per GPU (100k blocks / 8 GPUs)")
     ap.add_argument("--mix", choices=["c2", "c5"], default="c2",
                     help="c5: 1%% of the batch replaced by edge-case / invalid tuples (BASELINE C5)")
     return ap.parse_args()
@@ -260,6 +263,12 @@ def main():
         c1 = None
         if not args.no_c1 and world == 1:
             c1 = c1_latency(eng, args.c1_reps, not args.no_cpu_baseline)
+        c5 = None
+        if not args.no_c5 and world == 1 and args.mix == "c2":
+            c5 = c5_leg(eng, dev, torch_stream, d_pub, d_sig, d_msg, d_off, msgs, offs, n, args.steps // 10 + 1)
+        c4 = None
+        if not args.no_c4 and world == 1:
+            c4 = c4_shard(eng, dev, args.c4_blocks)
         result = {
             "metric": "ed25519 verifies/sec at %d/8 MI355X" % world,
             "value": round(value, 1),
@@ -285,6 +294,8 @@ def main():
             "cpu_baseline_all_cores": cpu_all,
             "c2_keyset_variant": keyset,
             "c1_verifycommit_p50": c1,
+            "c5": c5,
+            "c4_shard": c4,
             "setup_s": round(t_gen, 2),
         }
         print(json.dumps(result), flush=True)
@@ -354,6 +365,52 @@ def c2_keyset(eng, dev, torch_stream, n, steps, warmup, peak):
                          "kernel_avg_ms": round(main_ms / max(1, ml), 4), "launches_per_step": ml,
                          "prep_kernel_ms": round(prep_ms, 4), "finish_kernel_ms": round(fin_ms, 4)},
             "config": {"workload": "C2 variant: %d signatures by %d validators (seeded), key cache on" % (n, nk)}}
+
+
+def c5_leg(eng, dev, torch_stream, d_pub, d_sig, d_msg, d_off, msgs, offs, n, steps):
+    """BASELINE C5 on the C2 batch: 1 % of the tuples replaced (seed 0x5EED) by the SURVEY §8c edge
+    classes (R/S/M bit flips, S + L, small-order A and R, non-canonical A with y >= p, R sign
+    flips) through the default generic path; verifies/s over `steps` timed passes, and the GPU's
+    decisions against the 16-thread C port on ALL n tuples (gate: 0 mismatches)."""
+    import torch
+    from tmed.workload import c5_mix
+    sys.path.insert(0, ROOT)
+    from oracle import port  # checker only
+    hp, hs = d_pub.cpu().numpy(), d_sig.cpu().numpy()
+    idx = c5_mix(hp, hs, seed=0x5EED)
+    p5, s5 = torch.from_numpy(hp).to(dev), torch.from_numpy(hs).to(dev)
+    o5 = torch.zeros(n, dtype=torch.uint8, device=dev)
+    st = torch_stream.cuda_stream
+    eng.verify_device(p5, s5, d_msg, d_off, o5, n, st)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.verify_device(p5, s5, d_msg, d_off, o5, n, st)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    gpu = o5.cpu().numpy()
+    nt = min(16, os.cpu_count() or 1)
+    t = time.perf_counter()
+    exp = port.verify_batch(hp, hs, msgs, offs.astype(np.uint64), nthreads=nt)
+    t_port = time.perf_counter() - t
+    return {"metric": "ed25519 verifies/sec at 1/8 MI355X, C5 adversarial mix", "value": round(n * steps / dt, 1),
+            "unit": "verifies/s", "steps": steps, "ms_per_step": round(dt / steps * 1e3, 3),
+            "signatures": n, "replaced": int(len(idx)), "valid": int(gpu.sum()), "expected_valid": int(exp.sum()),
+            "mismatches_vs_port": int((gpu != exp).sum()),
+            "checker": "oracle/ed25519_port.c on all %d tuples, %d threads, %.1f s" % (n, nt, t_port),
+            "config": {"workload": "C5: C2 batch with 1%% replaced by edge-case/invalid tuples, seed 0x5EED"}}
+
+
+def c4_shard(eng, dev, blocks):
+    """One GPU's share of BASELINE C4 (100k blocks / 8 GPUs): `blocks` blocks x 10,000 validators,
+    VerifyCommitLight per block through the pipelined blocksync seam (tmed_blocksync_verify),
+    key-cached; known-answer bad signatures every 97 blocks (before and after the 2/3 crossing),
+    every block's outcome checked (bench_commits.c4); verifies/s and the seam's host phases."""
+    sys.path.insert(0, ROOT)
+    import bench_commits
+    r = bench_commits.c4(eng, blocks, 10_000, 0, 1, dev, 1000, 128, corrupt_every=97)
+    r["metric"] = "blocksync replay verifies/s, one GPU's shard of C4 (VerifyCommitLight per block)"
+    return r
 
 
 def c1_latency(eng, reps, cpu):

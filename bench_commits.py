@@ -230,12 +230,35 @@ def c3(eng, headers: int, gap: int, use_keyset: bool, runs: int = 7, bisect_gap:
     return res
 
 
-def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, batch: int):
+def _c4_corrupt(commits, b0: int, every: int, upto: int):
+    """Known-answer corruption of a generated C4 window (every > 0): block b with b % every == 13
+    gets one flipped bit in the signature at index j = (b * 7919) % upto, before the 2/3 crossing
+    -> VerifyCommitLight must return "wrong signature (#j)" after verifying j + 1 signatures; block b
+    with b % every == 50 gets a flipped signature at index upto, past the crossing -> still ok, with
+    upto signatures verified (types/validator_set.go:740-761: the loop never reaches it).  Returns
+    the expected (code, idx, verified) per block."""
+    exp = []
+    for k, c in enumerate(commits):
+        b = b0 + k
+        if every and b % every == 13:
+            j = (b * 7919) % upto
+            c.sigs[j, 5] ^= 0x20
+            exp.append((4, j, j + 1))
+        else:
+            if every and b % every == 50 and upto < c.sigs.shape[0]:
+                c.sigs[upto, 40] ^= 0x01
+            exp.append((0, -1, upto))
+    return exp
+
+
+def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, batch: int, corrupt_every: int = 0):
     """Blocksync replay (BASELINE C4): VerifyCommitLight for every block of a contiguous shard
     of the chain per rank, through the pipelined blocksync seam (tmed_blocksync_verify, f4),
     key-cached.  Blocks are generated window by window on the GPU (untimed) and verified
     from host memory, as the reactor holds them; only the verification is timed.  Ranks
-    all-reduce int64 tallies and all-gather the per-block decision bitmap."""
+    all-reduce int64 tallies and all-gather the per-block decision bitmap.
+    corrupt_every > 0: known-answer bad signatures in some blocks (_c4_corrupt); every block's
+    outcome (code, error index, signatures verified) is checked against the expected one."""
     import torch
     import torch.distributed as dist
     import tmed.types as T
@@ -252,6 +275,9 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
     ok_bits = np.zeros(hi - lo, np.uint8)
     ver = 0
     dt = t_gen = 0.0
+    mism = 0
+    phase = np.zeros(3)
+    from tmed.types import seam_phase_us
     if world > 1:
         dist.barrier()
     for w0 in range(lo, hi, window):
@@ -259,16 +285,22 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
         tg = time.perf_counter()
         specs = [(seeds[order], addrs, b + 1, 0, block_id(b"c4-%d" % (b + 1)), T2023 + b, None) for b in range(w0, w1)]
         commits = sign_commits(eng, "test_chain_id", specs, sign_upto=upto)
+        exp = _c4_corrupt(commits, w0, corrupt_every, upto)
         win = T.BlocksyncWindow(vals, "test_chain_id", [c.block_id for c in commits], [c.height for c in commits],
                                 commits)
         t_gen += time.perf_counter() - tg
         t0 = time.perf_counter()
         win.run(eng, batch)
         dt += time.perf_counter() - t0
-        ok_bits[w0 - lo:w1 - lo] = win.codes() == 0
-        ver += int(win.verified().sum())
+        phase += np.asarray(seam_phase_us(), np.float64)
+        codes, vers = win.codes(), win.verified()
+        ok_bits[w0 - lo:w1 - lo] = codes == 0
+        ver += int(vers.sum())
+        for h, (ec, ei, ev) in enumerate(exp):
+            if codes[h] != ec or vers[h] != ev or (ec == 4 and win.res[h].idx != ei):
+                mism += 1
         del win, commits
-    tally = torch.tensor([int(ok_bits.sum()), hi - lo, ver], dtype=torch.int64, device=dev)
+    tally = torch.tensor([int(ok_bits.sum()), hi - lo, ver, mism], dtype=torch.int64, device=dev)
     tm = torch.tensor([dt], dtype=torch.float64, device=dev)
     per = -(-blocks // world)                   # largest shard: equal-size bitmaps for the all-gather
     bits = torch.from_numpy(np.packbits(np.pad(ok_bits, (0, per - (hi - lo))))).to(dev)
@@ -277,11 +309,17 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
         gathered = [torch.empty_like(bits) for _ in range(world)]
         dist.all_gather(gathered, bits)             # per-block decision bitmap
-    ok, nb, ver = (int(x) for x in tally.tolist())
+    ok, nb, ver, mism = (int(x) for x in tally.tolist())
     dt = float(tm.item())
     eng.keyset_free(vals.keyset)
+    n_bad = sum(1 for b in range(lo, hi) if corrupt_every and b % corrupt_every == 13)
     return {"metric": "blocksync replay verifies/s (VerifyCommitLight per block)", "value": round(ver / dt, 1),
-            "unit": "verifies/s", "blocks_per_s": round(nb / dt, 1), "blocks": nb, "all_ok": ok == nb,
+            "unit": "verifies/s", "blocks_per_s": round(nb / dt, 1), "blocks": nb,
+            "all_ok": ok == nb if not corrupt_every else None,
+            "blocks_ok": ok, "blocks_with_bad_signature": n_bad if world == 1 else None,
+            "outcome_mismatches": mism, "outcomes_checked": corrupt_every > 0,
+            "host_phase_ms_rank0": {"plan_and_staging": round(phase[0] / 1e3, 2), "wait_for_device": round(phase[1] / 1e3, 2),
+                                    "replay": round(phase[2] / 1e3, 2)},
             "verifies": ver, "seconds": round(dt, 4), "n_gpus": world,
             "config": {"workload": "C4: %d blocks x %d validators, VerifyCommitLight per block, key-cached, "
                                    "blocks sharded over %d GPU(s) (contiguous heights), %d-block windows, "
@@ -306,6 +344,7 @@ def main():
     ap.add_argument("--validators", type=int, default=10_000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-keyset", action="store_true")
+    ap.add_argument("--corrupt-every", type=int, default=97, help="C4: known-answer bad signatures every N blocks (0: none)")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -319,7 +358,7 @@ def main():
         elif cfg == "c3" and rank == 0:
             r = c3(eng, args.headers, args.gap, not args.no_keyset, args.runs, args.bisect_gap)
         elif cfg == "c4":
-            r = c4(eng, args.blocks, args.validators, rank, world, coll, args.window, args.batch)
+            r = c4(eng, args.blocks, args.validators, rank, world, coll, args.window, args.batch, args.corrupt_every)
         else:
             continue
         if rank == 0:

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--keys", type=int, default=10_000)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--sorted", action="store_true", help="signatures ordered by validator index (as in a commit)")
     args = ap.parse_args()
     import torch
     from tmed import Engine
@@ -43,6 +44,8 @@ def main():
     kseeds = seeds_from_tag(b"tmed-c2k-key", 0, nk)
     rng = np.random.default_rng(7 + rank)
     val_idx = rng.integers(0, nk, n).astype(np.uint32)
+    if args.sorted:
+        val_idx = np.arange(n, dtype=np.uint32) % nk
     msgs, offs = c2_messages(rank * n, n)
     d_seed = torch.from_numpy(kseeds[val_idx]).to(dev)
     d_msg = torch.from_numpy(np.concatenate([msgs, np.zeros(16, np.uint8)])).to(dev)
@@ -77,6 +80,11 @@ def main():
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     valid = int(d_out.sum().item())
+    eng.set_kernel_timing(True)
+    step()
+    torch.cuda.synchronize(dev)
+    (prep_ms, main_ms, fin_ms), (pl, ml, fl) = eng.kernel_times()
+    eng.set_kernel_timing(False)
     eng.keyset_free(ks)
     eng.close()
     if rank == 0:
@@ -86,6 +94,8 @@ def main():
             "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
             "all_valid": valid == n and ok_first == n, "keyset_build_s": round(t_ks, 3), "setup_s": round(t_gen, 2),
             "mads_per_verify_main": MADS_KEYSET_MAIN,
+            "kernel_ms": {"prep": round(prep_ms, 4), "main": round(main_ms, 4), "finish": round(fin_ms, 4)},
+            "sorted": args.sorted,
             "data": "synthetic (10k seeded keys, CanonicalVote sign-bytes, GPU RFC 8032 signer)",
             "config": {"workload": "C2 variant: %d signatures by %d validators, key cache on" % (n, nk)}}), flush=True)
 

@@ -183,12 +183,22 @@ def _go_div(a: int, b: int) -> int:
     return q if (a >= 0) == (b >= 0) else -q
 
 
+def _wrap64(x: int) -> int:
+    """int64 two's-complement wrap (Go's arithmetic on int64)."""
+    x &= (1 << 64) - 1
+    return x - (1 << 64) if x >> 63 else x
+
+
 def safe_mul(a: int, b: int):
+    """types/validator_set.go:1086-1105, with Go's wrapping: -MinInt64 == MinInt64, so for
+    b = MinInt64 (int64(Numerator) of 2^63) |b| stays negative and MaxInt64 / |b| truncates to 0."""
     if a == 0 or b == 0:
         return 0, False
-    if abs(a) > MAX_INT64 // abs(b):
+    abs_b = _wrap64(-b) if b < 0 else b
+    abs_a = _wrap64(-a) if a < 0 else a
+    if abs_a > _go_div(MAX_INT64, abs_b):
         return 0, True
-    return a * b, False
+    return _wrap64(a * b), False
 
 
 def _default_verify(pub, msg, sig):

@@ -66,12 +66,16 @@ struct PhaseClock {
   }
 };
 
-// safeMul (types/validator_set.go:1086-1105)
+// safeMul (types/validator_set.go:1086-1105), Go-exact: Go's unary minus and product wrap, so
+// -MinInt64 == MinInt64 (an int64(Numerator) of 2^63 gives |b| < 0 and MaxInt64 / |b| == 0).
+// Two's-complement wrapping through uint64 (C++ -INT64_MIN is undefined); INT64_MAX / INT64_MIN
+// is 0 in C++ as in Go (truncation), and |b| is never -1.
+static inline int64_t go_neg(int64_t x) { return (int64_t)(0 - (uint64_t)x); }
 bool safe_mul(int64_t a, int64_t b, int64_t *out) {
   if (a == 0 || b == 0) { *out = 0; return false; }
-  const int64_t ab = b < 0 ? -b : b, aa = a < 0 ? -a : a;
+  const int64_t ab = b < 0 ? go_neg(b) : b, aa = a < 0 ? go_neg(a) : a;
   if (aa > kMaxInt64 / ab) { *out = 0; return true; }
-  *out = a * b;
+  *out = (int64_t)((uint64_t)a * (uint64_t)b);
   return false;
 }
 
@@ -764,7 +768,7 @@ static int device_templates(const tmed_commit_request *reqs, size_t n, const std
   int rc = init_encoders(reqs, n, cands, enc, used, [&](size_t q, const tmed::VoteEncoder &e) {
     uint8_t *row = &tmpl[q * tmed::kVoteTmplBytes];
     memset(row, 0, tmed::kVoteTmplBytes);
-    if (!e.device_template(row, tmed::kVoteTmplBytes)) ok = false;
+    if (!e.device_template(row, tmed::kVoteTmplBytes, tmed::kVoteSlot)) ok = false;
     return true;
   });
   if (rc != TMED_OK) return rc;

@@ -353,11 +353,15 @@ __global__ __launch_bounds__(kThreadsPerBlock, TMED_PREP_R_WAVES) void verify_pr
 }
 
 // Digits of the recoded c / |d| straight from the hand-off (one dword per eight windows).
+// Lanes past count read all-zero digits (0x88888888): their hand-off positions hold a previous
+// batch's recodings, whose top digit (hs_top_digit) could leave [-8, 8] at this wave's W and
+// index past the lane's table rows.
 struct HsDigitsDev {
   const int4 *p2;
   uint32_t stride, slot;
+  bool active;
   __device__ __forceinline__ uint32_t word(int w) const {
-    return reinterpret_cast<const uint32_t *>(p2 + (size_t)(w >> 2) * stride + slot)[w & 3];
+    return active ? reinterpret_cast<const uint32_t *>(p2 + (size_t)(w >> 2) * stride + slot)[w & 3] : 0x88888888u;
   }
   __device__ __forceinline__ uint32_t cword(int w) const { return word(w); }
   __device__ __forceinline__ uint32_t dword(int w) const { return w < 5 ? word(8 + w) : 0x88888888u; }
@@ -404,7 +408,7 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_hs_kernel(
   if (W < 29) W = 29;
   if (W > 64) W = 64;
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const HsDigitsDev ds{prep2, stride, slot};
+  const HsDigitsDev ds{prep2, stride, slot, active};
   SlabTab ta{slab, slot};
   SlabTab tr{slab + (size_t)stride * 64, slot};
   B16Pf bl{comb16, sbl[wv], lane};
@@ -797,6 +801,150 @@ __global__ __launch_bounds__(kThreadsPerBlock, TMED_KS_PREP_WAVES) void verify_k
   prep_store(prep, stride, slot, k, s, dummy, ok);
 }
 
+// Key-cached Straus with the next comb row in flight (TMED_KS_PF): the 48 rows a signature
+// reads (32 from its key's radix-256 comb, 16 from the shared radix-2^16 comb of B) are random
+// 128-B lines of a multi-GB table, so a row loaded right before its addition leaves the wave
+// parked on HBM latency for most of it (rocprof: 0.35 of the mad peak, round 2).  Here the row
+// of addition t+1 is loaded into registers before addition t runs.  Schedule per 32-bit word q
+// of the recodings: A(4q), A(4q+1), B(2q), A(4q+2), A(4q+3), B(2q+1) — the same sum as
+// verify_main_comb_point<16>.  The first addition starts from the identity, so it is replaced
+// by the niels -> extended conversion (1 M instead of 7 M), and the last one stops at
+// projective (X, Y, Z) (3 M instead of 4 M for p1p1 -> p3).
+#ifndef TMED_KS_PF
+#define TMED_KS_PF 1
+#endif
+#ifndef TMED_KS_ROLL
+#define TMED_KS_ROLL 0  // 1: one addition per loop iteration (A/B of the loop body's code size)
+#endif
+struct CombRowPf {
+  int4 pv[8];
+  bool neg;
+  __device__ __forceinline__ void fetch(const int4 *row, bool n) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) pv[q] = row[q];
+    neg = n;
+  }
+  __device__ __forceinline__ void take(ge_niels &e) const {
+    fe *fs[3] = {&e.YpX, &e.YmX, &e.XY2d};
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int32_t w[4] = {pv[q].x, pv[q].y, pv[q].z, pv[q].w};
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const int f = 4 * q + c;
+        if (f < 30) fs[f / 10]->v[f % 10] = w[c];
+      }
+    }
+    niels_apply_sign(e, neg);
+  }
+};
+
+// (x, y) affine niels (y+x, y-x, 2dxy) -> extended (4x : 4y : 4 : 4xy): X = 2(a - b), Y = 2(a + b),
+// T = (a - b)(a + b) with a = y+x, b = y-x.
+__device__ __forceinline__ void ge_niels_to_p3(ge_p3 &r, const ge_niels &e) {
+  fe d, s;
+  fe_sub(d, e.YpX, e.YmX);
+  fe_add(s, e.YpX, e.YmX);
+  fe_mul(r.T, d, s);
+  fe_add(r.X, d, d);
+  fe_carry(r.X, r.X);  // the next addition's Y +- X must stay a 3-sum of carried values
+  fe_add(r.Y, s, s);
+  fe_carry(r.Y, r.Y);
+  fe_0(r.Z);
+  r.Z.v[0] = 4;
+}
+
+__device__ __forceinline__ const int4 *ks_arow(const int4 *ak, int w, uint32_t byte, bool &neg) {
+  const int d = (int)byte - 128;
+  neg = d < 0;
+  return ak + ((size_t)w * kCombEntries + (uint32_t)(neg ? -d : d)) * kCombEntryInt4;
+}
+__device__ __forceinline__ const int4 *ks_brow(const int4 *bc, int wb, uint32_t half, bool &neg) {
+  const int d = (int)half - 32768;
+  neg = d < 0;
+  return bc + ((size_t)wb * kB16Entries + (uint32_t)(neg ? -d : d)) * kCombEntryInt4;
+}
+
+// out (X : Y : Z) = [k](-A) + [s]B from the key's comb (ak) and the radix-2^16 comb of B (bc).
+__device__ __forceinline__ void keyset_straus_pf(ge_p2 &out, const uint32_t k[8], const uint32_t s[8],
+                                                 const int4 *ak, const int4 *bc) {
+  uint32_t kr[8], sr[8];
+  sc_recode256(kr, k);
+  sc_recode_b<16>(sr, s);
+  CombRowPf pf;
+  bool ng;
+  pf.fetch(ks_arow(ak, 0, kr[0] & 0xffu, ng), ng);
+  ge_p3 acc;
+  ge_p1p1 t;
+  ge_niels e;
+#if TMED_KS_ROLL
+  // one addition per iteration (small loop body); the step's role comes from uniform branches
+  uint32_t kc = kr[0], sc = sr[0];
+#pragma unroll 1
+  for (int tt = 0; tt < 48; tt++) {
+    const int q = tt / 6, st = tt - 6 * (tt / 6);
+    pf.take(e);
+    const int nx = st + 1;
+    if (nx == 6) {
+#pragma unroll
+      for (int m = 0; m < 7; m++) { kr[m] = kr[m + 1]; sr[m] = sr[m + 1]; }
+      kc = kr[0];
+      sc = sr[0];
+    }
+    const int4 *row;
+    if (nx == 6) {
+      row = ks_arow(ak, 4 * q + 4 < 32 ? 4 * q + 4 : 0, kc & 0xffu, ng);
+    } else if (nx == 2 || nx == 5) {
+      row = ks_brow(bc, 2 * q + (nx == 5), (sc >> (nx == 5 ? 16 : 0)) & 0xffffu, ng);
+    } else {
+      const int b = nx < 2 ? nx : nx - 1;
+      row = ks_arow(ak, 4 * q + b, (kc >> (8 * b)) & 0xffu, ng);
+    }
+    if (tt < 47) pf.fetch(row, ng);
+    if (tt == 0) {
+      ge_niels_to_p3(acc, e);
+    } else {
+      ge_madd_niels(t, acc, e, false);
+      if (tt == 47) ge_p1p1_to_p2(out, t);
+      else ge_p1p1_to_p3(acc, t);
+    }
+  }
+  return;
+#endif
+#pragma unroll 1
+  for (int q = 0; q < 8; q++) {
+    const uint32_t kc = kr[0], sc = sr[0];
+#pragma unroll
+    for (int m = 0; m < 7; m++) { kr[m] = kr[m + 1]; sr[m] = sr[m + 1]; }
+#pragma unroll
+    for (int st = 0; st < 6; st++) {
+      pf.take(e);
+      // the row of the next addition: A byte, A byte, B half, A, A, B, then the next word's A byte 0
+      const int nx = st + 1;
+      const int4 *row;
+      if (nx == 6) {
+        row = ks_arow(ak, 4 * q + 4 < 32 ? 4 * q + 4 : 0, kr[0] & 0xffu, ng);  // past the end: any row
+      } else if (nx == 2 || nx == 5) {
+        row = ks_brow(bc, 2 * q + (nx == 5), (sc >> (nx == 5 ? 16 : 0)) & 0xffffu, ng);
+      } else {
+        const int b = nx < 2 ? nx : nx - 1;  // byte of kc
+        row = ks_arow(ak, 4 * q + b, (kc >> (8 * b)) & 0xffu, ng);
+      }
+      if (q < 7 || st < 5) pf.fetch(row, ng);
+      if (st == 0 && q == 0) {
+        ge_niels_to_p3(acc, e);
+      } else {
+        ge_madd_niels(t, acc, e, false);
+        if (q == 7 && st == 5) {
+          ge_p1p1_to_p2(out, t);
+        } else {
+          ge_p1p1_to_p3(acc, t);
+        }
+      }
+    }
+  }
+}
+
 template <int WAVES>
 __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_keyset_main_kernel(
     const uint32_t *__restrict__ val_idx, const int4 *__restrict__ acomb, const int4 *__restrict__ bcomb,
@@ -816,10 +964,15 @@ __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_keyset_main_ke
   const bool ok = prep[(size_t)9 * stride + slot].x != 0;
 #pragma unroll
   for (int j = 0; j < 8; j++) { k[j] = (uint32_t)w[j]; s[j] = (uint32_t)w[8 + j]; }
+#if TMED_KS_PF
+  ge_p2 R;
+  keyset_straus_pf(R, k, s, acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4, bcomb);
+#else
   const GlobalComb ac{acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4};
   const GlobalComb16 bc{bcomb};
   ge_p3 R;
   verify_main_comb_point(R, k, s, ac, bc);
+#endif
   fin_store(fin, kFinCap, i - fin_base, R.X, R.Y, R.Z);
   out[i] = ok ? 1 : 0;
 }

@@ -23,8 +23,9 @@ struct VoteEncoder {
   uint8_t *write(uint8_t *out, int flag, int64_t sec, int32_t nanos) const;
   // Device template record for the on-device assembler (kernels.h kVoteTmplBytes):
   // [pre_len, bid_field_len, cid_field_len, 0] + pre + BlockID field + chain-id field.
-  // Returns false if it does not fit in `cap` bytes (very long chain IDs: host path).
-  bool device_template(uint8_t *out, size_t cap) const;
+  // Returns false if it does not fit in `cap` bytes, or if a vote's message could exceed `slot`
+  // bytes (the device writes vote i at i * slot): long chain IDs take the host path.
+  bool device_template(uint8_t *out, size_t cap, size_t slot) const;
 };
 
 }  // namespace tmed

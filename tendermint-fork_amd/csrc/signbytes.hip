@@ -94,9 +94,14 @@ uint8_t *VoteEncoder::write(uint8_t *w, int flag, int64_t sec, int32_t nanos) co
   return w;
 }
 
-bool VoteEncoder::device_template(uint8_t *out, size_t cap) const {
+bool VoteEncoder::device_template(uint8_t *out, size_t cap, size_t slot) const {
   const size_t need = 4 + (size_t)pre_len + (size_t)bid_field + (size_t)cid_field;
   if (need > cap || bid_field > 255 || cid_field > 255) return false;
+  // the longest message of this template: a Commit-flag vote whose timestamp has a 10-byte seconds
+  // varint and a 10-byte nanos varint (any int32 nanos crosses the ABI; negative ones are 10 bytes),
+  // i.e. ts_body <= 22 and the timestamp field <= 24 bytes
+  const size_t max_body = (size_t)pre_len + (size_t)bid_field + 24 + (size_t)cid_field;
+  if ((size_t)uvarint_len(max_body) + max_body > slot) return false;
   out[0] = (uint8_t)pre_len;
   out[1] = (uint8_t)bid_field;
   out[2] = (uint8_t)cid_field;

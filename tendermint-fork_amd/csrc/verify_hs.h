@@ -364,8 +364,9 @@ TMED_HD void hs_straus(ge_p2 &out, const DS &ds, const uint32_t er[8], int W, TA
     const int sh = 4 * (n & 7);
     int dc = (int)((cw >> sh) & 15u) - 8, dd = (int)((dw >> sh) & 15u) - 8;
     if (n == W - 1) {
-      dc = hs_top_digit(cw, (W & 7) ? cw : ds.cword(W >> 3), W);
-      dd = hs_top_digit(dw, (W & 7) ? dw : ds.dword(W >> 3), W);
+      // word W >> 3 holds nibble W; at W = 64 (the (k, 1) fallback) there is none and no carry
+      dc = hs_top_digit(cw, W < 64 ? ((W & 7) ? cw : ds.cword(W >> 3)) : 0u, W);
+      dd = hs_top_digit(dw, W < 64 ? ((W & 7) ? dw : ds.dword(W >> 3)) : 0u, W);
       ge_p3_0(r);
       if (TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc, dc < 0);
     } else {

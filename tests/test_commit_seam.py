@@ -182,3 +182,36 @@ def test_bad_mode_and_missing_block_id_return_einval():
         T.verify_commits(None, [(7, pv, "ei-chain", pbid(bid), 7, pc, 0, 0)], verifier=oracle_verifier)
     with pytest.raises(TmedError):  # VerifyCommit / Light need a BlockID
         T.verify_commits(None, [(T.MODE_LIGHT, pv, "ei-chain", None, 7, pc, 0, 0)], verifier=oracle_verifier)
+
+
+def test_safe_mul_wraps_like_go():
+    """safeMul (types/validator_set.go:1086-1105) with Go's int64 wrapping: a trust-level Numerator of
+    2^63 reaches safeMul as int64 MinInt64, whose negation is MinInt64 again, so MaxInt64 / |b| is 0
+    and any non-zero total power overflows (VERDICT r2 hygiene).  Oracle values are Go's by hand;
+    the seam (csrc/commit.hip safe_mul) must give the same error for that request."""
+    from oracle import commit as C
+    MIN = -(1 << 63)
+    assert C.safe_mul(10, MIN) == (0, True)
+    assert C.safe_mul(MIN, 1) == (MIN, False)   # |MinInt64| wraps negative: no overflow, product -2^63
+    assert C.safe_mul(MIN, -1) == (MIN, False)  # Go: MinInt64 * -1 wraps to MinInt64
+    assert C.safe_mul(3, -4) == (-12, False)
+    assert C.safe_mul(1 << 62, 2) == (0, True)
+    assert C.safe_mul(0, MIN) == (0, False)
+    vs, pv, cm, pc, bid = _one_commit()
+    exp = C.verify_commit_light_trusting(vs, "ei-chain", cm, MIN, 3)
+    assert "int64 overflow" in str(exp)
+    got = T.verify_commits(None, [(T.MODE_LIGHT_TRUSTING, pv, "ei-chain", None, 0, pc, MIN, 3)],
+                           verifier=oracle_verifier)[0]
+    assert same(got, exp), (got, exp)
+
+
+def test_edge_sign_bytes_host_encoder_cpu():
+    """The commits of tests/test_gpu_signbytes_edges.py (zero time.Time, epoch, nanos 999,999,999,
+    negative seconds, psh_total >= 2^28, heights >= 2^56, round 2^31-1, empty / 50 / 120 / 140-byte
+    chain IDs, Nil and Absent flags) through the seam with the host-side encoder (csrc/signbytes.hip
+    via tmed_verify_commits_with): equal to the oracle loops, the control commit included."""
+    from test_gpu_signbytes_edges import _requests
+    reqs, exp, _ = _requests(None)
+    got = T.verify_commits(None, reqs, verifier=oracle_verifier)
+    bad = [(q, str(g), str(e)) for q, (g, e) in enumerate(zip(got, exp)) if not same(g, e)]
+    assert not bad, bad

@@ -85,9 +85,12 @@ def test_c5_mix(vengine):
 def test_odd_slab_and_chunk_sizes(slots, chunk):
     """TMED_SLAB_SLOTS / TMED_CHUNK that are not multiples of the 256-lane block: the
     context rounds them up, so every lane of every launched block owns a slab slot and a batch
-    larger than the slab runs as several chunks with decisions equal to the oracle."""
+    larger than the slab runs as several chunks with decisions equal to the oracle.  TMED_GLAT_MAX=0
+    sends the batch through the throughput kernels (prep / prep_r / main chunks), not the latency
+    kernels that take small batches by default."""
     from tmed import Engine
-    saved = {k: os.environ.get(k) for k in ("TMED_SLAB_SLOTS", "TMED_CHUNK")}
+    saved = {k: os.environ.get(k) for k in ("TMED_SLAB_SLOTS", "TMED_CHUNK", "TMED_GLAT_MAX")}
+    os.environ["TMED_GLAT_MAX"] = "0"
     os.environ["TMED_SLAB_SLOTS"] = slots
     if chunk:
         os.environ["TMED_CHUNK"] = chunk
@@ -110,5 +113,38 @@ def test_odd_slab_and_chunk_sizes(slots, chunk):
         out = e.verify_arrays(pubs, sigs, msgs, offs.astype(np.uint32))
         exp = port.verify_batch(pubs, sigs, msgs, offs, 16)
         assert int((out != exp).sum()) == 0 and exp.sum() == n - len(range(0, n, 7))
+    finally:
+        e.close()
+
+
+def test_partial_chunk_after_full_slab():
+    """A full-slab batch, then batches of slab_slots - k: the lanes past count in the
+    last wave of verify_main_hs_kernel sit on hand-off positions that still hold the previous
+    batch's recodings; they must run on zero digits (HsDigitsDev.active) and the decisions of the
+    short batch must equal the oracle's."""
+    from tmed import Engine
+    saved = {k: os.environ.get(k) for k in ("TMED_SLAB_SLOTS", "TMED_GLAT_MAX")}
+    os.environ["TMED_GLAT_MAX"] = "0"
+    os.environ["TMED_SLAB_SLOTS"] = "2048"
+    try:
+        e = Engine(0)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    try:
+        n = 2048
+        rng = np.random.default_rng(123)
+        seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        offs = (np.arange(n + 1) * 114).astype(np.uint64)
+        msgs = rng.integers(0, 256, int(offs[-1]) + 16, dtype=np.uint8)
+        sigs, pubs = e.sign_arrays(seeds, msgs, offs.astype(np.uint32))
+        sigs[::5, 33] ^= 0x10
+        exp = port.verify_batch(pubs, sigs, msgs, offs, 16)
+        for m in (n, n - 1, n - 63, n - 200, n - 255, n, 1800):
+            out = e.verify_arrays(pubs[:m], sigs[:m], msgs, offs[: m + 1].astype(np.uint32))
+            assert int((out != exp[:m]).sum()) == 0, m
     finally:
         e.close()
