@@ -251,14 +251,17 @@ def _c4_corrupt(commits, b0: int, every: int, upto: int):
     return exp
 
 
-def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, batch: int, corrupt_every: int = 0):
+def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, batch: int, corrupt_every: int = 0,
+       pregen: bool = False):
     """Blocksync replay (BASELINE C4): VerifyCommitLight for every block of a contiguous shard
     of the chain per rank, through the pipelined blocksync seam (tmed_blocksync_verify, f4),
     key-cached.  Blocks are generated window by window on the GPU (untimed) and verified
     from host memory, as the reactor holds them; only the verification is timed.  Ranks
     all-reduce int64 tallies and all-gather the per-block decision bitmap.
     corrupt_every > 0: known-answer bad signatures in some blocks (_c4_corrupt); every block's
-    outcome (code, error index, signatures verified) is checked against the expected one."""
+    outcome (code, error index, signatures verified) is checked against the expected one.
+    pregen: generate every window of the shard before the timed part and start the ranks' timed
+    parts together (the host rehearsal: no rank's generation competes with another's seam)."""
     import torch
     import torch.distributed as dist
     import tmed.types as T
@@ -280,15 +283,16 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
     from tmed.types import seam_phase_us
     if world > 1:
         dist.barrier()
-    for w0 in range(lo, hi, window):
-        w1 = min(hi, w0 + window)
-        tg = time.perf_counter()
+    def gen(w0, w1):
         specs = [(seeds[order], addrs, b + 1, 0, block_id(b"c4-%d" % (b + 1)), T2023 + b, None) for b in range(w0, w1)]
         commits = sign_commits(eng, "test_chain_id", specs, sign_upto=upto)
         exp = _c4_corrupt(commits, w0, corrupt_every, upto)
         win = T.BlocksyncWindow(vals, "test_chain_id", [c.block_id for c in commits], [c.height for c in commits],
                                 commits)
-        t_gen += time.perf_counter() - tg
+        return win, exp, commits
+
+    def run(w0, w1, win, exp):
+        nonlocal dt, ver, mism, phase
         t0 = time.perf_counter()
         win.run(eng, batch)
         dt += time.perf_counter() - t0
@@ -299,16 +303,40 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
         for h, (ec, ei, ev) in enumerate(exp):
             if codes[h] != ec or vers[h] != ev or (ec == 4 and win.res[h].idx != ei):
                 mism += 1
-        del win, commits
-    tally = torch.tensor([int(ok_bits.sum()), hi - lo, ver, mism], dtype=torch.int64, device=dev)
-    tm = torch.tensor([dt], dtype=torch.float64, device=dev)
-    per = -(-blocks // world)                   # largest shard: equal-size bitmaps for the all-gather
-    bits = torch.from_numpy(np.packbits(np.pad(ok_bits, (0, per - (hi - lo))))).to(dev)
+
+    if pregen:  # every window of the shard generated first, then all ranks verify together
+        wins = []
+        tg = time.perf_counter()
+        for w0 in range(lo, hi, window):
+            w1 = min(hi, w0 + window)
+            wins.append((w0, w1) + gen(w0, w1))
+        t_gen += time.perf_counter() - tg
+        if world > 1:
+            dist.barrier()
+        for w0, w1, win, exp, _ in wins:
+            run(w0, w1, win, exp)
+        del wins
+    else:
+        for w0 in range(lo, hi, window):
+            w1 = min(hi, w0 + window)
+            tg = time.perf_counter()
+            win, exp, commits = gen(w0, w1)
+            t_gen += time.perf_counter() - tg
+            run(w0, w1, win, exp)
+            del win, commits
+    nbatch = -(-(hi - lo) // batch) if batch else 0
+    ph_all = [phase]
     if world > 1:
         dist.all_reduce(tally)                      # int64 tallies
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
         gathered = [torch.empty_like(bits) for _ in range(world)]
         dist.all_gather(gathered, bits)             # per-block decision bitmap
+        pt = torch.tensor(list(phase) + [dt, nbatch], dtype=torch.float64, device=dev)
+        pg = [torch.empty_like(pt) for _ in range(world)]
+        dist.all_gather(pg, pt)                     # per-rank host phases (diagnostics)
+        ph_all = [g.tolist() for g in pg]
+    else:
+        ph_all = [list(phase) + [dt, nbatch]]
     ok, nb, ver, mism = (int(x) for x in tally.tolist())
     dt = float(tm.item())
     eng.keyset_free(vals.keyset)
@@ -320,6 +348,10 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
             "outcome_mismatches": mism, "outcomes_checked": corrupt_every > 0,
             "host_phase_ms_rank0": {"plan_and_staging": round(phase[0] / 1e3, 2), "wait_for_device": round(phase[1] / 1e3, 2),
                                     "replay": round(phase[2] / 1e3, 2)},
+            "host_phase_per_batch_ms": [{"rank": r, "plan_and_staging": round(p[0] / 1e3 / max(1, p[4]), 3),
+                                         "wait_for_device": round(p[1] / 1e3 / max(1, p[4]), 3),
+                                         "replay": round(p[2] / 1e3 / max(1, p[4]), 3),
+                                         "batches": int(p[4]), "seconds": round(p[3], 3)} for r, p in enumerate(ph_all)],
             "verifies": ver, "seconds": round(dt, 4), "n_gpus": world,
             "config": {"workload": "C4: %d blocks x %d validators, VerifyCommitLight per block, key-cached, "
                                    "blocks sharded over %d GPU(s) (contiguous heights), %d-block windows, "
@@ -345,6 +377,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-keyset", action="store_true")
     ap.add_argument("--corrupt-every", type=int, default=97, help="C4: known-answer bad signatures every N blocks (0: none)")
+    ap.add_argument("--pregen", action="store_true", help="C4: generate the whole shard before timing (host rehearsal)")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -358,7 +391,8 @@ def main():
         elif cfg == "c3" and rank == 0:
             r = c3(eng, args.headers, args.gap, not args.no_keyset, args.runs, args.bisect_gap)
         elif cfg == "c4":
-            r = c4(eng, args.blocks, args.validators, rank, world, coll, args.window, args.batch, args.corrupt_every)
+            r = c4(eng, args.blocks, args.validators, rank, world, coll, args.window, args.batch, args.corrupt_every,
+                       args.pregen)
         else:
             continue
         if rank == 0:

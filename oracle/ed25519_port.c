@@ -404,6 +404,33 @@ int port_verify(const uint8_t *pub, const uint8_t *msg, size_t mlen, const uint8
   return memcmp(rb, sig, 32) == 0;
 }
 
+/* ZIP-215 (the opt-in cofactored mode; spec/core/encoding.md:52-54 names it, the reference's code
+ * does not use it): A and R decoded permissively (Go SetBytes: y >= p and x = 0 with the sign bit
+ * accepted), S < L, k = SHA-512(R_bytes || A_bytes || M) mod L, accept iff [8]([S]B - [k]A - R) = O.
+ * Parity of this rule with the reference is unpinned (no ZIP-215 code or vectors in it). */
+int port_verify_zip215(const uint8_t *pub, const uint8_t *msg, size_t mlen, const uint8_t *sig, size_t siglen) {
+  pthread_once(&init_once, do_init);
+  if (siglen != 64) return 0;
+  ge_p3 A, R;
+  if (ge_frombytes(&A, pub) != 0) return 0;
+  if (ge_frombytes(&R, sig) != 0) return 0;
+  if (!sc_is_canonical(sig + 32)) return 0;
+  sha512_ctx c; uint8_t h[64];
+  sha512_init(&c); sha512_update(&c, sig, 32); sha512_update(&c, pub, 32); sha512_update(&c, msg, mlen); sha512_final(&c, h);
+  uint64_t k[4]; sc_from_bytes64(k, h);
+  uint8_t kb[32]; sc_tobytes(kb, k);
+  ge_p3 negA = A; fe_neg(&negA.X, &A.X); fe_neg(&negA.T, &A.T);
+  ge_p2 Q; double_scalarmult(&Q, kb, &negA, sig + 32);  /* [S]B - [k]A */
+  ge_p3 q3;                                               /* (X:Y:Z) -> (XZ : YZ : Z^2 : XY) */
+  fe_mul(&q3.X, &Q.X, &Q.Z); fe_mul(&q3.Y, &Q.Y, &Q.Z); fe_mul(&q3.Z, &Q.Z, &Q.Z); fe_mul(&q3.T, &Q.X, &Q.Y);
+  ge_cached rc; p3_to_cached(&rc, &R);
+  ge_p1p1 t; ge_add(&t, &q3, &rc, 1);                     /* - R */
+  ge_p2 d; p1p1_to_p2(&d, &t);
+  for (int i = 0; i < 3; i++) { p2_dbl(&t, &d); p1p1_to_p2(&d, &t); }
+  fe zero; fe_0(&zero);
+  return fe_eq(&d.X, &zero) && fe_eq(&d.Y, &d.Z);
+}
+
 static void scalarmult_base(uint8_t out[32], const uint8_t s[32]) {
   uint8_t zero[32] = {0}; ge_p2 R; ge_p3 id; p3_0(&id);
   double_scalarmult(&R, zero, &id, s);
@@ -452,6 +479,7 @@ static void *worker(void *p) {
   for (size_t i = j->lo; i < j->hi; i++) {
     const uint8_t *m = j->msg + j->off[i]; size_t ml = (size_t)(j->off[i + 1] - j->off[i]);
     if (j->mode == 0) j->out[i] = (uint8_t)port_verify(j->pub + 32 * i, m, ml, j->sig + 64 * i, j->siglen ? j->siglen[i] : 64);
+    else if (j->mode == 2) j->out[i] = (uint8_t)port_verify_zip215(j->pub + 32 * i, m, ml, j->sig + 64 * i, j->siglen ? j->siglen[i] : 64);
     else { port_sign(j->seeds + 32 * i, m, ml, j->sig_out + 64 * i); port_pubkey_from_seed(j->seeds + 32 * i, j->pub_out + 32 * i); }
   }
   return NULL;
@@ -476,6 +504,14 @@ void port_verify_batch(const uint8_t *pub, const uint8_t *sig, const uint32_t *s
                        const uint64_t *off, size_t n, uint8_t *out, int nthreads) {
   job_t b; memset(&b, 0, sizeof b);
   b.pub = pub; b.sig = sig; b.siglen = siglen; b.msg = msg; b.off = off; b.out = out; b.mode = 0;
+  run_jobs(b, n, nthreads);
+}
+
+/* The same under the ZIP-215 rule (port_verify_zip215). */
+void port_verify_batch_zip215(const uint8_t *pub, const uint8_t *sig, const uint32_t *siglen, const uint8_t *msg,
+                              const uint64_t *off, size_t n, uint8_t *out, int nthreads) {
+  job_t b; memset(&b, 0, sizeof b);
+  b.pub = pub; b.sig = sig; b.siglen = siglen; b.msg = msg; b.off = off; b.out = out; b.mode = 2;
   run_jobs(b, n, nthreads);
 }
 

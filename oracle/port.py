@@ -32,6 +32,10 @@ def lib():
         l.port_verify.argtypes = [P, P, ctypes.c_size_t, P, ctypes.c_size_t]
         l.port_verify_batch.restype = None
         l.port_verify_batch.argtypes = [P, P, P, P, P, ctypes.c_size_t, P, ctypes.c_int]
+        l.port_verify_batch_zip215.restype = None
+        l.port_verify_batch_zip215.argtypes = [P, P, P, P, P, ctypes.c_size_t, P, ctypes.c_int]
+        l.port_verify_zip215.restype = ctypes.c_int
+        l.port_verify_zip215.argtypes = [P, P, ctypes.c_size_t, P, ctypes.c_size_t]
         l.port_sign_batch.restype = None
         l.port_sign_batch.argtypes = [P, P, P, ctypes.c_size_t, P, P, ctypes.c_int]
         l.port_sign.argtypes = [P, P, ctypes.c_size_t, P]
@@ -62,9 +66,15 @@ def pubkey_from_seed(seed: bytes) -> bytes:
     return out.raw
 
 
+def verify_zip215(pub: bytes, msg: bytes, sig: bytes) -> bool:
+    """The opt-in ZIP-215 rule (port_verify_zip215; parity with the reference unpinned)."""
+    return bool(lib().port_verify_zip215(pub, msg, len(msg), sig, len(sig)))
+
+
 def verify_batch(pubs: np.ndarray, sigs: np.ndarray, msgs: np.ndarray, offs: np.ndarray,
-                 nthreads: int = 1, siglens: np.ndarray | None = None) -> np.ndarray:
-    """pubs: (n,32) u8, sigs: (n,64) u8, msgs: flat u8, offs: (n+1,) u64 -> (n,) u8."""
+                 nthreads: int = 1, siglens: np.ndarray | None = None, zip215: bool = False) -> np.ndarray:
+    """pubs: (n,32) u8, sigs: (n,64) u8, msgs: flat u8, offs: (n+1,) u64 -> (n,) u8.
+    zip215: the opt-in cofactored rule (port_verify_batch_zip215) instead of Go 1.18's."""
     n = pubs.shape[0]
     pubs = np.ascontiguousarray(pubs, dtype=np.uint8)
     sigs = np.ascontiguousarray(sigs, dtype=np.uint8)
@@ -72,8 +82,8 @@ def verify_batch(pubs: np.ndarray, sigs: np.ndarray, msgs: np.ndarray, offs: np.
     offs = np.ascontiguousarray(offs, dtype=np.uint64)
     out = np.zeros(n, dtype=np.uint8)
     sl = None if siglens is None else np.ascontiguousarray(siglens, dtype=np.uint32)
-    lib().port_verify_batch(_ptr(pubs), _ptr(sigs), None if sl is None else _ptr(sl), _ptr(msgs),
-                            _ptr(offs), n, _ptr(out), nthreads)
+    fn = lib().port_verify_batch_zip215 if zip215 else lib().port_verify_batch
+    fn(_ptr(pubs), _ptr(sigs), None if sl is None else _ptr(sl), _ptr(msgs), _ptr(offs), n, _ptr(out), nthreads)
     return out
 
 

@@ -146,6 +146,7 @@ struct tmed_ctx {
   tmed::HostBuf h_a, h_b, h_msg, h_off, h_out, h_c;
   tmed::VoteSlot vslot[2];
   tmed::DevBuf d_merkle_a, d_merkle_b, d_merkle_idx;  // Merkle level digests (ping-pong) + level indexes
+  tmed::DevBuf d_korder;  // key-grouped order of a key-cached batch: counts / cursors + permutation
   std::unordered_map<uint64_t, tmed::Keyset> keysets;
   uint64_t next_keyset = 1;
   // The verify scratch (slab, prep hand-off, finish buffers) is shared by every call on the

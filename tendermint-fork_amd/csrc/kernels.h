@@ -85,12 +85,25 @@ hipError_t launch_comb_bases(const uint8_t *pubs, uint32_t n, int negate, uint8_
                              hipStream_t stream);
 // comb[key] from bases[key] (n * 32 workgroups of 128 lanes).
 hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStream_t stream);
-// Key-cached verification: key index per signature into a keyset.
-hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
+// Key-cached verification: key index per signature into a keyset of nkeys keys (an index
+// >= nkeys rejects that signature).  perm (nullable, n entries of scratch) + order_scratch
+// (key_order_scratch_words): the main and finish kernels visit each chunk's signatures in
+// key-grouped order (launch_key_order per chunk); decisions still land at out[i].
+hipError_t launch_verify_keyset(const uint32_t *val_idx, uint32_t nkeys, const uint8_t *key_pub, const uint8_t *key_ok,
                                 const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                 const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
                                 int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots = false,
-                                KernelTimer *timer = nullptr);
+                                KernelTimer *timer = nullptr, uint32_t *perm = nullptr,
+                                uint32_t *order_scratch = nullptr);
+// Key-grouped visiting order of a key-cached batch (counting sort of val_idx by groups of
+// consecutive keys, indices >= nkeys last): perm[0..n) = signature indices grouped by key.
+// scratch: key_order_scratch_words(n, nkeys) u32.  The comb rows of the lanes in flight then
+// come from few keys (TLB / L2 locality across a multi-GB key set).
+constexpr uint32_t kKeyOrderMaxKeys = 1u << 24;
+uint32_t key_order_scratch_words(uint32_t n, uint32_t nkeys);
+// perm[j] = index_base + i for the signatures i of val_idx[0..n) in key-grouped order.
+hipError_t launch_key_order(const uint32_t *val_idx, uint32_t n, uint32_t nkeys, uint32_t *scratch, uint32_t *perm,
+                            uint32_t index_base, hipStream_t stream);
 
 // Window-count statistics of the last half-size chunk in the prep hand-off (count lanes):
 // d_hist[0..64] per-lane W, d_hist[65..129] per-wave maximum W.
@@ -104,7 +117,7 @@ constexpr uint32_t kLatMax = 1u << 16;
 struct VoteAsm;
 // va (vote slots only): every lane of a signature's group assembles the vote's sign-bytes into
 // its slot first (identical bytes; no separate assemble_votes launch in front).
-hipError_t launch_verify_keyset_lat(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
+hipError_t launch_verify_keyset_lat(const uint32_t *val_idx, uint32_t nkeys, const uint8_t *key_pub, const uint8_t *key_ok,
                                     const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                     const uint32_t *off, uint32_t n, uint8_t *out, int4 *fin, int4 *dec,
                                     hipStream_t stream, bool msg_slots = false, const VoteAsm *va = nullptr);

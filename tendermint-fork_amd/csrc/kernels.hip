@@ -466,6 +466,7 @@ struct FinDev {
   const uint8_t *sig;
   uint8_t *out;
   uint32_t fin_base, lane, L, m;
+  const uint32_t *perm;  // position -> signature index (key-grouped order), or null
   __device__ __forceinline__ int count() const { return lane < m ? (int)((m - lane + L - 1) / L) : 0; }
   __device__ __forceinline__ uint32_t slot(int j) const { return lane + (uint32_t)j * L; }
   __device__ __forceinline__ void load_z(int j, fe &z) const {
@@ -501,35 +502,39 @@ struct FinDev {
     p.v[4] = b.x; p.v[5] = b.y; p.v[6] = b.z; p.v[7] = b.w;
     p.v[8] = c.x; p.v[9] = c.y;
   }
+  __device__ __forceinline__ uint32_t sig_index(int j) const {
+    const uint32_t p = fin_base + slot(j);
+    return perm ? perm[p] : p;
+  }
   __device__ __forceinline__ void load_r(int j, uint32_t Rw[8]) const {
-    load_row_words(Rw, sig + 64 * (size_t)(fin_base + slot(j)), 2);
+    load_row_words(Rw, sig + 64 * (size_t)sig_index(j), 2);
   }
   __device__ __forceinline__ void result(int j, bool ok) const {
-    uint8_t *o = out + fin_base + slot(j);
+    uint8_t *o = out + sig_index(j);
     *o = (*o && ok) ? 1 : 0;
   }
 };
 
 __global__ __launch_bounds__(kThreadsPerBlock) void verify_finish_kernel(
     const int4 *__restrict__ fin, int4 *__restrict__ pre, const uint8_t *__restrict__ sig, uint8_t *__restrict__ out,
-    uint32_t fin_base, uint32_t L, uint32_t m) {
+    uint32_t fin_base, uint32_t L, uint32_t m, const uint32_t *__restrict__ perm) {
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
   if (lane >= L) return;
-  FinDev a{fin, pre, sig, out, fin_base, lane, L, m};
+  FinDev a{fin, pre, sig, out, fin_base, lane, L, m, perm};
   finish_group(a);
 }
 
 // Finish launch for the m signatures at fin_base: group size G = m / 65536 clamped to
 // [1, 16] (65,536 lanes keep every SIMD busy; each lane pays one inversion per group).
 hipError_t launch_finish(const int4 *fin, int4 *pre, const uint8_t *sig, uint8_t *out, uint32_t fin_base, uint32_t m,
-                         hipStream_t stream) {
+                         hipStream_t stream, const uint32_t *perm = nullptr) {
   if (m == 0) return hipSuccess;
   uint32_t G = m / 65536;
   if (G < 1) G = 1;
   if (G > kFinGroupMax) G = kFinGroupMax;
   const uint32_t L = (m + G - 1) / G;
   hipLaunchKernelGGL(verify_finish_kernel, dim3((L + kThreadsPerBlock - 1) / kThreadsPerBlock),
-                     dim3(kThreadsPerBlock), 0, stream, fin, pre, sig, out, fin_base, L, m);
+                     dim3(kThreadsPerBlock), 0, stream, fin, pre, sig, out, fin_base, L, m, perm);
   return hipGetLastError();
 }
 
@@ -782,20 +787,22 @@ __device__ void comb_sign_one(uint32_t sg[16], uint32_t pb[8], const uint32_t se
 #define TMED_KS_PREP_WAVES 3  // 168 VGPRs, 27 spilled: keyed prep 0.445 -> 0.426 ms per 2^20 (A/B)
 #endif
 __global__ __launch_bounds__(kThreadsPerBlock, TMED_KS_PREP_WAVES) void verify_keyset_prep_kernel(
-    const uint32_t *__restrict__ val_idx, const uint8_t *__restrict__ key_pub, const uint8_t *__restrict__ key_ok,
-    const uint8_t *__restrict__ sig, MsgSrc ms, uint32_t base, uint32_t count, int4 *__restrict__ prep,
-    uint32_t stride) {
+    const uint32_t *__restrict__ val_idx, uint32_t nkeys, const uint8_t *__restrict__ key_pub,
+    const uint8_t *__restrict__ key_ok, const uint8_t *__restrict__ sig, MsgSrc ms, uint32_t base, uint32_t count,
+    int4 *__restrict__ prep, uint32_t stride) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   if (slot >= count) return;
   const uint32_t i = base + slot;
-  const uint32_t v = val_idx[i];
+  const uint32_t vi = val_idx[i];
+  const bool vin = vi < nkeys;  // an index past the key set rejects the signature (row 0 is read)
+  const uint32_t v = vin ? vi : 0u;
   uint32_t pw[8], sw[16], k[8], s[8];
   load_row_words(pw, key_pub + 32 * (size_t)v, 2);
   load_row_words(sw, sig + 64 * (size_t)i, 4);
   const uint8_t *m;
   uint32_t mlen;
   ms.get(i, m, mlen);
-  const bool ok = verify_prep_comb(pw, key_ok[v] != 0, sw, m, mlen, k, s);
+  const bool ok = verify_prep_comb(pw, vin && key_ok[v] != 0, sw, m, mlen, k, s);
   ge_p3 dummy;
   ge_p3_0(dummy);
   prep_store(prep, stride, slot, k, s, dummy, ok);
@@ -947,21 +954,26 @@ __device__ __forceinline__ void keyset_straus_pf(ge_p2 &out, const uint32_t k[8]
 
 template <int WAVES>
 __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_keyset_main_kernel(
-    const uint32_t *__restrict__ val_idx, const int4 *__restrict__ acomb, const int4 *__restrict__ bcomb,
-    uint32_t base, uint32_t count, const int4 *__restrict__ prep, uint32_t stride, int4 *__restrict__ fin,
-    uint32_t fin_base, uint8_t *__restrict__ out) {
+    const uint32_t *__restrict__ val_idx, uint32_t nkeys, const int4 *__restrict__ acomb,
+    const int4 *__restrict__ bcomb, uint32_t base, uint32_t count, const int4 *__restrict__ prep, uint32_t stride,
+    int4 *__restrict__ fin, uint32_t fin_base, uint8_t *__restrict__ out, const uint32_t *__restrict__ perm) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   if (slot >= count) return;
-  const uint32_t i = base + slot;
-  const uint32_t v = val_idx[i];
+  // visiting position pos (key-grouped when perm is set: perm holds this chunk's signature
+  // indices, so the prep hand-off of signature i is at slot i - base)
+  const uint32_t pos = base + slot;
+  const uint32_t i = perm ? perm[pos] : pos;
+  const uint32_t ps = i - base;
+  const uint32_t vi = val_idx[i];
+  const uint32_t v = vi < nkeys ? vi : 0u;  // the prep kernel rejected an index past the key set
   uint32_t k[8], s[8];
-  int32_t w[40];
+  int32_t w[16];
 #pragma unroll
-  for (int q = 0; q < 5; q++) {  // k, s, (A unused), ok at word 36
-    const int4 x = prep[(size_t)q * stride + slot];
+  for (int q = 0; q < 4; q++) {  // k, s; ok at word 36
+    const int4 x = prep[(size_t)q * stride + ps];
     w[4 * q] = x.x; w[4 * q + 1] = x.y; w[4 * q + 2] = x.z; w[4 * q + 3] = x.w;
   }
-  const bool ok = prep[(size_t)9 * stride + slot].x != 0;
+  const bool ok = prep[(size_t)9 * stride + ps].x != 0;
 #pragma unroll
   for (int j = 0; j < 8; j++) { k[j] = (uint32_t)w[j]; s[j] = (uint32_t)w[8 + j]; }
 #if TMED_KS_PF
@@ -973,8 +985,110 @@ __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_keyset_main_ke
   ge_p3 R;
   verify_main_comb_point(R, k, s, ac, bc);
 #endif
-  fin_store(fin, kFinCap, i - fin_base, R.X, R.Y, R.Z);
+  fin_store(fin, kFinCap, pos - fin_base, R.X, R.Y, R.Z);
   out[i] = ok ? 1 : 0;
+}
+
+// ---- key-grouped visiting order (launch_key_order) -------------------------------------
+// A counting sort of one chunk's signatures by key group (G consecutive keys per bin, G a power
+// of two chosen so that at most kKeyBins bins exist; indices past the key set form the last
+// bin).  Random-address global atomics run far below the streaming rate on this part, so every
+// tile of kKeyTile signatures counts in LDS and touches the global counters once per non-empty
+// bin, 64 consecutive bins per wave instruction: (1) per-bin totals, (2) one block turns them
+// into bin starts, (3) each tile reserves its range of every bin and places its signatures at
+// LDS-atomic ranks inside it (the order inside a bin is irrelevant).
+constexpr uint32_t kKeyBins = 4096, kKeyTile = 4096;
+
+__device__ __forceinline__ uint32_t key_bin(uint32_t v, uint32_t nkeys, uint32_t shift) {
+  return v < nkeys ? (v >> shift) : ((nkeys - 1) >> shift) + 1;
+}
+
+__global__ __launch_bounds__(256) void key_hist_kernel(const uint32_t *__restrict__ val_idx, uint32_t n,
+                                                       uint32_t nkeys, uint32_t shift, uint32_t nbins,
+                                                       uint32_t *__restrict__ total) {
+  __shared__ uint32_t h[kKeyBins];
+  for (uint32_t b = threadIdx.x; b < nbins; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  const uint32_t t0 = blockIdx.x * kKeyTile;
+  for (uint32_t j = threadIdx.x; j < kKeyTile; j += blockDim.x) {
+    const uint32_t i = t0 + j;
+    if (i < n) atomicAdd(&h[key_bin(val_idx[i], nkeys, shift)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nbins; b += blockDim.x)
+    if (h[b]) atomicAdd(&total[b], h[b]);
+}
+
+// Exclusive prefix sum of cnt[0..m) in place, one 1024-lane block (m <= kKeyBins): lane t scans
+// a contiguous run, the run totals are scanned in LDS, then the runs are rebased.
+__global__ __launch_bounds__(1024) void key_scan_kernel(uint32_t *__restrict__ cnt, uint32_t m) {
+  __shared__ uint32_t tot[1024];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (m + 1023) / 1024, lo = t * per, hi = lo + per < m ? lo + per : m;
+  uint32_t s = 0;
+  for (uint32_t j = lo; j < hi; j++) s += cnt[j];
+  tot[t] = s;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan of the run totals
+    const uint32_t x = t >= o ? tot[t - o] : 0u;
+    __syncthreads();
+    tot[t] += x;
+    __syncthreads();
+  }
+  uint32_t acc = t ? tot[t - 1] : 0u;
+  for (uint32_t j = lo; j < hi; j++) {
+    const uint32_t c = cnt[j];
+    cnt[j] = acc;
+    acc += c;
+  }
+}
+
+__global__ __launch_bounds__(256) void key_scatter_kernel(const uint32_t *__restrict__ val_idx, uint32_t n,
+                                                          uint32_t nkeys, uint32_t shift, uint32_t nbins,
+                                                          uint32_t *__restrict__ cursor, uint32_t index_base,
+                                                          uint32_t *__restrict__ perm) {
+  __shared__ uint32_t h[kKeyBins];
+  for (uint32_t b = threadIdx.x; b < nbins; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  const uint32_t t0 = blockIdx.x * kKeyTile;
+  for (uint32_t j = threadIdx.x; j < kKeyTile; j += blockDim.x) {
+    const uint32_t i = t0 + j;
+    if (i < n) atomicAdd(&h[key_bin(val_idx[i], nkeys, shift)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nbins; b += blockDim.x)
+    h[b] = h[b] ? atomicAdd(&cursor[b], h[b]) : 0u;  // this tile's range of bin b
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < kKeyTile; j += blockDim.x) {
+    const uint32_t i = t0 + j;
+    if (i < n) perm[atomicAdd(&h[key_bin(val_idx[i], nkeys, shift)], 1u)] = index_base + i;
+  }
+}
+
+static uint32_t key_shift(uint32_t nkeys) {
+  uint32_t shift = 0;
+  while (((nkeys - 1) >> shift) + 2 > kKeyBins) shift++;
+  return shift;
+}
+
+uint32_t key_order_scratch_words(uint32_t n, uint32_t nkeys) {
+  (void)n;
+  return ((nkeys - 1) >> key_shift(nkeys)) + 2;
+}
+
+hipError_t launch_key_order(const uint32_t *val_idx, uint32_t n, uint32_t nkeys, uint32_t *scratch, uint32_t *perm,
+                            uint32_t index_base, hipStream_t stream) {
+  if (nkeys == 0 || nkeys > kKeyOrderMaxKeys) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  const uint32_t shift = key_shift(nkeys), nbins = ((nkeys - 1) >> shift) + 2;
+  const uint32_t ntiles = (n + kKeyTile - 1) / kKeyTile;
+  hipError_t e = hipMemsetAsync(scratch, 0, (size_t)nbins * 4, stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(key_hist_kernel, dim3(ntiles), dim3(256), 0, stream, val_idx, n, nkeys, shift, nbins, scratch);
+  hipLaunchKernelGGL(key_scan_kernel, dim3(1), dim3(1024), 0, stream, scratch, nbins);
+  hipLaunchKernelGGL(key_scatter_kernel, dim3(ntiles), dim3(256), 0, stream, val_idx, n, nkeys, shift, nbins, scratch,
+                     index_base, perm);
+  return hipGetLastError();
 }
 
 hipError_t launch_comb_bases(const uint8_t *pubs, uint32_t n, int negate, uint8_t *ok, int32_t *bases,
@@ -1006,7 +1120,8 @@ __device__ __forceinline__ void shfl_down_fe(fe &o, const fe &f, int L) {
 }
 
 __global__ __launch_bounds__(64) void verify_keyset_lat_kernel(
-    const uint32_t *__restrict__ val_idx, const uint8_t *__restrict__ key_pub, const uint8_t *__restrict__ key_ok,
+    const uint32_t *__restrict__ val_idx, uint32_t nkeys, const uint8_t *__restrict__ key_pub,
+    const uint8_t *__restrict__ key_ok,
     const int4 *__restrict__ acomb, const int4 *__restrict__ bcomb, const uint8_t *__restrict__ sig, MsgSrc ms,
     uint32_t m, uint32_t nR, int4 *__restrict__ fin, int4 *__restrict__ dec, uint8_t *__restrict__ out, VoteAsm va,
     int assemble) {
@@ -1031,14 +1146,16 @@ __global__ __launch_bounds__(64) void verify_keyset_lat_kernel(
   const int r = (int)(threadIdx.x % kLatLanes);
   if (g >= m) return;  // whole 8-lane groups leave together: the shuffles stay inside live groups
   if (assemble) assemble_vote(va, g, const_cast<uint8_t *>(ms.msgs), const_cast<uint32_t *>(ms.off), tl[threadIdx.x]);
-  const uint32_t v = val_idx[g];
+  const uint32_t vi = val_idx[g];
+  const bool vin = vi < nkeys;  // an index past the key set rejects the signature (row 0 is read)
+  const uint32_t v = vin ? vi : 0u;
   uint32_t pw[8], sw[16], k[8], s[8], kr[8], sr[8];
   load_row_words(pw, key_pub + 32 * (size_t)v, 2);
   load_row_words(sw, sig + 64 * (size_t)g, 4);
   const uint8_t *msg;
   uint32_t mlen;
   ms.get(g, msg, mlen);
-  const bool ok = verify_prep_comb(pw, key_ok[v] != 0, sw, msg, mlen, k, s);
+  const bool ok = verify_prep_comb(pw, vin && key_ok[v] != 0, sw, msg, mlen, k, s);
   sc_recode256(kr, k);
   sc_recode256(sr, s);
   const GlobalComb ac{acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4};
@@ -1084,7 +1201,7 @@ __global__ __launch_bounds__(kThreadsPerBlock) void verify_lat_finish_kernel(con
   out[i] = ok ? 1 : 0;
 }
 
-hipError_t launch_verify_keyset_lat(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
+hipError_t launch_verify_keyset_lat(const uint32_t *val_idx, uint32_t nkeys, const uint8_t *key_pub, const uint8_t *key_ok,
                                     const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                     const uint32_t *off, uint32_t n, uint8_t *out, int4 *fin, int4 *dec,
                                     hipStream_t stream, bool msg_slots, const VoteAsm *va) {
@@ -1093,17 +1210,18 @@ hipError_t launch_verify_keyset_lat(const uint32_t *val_idx, const uint8_t *key_
   if (va && !msg_slots) return hipErrorInvalidValue;
   const MsgSrc ms{msgs, off, msg_slots};
   const uint32_t nR = (n + 63) / 64, nC = (n + 64 / kLatLanes - 1) / (64 / kLatLanes);
-  hipLaunchKernelGGL(verify_keyset_lat_kernel, dim3(nR + nC), dim3(64), 0, stream, val_idx, key_pub, key_ok, acomb,
+  hipLaunchKernelGGL(verify_keyset_lat_kernel, dim3(nR + nC), dim3(64), 0, stream, val_idx, nkeys, key_pub, key_ok, acomb,
                      bcomb, sig, ms, n, nR, fin, dec, out, va ? *va : VoteAsm{}, va ? 1 : 0);
   hipLaunchKernelGGL(verify_lat_finish_kernel, dim3((n + kThreadsPerBlock - 1) / kThreadsPerBlock),
                      dim3(kThreadsPerBlock), 0, stream, fin, dec, n, out);
   return hipGetLastError();
 }
 
-hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub, const uint8_t *key_ok,
+hipError_t launch_verify_keyset(const uint32_t *val_idx, uint32_t nkeys, const uint8_t *key_pub, const uint8_t *key_ok,
                                 const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                 const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
-                                int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots, KernelTimer *timer) {
+                                int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots, KernelTimer *timer,
+                                uint32_t *perm, uint32_t *order_scratch) {
   const MsgSrc ms{msgs, off, msg_slots};
   if (stride > kFinCap) stride = kFinCap;
   if (timer) timer->mark(stream, -1);
@@ -1112,8 +1230,12 @@ hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub,
     for (uint32_t base = fbase; base < fbase + m; base += stride) {
       const uint32_t count = (fbase + m - base) < stride ? (fbase + m - base) : stride;
       const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
+      if (perm) {  // key-grouped visiting order of this chunk (main + finish)
+        hipError_t e = launch_key_order(val_idx + base, count, nkeys, order_scratch, perm + base, base, stream);
+        if (e != hipSuccess) return e;
+      }
       hipLaunchKernelGGL(verify_keyset_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx,
-                         key_pub, key_ok, sig, ms, base, count, prep, stride);
+                         nkeys, key_pub, key_ok, sig, ms, base, count, prep, stride);
       if (timer) timer->mark(stream, 0);
       static const int ks_waves = [] {  // A/B: waves/SIMD the key-cached main kernel is compiled for
         const char *v = getenv("TMED_KS_WAVES");
@@ -1121,15 +1243,15 @@ hipError_t launch_verify_keyset(const uint32_t *val_idx, const uint8_t *key_pub,
       }();
       if (ks_waves >= 3)
         hipLaunchKernelGGL(verify_keyset_main_kernel<3>, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx,
-                           acomb, bcomb, base, count, prep, stride, fin, fbase, out);
+                           nkeys, acomb, bcomb, base, count, prep, stride, fin, fbase, out, perm);
       else
         hipLaunchKernelGGL(verify_keyset_main_kernel<2>, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx,
-                           acomb, bcomb, base, count, prep, stride, fin, fbase, out);
+                           nkeys, acomb, bcomb, base, count, prep, stride, fin, fbase, out, perm);
       if (timer) timer->mark(stream, 1);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
-    hipError_t e = launch_finish(fin, fin_pre, sig, out, fbase, m, stream);
+    hipError_t e = launch_finish(fin, fin_pre, sig, out, fbase, m, stream, perm);
     if (timer) timer->mark(stream, 2);
     if (e != hipSuccess) return e;
   }

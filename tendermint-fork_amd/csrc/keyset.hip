@@ -34,6 +34,19 @@ void free_keyset(Keyset &k) {
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Key-grouped visiting order for the throughput kernels (launch_key_order): the comb rows a
+// signature reads are random 128-B lines of its key's 528-KB comb; with the signatures of a
+// 10k-key set in random order the lanes in flight span the whole 5.3 GB and the main kernel
+// ran 3.27 ms per 2^20 against 2.02 ms with them in key order (profiles/r03/s3).  Env
+// TMED_KEY_ORDER=0 turns it off.
+static bool key_order_on(const Keyset &k, uint32_t n) {
+  static const bool on = [] {
+    const char *v = getenv("TMED_KEY_ORDER");
+    return !(v && v[0] == '0');
+  }();
+  return on && n >= 4096 && k.n > 1 && k.n <= kKeyOrderMaxKeys;
+}
+
 // Key-cached batch on the context's stream: latency kernels for small batches (C1: one
 // commit), the throughput kernels (prep / comb main / batched finish) above c->lat_max.
 static hipError_t keyset_verify(tmed_ctx *c, const Keyset &k, const uint32_t *d_idx, const uint8_t *d_sig,
@@ -41,12 +54,22 @@ static hipError_t keyset_verify(tmed_ctx *c, const Keyset &k, const uint32_t *d_
                                 hipStream_t s, bool msg_slots, const VoteAsm *va = nullptr) {
   c->last_hs_count = 0;  // d_prep now holds another path's hand-off (tmed_window_stats)
   if (n <= c->lat_max)
-    return launch_verify_keyset_lat(d_idx, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb, d_sig, d_msgs, d_off, n, d_out,
+    return launch_verify_keyset_lat(d_idx, (uint32_t)k.n, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb, d_sig, d_msgs, d_off, n, d_out,
                                     c->d_fin, c->d_fin_pre, s, msg_slots, va);
   if (va) return hipErrorInvalidValue;
-  return launch_verify_keyset(d_idx, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb16, d_sig, d_msgs, d_off, n, d_out, c->d_prep,
-                              c->slab_slots, c->d_fin, c->d_fin_pre, s, msg_slots,
-                              (c->timing && !msg_slots) ? &c->timer : nullptr);
+  KernelTimer *timer = (c->timing && !msg_slots) ? &c->timer : nullptr;
+  uint32_t *perm = nullptr, *scratch = nullptr;
+  if (key_order_on(k, n)) {
+    const size_t sw = key_order_scratch_words(n, (uint32_t)k.n);
+    hipError_t e = c->d_korder.ensure((sw + (size_t)n) * 4);
+    if (e != hipSuccess) return e;
+    scratch = (uint32_t *)c->d_korder.p;
+    perm = scratch + sw;
+  }
+  // (the key order runs in front of each chunk's prep and is charged to prep by the timer)
+  return launch_verify_keyset(d_idx, (uint32_t)k.n, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb16, d_sig, d_msgs, d_off, n,
+                              d_out, c->d_prep, c->slab_slots, c->d_fin, c->d_fin_pre, s, msg_slots, timer, perm,
+                              scratch);
 }
 
 int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st, int slot) {

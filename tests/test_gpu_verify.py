@@ -215,3 +215,49 @@ def test_keyset_golden_and_random(keyset_engine, golden):
         assert (out == exp).all() and exp.sum() == n - len(range(0, n, 97))
     finally:
         engine.keyset_free(h)
+
+
+@pytest.mark.parametrize("lat_max", [0, 1 << 16])
+def test_keyset_key_order_and_bad_indices(lat_max):
+    """The throughput kernels visit a key-cached batch in key-grouped order (launch_key_order,
+    n >= 4096): 20k signatures by 500 keys in random order must give the port's decisions at
+    their own indices.  Through the device entry point (no host validation of val_idx) indices
+    past the key set (500, 2^32 - 1) reject their signature instead of reading past the combs —
+    in the throughput kernels (TMED_LAT_MAX=0) and in the latency kernels."""
+    import torch
+    from conftest import engine_with_env
+    eng = engine_with_env(TMED_LAT_MAX=lat_max)
+    rng, seeds, msgs, offs = _random_batch(500, 91, (110, 125))
+    _, pubs = port.sign_batch(seeds, msgs, offs, 8)
+    h = eng.keyset_load(pubs)
+    try:
+        n = 20_000
+        vi = rng.integers(0, 500, n).astype(np.uint32)
+        lens = rng.integers(100, 160, n)
+        o2 = np.zeros(n + 1, np.uint64)
+        o2[1:] = np.cumsum(lens)
+        m2 = rng.integers(0, 256, int(o2[-1]) + 16, dtype=np.uint8)
+        sig2, _ = port.sign_batch(seeds[vi], m2, o2, 16)
+        sig2[::101, 9] ^= 4
+        exp = port.verify_batch(pubs[vi], sig2, m2, o2, 16)
+        out = eng.verify_keyset_arrays(h, vi, sig2, m2, o2.astype(np.uint32))
+        assert int((out != exp).sum()) == 0
+        bad = np.arange(7, n, 997)
+        vi_bad = vi.copy()
+        vi_bad[bad[::2]] = 500
+        vi_bad[bad[1::2]] = 0xFFFFFFFF
+        exp_bad = exp.copy()
+        exp_bad[bad] = 0
+        dev = torch.device("cuda", 0)
+        d_vi = torch.from_numpy(vi_bad.view(np.int32)).to(dev)
+        d_sig = torch.from_numpy(sig2).to(dev)
+        d_msg = torch.from_numpy(m2).to(dev)
+        d_off = torch.from_numpy(o2.astype(np.uint32).view(np.int32)).to(dev)
+        d_out = torch.zeros(n, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
+        eng.verify_keyset_device(h, d_vi, d_sig, d_msg, d_off, d_out, n, 0)
+        torch.cuda.synchronize(dev)
+        assert int((d_out.cpu().numpy() != exp_bad).sum()) == 0
+    finally:
+        eng.keyset_free(h)
+        eng.close()
