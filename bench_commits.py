@@ -324,6 +324,10 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
             t_gen += time.perf_counter() - tg
             run(w0, w1, win, exp)
             del win, commits
+    tally = torch.tensor([int(ok_bits.sum()), hi - lo, ver, mism], dtype=torch.int64, device=dev)
+    tm = torch.tensor([dt], dtype=torch.float64, device=dev)
+    per = -(-blocks // world)                   # largest shard: equal-size bitmaps for the all-gather
+    bits = torch.from_numpy(np.packbits(np.pad(ok_bits, (0, per - (hi - lo))))).to(dev)
     nbatch = -(-(hi - lo) // batch) if batch else 0
     ph_all = [phase]
     if world > 1:
