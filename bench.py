@@ -69,9 +69,10 @@ if MAIN_VARIANT == 6:
     MADS_MAIN = (HS_W - 1) * (16 * SQ + 13 * MUL) + HS_W * 15 * MUL + 8 * 14 * MUL + 2 * MADS_TABLE_HS + 2 * MUL
     MADS_PER_VERIFY_GENERIC = MADS_MAIN + 2 * MADS_DECODE + MADS_SCALAR + 64 + 188
     MAIN_KERNEL = "verify_main_hs_kernel"
-# key-cached main kernel (C2 variant): 32 A-comb + 16 radix-2^16 B-comb mixed additions (3M),
-# each followed by p1p1->p3 (4M)
-MADS_KEYSET_MAIN = 48 * 7 * MUL
+# key-cached main kernel (C2 variant, kernels.hip keyset_straus_pf): 48 comb rows (32 of the key's
+# radix-256 comb, 16 of the radix-2^16 comb of B); the first is converted niels -> extended (1 M),
+# the next 46 are mixed additions (3 M) + p1p1 -> p3 (4 M), the last stops at projective (3 M + 3 M)
+MADS_KEYSET_MAIN = (1 + 46 * 7 + 6) * MUL
 
 
 def parse():
@@ -353,6 +354,7 @@ def c2_keyset(eng, dev, torch_stream, n, steps, warmup, peak):
     eng.set_kernel_timing(False)
     eng.keyset_free(ks)
     achieved = n * MADS_KEYSET_MAIN / (main_ms * 1e-3) / 1e12 if main_ms > 0 else None
+    traffic, traffic_src = pmc_traffic(n / max(1, ml), "verify_keyset_main_kernel")
     return {"metric": "ed25519 verifies/sec at 1/8 MI355X, key cache on (C2 variant: 10k reused keys)",
             "value": round(n * steps / dt, 1), "unit": "verifies/s", "steps": steps,
             "ms_per_step": round(dt / steps * 1e3, 3), "all_valid": valid == n and ok_first == n,
@@ -361,7 +363,10 @@ def c2_keyset(eng, dev, torch_stream, n, steps, warmup, peak):
                          "achieved": round(achieved, 3) if achieved else None,
                          "peak": round(peak, 3) if peak else None, "unit": "Tmad/s",
                          "frac": round(achieved / peak, 4) if (achieved and peak) else None,
+                         "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_source": traffic_src,
                          "mads_per_verify_main": MADS_KEYSET_MAIN,
+                         "visiting_order": "key-grouped (launch_key_order, charged to prep_kernel_ms)",
                          "kernel_avg_ms": round(main_ms / max(1, ml), 4), "launches_per_step": ml,
                          "prep_kernel_ms": round(prep_ms, 4), "finish_kernel_ms": round(fin_ms, 4)},
             "config": {"workload": "C2 variant: %d signatures by %d validators (seeded), key cache on" % (n, nk)}}
@@ -424,10 +429,11 @@ def c1_latency(eng, reps, cpu):
             if k in r}
 
 
-def pmc_traffic(sigs_per_launch):
-    """HBM bytes per main-kernel launch from the committed rocprofv3 --pmc summary
-    (tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE per signature, gfx950-corrected),
-    scaled to this run's launch size; (None, None) when no summary is present."""
+def pmc_traffic(sigs_per_launch, kernel=None):
+    """HBM bytes per launch of `kernel` (default: the generic main kernel) from the committed
+    rocprofv3 --pmc summary (tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE per signature,
+    gfx950-corrected), scaled to this run's launch size; (None, None) when no summary is present."""
+    kernel = kernel or MAIN_KERNEL
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as fh:
@@ -435,7 +441,7 @@ def pmc_traffic(sigs_per_launch):
     except (OSError, ValueError):
         return None, None
     for k, d in pmc.items():
-        if k.split("<")[0] == MAIN_KERNEL and "hbm_bytes_per_sig" in d:
+        if k.split("<")[0] == kernel and "hbm_bytes_per_sig" in d:
             return round(d["hbm_bytes_per_sig"] * sigs_per_launch), "profiles/pmc_summary.json[%s]" % k
     return None, None
 

@@ -350,10 +350,11 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
             "all_ok": ok == nb if not corrupt_every else None,
             "blocks_ok": ok, "blocks_with_bad_signature": n_bad if world == 1 else None,
             "outcome_mismatches": mism, "outcomes_checked": corrupt_every > 0,
-            "host_phase_ms_rank0": {"plan_and_staging": round(phase[0] / 1e3, 2), "wait_for_device": round(phase[1] / 1e3, 2),
+            "host_phase_ms_rank0": {"plan_and_staging": round(phase[0] / 1e3, 2),
+                                    "enqueue_and_wait_for_device": round(phase[1] / 1e3, 2),
                                     "replay": round(phase[2] / 1e3, 2)},
             "host_phase_per_batch_ms": [{"rank": r, "plan_and_staging": round(p[0] / 1e3 / max(1, p[4]), 3),
-                                         "wait_for_device": round(p[1] / 1e3 / max(1, p[4]), 3),
+                                         "enqueue_and_wait_for_device": round(p[1] / 1e3 / max(1, p[4]), 3),
                                          "replay": round(p[2] / 1e3 / max(1, p[4]), 3),
                                          "batches": int(p[4]), "seconds": round(p[3], 3)} for r, p in enumerate(ph_all)],
             "verifies": ver, "seconds": round(dt, 4), "n_gpus": world,

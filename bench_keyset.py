@@ -18,9 +18,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "tendermint-fork_amd"))
 
 MUL, SQ = 100, 55
-# key-cached main kernel: 32 A-comb + 16 radix-2^16 B-comb mixed additions (3M), each followed
-# by p1p1->p3 (4M)
-MADS_KEYSET_MAIN = 48 * 7 * MUL
+# key-cached main kernel (kernels.hip keyset_straus_pf): first row niels -> extended (1 M), 46 mixed
+# additions + p1p1 -> p3 (7 M), the last to projective (6 M)
+MADS_KEYSET_MAIN = (1 + 46 * 7 + 6) * MUL
 
 
 def main():

@@ -132,6 +132,30 @@ int tmed_verify_batch_keyset_device(tmed_ctx *ctx, uint64_t handle, const uint32
                                     const uint8_t *d_msgs, const uint32_t *d_msg_off, size_t n, uint8_t *d_out_valid,
                                     void *stream);
 
+/* ---------------------------------------------------------------- ZIP-215 (opt-in) */
+
+/*
+ * The OPT-IN ZIP-215 rule (spec/core/encoding.md:52-54: "Tendermint adopted zip215 for verification
+ * of ed25519 signatures ... released in 0.35"; the reference's own code, crypto/ed25519/ed25519.go:
+ * 148-155, verifies with Go 1.18's cofactorless Verify, which tmed_verify_batch reproduces and which
+ * stays the default).  Rule: A and R decoded permissively (y >= p and x = 0 with the sign bit
+ * accepted), S < L, k = SHA-512(R || A || M) mod L, accept iff [8]([S]B - R - [k]A) = O.
+ * Chunks of up to 2^20 signatures are checked as ONE randomized batch equation (Pippenger MSM with
+ * secret 127-bit weights from getrandom); a failing chunk is bisected and the failing groups are
+ * decided signature by signature by the exact single check, so out_valid[i] equals the ZIP-215
+ * single-signature decision for every i.  sig_lens as in tmed_verify_batch.
+ */
+int tmed_verify_batch_zip215(tmed_ctx *ctx, const uint8_t *pubkeys, const uint8_t *sigs, const uint32_t *sig_lens,
+                             const uint8_t *msgs, const uint32_t *msg_off, size_t n, uint8_t *out_valid);
+int tmed_verify_batch_zip215_device(tmed_ctx *ctx, const uint8_t *d_pubkeys, const uint8_t *d_sigs,
+                                    const uint8_t *d_msgs, const uint32_t *d_msg_off, size_t n, uint8_t *d_out_valid,
+                                    void *stream);
+/* Tests only: fix the batch weights' 32-byte seed for this thread's calls (NULL: getrandom again). */
+int tmed_zip215_set_seed(const uint8_t *seed32);
+/* This thread's last ZIP-215 call: chunks, batch equations evaluated, groups decided signature by
+ * signature, signatures decided singly. */
+int tmed_zip215_stats(uint32_t out[4]);
+
 /* ---------------------------------------------------------------- commits */
 
 /*

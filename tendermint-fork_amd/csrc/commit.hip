@@ -871,8 +871,9 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
                          tmed_commit_result *out) {
   BsBatch slots[2];
   int rc = TMED_OK;
-  // tmed_seam_phase_us for a pipelined call: host plan + staging, host time blocked on the
-  // device (votes_collect), host scatter + replay — the first and last overlap device work.
+  // tmed_seam_phase_us for a pipelined call: host plan + templates + staging, host time blocked on
+  // the device (enqueueing the copies and kernels, votes_collect), host replay — the first and
+  // last overlap device work.
   using clock = std::chrono::steady_clock;
   auto us = [](clock::time_point a, clock::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
   double ph[3] = {0, 0, 0};
@@ -915,10 +916,12 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
       if (fits && m <= 0xffffffffu) {
         rc = stage_group(ctx, rq, b.n, b.cands, nullptr, (uint32_t)m, keyset, b.tmpl.data(), (int)(idx & 1), b.st);
         clk.lap("stage");
+        const auto te = clock::now();
+        ph[0] += us(tp, te);
         if (rc == TMED_OK) rc = tmed::votes_enqueue(ctx, b.st);
         clk.lap("enqueue");
+        ph[1] += us(te, clock::now());  // queueing copies / launches can block behind a busy device
         b.device = rc == TMED_OK;
-        ph[0] += us(tp, clock::now());
       } else {  // oversize template: host-assembled messages, synchronous (drain the pipeline first)
         rc = finish(prev);
         lk.unlock();

@@ -71,6 +71,10 @@ int build_comb(tmed_ctx *c, const uint8_t *d_pubs, size_t n, int negate, uint8_t
 // Commit-seam device path (f1): stage votes (key refs, signatures, per-commit templates,
 // template index / flag / timestamp per vote), assemble sign-bytes on the device, verify
 // (generic when keyset == 0, key-cached otherwise), return one byte per vote.
+// Opt-in ZIP-215 rule (zip215.hip): batch equation by MSM, bisection, exact single-check fallback.
+int zip215_verify_device(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
+                         uint32_t n, uint8_t *out, hipStream_t s, bool msg_slots);
+
 int verify_votes_device(tmed_ctx *c, uint64_t keyset, const uint8_t *keys, const uint8_t *sigs,
                         const uint8_t *tmpl, size_t n_tmpl, const uint32_t *tmpl_idx, const uint8_t *flags,
                         const int64_t *ts_sec, const int32_t *ts_nanos, uint32_t m, uint8_t *out);
@@ -147,6 +151,7 @@ struct tmed_ctx {
   tmed::VoteSlot vslot[2];
   tmed::DevBuf d_merkle_a, d_merkle_b, d_merkle_idx;  // Merkle level digests (ping-pong) + level indexes
   tmed::DevBuf d_korder;  // key-grouped order of a key-cached batch: counts / cursors + permutation
+  tmed::DevBuf d_zip;     // ZIP-215 batch mode scratch (zip215.hip zip_bufs: points, digits, sort, buckets)
   std::unordered_map<uint64_t, tmed::Keyset> keysets;
   uint64_t next_keyset = 1;
   // The verify scratch (slab, prep hand-off, finish buffers) is shared by every call on the

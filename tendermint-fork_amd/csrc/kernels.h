@@ -58,7 +58,16 @@ hipError_t launch_build_bcomb16(const int32_t *d_bases, int4 *comb, hipStream_t 
 hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                          uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, BTabs btab,
                          int4 *prep, int4 *fin, int4 *fin_pre, hipStream_t stream, uint32_t chunk = 0,
-                         int main_waves = 6, bool msg_slots = false, KernelTimer *timer = nullptr);
+                         int main_waves = 6, bool msg_slots = false, KernelTimer *timer = nullptr,
+                         bool zip215 = false);
+
+// The generic prep alone (k, S checks, decode of A) for signatures [base, base + count) into prep
+// slots 0..count-1 (the ZIP-215 batch mode's first phase).
+hipError_t launch_verify_prep(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
+                              bool msg_slots, uint32_t base, uint32_t count, int4 *prep, uint32_t stride,
+                              hipStream_t stream);
+// ZIP-215 (opt-in) batch verification of device-resident tuples (zip215.hip); ctx-level.
+constexpr uint32_t kZipMax = 1u << 20;  // signatures per batch equation (one MSM)
 
 // RFC 8032 signer (synthetic commits) on the shared comb of B.
 hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t *off, uint32_t n, uint8_t *sig_out,

@@ -299,7 +299,7 @@ static_assert((kPrepInt4 + kPrepHsInt4) * 16 <= kPrepSlotBytes, "prep slot too s
 #endif
 __global__ __launch_bounds__(kThreadsPerBlock, TMED_PREP_R_WAVES) void verify_prep_r_kernel(
     const uint8_t *__restrict__ sig, uint32_t base, uint32_t count, const int4 *__restrict__ prep,
-    int4 *__restrict__ prep2, uint32_t stride, uint32_t *__restrict__ place) {
+    int4 *__restrict__ prep2, uint32_t stride, uint32_t *__restrict__ place, int zip215) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   if (slot >= count) return;
   int32_t w[64];
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(kThreadsPerBlock, TMED_PREP_R_WAVES) void verify_pr
   fe Rx, Ry;
   bool dneg;
   int W;
-  const bool rok = hs_prep_r(k, s, Rw, cr, dr, er, dneg, Rx, Ry, W);
+  const bool rok = hs_prep_r(k, s, Rw, cr, dr, er, dneg, Rx, Ry, W, zip215 != 0);
 #pragma unroll
   for (int j = 0; j < 8; j++) { w[j] = (int32_t)cr[j]; w[13 + j] = (int32_t)er[j]; }
 #pragma unroll
@@ -374,7 +374,7 @@ struct HsDigitsDev {
 // past count run on the identity and store nothing.
 __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_hs_kernel(
     uint32_t base, uint32_t count, const int4 *__restrict__ prep, const int4 *__restrict__ prep2, uint32_t stride,
-    int4 *__restrict__ slab, const int4 *__restrict__ comb16, uint8_t *__restrict__ out) {
+    int4 *__restrict__ slab, const int4 *__restrict__ comb16, uint8_t *__restrict__ out, int zip215) {
   __shared__ int4 sbl[kThreadsPerBlock / 64][8 * 64];
   __shared__ int4 sbh[kThreadsPerBlock / 64][8 * 64];
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // position in the placed hand-off
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_hs_kernel(
   SlabTab tr{slab + (size_t)stride * 64, slot};
   B16Pf bl{comb16, sbl[wv], lane};
   B16Pf bh{comb16 + (size_t)8 * kB16Entries * kCombEntryInt4, sbh[wv], lane};
-  const bool id = verify_main_hs(ds, (flags & 2) != 0, er, W, A, Rx, Ry, ta, tr, bl, bh);
+  const bool id = verify_main_hs(ds, (flags & 2) != 0, er, W, A, Rx, Ry, ta, tr, bl, bh, zip215 != 0);
   if (active) out[base + (uint32_t)w[42]] = ((flags & 1) && id) ? 1 : 0;
 }
 
@@ -571,7 +571,7 @@ uint32_t grid_for(size_t n, uint32_t max_blocks) {
 hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                          uint32_t n, uint8_t *out, int4 *slab, uint32_t slab_stride, BTabs btab,
                          int4 *prep, int4 *fin, int4 *fin_pre, hipStream_t stream, uint32_t chunk, int main_waves,
-                         bool msg_slots, KernelTimer *timer) {
+                         bool msg_slots, KernelTimer *timer, bool zip215) {
   const MsgSrc ms{msgs, off, msg_slots};
   // Chunks of at most slab_stride signatures (the per-lane tables and the prep hand-off are
   // sized for one chunk; tmed_init keeps both multiples of kThreadsPerBlock, so every lane of
@@ -579,7 +579,7 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
   // once per kFinCap block.
   if (chunk == 0 || chunk > slab_stride) chunk = slab_stride;
   if (chunk % kThreadsPerBlock != 0 || slab_stride % kThreadsPerBlock != 0) return hipErrorInvalidValue;
-  const bool hs = main_waves != 5;
+  const bool hs = main_waves != 5 || zip215;  // the ZIP-215 rule runs on the half-size path only
   // placement counters of the half-size hand-off: the tail of the prep allocation (kPrepTailBytes)
   uint32_t *place = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(prep) + (size_t)slab_stride * kPrepSlotBytes);
   if (timer) timer->mark(stream, -1);
@@ -595,10 +595,10 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
       if (hs) {  // default: half-size scalars (verify_hs.h): R decode + lattice, main; no finish
         int4 *prep2 = prep + (size_t)kPrepInt4 * slab_stride;
         hipLaunchKernelGGL(verify_prep_r_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base, count,
-                           prep, prep2, slab_stride, place);
+                           prep, prep2, slab_stride, place, zip215 ? 1 : 0);
         if (timer) timer->mark(stream, 0);
         hipLaunchKernelGGL(verify_main_hs_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base, count, prep,
-                           prep2, slab_stride, slab, btab.comb16, out);
+                           prep2, slab_stride, slab, btab.comb16, out, zip215 ? 1 : 0);
       } else {  // fallback 5: full-length Straus + batched finish
         hipLaunchKernelGGL(verify_main_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base, count, prep,
                            slab_stride, slab, btab.b16, fin, fbase, out);
@@ -612,6 +612,17 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+hipError_t launch_verify_prep(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
+                              bool msg_slots, uint32_t base, uint32_t count, int4 *prep, uint32_t stride,
+                              hipStream_t stream) {
+  if (count == 0) return hipSuccess;
+  if (count > stride) return hipErrorInvalidValue;
+  const MsgSrc ms{msgs, off, msg_slots};
+  hipLaunchKernelGGL(verify_prep_kernel, dim3((count + kThreadsPerBlock - 1) / kThreadsPerBlock),
+                     dim3(kThreadsPerBlock), 0, stream, pub, sig, ms, base, count, prep, stride, nullptr);
+  return hipGetLastError();
 }
 
 hipError_t launch_sign(const uint8_t *seeds, const uint8_t *msgs, const uint32_t *off, uint32_t n, uint8_t *sig_out,

@@ -301,9 +301,20 @@ TMED_HD void hs_scalars(const uint32_t k[8], const uint32_t s[8], uint32_t cr[8]
 // Phase 1b of the half-size path (after verify_prep's hash / S check / decode of A): strict
 // decode of R (affine; the identity when it does not decode) and hs_scalars; returns the R
 // verdict.
+// permissive (the opt-in ZIP-215 rule): R decoded like A (Point.SetBytes: y >= p and x = 0 with
+// the sign bit accepted) instead of strictly.
 TMED_HD bool hs_prep_r(const uint32_t k[8], const uint32_t s[8], const uint32_t Rw[8], uint32_t cr[8],
-                       uint32_t dr[8], uint32_t er[8], bool &dneg, fe &Rx, fe &Ry, int &W) {
-  const bool rok = r_decode_strict(Rx, Ry, Rw);
+                       uint32_t dr[8], uint32_t er[8], bool &dneg, fe &Rx, fe &Ry, int &W,
+                       bool permissive = false) {
+  bool rok;
+  if (permissive) {
+    ge_p3 P;
+    rok = ge_frombytes_go(P, Rw);
+    fe_copy(Rx, P.X);
+    fe_copy(Ry, P.Y);
+  } else {
+    rok = r_decode_strict(Rx, Ry, Rw);
+  }
   if (!rok) { fe_0(Rx); fe_1(Ry); }
   hs_scalars(k, s, cr, dr, er, dneg, W);
   return rok;
@@ -416,11 +427,24 @@ TMED_HD void hs_straus(ge_p2 &out, const DS &ds, const uint32_t er[8], int W, TA
 // (X : Y : Z) is the identity: X = 0 and Y = Z (Z != 0 for the complete formulas).
 TMED_HD bool p2_is_identity(const ge_p2 &q) { return fe_iszero(q.X) && fe_equal(q.Y, q.Z) && !fe_iszero(q.Z); }
 
+// [8] q (three doublings): the cofactored test of the opt-in ZIP-215 rule, [8][d](SB - kA - R) = O,
+// exact by the same argument as the cofactorless one ([d] with d odd permutes E[8] and is
+// injective on the order-L part).
+TMED_HD void p2_mul8(ge_p2 &q) {
+  ge_p1p1 t;
+#pragma unroll 1
+  for (int i = 0; i < 3; i++) {
+    ge_p2_dbl(t, q);
+    ge_p1p1_to_p2(q, t);
+  }
+}
+
 // Phase 2 of the half-size path: tables of -A and -sign(d) R, the 3-point sum, the
-// identity test.  A: affine extended (Z = 1, T set); R: affine (x, y).
+// identity test (of [8] times the sum when cofactor8: ZIP-215).  A: affine extended (Z = 1,
+// T set); R: affine (x, y).
 template <class DS, class TA, class TR, class BL, class BH>
 TMED_HD bool verify_main_hs(const DS &ds, bool dneg, const uint32_t er[8], int W, const ge_p3 &A, const fe &Rx,
-                            const fe &Ry, TA &ta, TR &tr, BL &bl, BH &bh) {
+                            const fe &Ry, TA &ta, TR &tr, BL &bl, BH &bh, bool cofactor8 = false) {
   ge_p3 P;  // -A (affine: the decoded key)
   fe_neg(P.X, A.X);
   fe_copy(P.Y, A.Y);
@@ -433,6 +457,7 @@ TMED_HD bool verify_main_hs(const DS &ds, bool dneg, const uint32_t er[8], int W
   build_table_affine(tr, P);
   ge_p2 q;
   hs_straus(q, ds, er, W, ta, tr, bl, bh);
+  if (cofactor8) p2_mul8(q);
   return p2_is_identity(q);
 }
 

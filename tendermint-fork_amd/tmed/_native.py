@@ -78,6 +78,10 @@ def lib() -> ctypes.CDLL:
     l.tmed_last_kernel_ms.argtypes = [P]
     l.tmed_window_stats.restype = I
     l.tmed_window_stats.argtypes = [P, P, P]
+    l.tmed_verify_batch_zip215.argtypes = [P, P, P, P, P, P, SZ, P]
+    l.tmed_verify_batch_zip215_device.argtypes = [P, P, P, P, P, SZ, P, P]
+    l.tmed_zip215_set_seed.argtypes = [P]
+    l.tmed_zip215_stats.argtypes = [P]
     _lib = l
     return l
 
@@ -92,4 +96,5 @@ EXPORTED_SYMBOLS = [
     "tmed_set_kernel_timing", "tmed_kernel_times", "tmed_blocksync_verify",
     "tmed_merkle_roots", "tmed_valset_hashes", "tmed_header_hashes", "tmed_partset_roots",
     "tmed_verify_commits_multi", "tmed_blocksync_verify_multi", "tmed_window_stats", "tmed_seam_phase_us",
+    "tmed_verify_batch_zip215", "tmed_verify_batch_zip215_device", "tmed_zip215_set_seed", "tmed_zip215_stats",
 ]

@@ -72,6 +72,47 @@ class Engine:
             raise TmedError(rc, "tmed_verify_batch")
         return out
 
+    def verify_zip215_arrays(self, pubs: np.ndarray, sigs: np.ndarray, msgs: np.ndarray, offs: np.ndarray,
+                             sig_lens: np.ndarray | None = None) -> np.ndarray:
+        """The opt-in ZIP-215 rule (tmed_verify_batch_zip215): randomized batch equation by MSM,
+        bisection, exact single-signature fallback — decisions equal the ZIP-215 single check."""
+        n = pubs.shape[0]
+        out = np.zeros(n, dtype=np.uint8)
+        if n == 0:
+            return out
+        pubs = np.ascontiguousarray(pubs, dtype=np.uint8).reshape(n, 32)
+        sigs = np.ascontiguousarray(sigs, dtype=np.uint8).reshape(n, 64)
+        msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint32)
+        sl = None if sig_lens is None else np.ascontiguousarray(sig_lens, dtype=np.uint32)
+        rc = lib().tmed_verify_batch_zip215(self._h, _p(pubs), _p(sigs), None if sl is None else _p(sl), _p(msgs),
+                                            _p(offs), n, _p(out))
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_verify_batch_zip215")
+        return out
+
+    def verify_zip215_device(self, d_pub, d_sig, d_msg, d_off, d_out, n: int, stream=None) -> None:
+        s = ctypes.c_void_p(stream) if stream else None
+        rc = lib().tmed_verify_batch_zip215_device(self._h, d_pub.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
+                                                   d_off.data_ptr(), n, d_out.data_ptr(), s)
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_verify_batch_zip215_device")
+
+    @staticmethod
+    def zip215_set_seed(seed: bytes | None) -> None:
+        """Tests only: fixed batch-weight seed for this thread (None: getrandom per call)."""
+        rc = lib().tmed_zip215_set_seed(None if seed is None else ctypes.c_char_p(bytes(seed)))
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_zip215_set_seed")
+
+    @staticmethod
+    def zip215_stats() -> dict:
+        out = (ctypes.c_uint32 * 4)()
+        rc = lib().tmed_zip215_stats(out)
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_zip215_stats")
+        return {"chunks": out[0], "equations": out[1], "single_groups": out[2], "single_sigs": out[3]}
+
     def verify_batch(self, pubs: Sequence[bytes], msgs: Sequence[bytes], sigs: Sequence[bytes]) -> np.ndarray:
         """Decisions for (pub[i], msg[i], sig[i]); sigs of any length (len != 64 -> 0)."""
         n = len(pubs)
