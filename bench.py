@@ -91,6 +91,7 @@ def parse():
     ap.add_argument("--c1-reps", type=int, default=1000)
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 adversarial-mix leg")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 one-GPU-shard blocksync leg")
+    ap.add_argument("--no-zip215", action="store_true", help="skip the opt-in ZIP-215 batch-mode leg")
     ap.add_argument("--c4-blocks", type=int, default=12_500, help="C4 shard: blocks per GPU (100k blocks / 8 GPUs)")
     ap.add_argument("--mix", choices=["c2", "c5"], default="c2",
                     help="c5: 1%% of the batch replaced by edge-case / invalid tuples (BASELINE C5)")
@@ -267,6 +268,9 @@ def main():
         c5 = None
         if not args.no_c5 and world == 1 and args.mix == "c2":
             c5 = c5_leg(eng, dev, torch_stream, d_pub, d_sig, d_msg, d_off, msgs, offs, n, args.steps // 10 + 1)
+        zip_leg = None
+        if not args.no_zip215 and world == 1 and args.mix == "c2":
+            zip_leg = zip215_leg(eng, dev, torch_stream, d_pub, d_sig, d_msg, d_off, msgs, offs, n, args.steps // 10 + 1)
         c4 = None
         if not args.no_c4 and world == 1:
             c4 = c4_shard(eng, dev, args.c4_blocks)
@@ -296,6 +300,7 @@ def main():
             "c2_keyset_variant": keyset,
             "c1_verifycommit_p50": c1,
             "c5": c5,
+            "zip215_batch_mode": zip_leg,
             "c4_shard": c4,
             "setup_s": round(t_gen, 2),
         }
@@ -404,6 +409,51 @@ def c5_leg(eng, dev, torch_stream, d_pub, d_sig, d_msg, d_off, msgs, offs, n, st
             "mismatches_vs_port": int((gpu != exp).sum()),
             "checker": "oracle/ed25519_port.c on all %d tuples, %d threads, %.1f s" % (n, nt, t_port),
             "config": {"workload": "C5: C2 batch with 1%% replaced by edge-case/invalid tuples, seed 0x5EED"}}
+
+
+def zip215_leg(eng, dev, torch_stream, d_pub, d_sig, d_msg, d_off, msgs, offs, n, steps):
+    """The opt-in ZIP-215 mode (tmed_verify_batch_zip215_device; spec/core/encoding.md:52-54), NOT the
+    reference's default rule: the C2 batch as one randomized batch equation (GPU Pippenger MSM), and
+    the C5 mix (1% edge/invalid: the equation fails, bisection, exact single checks).  verifies/s,
+    the engine's equation / single-check counts, and decisions against the C port's ZIP-215 rule
+    (oracle/ed25519_port.c port_verify_zip215, 16 threads) on every tuple."""
+    import torch
+    from tmed import Engine
+    from tmed.workload import c5_mix
+    sys.path.insert(0, ROOT)
+    from oracle import port  # checker only
+    st = torch_stream.cuda_stream
+    res = {"metric": "ed25519 verifies/sec at 1/8 MI355X, opt-in ZIP-215 batch mode (not the reference rule)",
+           "unit": "verifies/s", "rule": "ZIP-215: permissive A/R decoding, S < L, [8](SB - R - kA) = O"}
+    nt = min(16, os.cpu_count() or 1)
+    hp, hs = d_pub.cpu().numpy(), d_sig.cpu().numpy()
+    o = offs.astype(np.uint64)
+    for name, mix in (("c2", False), ("c5", True)):
+        p, sg = hp, hs
+        if mix:
+            p, sg = hp.copy(), hs.copy()
+            c5_mix(p, sg, seed=0x5EED)
+        dp, ds = torch.from_numpy(p).to(dev), torch.from_numpy(sg).to(dev)
+        out = torch.zeros(n, dtype=torch.uint8, device=dev)
+        eng.verify_zip215_device(dp, ds, d_msg, d_off, out, n, st)
+        torch.cuda.synchronize(dev)
+        k = steps if not mix else max(1, steps // 4)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            eng.verify_zip215_device(dp, ds, d_msg, d_off, out, n, st)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        stats = Engine.zip215_stats()
+        gpu = out.cpu().numpy()
+        exp = port.verify_batch(p, sg, msgs, o, nthreads=nt, zip215=True)
+        res[name] = {"value": round(n * k / dt, 1), "ms_per_step": round(dt / k * 1e3, 3), "steps": k,
+                     "valid": int(gpu.sum()), "mismatches_vs_port_zip215": int((gpu != exp).sum()),
+                     "engine": stats}
+        del dp, ds, out
+    res["value"] = res["c2"]["value"]
+    res["config"] = {"workload": "C2 batch (and the C5 mix) of %d signatures in ZIP-215 batch mode" % n,
+                     "checker": "oracle/ed25519_port.c port_verify_zip215 on all tuples, %d threads" % nt}
+    return res
 
 
 def c4_shard(eng, dev, blocks):

@@ -141,7 +141,7 @@ int tmed_verify_batch_keyset_device(tmed_ctx *ctx, uint64_t handle, const uint32
  * stays the default).  Rule: A and R decoded permissively (y >= p and x = 0 with the sign bit
  * accepted), S < L, k = SHA-512(R || A || M) mod L, accept iff [8]([S]B - R - [k]A) = O.
  * Chunks of up to 2^20 signatures are checked as ONE randomized batch equation (Pippenger MSM with
- * secret 127-bit weights from getrandom); a failing chunk is bisected and the failing groups are
+ * secret 126-bit weights from getrandom); a failing chunk is bisected and the failing groups are
  * decided signature by signature by the exact single check, so out_valid[i] equals the ZIP-215
  * single-signature decision for every i.  sig_lens as in tmed_verify_batch.
  */

@@ -8,13 +8,13 @@
 // accept iff [8]([S]B - R - [k]A) = O.  Restated in oracle/zip215.py; parity unpinned by the
 // reference (it holds no ZIP-215 code or vectors).
 //
-// A chunk of N <= kZipMax signatures is checked as ONE equation with secret random 127-bit z_i
+// A chunk of N <= kZipMax signatures is checked as ONE equation with secret random 126-bit z_i
 // (SHA-512 of a per-call 32-byte seed and the signature index):
 //   [8]( [sum z_i S_i] B + sum_i [z_i k_i](-A_i) + sum_i [z_i](-R_i) ) = O,
 // i.e. one multi-scalar multiplication over 2N points plus one fixed-base product.  Scalars mod L
 // are exact here: the factor 8 removes every torsion component a reduction mod L could change.
 // The MSM is Pippenger with signed radix-2^16 digits (16 windows for the A scalars, 8 for the
-// 127-bit z), on the GPU:
+// 126-bit z), on the GPU:
 //   zip_prep_r_kernel   decode R, z, z k mod L, z S mod L, niels rows of -A / -R, the digits
 //   zip_bsum_*          sum z_i S_i mod L
 //   zip_sort_*          per window, a stable two-pass LSD counting sort of (|digit|, point) by
@@ -29,11 +29,14 @@
 // A chunk whose equation fails is bisected (the same MSM over halves of its signatures, prep
 // data reused); a group that still fails is decided signature by signature by the exact ZIP-215
 // single check (the half-size kernels with a permissive R decode and a [8] before the identity
-// test).  Every accepted group is all-valid with probability >= 1 - 2^-126 per failing signature
+// test).  Every accepted group is all-valid with probability >= 1 - 2^-125 per failing signature
 // (the z are secret); every rejected signature comes from the exact single check.
 #include <hip/hip_runtime.h>
 #include <string.h>
 #include <sys/random.h>
+
+#include <stdio.h>
+#include <stdlib.h>
 
 #include <vector>
 
@@ -77,8 +80,9 @@ __device__ __forceinline__ void niels_row_store(int4 *row, const fe &x, const fe
   }
 }
 
-// z_i: SHA-512(seed || LE64(index)) (one block), 127 bits with bit 126 set (non-zero, and the
-// signed radix-2^16 recoding of z stays within 8 windows).
+// z_i: SHA-512(seed || LE64(index)) (one block), 126 bits with bit 125 set: non-zero, and the
+// signed radix-2^16 recoding of z stays within 8 windows (with 127 bits the top halfword 0x7fff
+// plus the recoding's bias and carry overflowed into a ninth window about once per 2^16 z).
 __device__ __forceinline__ void zip_scalar_z(uint32_t z[8], const uint32_t seed[8], uint64_t index) {
   uint64_t w[16];
 #pragma unroll
@@ -100,7 +104,7 @@ __device__ __forceinline__ void zip_scalar_z(uint32_t z[8], const uint32_t seed[
   z[0] = (uint32_t)st[0];
   z[1] = (uint32_t)(st[0] >> 32);
   z[2] = (uint32_t)st[1];
-  z[3] = ((uint32_t)(st[1] >> 32) & 0x3fffffffu) | 0x40000000u;
+  z[3] = ((uint32_t)(st[1] >> 32) & 0x1fffffffu) | 0x20000000u;
   z[4] = z[5] = z[6] = z[7] = 0;
 }
 
@@ -648,6 +652,31 @@ hipError_t zip_msm(tmed_ctx *c, const ZipBufs &z, uint32_t N, uint32_t lo, uint3
   hipLaunchKernelGGL(zip_sort_hist_kernel<1>, sg, dim3(kSortWaves * 64), 0, s, a);
   hipLaunchKernelGGL(zip_sort_scan_kernel, dim3(kZipWin), dim3(1024), 0, s, a.hist, a.tiles);
   hipLaunchKernelGGL(zip_sort_scatter_kernel<1>, sg, dim3(kSortWaves * 64), 0, s, a);
+  if (getenv("TMED_ZIP_DEBUG")) {  // diagnostics: the sorted windows against the digits
+    hipStreamSynchronize(s);
+    std::vector<int16_t> dg((size_t)kZipWin * 2 * N);
+    hipMemcpy(dg.data(), z.dig, dg.size() * 2, hipMemcpyDeviceToHost);
+    for (int w = 0; w < kZipWin; w++) {
+      const uint32_t M = (w < kZipZWin ? 2u : 1u) * cnt;
+      std::vector<uint16_t> kk(M);
+      std::vector<uint32_t> vv(M);
+      hipMemcpy(kk.data(), z.keys[1] + (size_t)w * z.cap, M * 2, hipMemcpyDeviceToHost);
+      hipMemcpy(vv.data(), z.vals[1] + (size_t)w * z.cap, M * 4, hipMemcpyDeviceToHost);
+      size_t unsorted = 0, badkey = 0, dup = 0;
+      std::vector<uint8_t> seen(2 * (size_t)N, 0);
+      for (uint32_t e = 0; e < M; e++) {
+        if (e && kk[e] < kk[e - 1]) unsorted++;
+        const uint32_t j = vv[e] & 0x7fffffffu;
+        if (j >= 2 * N) { badkey++; continue; }
+        if (seen[j]++) dup++;
+        const int d = dg[(size_t)w * 2 * N + j];
+        if ((uint32_t)(d < 0 ? -d : d) != kk[e] || ((vv[e] >> 31) != 0) != (d < 0)) badkey++;
+      }
+      if (unsorted || badkey || dup)
+        fprintf(stderr, "[zip] lo=%u cnt=%u window %d: M=%u unsorted=%zu badkey=%zu dup=%zu\n", lo, cnt, w, M,
+                unsorted, badkey, dup);
+    }
+  }
   uint32_t n_it[4] = {kZipLanes, (kZipLanes + 63) / 64, ((kZipLanes + 63) / 64 + 63) / 64, 1};
   ZipItems it[4];
   for (int L = 0; L < 4; L++) it[L] = ZipItems{z.items[L], n_it[L]};
