@@ -1130,6 +1130,41 @@ __device__ __forceinline__ void shfl_down_fe(fe &o, const fe &f, int L) {
   for (int i = 0; i < 10; i++) o.v[i] = __shfl_down(f.v[i], (unsigned)L, kLatLanes);
 }
 
+// comb_partial (verify_core.h) with the next comb row in flight and the first row converted
+// instead of added to the identity: lane rr's 8 rows are A(w), B(w) for w = rr, rr+8, rr+16, rr+24.
+__device__ __forceinline__ const int4 *lat_row(const int4 *comb, int w, uint32_t byte, bool &neg) {
+  const int d = (int)byte - 128;
+  neg = d < 0;
+  return comb + ((size_t)w * kCombEntries + (uint32_t)(neg ? -d : d)) * kCombEntryInt4;
+}
+__device__ __forceinline__ void comb_partial_pf(ge_p3 &acc, const uint32_t kr[8], const uint32_t sr[8], int rr,
+                                                const int4 *ac, const int4 *bc) {
+  const int sh = 8 * (rr & 3);
+  CombRowPf pf;
+  bool ng;
+  pf.fetch(lat_row(ac, rr, ((rr & 4) ? kr[1] : kr[0]) >> sh & 0xffu, ng), ng);
+  ge_p1p1 t;
+  ge_niels e;
+#pragma unroll
+  for (int st = 0; st < 8; st++) {
+    const int q = st >> 1;
+    pf.take(e);
+    if (st < 7) {  // the row of step st + 1
+      const int nq = (st + 1) >> 1, w = rr + 8 * nq;
+      const uint32_t word = (st + 1) & 1 ? ((rr & 4) ? sr[2 * nq + 1] : sr[2 * nq])
+                                         : ((rr & 4) ? kr[2 * nq + 1] : kr[2 * nq]);
+      pf.fetch(lat_row((st + 1) & 1 ? bc : ac, w, (word >> sh) & 0xffu, ng), ng);
+    }
+    (void)q;
+    if (st == 0) {
+      ge_niels_to_p3(acc, e);
+    } else {
+      ge_madd_niels(t, acc, e, false);
+      ge_p1p1_to_p3(acc, t);
+    }
+  }
+}
+
 __global__ __launch_bounds__(64) void verify_keyset_lat_kernel(
     const uint32_t *__restrict__ val_idx, uint32_t nkeys, const uint8_t *__restrict__ key_pub,
     const uint8_t *__restrict__ key_ok,
@@ -1169,10 +1204,8 @@ __global__ __launch_bounds__(64) void verify_keyset_lat_kernel(
   const bool ok = verify_prep_comb(pw, vin && key_ok[v] != 0, sw, msg, mlen, k, s);
   sc_recode256(kr, k);
   sc_recode256(sr, s);
-  const GlobalComb ac{acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4};
-  const GlobalComb bc{bcomb};
   ge_p3 acc, o;
-  comb_partial(acc, kr, sr, r, ac, bc);
+  comb_partial_pf(acc, kr, sr, r, acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4, bcomb);
 #pragma unroll 1
   for (int L = 1; L < kLatLanes; L <<= 1) {
     shfl_down_fe(o.X, acc.X, L);

@@ -44,13 +44,27 @@
 #include "kernel_util.h"
 #include "verify_core.h"
 #include "verify_hs.h"
+#include "quad.h"
 
 namespace tmed {
 
 constexpr int kZipWin = 16;       // radix-2^16 windows of the A scalars (z: windows 0..7)
 constexpr int kZipZWin = 8;
 constexpr uint32_t kZipRow = 8;   // int4 per niels point row (128 B)
-constexpr uint32_t kZipLanes = 8193;  // accumulation lanes per window: buckets 4l..4l+3, |digit| <= 32768
+// Accumulation lanes per window, balanced at ~cnt/8192 entries each: a lane owns g consecutive
+// buckets |digit| = g l .. g l + g - 1 (and, for the top A window, h = 2 lanes split each group):
+// windows 0..7 (A and R points, 2 cnt entries over 32768 buckets): g = 2, 16385 groups;
+// windows 8..14 (A only): g = 4, 8193 groups; window 15 (the top 13 bits of a < L: digits 0..4097,
+// 8x fewer buckets): g = 1, 4098 groups, h = 2.
+constexpr uint32_t kZipItemsMax = 16385;
+__host__ __device__ __forceinline__ int zip_glog(int w) { return w < 8 ? 1 : (w < 15 ? 2 : 0); }
+__host__ __device__ __forceinline__ uint32_t zip_groups(int w) { return w < 8 ? 16385u : (w < 15 ? 8193u : 4098u); }
+__host__ __device__ __forceinline__ uint32_t zip_h(int w) { return w == 15 ? 2u : 1u; }
+__host__ __device__ __forceinline__ uint32_t zip_level_items(int w, int level) {
+  uint32_t n = zip_groups(w);
+  for (int L = 0; L < level; L++) n = (n + 63) / 64;
+  return n;
+}
 constexpr uint32_t kSortTileE = 8192;  // entries per sort tile (one wave, 128 rounds of 64)
 constexpr uint32_t kSortWaves = 4;
 
@@ -390,37 +404,48 @@ struct ZipRowPf {
   }
 };
 
-// The four bucket sums of a lane go to bsum ([q][w][l] rows, 4 points) as each is finished, so the
-// accumulation loop keeps only the accumulator and the prefetched row live; the running sums are
-// formed afterwards from the stored buckets.
-__global__ __launch_bounds__(256, 2) void zip_accum_kernel(const uint16_t *__restrict__ keys,
+#ifndef TMED_ZIP_ACC_WAVES
+#define TMED_ZIP_ACC_WAVES 2
+#endif
+// The bucket sums of a lane go to bsum ([point][q][w][lane] rows) as each is finished, so the
+// accumulation loop keeps only the accumulator, the prefetched row and the next entry live; the
+// weighted sums S = sum_q B_q, T = sum_q q B_q of the lane's g buckets are formed afterwards.
+// Row i + 1 and entry i + 2 are loaded while addition i runs.
+__global__ __launch_bounds__(256, TMED_ZIP_ACC_WAVES) void zip_accum_kernel(const uint16_t *__restrict__ keys,
                                                            const uint32_t *__restrict__ vals, uint32_t cap,
                                                            uint32_t cnt, const int4 *__restrict__ pts,
                                                            ZipItems bsum, ZipItems out) {
   const int w = blockIdx.y;
-  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t h = zip_h(w), g = 1u << zip_glog(w), ng = zip_groups(w), lanes = ng * h;
+  if (blockIdx.x * blockDim.x >= lanes) return;  // the whole block past this window's lanes
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t grp = t / h, part = t % h;
   const uint32_t M = (w < kZipZWin ? 2u : 1u) * cnt;
   const uint16_t *k = keys + (size_t)w * cap;
   const uint32_t *v = vals + (size_t)w * cap;
-  const bool lane_ok = l < kZipLanes;
-  const uint32_t v0 = 4 * l;
-  // bucket boundaries: [b[q], b[q+1]) holds |digit| = 4l + q (v = 0 skipped: weight 0)
-  uint32_t b[5];
+  const bool lane_ok = t < lanes;
+  const uint32_t v0 = g * grp;
+  // bucket boundaries: [b[q], b[q+1]) holds |digit| = v0 + q (v = 0 skipped: weight 0); kept in
+  // LDS (indexed by the rolled bucket loop without register-array indexing)
+  __shared__ uint32_t bnd[5][256];
 #pragma unroll
   for (int q = 0; q < 5; q++) {
     const uint32_t key = v0 + (uint32_t)q;
-    b[q] = lane_ok ? lower_bound16(k, M, (l == 0 && q == 0) ? 1u : key) : 0u;
+    bnd[q][threadIdx.x] = (lane_ok && (uint32_t)q <= g) ? lower_bound16(k, M, key == 0 ? 1u : key) : 0u;
   }
   ge_p3 acc;
-  ge_p1p1 t;
+  ge_p1p1 t1;
   ge_niels e;
   ZipRowPf pf;
 #pragma unroll 1
-  for (int q = 0; q < 4; q++) {
-    const uint32_t lo = b[q], hi = b[q + 1];
-    const uint32_t nq = hi - lo;
-    // wave-uniform trip count: the largest run of the wave
-    uint32_t mx = nq;
+  for (uint32_t q = 0; q < g; q++) {
+    uint32_t lo = bnd[q][threadIdx.x], hi = bnd[q + 1][threadIdx.x];
+    if (h == 2) {  // the two lanes of a group take the halves of each bucket's run
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if (part == 0) hi = mid; else lo = mid;
+    }
+    const uint32_t nq = lane_ok ? hi - lo : 0u;
+    uint32_t mx = nq;  // wave-uniform trip count: the largest run of the wave
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       const uint32_t x = (uint32_t)__shfl_xor((int)mx, o);
@@ -428,37 +453,45 @@ __global__ __launch_bounds__(256, 2) void zip_accum_kernel(const uint16_t *__res
     }
     mx = __builtin_amdgcn_readfirstlane(mx);
     ge_p3_0(acc);
+    uint32_t vn = 0;
     if (nq) {
       const uint32_t vv = v[lo];
       pf.fetch(pts + (size_t)(vv & 0x7fffffffu) * kZipRow, (vv >> 31) != 0);
+      if (nq > 1) vn = v[lo + 1];
     }
 #pragma unroll 1
     for (uint32_t i = 0; i < mx; i++) {
       if (i < nq) {
         pf.take(e);
-        if (i + 1 < nq) {
-          const uint32_t vv = v[lo + i + 1];
-          pf.fetch(pts + (size_t)(vv & 0x7fffffffu) * kZipRow, (vv >> 31) != 0);
-        }
-        ge_madd_niels(t, acc, e, false);
-        ge_p1p1_to_p3(acc, t);
+        if (i + 1 < nq) pf.fetch(pts + (size_t)(vn & 0x7fffffffu) * kZipRow, (vn >> 31) != 0);
+        if (i + 2 < nq) vn = v[lo + i + 2];
+        ge_madd_niels(t1, acc, e, false);
+        ge_p1p1_to_p3(acc, t1);
       }
     }
-    if (lane_ok) p3_store_rows(bsum.at(w, l, q), bsum.qstride(), acc);
+    if (lane_ok) p3_store_rows(bsum.at(w, t, (int)q), bsum.qstride(), acc);
   }
-  if (!lane_ok) return;
-  // S = B0 + B1 + B2 + B3, T = 1 B1 + 2 B2 + 3 B3 = B3 + (B3 + B2) + (B3 + B2 + B1)
+}
+
+// S = sum B_q, T = sum q B_q = B_{g-1} + (B_{g-1} + B_{g-2}) + ... (running sums from the top) of
+// each accumulation lane's g bucket sums -> item t.  With h = 2 the level-0 reduction adds the two
+// halves of a group (items 2 grp, 2 grp + 1) before weighting: S and T are linear in the buckets.
+__global__ __launch_bounds__(256) void zip_bucket_weights_kernel(ZipItems bsum, ZipItems out) {
+  const int w = blockIdx.y;
+  const uint32_t g = 1u << zip_glog(w), lanes = zip_groups(w) * zip_h(w);
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= lanes) return;
   ge_p3 run, tsum, bq;
-  p3_load_rows(run, bsum.at(w, l, 3), bsum.qstride());
-  tsum = run;
+  p3_load_rows(run, bsum.at(w, t, (int)g - 1), bsum.qstride());
+  if (g > 1) tsum = run; else ge_p3_0(tsum);
 #pragma unroll 1
-  for (int q = 2; q >= 0; q--) {
-    p3_load_rows(bq, bsum.at(w, l, q), bsum.qstride());
+  for (int q = (int)g - 2; q >= 0; q--) {
+    p3_load_rows(bq, bsum.at(w, t, q), bsum.qstride());
     ge_p3_add(run, bq);
     if (q > 0) ge_p3_add(tsum, run);
   }
-  p3_store_rows(out.at(w, l, 0), out.qstride(), run);
-  p3_store_rows(out.at(w, l, 1), out.qstride(), tsum);
+  p3_store_rows(out.at(w, t, 0), out.qstride(), run);
+  p3_store_rows(out.at(w, t, 1), out.qstride(), tsum);
 }
 
 // ---------------------------------------------------------------- wavefront bucket reduction
@@ -472,13 +505,26 @@ __device__ __forceinline__ void shfl_p3(ge_p3 &o, const ge_p3 &p, int src, bool 
       fo[f]->v[j] = down ? __shfl_down(fi[f]->v[j], (unsigned)delta) : __shfl(fi[f]->v[j], src);
 }
 
-// One wave per 64 consecutive items of a window: (S', T') = (sum S_r, [2^dlog2] sum_r r S_r + sum T_r).
-// sum_r r S_r = sum_{r >= 1} Suf_r with Suf_r = sum_{q >= r} S_q (Kogge-Stone suffix scan).
-__global__ __launch_bounds__(64) void zip_reduce_kernel(ZipItems in, uint32_t n_items, int dlog2, ZipItems out) {
+// One wave per 64 consecutive items of a window at reduction level `level`: (S', T') =
+// (sum S_r, [2^dlog2] sum_r r S_r + sum T_r), with dlog2 = log2 of the items' weight step (g of the
+// window at level 0, x64 per level).  sum_r r S_r = sum_{r >= 1} Suf_r, Suf_r = sum_{q >= r} S_q
+// (Kogge-Stone suffix scan).
+__global__ __launch_bounds__(64) void zip_reduce_kernel(ZipItems in, int level, ZipItems out) {
   const int w = blockIdx.y;
+  const uint32_t n_items = zip_level_items(w, level);
+  if (blockIdx.x * 64 >= n_items) return;
+  const int dlog2 = zip_glog(w) + 6 * level;
   const uint32_t r = threadIdx.x, i = blockIdx.x * 64 + r;
   ge_p3 S, T;
-  if (i < n_items) {
+  if (i < n_items && level == 0 && zip_h(w) == 2) {  // the two accumulation lanes of group i
+    ge_p3 o;
+    p3_load_rows(S, in.at(w, 2 * i, 0), in.qstride());
+    p3_load_rows(o, in.at(w, 2 * i + 1, 0), in.qstride());
+    ge_p3_add(S, o);
+    p3_load_rows(T, in.at(w, 2 * i, 1), in.qstride());
+    p3_load_rows(o, in.at(w, 2 * i + 1, 1), in.qstride());
+    ge_p3_add(T, o);
+  } else if (i < n_items) {
     p3_load_rows(S, in.at(w, i, 0), in.qstride());
     p3_load_rows(T, in.at(w, i, 1), in.qstride());
   } else {
@@ -506,7 +552,7 @@ __global__ __launch_bounds__(64) void zip_reduce_kernel(ZipItems in, uint32_t n_
   ge_p1p1 t;
   ge_p3_to_p2(q, S);
   ge_p3 U = S;
-  if (dlog2 > 0) {
+  if (dlog2 > 0) {  // (level 0 of the top window: g = 1, no doubling)
 #pragma unroll 1
     for (int k = 0; k < dlog2; k++) {
       ge_p2_dbl(t, q);
@@ -520,53 +566,50 @@ __global__ __launch_bounds__(64) void zip_reduce_kernel(ZipItems in, uint32_t n_
 }
 
 // ---------------------------------------------------------------- final check
-// total = sum_w 2^(16 w) W_w + [ctot] B; flag = ([8] total == O).
+// total = sum_w 2^(16 w) W_w + [ctot] B; flag = ([8] total == O).  The 240 doublings of the Horner
+// chain are serial, so ONE quad runs it with the 4-way split formulas (quad.h): each lane computes
+// one coordinate's products of every doubling / addition (~3x less latency than one lane).
 __global__ __launch_bounds__(64) void zip_final_kernel(ZipItems wins, const uint32_t *__restrict__ ctot,
                                                        const int4 *__restrict__ bcomb16, uint32_t *__restrict__ flag) {
-  if (threadIdx.x != 0) return;
-  ge_p3 acc, Wv;
-  p3_load_rows(acc, wins.at(kZipWin - 1, 0, 1), wins.qstride());
-  ge_p1p1 t;
-  ge_p2 q;
+  if (threadIdx.x >= 4) return;  // quad 0
+  const QuadK K(threadIdx.x);
+  auto coord = [&](int w, fe &c) {  // lane r: coordinate r (X, Y, Z, T) of W_w
+    const int4 *src = wins.at(w, 0, 1);
+    int32_t a[40];
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+      const int4 x = src[(size_t)q * wins.qstride()];
+      a[4 * q] = x.x; a[4 * q + 1] = x.y; a[4 * q + 2] = x.z; a[4 * q + 3] = x.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 10; j++) c.v[j] = a[10 * K.r + j];
+  };
+  fe v, wv, c;
+  coord(kZipWin - 1, v);
 #pragma unroll 1
   for (int w = kZipWin - 2; w >= 0; w--) {
-    ge_p3_to_p2(q, acc);
 #pragma unroll 1
-    for (int k = 0; k < 16; k++) {
-      ge_p2_dbl(t, q);
-      if (k < 15) ge_p1p1_to_p2(q, t);
-    }
-    ge_p1p1_to_p3(acc, t);
-    p3_load_rows(Wv, wins.at(w, 0, 1), wins.qstride());
-    ge_p3_add(acc, Wv);
+    for (int d = 0; d < 16; d++) quad_dbl(v, K);
+    coord(w, wv);
+    quad_to_cached(c, wv, K);
+    quad_add(v, c, K);
   }
-  uint32_t c[8], cr[8];
+  uint32_t cw[8], cr[8];
 #pragma unroll
-  for (int j = 0; j < 8; j++) c[j] = ctot[j];
-  sc_recode_b<16>(cr, c);
-  ge_niels e;
+  for (int j = 0; j < 8; j++) cw[j] = ctot[j];
+  sc_recode_b<16>(cr, cw);
 #pragma unroll 1
   for (int w = 0; w < 16; w++) {
     const int d = (int)((cr[w >> 1] >> (16 * (w & 1))) & 0xffffu) - 32768;
-    const int4 *row = bcomb16 + ((size_t)w * kB16Entries + (uint32_t)(d < 0 ? -d : d)) * kCombEntryInt4;
-    fe *fs[3] = {&e.YpX, &e.YmX, &e.XY2d};
-#pragma unroll
-    for (int qq = 0; qq < 8; qq++) {
-      const int4 v = row[qq];
-      const int32_t wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int cc = 0; cc < 4; cc++) {
-        const int f = 4 * qq + cc;
-        if (f < 30) fs[f / 10]->v[f % 10] = wv[cc];
-      }
-    }
-    niels_apply_sign(e, d < 0);
-    ge_madd_niels(t, acc, e, false);
-    ge_p1p1_to_p3(acc, t);
+    comb_take(c, bcomb16 + (size_t)w * kB16Entries * kCombEntryInt4, d, K);
+    quad_add(v, c, K);
   }
-  ge_p3_to_p2(q, acc);
-  p2_mul8(q);
-  flag[0] = p2_is_identity(q) ? 1u : 0u;
+#pragma unroll 1
+  for (int d = 0; d < 3; d++) quad_dbl(v, K);  // [8]
+  fe X, Y, Z;
+#pragma unroll
+  for (int j = 0; j < 10; j++) { X.v[j] = qbcast(v.v[j], 0); Y.v[j] = qbcast(v.v[j], 1); Z.v[j] = qbcast(v.v[j], 2); }
+  if (threadIdx.x == 0) flag[0] = (fe_iszero(X) && fe_equal(Y, Z) && !fe_iszero(Z)) ? 1u : 0u;
 }
 
 }  // namespace tmed
@@ -606,9 +649,9 @@ hipError_t zip_bufs(tmed_ctx *c, ZipBufs &z) {
   const size_t o_hist = take((size_t)kZipWin * 256 * tiles * 4), o_part = take((N / 256 + 1) * 8 * 8);
   const size_t o_ctot = take(64);
   size_t o_it[4];
-  uint32_t n_it[4] = {kZipLanes, (kZipLanes + 63) / 64, ((kZipLanes + 63) / 64 + 63) / 64, 1};
+  uint32_t n_it[4] = {kZipItemsMax, (kZipItemsMax + 63) / 64, ((kZipItemsMax + 63) / 64 + 63) / 64, 1};
   for (int L = 0; L < 4; L++) o_it[L] = take((size_t)20 * kZipWin * n_it[L] * 16);
-  const size_t o_bsum = take((size_t)40 * kZipWin * kZipLanes * 16);
+  const size_t o_bsum = take((size_t)40 * kZipWin * kZipItemsMax * 16);
   const size_t o_flag = take(16), o_seed = take(32);
   hipError_t e = c->d_zip.ensure(off);
   if (e != hipSuccess) return e;
@@ -677,17 +720,15 @@ hipError_t zip_msm(tmed_ctx *c, const ZipBufs &z, uint32_t N, uint32_t lo, uint3
                 unsorted, badkey, dup);
     }
   }
-  uint32_t n_it[4] = {kZipLanes, (kZipLanes + 63) / 64, ((kZipLanes + 63) / 64 + 63) / 64, 1};
+  uint32_t n_it[4] = {kZipItemsMax, (kZipItemsMax + 63) / 64, ((kZipItemsMax + 63) / 64 + 63) / 64, 1};
   ZipItems it[4];
   for (int L = 0; L < 4; L++) it[L] = ZipItems{z.items[L], n_it[L]};
-  hipLaunchKernelGGL(zip_accum_kernel, dim3((kZipLanes + 255) / 256, kZipWin), dim3(256), 0, s, z.keys[1], z.vals[1],
-                     z.cap, cnt, z.pts, ZipItems{z.bsum, kZipLanes}, it[0]);
-  int dlog2 = 2;  // level-0 items weigh 4 l
-  for (int L = 0; L < 3; L++) {
-    hipLaunchKernelGGL(zip_reduce_kernel, dim3((n_it[L] + 63) / 64, kZipWin), dim3(64), 0, s, it[L], n_it[L], dlog2,
-                       it[L + 1]);
-    dlog2 += 6;
-  }
+  hipLaunchKernelGGL(zip_accum_kernel, dim3((kZipItemsMax + 255) / 256, kZipWin), dim3(256), 0, s, z.keys[1],
+                     z.vals[1], z.cap, cnt, z.pts, ZipItems{z.bsum, kZipItemsMax}, it[0]);
+  hipLaunchKernelGGL(zip_bucket_weights_kernel, dim3((kZipItemsMax + 255) / 256, kZipWin), dim3(256), 0, s,
+                     ZipItems{z.bsum, kZipItemsMax}, it[0]);
+  for (int L = 0; L < 3; L++)
+    hipLaunchKernelGGL(zip_reduce_kernel, dim3((n_it[L] + 63) / 64, kZipWin), dim3(64), 0, s, it[L], L, it[L + 1]);
   hipLaunchKernelGGL(zip_final_kernel, dim3(1), dim3(64), 0, s, it[3], z.ctot, c->d_bcomb16, z.flag);
   return hipGetLastError();
 }
