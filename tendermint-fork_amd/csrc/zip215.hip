@@ -19,12 +19,12 @@
 //   zip_bsum_*          sum z_i S_i mod L
 //   zip_sort_*          per window, a stable two-pass LSD counting sort of (|digit|, point) by
 //                       |digit| (8-bit passes; every tile is ranked by ONE wave with ballot
-//                       matching, no global atomics)
+//                       matching into LDS and written out in bin order; no global atomics)
 //   zip_accum_kernel    lane l of window w owns buckets 4l..4l+3: mixed additions of their
 //                       points (sorted runs, next row prefetched), then the bucket-weighted
 //                       running sums S_l = sum B_v, T_l = sum (v - 4l) B_v
-//   zip_reduce_kernel   wavefront-level bucket reduction: 64 items per wave by a suffix scan and
-//                       two trees over DPP shuffles, sum (d i S_i + T_i) -> one item; 3 levels
+//   zip_reduce*_kernel  wavefront-level bucket reduction: 64 items per wave by a suffix scan and
+//                       two trees over shuffles, sum (d i S_i + T_i) -> one item; 3 levels in 2 launches
 //   zip_final_kernel    Horner over the 16 windows, + [sum z S] B (radix-2^16 comb), x8, = O?
 // A chunk whose equation fails is bisected (the same MSM over halves of its signatures, prep
 // data reused); a group that still fails is decided signature by signature by the exact ZIP-215
@@ -65,7 +65,7 @@ __host__ __device__ __forceinline__ uint32_t zip_level_items(int w, int level) {
   for (int L = 0; L < level; L++) n = (n + 63) / 64;
   return n;
 }
-constexpr uint32_t kSortTileE = 8192;  // entries per sort tile (one wave, 128 rounds of 64)
+constexpr uint32_t kSortTileE = 4096;  // entries per sort tile (one wave, 64 rounds of 64)
 constexpr uint32_t kSortWaves = 4;
 
 // ---------------------------------------------------------------- prep (after verify_prep)
@@ -125,7 +125,10 @@ __device__ __forceinline__ void zip_scalar_z(uint32_t z[8], const uint32_t seed[
 // One lane per signature of the chunk (after verify_prep_kernel wrote k, S, A, ok).  Point rows:
 // [0, cnt) = -A_i, [cnt, 2 cnt) = -R_i; digits dig[w][row] (int16, signed radix 2^16); cs = z S.
 // Invalid signatures (A or R not on the curve, S >= L) get z = 0: no contribution, out[i] = 0.
-__global__ __launch_bounds__(kThreadsPerBlock) void zip_prep_r_kernel(
+#ifndef TMED_ZIP_PREP_WAVES
+#define TMED_ZIP_PREP_WAVES 2
+#endif
+__global__ __launch_bounds__(kThreadsPerBlock, TMED_ZIP_PREP_WAVES) void zip_prep_r_kernel(
     const uint8_t *__restrict__ sig, uint32_t base, uint32_t cnt, const int4 *__restrict__ prep, uint32_t stride,
     const uint32_t *__restrict__ seed, uint64_t index_base, int4 *__restrict__ pts, int16_t *__restrict__ dig,
     int4 *__restrict__ cs, uint32_t cs_stride, uint8_t *__restrict__ out) {
@@ -237,8 +240,8 @@ struct ZipSortArgs {
   uint16_t *keys[2];
   uint32_t *vals[2];
   uint32_t cap;    // per-window capacity of keys / vals (2N)
-  uint32_t *hist;  // [w][bin][tile]
-  uint32_t tiles;  // tile stride of hist (= cap / kSortTileE rounded up)
+  uint32_t *hist;  // [w][tile + 1][bin]: counts, then offsets (zip_sort_scan_kernel)
+  uint32_t tiles;  // tiles of this sort (row stride of hist: tiles + 1)
 };
 
 __device__ __forceinline__ uint32_t zip_m(const ZipSortArgs &a, int w) { return (w < kZipZWin ? 2u : 1u) * a.cnt; }
@@ -273,53 +276,97 @@ __global__ __launch_bounds__(kSortWaves * 64) void zip_sort_hist_kernel(ZipSortA
     }
   }
   if (tile < a.tiles)
-    for (uint32_t b = lane; b < 256; b += 64) a.hist[((size_t)w * 256 + b) * a.tiles + tile] = h[wave][b];
+    for (uint32_t b = lane; b < 256; b += 64) a.hist[((size_t)w * (a.tiles + 1) + tile) * 256 + b] = h[wave][b];
 }
 
-// Per window: exclusive scan of hist[w] (256 bins x tiles, bin-major) in place.
+// Per window: hist[w] is [tile][bin] (+ one row of bin starts).  Thread (seg, b) of the 1024 sums
+// its quarter of column b (coalesced: consecutive threads, consecutive bins), the quarters and the
+// bin totals are scanned in LDS, then the thread rewrites its quarter as exclusive prefixes; tile
+// t's range of bin b starts at row[tiles][b] + [t][b].
 __global__ __launch_bounds__(1024) void zip_sort_scan_kernel(uint32_t *__restrict__ hist, uint32_t tiles) {
-  __shared__ uint32_t tot[1024];
-  uint32_t *cnt = hist + (size_t)blockIdx.x * 256 * tiles;
-  const uint32_t m = 256 * tiles, t = threadIdx.x;
-  const uint32_t per = (m + 1023) / 1024, lo = t * per, hi = lo + per < m ? lo + per : m;
-  uint32_t s = 0;
-  for (uint32_t j = lo; j < hi; j++) s += cnt[j];
-  tot[t] = s;
+  __shared__ uint32_t part[4][256], tot[256], colsum[256];
+  uint32_t *h = hist + (size_t)blockIdx.x * (tiles + 1) * 256;
+  const uint32_t b = threadIdx.x & 255u, seg = threadIdx.x >> 8;
+  const uint32_t per = (tiles + 3) / 4, t0 = seg * per < tiles ? seg * per : tiles;
+  const uint32_t t1 = t0 + per < tiles ? t0 + per : tiles;
+  uint32_t acc = 0;
+  for (uint32_t t = t0; t < t1; t++) acc += h[(size_t)t * 256 + b];
+  part[seg][b] = acc;
   __syncthreads();
-  for (uint32_t o = 1; o < 1024; o <<= 1) {
-    const uint32_t x = t >= o ? tot[t - o] : 0u;
+  if (seg == 0) {
+    uint32_t run = 0;
+    for (int q = 0; q < 4; q++) { const uint32_t c = part[q][b]; part[q][b] = run; run += c; }
+    colsum[b] = run;
+    tot[b] = run;
+  }
+  __syncthreads();
+  for (uint32_t o = 1; o < 256; o <<= 1) {  // inclusive scan of the bin totals
+    const uint32_t x = (seg == 0 && b >= o) ? tot[b - o] : 0u;
     __syncthreads();
-    tot[t] += x;
+    if (seg == 0) tot[b] += x;
     __syncthreads();
   }
-  uint32_t acc = t ? tot[t - 1] : 0u;
-  for (uint32_t j = lo; j < hi; j++) {
-    const uint32_t c = cnt[j];
-    cnt[j] = acc;
-    acc += c;
+  uint32_t run = part[seg][b];
+  for (uint32_t t = t0; t < t1; t++) {
+    const uint32_t c = h[(size_t)t * 256 + b];
+    h[(size_t)t * 256 + b] = run;
+    run += c;
   }
+  if (seg == 0) h[(size_t)tiles * 256 + b] = tot[b] - colsum[b];  // exclusive bin start
 }
 
-// Stable scatter: one wave per tile, rounds of 64 consecutive entries; lanes with equal bins are
-// ranked in lane order by ballot matching on the 8 bin bits, and the bin's running position
-// lives in LDS (read by all lanes, then advanced by the group's last lane).
+// Stable scatter: ONE wave (one workgroup) per tile.  The tile is first ranked into LDS in bin
+// order — rounds of 64 consecutive entries; lanes with equal bins are ranked in lane order by
+// ballot matching on the 8 bin bits, the bin's running position lives in LDS (read by all lanes,
+// then advanced by the group's last lane) — and then written out in that order, so consecutive
+// lanes store consecutive addresses of a bin's run (a direct scatter touched 64 lines per store
+// instruction and was store-transaction bound: 0.5 ms per pass per 2^20 signatures).
 template <int PASS>
-__global__ __launch_bounds__(kSortWaves * 64) void zip_sort_scatter_kernel(ZipSortArgs a) {
-  __shared__ uint32_t run[kSortWaves][256];
+__global__ __launch_bounds__(64) void zip_sort_scatter_kernel(ZipSortArgs a) {
+  __shared__ uint16_t sk[kSortTileE];
+  __shared__ uint32_t sv[kSortTileE];
+  __shared__ uint32_t lstart[256], gbase[256], run[256];
   const int w = blockIdx.y;
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const uint32_t tile = blockIdx.x * kSortWaves + wave;
+  const uint32_t lane = threadIdx.x, tile = blockIdx.x;
   const uint32_t M = zip_m(a, w), e0 = tile * kSortTileE;
   if (tile >= a.tiles || e0 >= M) return;
-  for (uint32_t b = lane; b < 256; b += 64) run[wave][b] = a.hist[((size_t)w * 256 + b) * a.tiles + tile];
+  const uint32_t nt = M - e0 < kSortTileE ? M - e0 : kSortTileE;
+  for (uint32_t b = lane; b < 256; b += 64) run[b] = 0;
+  for (uint32_t j = lane; j < nt; j += 64) {  // the tile's own counts
+    uint32_t key, val;
+    zip_entry<PASS>(a, w, e0 + j, key, val);
+    atomicAdd(&run[PASS == 0 ? (key & 0xffu) : (key >> 8)], 1u);
+  }
+  __builtin_amdgcn_wave_barrier();
+  {  // exclusive scan of the 256 counts: 4 per lane, then a wave scan of the lane sums
+    uint32_t c[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) { c[q] = run[4 * lane + q]; sum += c[q]; }
+    uint32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t x = (uint32_t)__shfl_up((int)inc, (unsigned)o);
+      if (lane >= (uint32_t)o) inc += x;
+    }
+    uint32_t ex = inc - sum;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t b = 4 * lane + q;
+      lstart[b] = ex;
+      run[b] = ex;
+      const uint32_t *hw = a.hist + (size_t)w * (a.tiles + 1) * 256;
+      gbase[b] = hw[(size_t)a.tiles * 256 + b] + hw[(size_t)tile * 256 + b];
+      ex += c[q];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  uint16_t *ko = a.keys[PASS] + (size_t)w * a.cap;
-  uint32_t *vo = a.vals[PASS] + (size_t)w * a.cap;
-  for (uint32_t r = 0; r < kSortTileE / 64; r++) {
-    const uint32_t e = e0 + r * 64 + lane;
-    const bool act = e < M;
+  for (uint32_t r = 0; r * 64 < nt; r++) {
+    const uint32_t j = r * 64 + lane;
+    const bool act = j < nt;
     uint32_t key = 0, val = 0;
-    if (act) zip_entry<PASS>(a, w, e, key, val);
+    if (act) zip_entry<PASS>(a, w, e0 + j, key, val);
     const uint32_t bin = PASS == 0 ? (key & 0xffu) : (key >> 8);
     uint64_t m = __ballot(act);
 #pragma unroll
@@ -327,14 +374,24 @@ __global__ __launch_bounds__(kSortWaves * 64) void zip_sort_scatter_kernel(ZipSo
       const uint64_t bs = __ballot((bin >> bit) & 1u);
       m &= ((bin >> bit) & 1u) ? bs : ~bs;
     }
-    const uint32_t pos = act ? run[wave][bin] + (uint32_t)__builtin_popcountll(m & below) : 0u;
+    const uint32_t pos = act ? run[bin] + (uint32_t)__builtin_popcountll(m & below) : 0u;
     __builtin_amdgcn_wave_barrier();
-    if (act && (m >> lane) == 1ull) run[wave][bin] += (uint32_t)__builtin_popcountll(m);  // the group's last lane
+    if (act && (m >> lane) == 1ull) run[bin] += (uint32_t)__builtin_popcountll(m);  // the group's last lane
     __builtin_amdgcn_wave_barrier();
     if (act) {
-      ko[pos] = (uint16_t)key;
-      vo[pos] = val;
+      sk[pos] = (uint16_t)key;
+      sv[pos] = val;
     }
+  }
+  __builtin_amdgcn_wave_barrier();
+  uint16_t *ko = a.keys[PASS] + (size_t)w * a.cap;
+  uint32_t *vo = a.vals[PASS] + (size_t)w * a.cap;
+  for (uint32_t j = lane; j < nt; j += 64) {
+    const uint32_t key = sk[j];
+    const uint32_t b = PASS == 0 ? (key & 0xffu) : (key >> 8);
+    const uint32_t gp = gbase[b] + (j - lstart[b]);
+    ko[gp] = (uint16_t)key;
+    vo[gp] = sv[j];
   }
 }
 
@@ -509,14 +566,49 @@ __device__ __forceinline__ void shfl_p3(ge_p3 &o, const ge_p3 &p, int src, bool 
 // (sum S_r, [2^dlog2] sum_r r S_r + sum T_r), with dlog2 = log2 of the items' weight step (g of the
 // window at level 0, x64 per level).  sum_r r S_r = sum_{r >= 1} Suf_r, Suf_r = sum_{q >= r} S_q
 // (Kogge-Stone suffix scan).
-__global__ __launch_bounds__(64) void zip_reduce_kernel(ZipItems in, int level, ZipItems out) {
+// The wave's 64 items (S_r, T_r) (lane r) -> on lane 0: Sout = sum S_r, Tout = [2^dlog2] sum_r r S_r
+// + sum T_r.
+__device__ __forceinline__ void zip_wave_reduce(ge_p3 &S, ge_p3 &T, int dlog2, uint32_t r, ge_p3 &Sout,
+                                                ge_p3 &Tout) {
+  ge_p3 o;
+#pragma unroll 1
+  for (int d = 1; d < 64; d <<= 1) {  // suffix sums
+    shfl_p3(o, S, 0, true, d);
+    if (r + d < 64) ge_p3_add(S, o);
+  }
+  shfl_p3(Sout, S, 0, false, 0);  // Suf_0 = sum S
+  if (r == 0) ge_p3_0(S);         // U = sum_{r >= 1} Suf_r
+#pragma unroll 1
+  for (int d = 32; d > 0; d >>= 1) {  // two trees: U and sum T
+    shfl_p3(o, S, 0, true, d);
+    if (r < (uint32_t)d) ge_p3_add(S, o);
+    shfl_p3(o, T, 0, true, d);
+    if (r < (uint32_t)d) ge_p3_add(T, o);
+  }
+  Tout = S;
+  if (r == 0 && dlog2 > 0) {  // (level 0 of the top window: g = 1, no doubling)
+    ge_p2 q;
+    ge_p1p1 t;
+    ge_p3_to_p2(q, S);
+#pragma unroll 1
+    for (int k = 0; k < dlog2; k++) {
+      ge_p2_dbl(t, q);
+      if (k + 1 < dlog2) ge_p1p1_to_p2(q, t);
+    }
+    ge_p1p1_to_p3(Tout, t);
+  }
+  if (r == 0) ge_p3_add(Tout, T);
+}
+
+// Level 0: one wave per 64 items of a window (the top window's items are the sums of its two
+// accumulation lanes per group).
+__global__ __launch_bounds__(64) void zip_reduce_kernel(ZipItems in, ZipItems out) {
   const int w = blockIdx.y;
-  const uint32_t n_items = zip_level_items(w, level);
+  const uint32_t n_items = zip_level_items(w, 0);
   if (blockIdx.x * 64 >= n_items) return;
-  const int dlog2 = zip_glog(w) + 6 * level;
   const uint32_t r = threadIdx.x, i = blockIdx.x * 64 + r;
   ge_p3 S, T;
-  if (i < n_items && level == 0 && zip_h(w) == 2) {  // the two accumulation lanes of group i
+  if (i < n_items && zip_h(w) == 2) {  // the two accumulation lanes of group i
     ge_p3 o;
     p3_load_rows(S, in.at(w, 2 * i, 0), in.qstride());
     p3_load_rows(o, in.at(w, 2 * i + 1, 0), in.qstride());
@@ -531,38 +623,50 @@ __global__ __launch_bounds__(64) void zip_reduce_kernel(ZipItems in, int level, 
     ge_p3_0(S);
     ge_p3_0(T);
   }
-  ge_p3 o;
-#pragma unroll 1
-  for (int d = 1; d < 64; d <<= 1) {  // suffix sums
-    shfl_p3(o, S, 0, true, d);
-    if (r + d < 64) ge_p3_add(S, o);
-  }
-  ge_p3 Stot;
-  shfl_p3(Stot, S, 0, false, 0);  // Suf_0 = sum S
-  if (r == 0) ge_p3_0(S);         // U = sum_{r >= 1} Suf_r
-#pragma unroll 1
-  for (int d = 32; d > 0; d >>= 1) {  // two trees: U and sum T
-    shfl_p3(o, S, 0, true, d);
-    if (r < (uint32_t)d) ge_p3_add(S, o);
-    shfl_p3(o, T, 0, true, d);
-    if (r < (uint32_t)d) ge_p3_add(T, o);
-  }
+  ge_p3 So, To;
+  zip_wave_reduce(S, T, zip_glog(w), r, So, To);
   if (r != 0) return;
-  ge_p2 q;
-  ge_p1p1 t;
-  ge_p3_to_p2(q, S);
-  ge_p3 U = S;
-  if (dlog2 > 0) {  // (level 0 of the top window: g = 1, no doubling)
-#pragma unroll 1
-    for (int k = 0; k < dlog2; k++) {
-      ge_p2_dbl(t, q);
-      if (k + 1 < dlog2) ge_p1p1_to_p2(q, t);
-    }
-    ge_p1p1_to_p3(U, t);
+  p3_store_rows(out.at(w, blockIdx.x, 0), out.qstride(), So);
+  p3_store_rows(out.at(w, blockIdx.x, 1), out.qstride(), To);
+}
+
+// Levels 1 and 2 in one workgroup per window: wave j reduces level-1 items 64 j .. 64 j + 63 into
+// LDS, then wave 0 reduces those (<= 5) into the window's value.
+constexpr int kZipL1Waves = 5;  // ceil(ceil(kZipItemsMax / 64) / 64)
+__global__ __launch_bounds__(64 * kZipL1Waves) void zip_reduce12_kernel(ZipItems in, ZipItems out) {
+  __shared__ int32_t lds[kZipL1Waves][2][40];
+  const int w = blockIdx.y;
+  const uint32_t wave = threadIdx.x >> 6, r = threadIdx.x & 63u;
+  const uint32_t n1 = zip_level_items(w, 1), n2 = zip_level_items(w, 2);
+  const uint32_t i = wave * 64 + r;
+  ge_p3 S, T, So, To;
+  if (i < n1) {
+    p3_load_rows(S, in.at(w, i, 0), in.qstride());
+    p3_load_rows(T, in.at(w, i, 1), in.qstride());
+  } else {
+    ge_p3_0(S);
+    ge_p3_0(T);
   }
-  ge_p3_add(U, T);
-  p3_store_rows(out.at(w, blockIdx.x, 0), out.qstride(), Stot);
-  p3_store_rows(out.at(w, blockIdx.x, 1), out.qstride(), U);
+  if (wave < n2) {  // (uniform per wave)
+    zip_wave_reduce(S, T, zip_glog(w) + 6, r, So, To);
+    if (r == 0) {
+      const fe *fs[4] = {&So.X, &So.Y, &So.Z, &So.T}, *ft[4] = {&To.X, &To.Y, &To.Z, &To.T};
+      for (int f = 0; f < 40; f++) { lds[wave][0][f] = fs[f / 10]->v[f % 10]; lds[wave][1][f] = ft[f / 10]->v[f % 10]; }
+    }
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  if (r < n2) {
+    fe *fs[4] = {&S.X, &S.Y, &S.Z, &S.T}, *ft[4] = {&T.X, &T.Y, &T.Z, &T.T};
+    for (int f = 0; f < 40; f++) { fs[f / 10]->v[f % 10] = lds[r][0][f]; ft[f / 10]->v[f % 10] = lds[r][1][f]; }
+  } else {
+    ge_p3_0(S);
+    ge_p3_0(T);
+  }
+  zip_wave_reduce(S, T, zip_glog(w) + 12, r, So, To);
+  if (r != 0) return;
+  p3_store_rows(out.at(w, 0, 0), out.qstride(), So);
+  p3_store_rows(out.at(w, 0, 1), out.qstride(), To);
 }
 
 // ---------------------------------------------------------------- final check
@@ -646,7 +750,7 @@ hipError_t zip_bufs(tmed_ctx *c, ZipBufs &z) {
   const size_t o_pts = take(rows * kZipRow * 16), o_dig = take((size_t)kZipWin * rows * 2), o_cs = take(N * 32);
   size_t o_k[2], o_v[2];
   for (int p = 0; p < 2; p++) { o_k[p] = take((size_t)kZipWin * cap * 2); o_v[p] = take((size_t)kZipWin * cap * 4); }
-  const size_t o_hist = take((size_t)kZipWin * 256 * tiles * 4), o_part = take((N / 256 + 1) * 8 * 8);
+  const size_t o_hist = take((size_t)kZipWin * 256 * (tiles + 1) * 4), o_part = take((N / 256 + 1) * 8 * 8);
   const size_t o_ctot = take(64);
   size_t o_it[4];
   uint32_t n_it[4] = {kZipItemsMax, (kZipItemsMax + 63) / 64, ((kZipItemsMax + 63) / 64 + 63) / 64, 1};
@@ -691,10 +795,11 @@ hipError_t zip_msm(tmed_ctx *c, const ZipBufs &z, uint32_t N, uint32_t lo, uint3
   const dim3 sg((a.tiles + kSortWaves - 1) / kSortWaves, kZipWin);
   hipLaunchKernelGGL(zip_sort_hist_kernel<0>, sg, dim3(kSortWaves * 64), 0, s, a);
   hipLaunchKernelGGL(zip_sort_scan_kernel, dim3(kZipWin), dim3(1024), 0, s, a.hist, a.tiles);
-  hipLaunchKernelGGL(zip_sort_scatter_kernel<0>, sg, dim3(kSortWaves * 64), 0, s, a);
+  const dim3 sc(a.tiles, kZipWin);
+  hipLaunchKernelGGL(zip_sort_scatter_kernel<0>, sc, dim3(64), 0, s, a);
   hipLaunchKernelGGL(zip_sort_hist_kernel<1>, sg, dim3(kSortWaves * 64), 0, s, a);
   hipLaunchKernelGGL(zip_sort_scan_kernel, dim3(kZipWin), dim3(1024), 0, s, a.hist, a.tiles);
-  hipLaunchKernelGGL(zip_sort_scatter_kernel<1>, sg, dim3(kSortWaves * 64), 0, s, a);
+  hipLaunchKernelGGL(zip_sort_scatter_kernel<1>, sc, dim3(64), 0, s, a);
   if (getenv("TMED_ZIP_DEBUG")) {  // diagnostics: the sorted windows against the digits
     hipStreamSynchronize(s);
     std::vector<int16_t> dg((size_t)kZipWin * 2 * N);
@@ -727,8 +832,8 @@ hipError_t zip_msm(tmed_ctx *c, const ZipBufs &z, uint32_t N, uint32_t lo, uint3
                      z.vals[1], z.cap, cnt, z.pts, ZipItems{z.bsum, kZipItemsMax}, it[0]);
   hipLaunchKernelGGL(zip_bucket_weights_kernel, dim3((kZipItemsMax + 255) / 256, kZipWin), dim3(256), 0, s,
                      ZipItems{z.bsum, kZipItemsMax}, it[0]);
-  for (int L = 0; L < 3; L++)
-    hipLaunchKernelGGL(zip_reduce_kernel, dim3((n_it[L] + 63) / 64, kZipWin), dim3(64), 0, s, it[L], L, it[L + 1]);
+  hipLaunchKernelGGL(zip_reduce_kernel, dim3((n_it[0] + 63) / 64, kZipWin), dim3(64), 0, s, it[0], it[1]);
+  hipLaunchKernelGGL(zip_reduce12_kernel, dim3(1, kZipWin), dim3(64 * kZipL1Waves), 0, s, it[1], it[3]);
   hipLaunchKernelGGL(zip_final_kernel, dim3(1), dim3(64), 0, s, it[3], z.ctot, c->d_bcomb16, z.flag);
   return hipGetLastError();
 }
