@@ -23,6 +23,14 @@ Extra JSON fields:
   c2_keyset_variant    the second C2 variant: 10k reused keys, key cache on.
   c1_verifycommit_p50  the metric's second half: VerifyCommit p50 latency @175 validators
                 through the seam, generic and key-cached, with its 1-thread CPU baseline.
+  c5_adversarial       C5: the C2 batch with 1% invalid signatures of every failure class
+                (tmed.workload.c5_mix), rate and mismatches against the port's bits.
+  c4_shard             C4 (blocksync, 12,500 blocks x 175 validators per rank = 100k blocks over 8 GPUs) through the commit
+                seam: commits/s and signatures/s, outcome mismatches against the oracle, and the
+                per-rank host phase split (plan+staging / enqueue+device wait / replay).
+  zip215_batch_mode    the OPT-IN ZIP-215 rule (tmed_verify_batch_zip215): C2 all valid (one
+                randomized batch equation per 2^20 chunk) and the C5 mix (bisection + exact
+                single checks), each against the port's ZIP-215 bits, with the call's statistics.
 `--gpus N` without a torchrun environment starts N ranks itself (a child torch.distributed.run).
 """
 from __future__ import annotations

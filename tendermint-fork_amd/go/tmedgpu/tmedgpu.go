@@ -346,6 +346,63 @@ func (e *Engine) MerkleRoots(trees [][][]byte) ([][32]byte, error) {
 	return append([][32]byte(nil), out...), nil
 }
 
+// batchArgs packs n (pubkey, message, signature) tuples for tmed_verify_batch(_zip215):
+// pubKeys n x 32, sigs as given (the lengths travel so a wrong-length signature is rejected
+// exactly as ed25519.Verify rejects it), messages concatenated with offsets.
+func batchArgs(a *arena, pubKeys []byte, msgs, sigs [][]byte) (pk, sg *C.uint8_t, sl *C.uint32_t,
+	mg *C.uint8_t, mo *C.uint32_t) {
+	n := len(msgs)
+	sigBuf := make([]byte, 64*n)
+	lens := make([]uint32, n)
+	off := make([]uint32, n+1)
+	var flat []byte
+	for i := 0; i < n; i++ {
+		copy(sigBuf[64*i:64*i+64], sigs[i])
+		lens[i] = uint32(len(sigs[i]))
+		flat = append(flat, msgs[i]...)
+		off[i+1] = uint32(len(flat))
+	}
+	flat = append(flat, make([]byte, 16)...) // the device reader may touch past the last message
+	return a.bytes(pubKeys), a.bytes(sigBuf), a.u32(lens), a.bytes(flat), a.u32(off)
+}
+
+// VerifyBatch returns ed25519.Verify (Go 1.18 rule, crypto/ed25519/ed25519.go:148-155) of every
+// tuple (tmed_verify_batch).
+func (e *Engine) VerifyBatch(pubKeys []byte, msgs, sigs [][]byte) ([]bool, error) {
+	return e.batch(pubKeys, msgs, sigs, false)
+}
+
+// VerifyBatchZIP215 returns the ZIP-215 decision of every tuple (tmed_verify_batch_zip215):
+// OPT-IN, for chains that adopt the rule of spec/core/encoding.md:52-54.
+func (e *Engine) VerifyBatchZIP215(pubKeys []byte, msgs, sigs [][]byte) ([]bool, error) {
+	return e.batch(pubKeys, msgs, sigs, true)
+}
+
+func (e *Engine) batch(pubKeys []byte, msgs, sigs [][]byte, zip215 bool) ([]bool, error) {
+	n := len(msgs)
+	if n == 0 {
+		return nil, nil
+	}
+	var a arena
+	defer a.free()
+	pk, sg, sl, mg, mo := batchArgs(&a, pubKeys, msgs, sigs)
+	out := (*[1 << 28]C.uint8_t)(a.alloc(uintptr(n)))[:n:n]
+	var rc C.int
+	if zip215 {
+		rc = C.tmed_verify_batch_zip215(e.ctx, pk, sg, sl, mg, mo, C.size_t(n), &out[0])
+	} else {
+		rc = C.tmed_verify_batch(e.ctx, pk, sg, sl, mg, mo, C.size_t(n), &out[0])
+	}
+	if rc != 0 {
+		return nil, errors.New(C.GoString(C.tmed_strerror(rc)))
+	}
+	ok := make([]bool, n)
+	for i := range ok {
+		ok[i] = out[i] != 0
+	}
+	return ok, nil
+}
+
 // Pool is one engine per GPU of the node, used from ONE process (a Tendermint node):
 // tmed_verify_commits_multi / tmed_blocksync_verify_multi shard the work over the contexts
 // concurrently; no collective is needed since host memory is shared.

@@ -11,7 +11,7 @@ STEPS="${*:-tests bench prof}"
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 900 python -m pytest tests -x -q -m gpu > $OUT/gpu_tests.log 2>&1; rc=$?
+      timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1; rc=$?
       echo "tests rc=$rc" | tee -a $OUT/gpu_tests.log ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?
@@ -21,7 +21,7 @@ for s in $STEPS; do
       echo "bench rc=$rc" | tee -a $OUT/bench.log; tail -1 $OUT/bench.log ;;
     prof)
       cd /tmp && export TMPDIR=/tmp
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-c1 --no-keyset > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1; rc=$?
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline ${PROF_ARGS:-} > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1; rc=$?
       cd $GRAFT_REPO_ROOT; echo "prof rc=$rc" | tee -a $OUT/prof.log ;;
     variants)
       rc=0
@@ -52,7 +52,7 @@ for s in $STEPS; do
       IFS='|' read -ra SETS <<< "$PMC_SETS"
       for ctr in "${SETS[@]}"; do
         tag=$(echo $ctr | tr ' ' '_')
-        timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$OUT/pmc_$tag -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-peak --no-c1 --no-keyset > $GRAFT_REPO_ROOT/$OUT/pmc_$tag.log 2>&1; rc=$?
+        timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$OUT/pmc_$tag -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-peak --no-c1 --no-c4 --no-c5 --no-zip215 > $GRAFT_REPO_ROOT/$OUT/pmc_$tag.log 2>&1; rc=$?
         echo "pmc $ctr rc=$rc" | tee -a $GRAFT_REPO_ROOT/$OUT/pmc.log
         if fatal $rc; then break; fi
       done
