@@ -115,6 +115,19 @@ int main() {
     printf("{\"op\": \"%s\", \"ms\": %.3f, \"ns_per_op_all_lanes\": %.4f, \"Gop_s\": %.2f}\n", k.name, ms, per,
            (double)n * iters * k.ops / (ms * 1e-3) / 1e9);
   }
+  // Lone wave (one 64-lane block): the latency regime of the C1 kernels' serial chains.
+  for (auto &k : ks) {
+    const int it1 = 2550;
+    hipLaunchKernelGGL(k.k, dim3(1), dim3(64), 0, 0, d, 64, 10);
+    hipEventRecord(a, 0);
+    hipLaunchKernelGGL(k.k, dim3(1), dim3(64), 0, 0, d, 64, it1);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    printf("{\"op\": \"%s\", \"lone_wave\": true, \"ns_per_op_per_chain\": %.2f}\n", k.name,
+           (double)ms * 1e6 / it1 / k.ops);
+  }
   return 0;
 }
 #endif
