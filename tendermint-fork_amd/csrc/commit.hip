@@ -863,13 +863,30 @@ struct BsBatch {
 };
 }  // namespace
 
-// Two-slot pipeline over batches of bsz requests whose validator sets share one key set
-// (0 = generic keys): batch b is planned, staged and queued while the device verifies batch
-// b-1, which is then collected and replayed (f4).  Same results as one run_seam over all
+// Pipeline over batches of up to bsz requests whose validator sets share one key set (0 = generic
+// keys): batch b is planned, staged and queued while the device copies in and verifies the batch
+// before it, which is then collected and replayed (f4).  Same results as one run_seam over all
 // requests; the caller has checked every request (check_request) beforehand.
+// TMED_PIPE_SLOTS=3 keeps a third batch in flight (the host plans b+1 while b-1 and b are on the
+// device; the first two batches are a quarter and half of bsz so the device starts sooner).  On
+// the GPU box's 16-CPU share it was SLOWER: the host staging of batch b then overlaps the copy
+// engine reading batch b-1 out of pinned memory and takes twice as long (C4 166-172 against
+// 181-191 M verifies/s, profiles/r03/c4_pipe/), so two slots stay the default.
+constexpr int kPipeSlots = 3;
+static_assert(kPipeSlots <= (int)(sizeof(((tmed_ctx *)nullptr)->vslot) / sizeof(tmed::VoteSlot)),
+              "one context vote slot per pipeline slot");
+static int pipe_slots() {
+  static const int n = [] {
+    const char *v = getenv("TMED_PIPE_SLOTS");  // 3: three batches in flight (see above)
+    return v && v[0] == '3' ? 3 : 2;
+  }();
+  return n;
+}
+
 static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t nb, size_t bsz, uint64_t keyset,
                          tmed_commit_result *out) {
-  BsBatch slots[2];
+  BsBatch slots[kPipeSlots];
+  const int ns = pipe_slots();
   int rc = TMED_OK;
   // tmed_seam_phase_us for a pipelined call: host plan + templates + staging, host time blocked on
   // the device (enqueueing the copies and kernels, votes_collect), host replay — the first and
@@ -898,15 +915,18 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
   };
   std::unique_lock<std::mutex> lk(ctx->mu);
   size_t idx = 0;
-  for (size_t lo = 0; lo < nb && rc == TMED_OK; lo += bsz, idx++) {
+  for (size_t lo = 0; lo < nb && rc == TMED_OK; idx++) {
     PhaseClock clk;
-    BsBatch &b = slots[idx & 1];
-    BsBatch &prev = slots[(idx + 1) & 1];
+    BsBatch &b = slots[idx % ns];
+    BsBatch &mid = slots[(idx + ns - 1) % ns];  // batch idx-1 (in flight; with two slots the same as old)
+    BsBatch &old = slots[(idx + 1) % ns];       // batch idx-ns+1: collected once batch idx is queued
+    const size_t want = ns == 2 ? bsz : idx == 0 ? std::max<size_t>(1, bsz / 4) : idx == 1 ? std::max<size_t>(1, bsz / 2) : bsz;
     b.lo = lo;
-    b.n = std::min(bsz, nb - lo);
-    const tmed_commit_request *rq = reqs + lo;
+    b.n = std::min(want, nb - lo);
+    lo += b.n;
+    const tmed_commit_request *rq = reqs + b.lo;
     const auto tp = clock::now();
-    rc = seam_plan(rq, b.n, out + lo, b.plans, b.cands);
+    rc = seam_plan(rq, b.n, out + b.lo, b.plans, b.cands);
     clk.lap("plan");
     const size_t m = b.cands.size();
     bool fits = true;
@@ -914,7 +934,8 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
     clk.lap("templates");
     if (rc == TMED_OK && m) {
       if (fits && m <= 0xffffffffu) {
-        rc = stage_group(ctx, rq, b.n, b.cands, nullptr, (uint32_t)m, keyset, b.tmpl.data(), (int)(idx & 1), b.st);
+        rc = stage_group(ctx, rq, b.n, b.cands, nullptr, (uint32_t)m, keyset, b.tmpl.data(), (int)(idx % ns),
+                         b.st);
         clk.lap("stage");
         const auto te = clock::now();
         ph[0] += us(tp, te);
@@ -923,21 +944,24 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
         ph[1] += us(te, clock::now());  // queueing copies / launches can block behind a busy device
         b.device = rc == TMED_OK;
       } else {  // oversize template: host-assembled messages, synchronous (drain the pipeline first)
-        rc = finish(prev);
+        rc = finish(old);
+        if (rc == TMED_OK) rc = finish(mid);
         lk.unlock();
         b.valid.assign(m, 0);
         if (rc == TMED_OK) rc = ctx_verify_host_msgs(ctx, rq, b.n, b.cands, b.valid.data());
         lk.lock();
       }
     }
-    if (rc == TMED_OK) rc = finish(prev);  // overlaps the device work of batch b
-    clk.lap("finish_prev");
-    if (trace_on() && prev.st.m)
-      fprintf(stderr, "[tmed] blocksync prev batch kernels %.0fus\n", 1000.0 * ctx->last_ms);
+    const bool traced = trace_on() && old.n && old.st.m;
+    if (rc == TMED_OK) rc = finish(old);  // overlaps the device work of batches idx-1 and idx
+    clk.lap("finish_old");
+    if (traced)
+      fprintf(stderr, "[tmed] blocksync collected batch: kernels %.0fus copy-in %.0fus copy end -> kernels %.0fus\n",
+              1000.0 * ctx->last_ms, 1000.0 * ctx->last_copy_ms, 1000.0 * ctx->last_copy_gap_ms);
     clk.emit("pipelined batch", b.n, m);
   }
-  for (BsBatch &b : slots)
-    if (rc == TMED_OK) rc = finish(b);
+  for (int k = 0; k < ns; k++)  // oldest first
+    if (rc == TMED_OK) rc = finish(slots[(idx + k) % ns]);
   if (rc != TMED_OK) (void)hipStreamSynchronize(ctx->stream);
   for (int k = 0; k < 3; k++) g_seam_us[k] = ph[k];
   return rc;

@@ -80,11 +80,11 @@ int verify_votes_device(tmed_ctx *c, uint64_t keyset, const uint8_t *keys, const
                         const int64_t *ts_sec, const int32_t *ts_nanos, uint32_t m, uint8_t *out);
 
 // Zero-copy form of the same: votes_stage() returns pointers into the pinned staging area
-// of one of the context's two vote slots; the caller fills them; votes_enqueue() queues
+// of one of the context's vote slots; the caller fills them; votes_enqueue() queues
 // copy-in, assembly, verification and copy-out on the context stream; votes_collect()
-// waits for that slot and returns the bits.  votes_launch() = enqueue + collect.  Two
+// waits for that slot and returns the bits.  votes_launch() = enqueue + collect.  Three
 // slots let a pipelined caller (tmed_blocksync_verify) stage batch b+1 on the host while
-// the device runs batch b.  The caller holds ctx->mu across stage..collect.
+// the device copies batch b in and runs batch b-1.  The caller holds ctx->mu across stage..collect.
 struct VoteStage {
   int slot = 0;
   const Keyset *ks = nullptr;
@@ -98,6 +98,7 @@ struct VoteStage {
   bool zc = false;  // the kernels read the pinned staging buffer directly (votes_enqueue)
   bool timed = true;  // kernel-time events recorded (tmed_last_kernel_ms)
   bool keys_checked = false;  // every key-set index < the key set's size (checked while staging)
+  bool copy_timed = false;    // cp0 / cp1 recorded around the copy-in (TMED_TRACE)
 };
 // staged-vote batches up to this size skip the copies (kernels read / write pinned host memory)
 constexpr size_t kVoteZeroCopyMax = 256u << 10;
@@ -118,6 +119,7 @@ struct VoteSlot {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the device work of the slot's last batch
   hipEvent_t done = nullptr;                // after its copy-out
   hipEvent_t copied = nullptr;              // its staged votes are on the device (copy stream)
+  hipEvent_t cp0 = nullptr, cp1 = nullptr;  // around its copy-in (TMED_TRACE only)
 };
 }  // namespace tmed
 
@@ -127,10 +129,12 @@ struct tmed_ctx {
   hipStream_t copy_stream = nullptr;  // H2D of staged votes, so batch b's copy overlaps b-1's kernels
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
+  float last_copy_ms = 0.f, last_copy_gap_ms = 0.f;  // TMED_TRACE: copy-in of the last collected batch, copy end -> kernels
   std::mutex mu;
   int4 *d_bcomb = nullptr;  // signed radix-256 comb of +B (shared)
   int4 *d_b16 = nullptr;    // j*B, j = 0..32768 (main-kernel variant 5), built at init
   int4 *d_bcomb16 = nullptr;  // radix-2^16 comb of +B (key-cached throughput kernel), 67 MB
+  int4 *d_b26 = nullptr;      // radix-2^26 B tables of the half-size main kernel (8.6 GB, shared per device)
   int4 *d_slab = nullptr;
   int4 *d_prep = nullptr;
   int4 *d_fin = nullptr;      // batched-finish hand-off (kFinBytes)
@@ -148,7 +152,7 @@ struct tmed_ctx {
   tmed::KernelTimer timer;
   tmed::DevBuf d_a, d_b, d_msg, d_off, d_out, d_c;
   tmed::HostBuf h_a, h_b, h_msg, h_off, h_out, h_c;
-  tmed::VoteSlot vslot[2];
+  tmed::VoteSlot vslot[3];  // the blocksync pipeline (commit.hip run_pipelined: two slots, three with TMED_PIPE_SLOTS=3)
   tmed::DevBuf d_merkle_a, d_merkle_b, d_merkle_idx;  // Merkle level digests (ping-pong) + level indexes
   tmed::DevBuf d_korder;  // key-grouped order of a key-cached batch: counts / cursors + permutation
   tmed::DevBuf d_zip;     // ZIP-215 batch mode scratch (zip215.hip zip_bufs: points, digits, sort, buckets)
@@ -196,7 +200,7 @@ inline hipError_t generic_verify(tmed_ctx *c, const uint8_t *pub, const uint8_t 
     return launch_verify_glat(pub, sig, msgs, off, n, out, c->d_bcomb16, c->d_glat, s, msg_slots, timer, va);
   }
   if (va) return hipErrorInvalidValue;
-  hipError_t e = launch_verify(pub, sig, msgs, off, n, out, c->d_slab, c->slab_slots, BTabs{c->d_b16, c->d_bcomb16},
+  hipError_t e = launch_verify(pub, sig, msgs, off, n, out, c->d_slab, c->slab_slots, BTabs{c->d_b16, c->d_bcomb16, c->d_b26},
                                c->d_prep, c->d_fin, c->d_fin_pre, s, c->chunk, c->main_waves, msg_slots, timer);
   c->last_hs_count = (e != hipSuccess || c->main_waves == 5) ? 0 : last_chunk_count(n, c->chunk);
   return e;

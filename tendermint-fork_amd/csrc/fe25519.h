@@ -204,6 +204,36 @@ TMED_HD void fe_sq(fe &h, const fe &f) {
 #endif
 }
 
+// h = f^2 for a CARRIED f (one carried value, e.g. any mul / sq output, not a sum):
+// fe_sq1c_fused's 13 premultiplied copies (x2 of limbs 0, 1, 2, 3, 5, 7, x19 of 6, 8, x38 of
+// 5..9; x38 of 6, 8 as 2 * x19) instead of fe_sq's 19.
+#ifndef TMED_FE_SQC
+#define TMED_FE_SQC 1  // A/B knob: 0 = carried inputs take the general fe_sq
+#endif
+struct fe_premul_c {
+  int32_t x[10], x2[10], x19[10], x38[10];
+  TMED_HDM explicit fe_premul_c(const fe &f) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      x[i] = f.v[i];
+      x2[i] = dbl32(f.v[i]);
+      x19[i] = mul19(f.v[i]);
+      x38[i] = (i == 6 || i == 8) ? dbl32(x19[i]) : mul38(f.v[i]);
+    }
+  }
+};
+
+TMED_HD void fe_sqc(fe &h, const fe &f) {
+#if TMED_FE_SQC
+  const fe_premul_c p(f);
+  int64_t acc[10];
+  fe_sq1c_fused(acc, p.x, p.x2, p.x19, p.x38);
+  fe_fused_fin(h, acc);
+#else
+  fe_sq(h, f);
+#endif
+}
+
 // h = 2 f^2 (f carried)
 TMED_HD void fe_sq2(fe &h, const fe &f) {
   const fe_premul p(f);
@@ -255,6 +285,19 @@ TMED_HD void fe_sq_x2(fe &h0, const fe &f0, fe &h1, const fe &f1) {
 #endif
 }
 
+// h0 = f0^2, h1 = f1^2 for carried f0, f1 (fe_sqc)
+TMED_HD void fe_sqc_x2(fe &h0, const fe &f0, fe &h1, const fe &f1) {
+#if TMED_FE_SQC && TMED_FE_FUSED >= 2
+  const fe_premul_c a(f0), b(f1);
+  int64_t H0[10], H1[10];
+  fe_sq1c_fused_x2(H0, H1, a.x, a.x2, a.x19, a.x38, b.x, b.x2, b.x19, b.x38);
+  fe_fused_fin(h0, H0);
+  fe_fused_fin(h1, H1);
+#else
+  fe_sq_x2(h0, f0, h1, f1);
+#endif
+}
+
 // h0 = 2 f0^2 (f0 carried), h1 = f1^2
 TMED_HD void fe_sq2_sq(fe &h0, const fe &f0, fe &h1, const fe &f1) {
 #if TMED_FE_FUSED >= 2
@@ -271,19 +314,20 @@ TMED_HD void fe_sq2_sq(fe &h0, const fe &f0, fe &h1, const fe &f1) {
 #endif
 }
 
+// f carried (every caller squares a product output)
 TMED_HD void fe_sqn(fe &h, const fe &f, int n) {
-  fe_sq(h, f);
+  fe_sqc(h, f);
 #pragma unroll 1
-  for (int i = 1; i < n; i++) fe_sq(h, h);
+  for (int i = 1; i < n; i++) fe_sqc(h, h);
 }
 
 // z^(2^250 - 1) and z^11 (shared prefix of the inversion / (p-5)/8 chains)
 TMED_HD void fe_pow250(fe &z250, fe &z11, const fe &z) {
   fe z2, z9, t, a, b, c;
-  fe_sq(z2, z);
+  fe_sqc(z2, z);                            // z carried (a product output at every call site)
   fe_sqn(t, z2, 2); fe_mul(z9, t, z);
   fe_mul(z11, z9, z2);
-  fe_sq(t, z11); fe_mul(a, t, z9);          // a = z^(2^5-1)
+  fe_sqc(t, z11); fe_mul(a, t, z9);         // a = z^(2^5-1)
   fe_sqn(t, a, 5); fe_mul(b, t, a);         // b = 2^10-1
   fe_sqn(t, b, 10); fe_mul(c, t, b);        // c = 2^20-1
   fe_sqn(t, c, 20); fe_mul(t, t, c);        // 2^40-1

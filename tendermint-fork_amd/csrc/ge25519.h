@@ -31,13 +31,21 @@ TMED_HD void ge_cached_0(ge_cached &h) { fe_1(h.YpX); fe_1(h.YmX); fe_1(h.Z); fe
 TMED_HD void ge_niels_0(ge_niels &h) { fe_1(h.YpX); fe_1(h.YmX); fe_0(h.XY2d); }
 
 // (Independent products in pairs, fe_mul_x2; p1p1 -> p3 pairs only X, Y: a second pair spilled
-// in verify_main_hs_kernel.)
+// in verify_main_hs_kernel.)  fe_mul(h, f, g) premultiplies g by 19 (nine v_mul_lo_u32) and
+// f's odd limbs by 2: the operands are ordered so that only T and Y are ever g (and X, Z f),
+// and the compiler shares those copies between the products: 18 instead of 27 x19 copies in
+// p1p1 -> p3, 10 instead of 15 x2 copies in p1p1 -> p2.
+#ifndef TMED_P1P1_VC
+#define TMED_P1P1_VC 1  // A/B knob: 0 = Y * Z with Y as f (the round-2 order)
+#endif
 TMED_HD void ge_p1p1_to_p2(ge_p2 &r, const ge_p1p1 &p) {
-  fe_mul_x2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
+  if (TMED_P1P1_VC) fe_mul_x2(r.X, p.X, p.T, r.Y, p.Z, p.Y);
+  else fe_mul_x2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.Z, p.T);
 }
 TMED_HD void ge_p1p1_to_p3(ge_p3 &r, const ge_p1p1 &p) {
-  fe_mul_x2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
+  if (TMED_P1P1_VC) fe_mul_x2(r.X, p.X, p.T, r.Y, p.Z, p.Y);
+  else fe_mul_x2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.Z, p.T);
   fe_mul(r.T, p.X, p.Y);
 }
@@ -53,7 +61,7 @@ TMED_HD void ge_p3_to_cached(ge_cached &r, const ge_p3 &p) {
 // r = 2p.  4 squarings; outputs are <= 3-sums (see fe25519.h).
 TMED_HD void ge_p2_dbl(ge_p1p1 &r, const ge_p2 &p) {
   fe xx, yy, b, a, t;
-  fe_sq_x2(xx, p.X, yy, p.Y);
+  fe_sqc_x2(xx, p.X, yy, p.Y);  // X, Y carried: product outputs, decoded or identity coordinates
   fe_add(t, p.X, p.Y);
   fe_sq2_sq(b, p.Z, a, t);
   fe_add(r.Y, yy, xx);
@@ -120,18 +128,18 @@ TMED_HD bool ge_frombytes_go(ge_p3 &h, const uint32_t w[8]) {
   fe y, u, v, v3, uv7, r, chk, t, one, d, sqrtm1;
   fe_const_d(d); fe_const_sqrtm1(sqrtm1); fe_1(one);
   fe_from_words(y, w);
-  fe_sq(u, y);
+  fe_sqc(u, y);
   fe_mul(v, u, d);
   fe_sub(u, u, one); fe_carry(u, u);       // u = y^2 - 1
   fe_add(v, v, one); fe_carry(v, v);       // v = d y^2 + 1
   // SqrtRatio(u, v): r = (u v^3) (u v^7)^((p-5)/8)
-  fe_sq(t, v); fe_mul(v3, t, v);           // v^3
-  fe_sq(t, v3); fe_mul(uv7, t, v);         // v^7
+  fe_sqc(t, v); fe_mul(v3, t, v);          // v^3
+  fe_sqc(t, v3); fe_mul(uv7, t, v);        // v^7
   fe_mul(uv7, uv7, u);                     // u v^7
   fe_pow22523(t, uv7);
   fe_mul(r, u, v3);
   fe_mul(r, r, t);
-  fe_sq(t, r); fe_mul(chk, v, t);          // check = v r^2
+  fe_sqc(t, r); fe_mul(chk, v, t);         // check = v r^2
   fe uneg; fe_neg(uneg, u);
   const bool correct = fe_equal(chk, u);
   const bool flipped = fe_equal(chk, uneg);

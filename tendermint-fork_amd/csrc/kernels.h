@@ -46,7 +46,13 @@ constexpr size_t kFinPreBytes = (size_t)kFinPreStride * 3 * 16;
 struct BTabs {
   const int4 *b16;
   const int4 *comb16;
+  const int4 *b26 = nullptr;  // radix-2^26 B windows of the half-size main kernel (null: radix 2^16)
 };
+// j * B and j * 2^128 B for j = 0..2^25 (affine niels, 128-B rows): the two radix-2^26 tables of
+// verify_main_hs_kernel<26>, 8.6 GB, built once per device (tmed_capi.hip b26_acquire).
+constexpr uint32_t kB26Entries = (1u << 25) + 1;
+constexpr size_t kB26Bytes = 2 * (size_t)kB26Entries * 128;
+hipError_t launch_build_b26(const int4 *comb16, int4 *tab, hipStream_t stream);
 constexpr uint32_t kB16Entries = 32769;
 constexpr size_t kB16Bytes = (size_t)kB16Entries * 128;
 hipError_t launch_build_b16(int4 *tab, hipStream_t stream);

@@ -104,12 +104,13 @@ struct SlabTab {
 typedef __attribute__((address_space(1))) void global_void;
 typedef __attribute__((address_space(3))) void lds_void;
 
-// Radix-2^16 B table (double_scalarmult<16>): j*B, j = 0..32768, affine niels in 128-B rows
+// Radix-2^16 / 2^26 B table (double_scalarmult<16>, hs_straus): j*B, j = 0..32768 / 2^25, affine niels in 128-B rows
 // (kCombEntryInt4 int4, 4.2 MB, L2/MALL-resident).  The entry of the next B window is fetched
 // into LDS with global_load_lds_dwordx4 right after the current B addition, 16 doublings
 // before it is needed; buf is this wave's [8][64] int4 region (lane l's piece q at q*64+l).
-struct B16Pf {
-  static constexpr int kBits = 16;
+template <int BITS>
+struct BPf {
+  static constexpr int kBits = BITS;
   const int4 *tab;
   int4 *buf;
   uint32_t lane;
@@ -234,14 +235,32 @@ __global__ __launch_bounds__(kThreadsPerBlock, TMED_PREP_WAVES) void verify_prep
 }
 
 // ---- f1: CanonicalVote sign-bytes assembled on the device ----------
-// (votes_dev.h assemble_vote; this kernel serves the throughput and key-cached paths, the
-// generic latency kernels assemble in their hash lanes.)
-__global__ __launch_bounds__(kThreadsPerBlock) void assemble_votes_kernel(VoteAsm va, uint32_t n, uint8_t *__restrict__ out,
-                                                                        uint32_t *__restrict__ out_len) {
-  __shared__ int4 tl[kThreadsPerBlock][kVoteTmplBytes / 16];
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  assemble_vote(va, i, out, out_len, tl[threadIdx.x]);
+// (votes_dev.h assemble_vote_into; this kernel serves the throughput and key-cached paths, the
+// latency kernels assemble in their hash lanes.)  One wave per block: every lane assembles its
+// vote in LDS (byte stores to LDS, beside its staged template), then the wave writes its 64
+// consecutive 256-B slots as sixteen coalesced 1-KB rows.  Assembled straight into the global
+// slots, each lane's ~114 byte stores went to 64 different lines per instruction: 0.29 ms per
+// 853k-vote blocksync batch (profiles/r03/fin2/kernel_stats.csv).
+constexpr uint32_t kAsmLanes = 64;
+__global__ __launch_bounds__(kAsmLanes) void assemble_votes_kernel(VoteAsm va, uint32_t n, uint8_t *__restrict__ out,
+                                                                  uint32_t *__restrict__ out_len) {
+  __shared__ int4 tl[kAsmLanes][kVoteTmplBytes / 16];
+  __shared__ int4 ob[kAsmLanes][kVoteSlot / 16];
+  const uint32_t lane = threadIdx.x, i0 = blockIdx.x * kAsmLanes, i = i0 + lane;
+  if (i < n) {
+#pragma unroll
+    for (int q = 0; q < (int)(kVoteSlot / 16); q++) ob[lane][q] = make_int4(0, 0, 0, 0);
+    out_len[i] = assemble_vote_into(va, i, reinterpret_cast<uint8_t *>(ob[lane]), tl[lane]);
+  }
+  __syncthreads();
+  const uint32_t nslots = n - i0 < kAsmLanes ? n - i0 : kAsmLanes;
+  int4 *dst = reinterpret_cast<int4 *>(out + (size_t)i0 * kVoteSlot);
+  const int4 *src = &ob[0][0];
+#pragma unroll
+  for (uint32_t q = 0; q < kVoteSlot / 16; q++) {
+    const uint32_t c = q * kAsmLanes + lane;  // int4 index in the wave's 16-KB run of slots
+    if (c / (kVoteSlot / 16) < nslots) dst[c] = src[c];
+  }
 }
 
 // Projective R' of signature slot (X, Y, Z: 30 limbs + 2 pad = 8 int4), stored [q][slot].
@@ -270,7 +289,7 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_kernel(
   ge_p3 A;
   const bool ok = prep_load(prep, stride, slot, k, s, A);
   ge_p2 R;
-  B16Pf bt{b16, sb16[threadIdx.x >> 6], threadIdx.x & 63u};
+  BPf<16> bt{b16, sb16[threadIdx.x >> 6], threadIdx.x & 63u};
   SlabTab tab{slab, slot};
   verify_main_point(R, k, s, A, tab, bt);
   fin_store(fin, kFinCap, i - fin_base, R.X, R.Y, R.Z);
@@ -316,7 +335,7 @@ __global__ __launch_bounds__(kThreadsPerBlock, TMED_PREP_R_WAVES) void verify_pr
   fe Rx, Ry;
   bool dneg;
   int W;
-  const bool rok = hs_prep_r(k, s, Rw, cr, dr, er, dneg, Rx, Ry, W, zip215 != 0);
+  const bool rok = hs_prep_r(k, s, Rw, cr, dr, er, dneg, Rx, Ry, W, zip215 != 0, /*raw_e=*/true);
 #pragma unroll
   for (int j = 0; j < 8; j++) { w[j] = (int32_t)cr[j]; w[13 + j] = (int32_t)er[j]; }
 #pragma unroll
@@ -372,11 +391,22 @@ struct HsDigitsDev {
 // radix-2^16 comb (each entry fetched into LDS 16 doublings ahead), identity test.  Every
 // lane of the grid stays to the end (the wave maximum of W is a shuffle reduction); lanes
 // past count run on the identity and store nothing.
-__global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_hs_kernel(
+#ifndef TMED_HS_WAVES
+#define TMED_HS_WAVES 2  // waves per SIMD of the half-size main kernel (248 VGPRs at 2)
+#endif
+// BB: radix of the B windows — 26 (the default: btab, two 2^25-entry tables, ten B additions) or
+// 16 (windows 0 and 8 of the 2^16 comb, sixteen; when the 8.6-GB tables are unavailable).  The
+// hand-off carries e unrecoded (hs_prep_r raw_e); radix 16 recodes it here.
+template <int BB>
+__global__ __launch_bounds__(kThreadsPerBlock, TMED_HS_WAVES) void verify_main_hs_kernel(
     uint32_t base, uint32_t count, const int4 *__restrict__ prep, const int4 *__restrict__ prep2, uint32_t stride,
-    int4 *__restrict__ slab, const int4 *__restrict__ comb16, uint8_t *__restrict__ out, int zip215) {
+    int4 *__restrict__ slab, const int4 *__restrict__ btab, uint8_t *__restrict__ out, int zip215) {
   __shared__ int4 sbl[kThreadsPerBlock / 64][8 * 64];
+#if TMED_B16_ONEBUF
+  auto &sbh = sbl;
+#else
   __shared__ int4 sbh[kThreadsPerBlock / 64][8 * 64];
+#endif
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // position in the placed hand-off
   const bool active = slot < count;
   int32_t w[64];
@@ -388,6 +418,12 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_hs_kernel(
   uint32_t er[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) er[j] = (uint32_t)w[13 + j];
+  if (BB == 16) {
+    uint32_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) e[j] = er[j];
+    sc_recode_b<16>(er, e);
+  }
   fe Rx, Ry;
 #pragma unroll
   for (int j = 0; j < 10; j++) { Rx.v[j] = w[21 + j]; Ry.v[j] = w[31 + j]; }
@@ -411,8 +447,10 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_hs_kernel(
   const HsDigitsDev ds{prep2, stride, slot, active};
   SlabTab ta{slab, slot};
   SlabTab tr{slab + (size_t)stride * 64, slot};
-  B16Pf bl{comb16, sbl[wv], lane};
-  B16Pf bh{comb16 + (size_t)8 * kB16Entries * kCombEntryInt4, sbh[wv], lane};
+  // the high table: the second radix-2^26 table, or window 8 (j * 2^128 B) of the 2^16 comb
+  const size_t hi = BB == 26 ? (size_t)kB26Entries * kCombEntryInt4 : (size_t)8 * kB16Entries * kCombEntryInt4;
+  BPf<BB> bl{btab, sbl[wv], lane};
+  BPf<BB> bh{btab + hi, sbh[wv], lane};
   const bool id = verify_main_hs(ds, (flags & 2) != 0, er, W, A, Rx, Ry, ta, tr, bl, bh, zip215 != 0);
   if (active) out[base + (uint32_t)w[42]] = ((flags & 1) && id) ? 1 : 0;
 }
@@ -597,8 +635,12 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
         hipLaunchKernelGGL(verify_prep_r_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base, count,
                            prep, prep2, slab_stride, place, zip215 ? 1 : 0);
         if (timer) timer->mark(stream, 0);
-        hipLaunchKernelGGL(verify_main_hs_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base, count, prep,
-                           prep2, slab_stride, slab, btab.comb16, out, zip215 ? 1 : 0);
+        if (btab.b26)
+          hipLaunchKernelGGL(verify_main_hs_kernel<26>, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base, count,
+                             prep, prep2, slab_stride, slab, btab.b26, out, zip215 ? 1 : 0);
+        else
+          hipLaunchKernelGGL(verify_main_hs_kernel<16>, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base, count,
+                             prep, prep2, slab_stride, slab, btab.comb16, out, zip215 ? 1 : 0);
       } else {  // fallback 5: full-length Straus + batched finish
         hipLaunchKernelGGL(verify_main_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base, count, prep,
                            slab_stride, slab, btab.b16, fin, fbase, out);
@@ -785,6 +827,43 @@ void host_bcomb16_bases(int32_t out[16 * 40]) {
 
 hipError_t launch_build_bcomb16(const int32_t *d_bases, int4 *comb, hipStream_t stream) {
   hipLaunchKernelGGL(bcomb16_fill_kernel, dim3((16u * kB16Entries + 255) / 256), dim3(256), 0, stream, d_bases, comb);
+  return hipGetLastError();
+}
+
+// Entry (t, j) of the radix-2^26 B tables: j * 2^(128 t) B for j = 0..2^25 (t = 0, 1), from
+// windows 8t and 8t + 1 of the radix-2^16 comb (j = d0 + 2^16 d1, d0 signed: two mixed
+// additions), then affine niels with one inversion (per entry: ~15k mads, 2^26 entries, once
+// per device).
+__global__ __launch_bounds__(256) void b26_fill_kernel(const int4 *__restrict__ comb16, int4 *__restrict__ tab) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= 2u * kB26Entries) return;
+  const uint32_t t = g / kB26Entries, j = g % kB26Entries;
+  ge_niels e;
+  if (j == 0) {
+    ge_niels_0(e);
+  } else {
+    int d0 = (int)(j & 0xffffu);
+    uint32_t d1 = j >> 16;
+    if (d0 >= 32768) { d0 -= 65536; d1++; }
+    const GlobalComb16 bc{comb16};
+    ge_p3 P;
+    ge_p1p1 q;
+    ge_niels n;
+    ge_p3_0(P);
+    bc.load(8 * (int)t, d0 < 0 ? -d0 : d0, n);
+    niels_apply_sign(n, d0 < 0);
+    ge_madd_niels(q, P, n, false);
+    ge_p1p1_to_p3(P, q);
+    bc.load(8 * (int)t + 1, (int)d1, n);
+    ge_madd_niels(q, P, n, false);
+    ge_p1p1_to_p3(P, q);
+    ge_p3_to_niels(e, P);
+  }
+  niels_store(tab + (size_t)g * kCombEntryInt4, e);
+}
+
+hipError_t launch_build_b26(const int4 *comb16, int4 *tab, hipStream_t stream) {
+  hipLaunchKernelGGL(b26_fill_kernel, dim3((2u * kB26Entries + 255) / 256), dim3(256), 0, stream, comb16, tab);
   return hipGetLastError();
 }
 
@@ -1310,8 +1389,8 @@ hipError_t launch_assemble_votes(const uint8_t *tmpl, const uint32_t *tmpl_idx, 
                                  const int64_t *ts_sec, const int32_t *ts_nanos, uint32_t n, uint8_t *out,
                                  uint32_t *out_len, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(assemble_votes_kernel, dim3((n + kThreadsPerBlock - 1) / kThreadsPerBlock),
-                     dim3(kThreadsPerBlock), 0, stream, VoteAsm{tmpl, tmpl_idx, flags, ts_sec, ts_nanos}, n, out, out_len);
+  hipLaunchKernelGGL(assemble_votes_kernel, dim3((n + kAsmLanes - 1) / kAsmLanes), dim3(kAsmLanes), 0, stream,
+                     VoteAsm{tmpl, tmpl_idx, flags, ts_sec, ts_nanos}, n, out, out_len);
   return hipGetLastError();
 }
 

@@ -146,7 +146,13 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
     if (e == hipSuccess) e = hipHostGetDevicePointer(&dout, vs.h_out.p, 0);
     if (e == hipSuccess) { d = (uint8_t *)dh; out_dev = (uint8_t *)dout; }
   } else if (st.total >= (1u << 20)) {
-    e = hipMemcpyAsync(d, vs.h_votes.p, st.total, hipMemcpyHostToDevice, c->copy_stream);
+    static const bool trace = getenv("TMED_TRACE") != nullptr;
+    st.copy_timed = trace;
+    if (trace && !vs.cp0 && e == hipSuccess) e = hipEventCreate(&vs.cp0);
+    if (trace && !vs.cp1 && e == hipSuccess) e = hipEventCreate(&vs.cp1);
+    if (trace && e == hipSuccess) e = hipEventRecord(vs.cp0, c->copy_stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d, vs.h_votes.p, st.total, hipMemcpyHostToDevice, c->copy_stream);
+    if (trace && e == hipSuccess) e = hipEventRecord(vs.cp1, c->copy_stream);
     if (e == hipSuccess) e = hipEventRecord(vs.copied, c->copy_stream);
     if (e == hipSuccess) e = hipStreamWaitEvent(s, vs.copied, 0);
   } else {
@@ -186,6 +192,11 @@ int votes_collect(tmed_ctx *c, const VoteStage &st, uint8_t *out) {
   if (e != hipSuccess) return map_err(e);
   c->last_ms = 0.f;
   if (st.timed) (void)hipEventElapsedTime(&c->last_ms, vs.ev0, vs.ev1);
+  c->last_copy_ms = c->last_copy_gap_ms = 0.f;
+  if (st.copy_timed) {
+    (void)hipEventElapsedTime(&c->last_copy_ms, vs.cp0, vs.cp1);
+    if (st.timed) (void)hipEventElapsedTime(&c->last_copy_gap_ms, vs.cp1, vs.ev0);
+  }
   memcpy(out, vs.h_out.p, st.m);
   return TMED_OK;
 }

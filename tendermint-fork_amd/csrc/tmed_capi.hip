@@ -41,6 +41,52 @@ const char *tmed_strerror(int code) {
   }
 }
 
+// The radix-2^26 B tables (kernels.h kB26Bytes) are the same for every context of a device: built
+// by the first context, shared, freed with the last.  TMED_B26=0, or an allocation that fails,
+// leaves the main kernel on the radix-2^16 windows of the context's own comb.
+namespace {
+struct B26Share {
+  int4 *p = nullptr;
+  int refs = 0;
+};
+std::mutex g_b26_mu;
+B26Share g_b26[64];
+}  // namespace
+
+static int4 *b26_acquire(int device, const int4 *comb16, hipStream_t s) {
+  static const bool on = [] {
+    const char *v = getenv("TMED_B26");
+    return !(v && v[0] == '0');
+  }();
+  if (!on || device < 0 || device >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(g_b26_mu);
+  B26Share &b = g_b26[device];
+  if (!b.p) {
+    int4 *p = nullptr;
+    if (hipMalloc((void **)&p, kB26Bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    if (launch_build_b26(comb16, p, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+      (void)hipFree(p);
+      return nullptr;
+    }
+    b.p = p;
+  }
+  b.refs++;
+  return b.p;
+}
+
+static void b26_release(int device, int4 *p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_b26_mu);
+  B26Share &b = g_b26[device];
+  if (b.p == p && --b.refs == 0) {
+    (void)hipFree(b.p);
+    b.p = nullptr;
+  }
+}
+
 int tmed_init(int device, tmed_ctx **out) {
   if (!out) return TMED_EINVAL;
   *out = nullptr;
@@ -103,6 +149,7 @@ int tmed_init(int device, tmed_ctx **out) {
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (d_bases) (void)hipFree(d_bases);
   }
+  if (e == hipSuccess) c->d_b26 = b26_acquire(device, c->d_bcomb16, c->stream);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_bcomb, kCombBytesPerKey);
   if (e == hipSuccess) e = hipMalloc((void **)&d_bpub, 32);
   if (e == hipSuccess) e = hipMalloc((void **)&d_bok, 1);
@@ -134,6 +181,8 @@ void tmed_destroy(tmed_ctx *c) {
     if (v.ev1) hipEventDestroy(v.ev1);
     if (v.done) hipEventDestroy(v.done);
     if (v.copied) hipEventDestroy(v.copied);
+    if (v.cp0) hipEventDestroy(v.cp0);
+    if (v.cp1) hipEventDestroy(v.cp1);
   }
   for (auto &kv : c->keysets) free_keyset(kv.second);
   c->keysets.clear();
@@ -141,6 +190,7 @@ void tmed_destroy(tmed_ctx *c) {
   if (c->d_bcomb) hipFree(c->d_bcomb);
   if (c->d_b16) hipFree(c->d_b16);
   if (c->d_bcomb16) hipFree(c->d_bcomb16);
+  b26_release(c->device, c->d_b26);
   if (c->d_slab) hipFree(c->d_slab);
   if (c->d_prep) hipFree(c->d_prep);
   if (c->d_fin) hipFree(c->d_fin);

@@ -374,6 +374,19 @@ TMED_HD void ge_mul256(ge_p3 &P) {
   ge_p1p1_to_p3(P, t);
 }
 
+// Affine niels form (y + x, y - x, 2d x y) of a projective point: one inversion.
+TMED_HD void ge_p3_to_niels(ge_niels &out, const ge_p3 &p) {
+  fe zi, x, y, xy, d2;
+  fe_const_d2(d2);
+  fe_invert(zi, p.Z);
+  fe_mul(x, p.X, zi);
+  fe_mul(y, p.Y, zi);
+  fe_add(out.YpX, y, x); fe_carry(out.YpX, out.YpX);
+  fe_sub(out.YmX, y, x); fe_carry(out.YmX, out.YmX);
+  fe_mul(xy, x, y);
+  fe_mul(out.XY2d, xy, d2);
+}
+
 // out = j * base (j in 1..255) in niels form; branch-free double-and-add.
 TMED_HD void comb_entry(ge_niels &out, const ge_p3 &base, uint32_t j, int nbits = 8) {
   ge_cached cP;
@@ -395,15 +408,7 @@ TMED_HD void comb_entry(ge_niels &out, const ge_p3 &base, uint32_t j, int nbits 
     fe_select(acc.Z, acc.Z, sum.Z, bit);
     fe_select(acc.T, acc.T, sum.T, bit);
   }
-  fe zi, x, y, xy, d2;
-  fe_const_d2(d2);
-  fe_invert(zi, acc.Z);
-  fe_mul(x, acc.X, zi);
-  fe_mul(y, acc.Y, zi);
-  fe_add(out.YpX, y, x); fe_carry(out.YpX, out.YpX);
-  fe_sub(out.YmX, y, x); fe_carry(out.YmX, out.YmX);
-  fe_mul(xy, x, y);
-  fe_mul(out.XY2d, xy, d2);
+  ge_p3_to_niels(out, acc);
 }
 
 // Key-cached verification, phase 1: k = SHA-512(R||A||M) mod L and the S checks (A is

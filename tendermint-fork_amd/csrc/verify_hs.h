@@ -38,6 +38,10 @@
 #ifndef TMED_SLAB_PF
 #define TMED_SLAB_PF 1  // the default of kernels.hip (host builds follow the same order)
 #endif
+#ifndef TMED_B16_ONEBUF
+#define TMED_B16_ONEBUF 0  // 1: BL and BH share one prefetch buffer (the high row is fetched after the
+                           // low row is taken, the next low row after the high row is taken)
+#endif
 
 namespace tmed {
 
@@ -276,7 +280,7 @@ TMED_HD int hs_top_digit(uint32_t w_top, uint32_t w_next, int W) {
 // scalars — cr, dr: signed radix-16 (sc_recode16; dr words 5..7 are 0x88888888, i.e. zero
 // digits, since |d| < 2^150), er: signed radix-2^16 — and the window count W.
 TMED_HD void hs_scalars(const uint32_t k[8], const uint32_t s[8], uint32_t cr[8], uint32_t dr[8], uint32_t er[8],
-                        bool &dneg, int &W) {
+                        bool &dneg, int &W, bool raw_e = false) {
   uint32_t c[8], dm[8], e[8];
   W = sc_halfsize(c, dm, dneg, k);
   uint32_t zero[8];
@@ -295,7 +299,12 @@ TMED_HD void hs_scalars(const uint32_t k[8], const uint32_t s[8], uint32_t cr[8]
   for (int i = 0; i < 8; i++) e[i] = (dneg && nz) ? ne[i] : e[i];
   sc_recode16(cr, c);
   sc_recode16(dr, dm);
-  sc_recode_b<16>(er, e);
+  if (raw_e) {  // the radix-2^26 B windows recode e themselves (hs_b26_digits)
+#pragma unroll
+    for (int i = 0; i < 8; i++) er[i] = e[i];
+  } else {
+    sc_recode_b<16>(er, e);
+  }
 }
 
 // Phase 1b of the half-size path (after verify_prep's hash / S check / decode of A): strict
@@ -305,7 +314,7 @@ TMED_HD void hs_scalars(const uint32_t k[8], const uint32_t s[8], uint32_t cr[8]
 // the sign bit accepted) instead of strictly.
 TMED_HD bool hs_prep_r(const uint32_t k[8], const uint32_t s[8], const uint32_t Rw[8], uint32_t cr[8],
                        uint32_t dr[8], uint32_t er[8], bool &dneg, fe &Rx, fe &Ry, int &W,
-                       bool permissive = false) {
+                       bool permissive = false, bool raw_e = false) {
   bool rok;
   if (permissive) {
     ge_p3 P;
@@ -316,7 +325,7 @@ TMED_HD bool hs_prep_r(const uint32_t k[8], const uint32_t s[8], const uint32_t 
     rok = r_decode_strict(Rx, Ry, Rw);
   }
   if (!rok) { fe_0(Rx); fe_1(Ry); }
-  hs_scalars(k, s, cr, dr, er, dneg, W);
+  hs_scalars(k, s, cr, dr, er, dneg, W, raw_e);
   return rok;
 }
 
@@ -329,10 +338,11 @@ struct HsDigits {
 
 // Both phases of the half-size prep (the host simulation's single pass).
 TMED_HD bool verify_prep_hs(const uint32_t pubw[8], const uint32_t sigw[16], const uint8_t *msg, uint32_t mlen,
-                            HsDigits &dg, uint32_t er[8], bool &dneg, ge_p3 &A, fe &Rx, fe &Ry, int &W) {
+                            HsDigits &dg, uint32_t er[8], bool &dneg, ge_p3 &A, fe &Rx, fe &Ry, int &W,
+                            bool raw_e = false) {
   uint32_t k[8], s[8];
   const bool ok = verify_prep(pubw, sigw, msg, mlen, k, s, A);
-  const bool rok = hs_prep_r(k, s, sigw, dg.cr, dg.dr, er, dneg, Rx, Ry, W);
+  const bool rok = hs_prep_r(k, s, sigw, dg.cr, dg.dr, er, dneg, Rx, Ry, W, false, raw_e);
   return ok && rok;
 }
 
@@ -340,6 +350,43 @@ TMED_HD void words4_shl16(uint32_t x[4]) {
 #pragma unroll
   for (int i = 3; i > 0; i--) x[i] = (x[i] << 16) | (x[i - 1] >> 16);
   x[0] <<= 16;
+}
+
+// Radix-2^26 B windows (BL::kBits == 26): e = e_lo + 2^128 e_hi, each half as five signed digits
+// of 26 bits, d_m = bits [26m, 26m + 26) + bit (26m - 1) - 2^26 * bit (26m + 25), in [-2^25, 2^25]
+// (every digit from the bits alone, no carry chain; the halves are < 2^128, so bits 128, 129
+// are 0 and the top digit needs no carry out).  The tables hold j * B and j * 2^128 B for
+// j = 0..2^25 (kernels.hip b26_fill_kernel, 8.6 GB).  Digit m is added when 26m doublings remain:
+// at the end of windows 0, 13, 26 and after the second doubling of windows 6 and 19 — ten B
+// additions instead of the sixteen of radix 2^16 (-42 field multiplications per signature).
+TMED_HD int hs_b26_digit(const uint32_t x[4], int m) {
+  const int o = 26 * m, q = o >> 5, r = o & 31;
+  const uint64_t lo = x[q], hi = q + 1 < 4 ? x[q + 1] : 0u;
+  const uint32_t u = (uint32_t)(((hi << 32) | lo) >> r) & 0x3ffffffu;
+  const uint32_t below = m ? (x[(o - 1) >> 5] >> ((o - 1) & 31)) & 1u : 0u;
+  return (int)(u + below) - (int)((u >> 25) << 26);
+}
+TMED_HD void hs_b26_digits(int dl[5], int dh[5], const uint32_t er[8]) {
+  const uint32_t el[4] = {er[0], er[1], er[2], er[3]}, eh[4] = {er[4], er[5], er[6], er[7]};
+#pragma unroll
+  for (int m = 0; m < 5; m++) { dl[m] = hs_b26_digit(el, m); dh[m] = hs_b26_digit(eh, m); }
+}
+
+// The B step of position m (radix 2^26): r <- t (p1p1 -> p3) + digit lo + digit hi; leaves the sum
+// in t (p1p1); the next position's rows are fetched into the buffers right after each take.
+template <class BL, class BH>
+TMED_HD void hs_b26_add(ge_p1p1 &t, ge_p3 &r, int m, const int dl[5], const int dh[5], BL &bl, BH &bh) {
+  ge_niels nb;
+  ge_p1p1_to_p3(r, t);
+  bl.take(nb);
+  if (m > 0) bl.prefetch(dl[m - 1] < 0 ? -dl[m - 1] : dl[m - 1]);
+  niels_apply_sign(nb, dl[m] < 0);
+  ge_madd_niels(t, r, nb, false);
+  ge_p1p1_to_p3(r, t);
+  bh.take(nb);
+  if (m > 0) bh.prefetch(dh[m - 1] < 0 ? -dh[m - 1] : dh[m - 1]);
+  niels_apply_sign(nb, dh[m] < 0);
+  ge_madd_niels(t, r, nb, false);
 }
 
 // Q = [e]B + [c](-A) + [|d|](-sign(d) R) over W radix-16 windows (Straus, most significant
@@ -354,11 +401,18 @@ TMED_HD void words4_shl16(uint32_t x[4]) {
 // one B step ahead.  Needs 29 <= W <= 64.
 template <class DS, class TA, class TR, class BL, class BH>
 TMED_HD void hs_straus(ge_p2 &out, const DS &ds, const uint32_t er[8], int W, TA &ta, TR &tr, BL &bl, BH &bh) {
+  constexpr bool b26 = BL::kBits == 26;
+  static_assert(BL::kBits == 16 || BL::kBits == 26, "B windows of radix 2^16 or 2^26");
   uint32_t el[4] = {er[0], er[1], er[2], er[3]}, eh[4] = {er[4], er[5], er[6], er[7]};
-  {
+  int d26l[5] = {0, 0, 0, 0, 0}, d26h[5] = {0, 0, 0, 0, 0};
+  if (b26) {
+    hs_b26_digits(d26l, d26h, er);
+    bl.prefetch(d26l[4] < 0 ? -d26l[4] : d26l[4]);
+    bh.prefetch(d26h[4] < 0 ? -d26h[4] : d26h[4]);
+  } else {
     const int dl = (int)(el[3] >> 16) - 32768, dh = (int)(eh[3] >> 16) - 32768;
     bl.prefetch(dl < 0 ? -dl : dl);
-    bh.prefetch(dh < 0 ? -dh : dh);
+    if (!TMED_B16_ONEBUF) bh.prefetch(dh < 0 ? -dh : dh);
   }
   ge_p2 q;
   ge_p1p1 t;
@@ -384,6 +438,7 @@ TMED_HD void hs_straus(ge_p2 &out, const DS &ds, const uint32_t er[8], int W, TA
 #pragma unroll 1
       for (int k = 0; k < 3; k++) {
         ge_p2_dbl(t, q);
+        if (b26 && k == 1 && (n == 6 || n == 19)) hs_b26_add(t, r, n == 19 ? 3 : 1, d26l, d26h, bl, bh);  // 26m left
         ge_p1p1_to_p2(q, t);
       }
       if (TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc, dc < 0);  // the row load overlaps the last doubling
@@ -398,13 +453,17 @@ TMED_HD void hs_straus(ge_p2 &out, const DS &ds, const uint32_t er[8], int W, TA
     if (!TMED_SLAB_PF) tr.prefetch(dd < 0 ? -dd : dd, dd < 0);
     tr.take(ca);
     ge_add_cached_pre(t, r, ca, dd < 0);
-    if ((n & 3) == 0 && n <= 28) {
+    if (b26) {
+      if (n == 0 || n == 13 || n == 26) hs_b26_add(t, r, n / 13 * 2, d26l, d26h, bl, bh);
+    } else if ((n & 3) == 0 && n <= 28) {
       const int dl = (int)(el[3] >> 16) - 32768, dh = (int)(eh[3] >> 16) - 32768;
       words4_shl16(el);
       words4_shl16(eh);
       ge_p1p1_to_p3(r, t);
       bl.take(nb);
-      {
+      if (TMED_B16_ONEBUF) {  // one LDS row per wave: this window's high row goes where the low one was
+        bh.prefetch(dh < 0 ? -dh : dh);
+      } else {
         const int dn = (int)(el[3] >> 16) - 32768;
         bl.prefetch(dn < 0 ? -dn : dn);
       }
@@ -413,8 +472,9 @@ TMED_HD void hs_straus(ge_p2 &out, const DS &ds, const uint32_t er[8], int W, TA
       ge_p1p1_to_p3(r, t);
       bh.take(nb);
       {
-        const int dn = (int)(eh[3] >> 16) - 32768;
-        bh.prefetch(dn < 0 ? -dn : dn);
+        const int dn = (int)((TMED_B16_ONEBUF ? el[3] : eh[3]) >> 16) - 32768;
+        if (TMED_B16_ONEBUF) bl.prefetch(dn < 0 ? -dn : dn);
+        else bh.prefetch(dn < 0 ? -dn : dn);
       }
       niels_apply_sign(nb, dh < 0);
       ge_madd_niels(t, r, nb, false);

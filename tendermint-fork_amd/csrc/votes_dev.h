@@ -26,12 +26,12 @@ __device__ __forceinline__ uint32_t put_uvarint_dev(uint8_t *p, uint32_t pos, ui
   return pos;
 }
 
-// Vote i into its kVoteSlot-byte slot of out, its length into out_len[i].  tl: this lane's
-// kVoteTmplBytes of LDS — the template is staged there with sixteen independent 16-B loads, so
-// a template in pinned host memory (small batches, keyset.hip votes_enqueue) costs one bus round
-// trip instead of one per byte of the copy loops.
-__device__ __forceinline__ void assemble_vote(const VoteAsm &va, uint32_t i, uint8_t *__restrict__ out,
-                                              uint32_t *__restrict__ out_len, int4 *tl) {
+// Vote i into o (at most kVoteSlot bytes); returns its length.  tl: this lane's kVoteTmplBytes of
+// LDS — the template is staged there with sixteen independent 16-B loads, so a template in pinned
+// host memory (small batches, keyset.hip votes_enqueue) costs one bus round trip instead of one
+// per byte of the copy loops.
+__device__ __forceinline__ uint32_t assemble_vote_into(const VoteAsm &va, uint32_t i, uint8_t *__restrict__ o,
+                                                       int4 *tl) {
   {
     const int4 *src = reinterpret_cast<const int4 *>(va.tmpl + (size_t)va.tmpl_idx[i] * kVoteTmplBytes);
     int4 v[kVoteTmplBytes / 16];
@@ -46,7 +46,6 @@ __device__ __forceinline__ void assemble_vote(const VoteAsm &va, uint32_t i, uin
   const uint64_t s = (uint64_t)va.ts_sec[i], ns = (uint64_t)(int64_t)va.ts_nanos[i];
   const uint32_t ts_body = (s ? 1 + uvarint_len_dev(s) : 0) + (ns ? 1 + uvarint_len_dev(ns) : 0);
   const uint32_t body = pre_len + (with_bid ? bid_len : 0) + 1 + uvarint_len_dev(ts_body) + ts_body + cid_len;
-  uint8_t *o = out + (size_t)i * kVoteSlot;
   uint32_t p = put_uvarint_dev(o, 0, body);
   const uint8_t *src = t + 4;
   for (uint32_t j = 0; j < pre_len; j++) o[p++] = src[j];
@@ -59,7 +58,14 @@ __device__ __forceinline__ void assemble_vote(const VoteAsm &va, uint32_t i, uin
   if (s) { o[p++] = 0x08; p = put_uvarint_dev(o, p, s); }
   if (ns) { o[p++] = 0x10; p = put_uvarint_dev(o, p, ns); }
   for (uint32_t j = 0; j < cid_len; j++) o[p++] = src[j];
-  out_len[i] = p;
+  return p;
+}
+
+// Vote i into its kVoteSlot-byte slot of out, its length into out_len[i] (the latency kernels'
+// hash lanes, which assemble their own message in place).
+__device__ __forceinline__ void assemble_vote(const VoteAsm &va, uint32_t i, uint8_t *__restrict__ out,
+                                              uint32_t *__restrict__ out_len, int4 *tl) {
+  out_len[i] = assemble_vote_into(va, i, out + (size_t)i * kVoteSlot, tl);
 }
 
 }  // namespace tmed

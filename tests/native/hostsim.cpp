@@ -152,16 +152,44 @@ static const std::vector<ge_niels> &b16hi_tab() {
   return t;
 }
 
+// The radix-2^26 B tables of the default main kernel (j * B, j * 2^128 B for j = 0..2^25, 8.6 GB
+// on the device): entries computed on demand here (double-and-add, then the same affine niels
+// conversion as the device's b26_fill_kernel).
+struct HostB26Ref {
+  static constexpr int kBits = 26;
+  const ge_p3 *base;
+  int pf = 0;
+  void prefetch(int j) { pf = j; }
+  void take(ge_niels &n) const {
+    if (pf == 0) ge_niels_0(n);
+    else comb_entry(n, *base, (uint32_t)pf, 26);
+  }
+};
+static const ge_p3 *b26_bases() {
+  static ge_p3 b[2];
+  static bool init = false;
+  if (!init) {
+    ge_base_point(b[0]);
+    b[1] = b[0];
+    for (int i = 0; i < 16; i++) ge_mul256(b[1]);  // 2^128 B
+    init = true;
+  }
+  return b;
+}
+
 // wmin (optional): run signature i's Straus over max(W_i, wmin[i]) windows — the device runs every
 // lane of a wave over the wave's largest W, so a lane's top windows may lie above its own W.
-void hostsim_verify_batch_hs_w(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
-                               size_t n, uint8_t *out, int32_t *wins, const int32_t *wmin) {
+// b16: the radix-2^16 B windows (the device's fallback when the 2^26 tables are unavailable).
+static void verify_batch_hs_impl(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
+                                 size_t n, uint8_t *out, int32_t *wins, const int32_t *wmin, bool b16) {
   const ge_niels *lo = b16tab().data();
   const ge_niels *hi = b16hi_tab().data();
+  const ge_p3 *b26 = b26_bases();
 #pragma omp parallel for schedule(dynamic, 16)
   for (long i = 0; i < (long)n; i++) {
     HostTab ta, tr;
     HostBRef<16> bl{lo}, bh{hi};
+    HostB26Ref bl26{&b26[0]}, bh26{&b26[1]};
     uint32_t pw[8], sw[16], er[8];
     load_words8(pw, pub + 32 * i);
     load_words8(sw, sig + 64 * i);
@@ -171,17 +199,28 @@ void hostsim_verify_batch_hs_w(const uint8_t *pub, const uint8_t *sig, const uin
     fe Rx, Ry;
     int W;
     HsDigits dg;
-    const bool ok = verify_prep_hs(pw, sw, msgs + off[i], off[i + 1] - off[i], dg, er, dneg, A, Rx, Ry, W);
+    const bool ok = verify_prep_hs(pw, sw, msgs + off[i], off[i + 1] - off[i], dg, er, dneg, A, Rx, Ry, W, !b16);
     const int Wrun = (wmin && wmin[i] > W) ? (wmin[i] > 64 ? 64 : wmin[i]) : W;
-    const bool id = verify_main_hs(dg, dneg, er, Wrun, A, Rx, Ry, ta, tr, bl, bh);
+    const bool id = b16 ? verify_main_hs(dg, dneg, er, Wrun, A, Rx, Ry, ta, tr, bl, bh)
+                        : verify_main_hs(dg, dneg, er, Wrun, A, Rx, Ry, ta, tr, bl26, bh26);
     out[i] = ok && id ? 1 : 0;
     if (wins) wins[i] = W;
   }
 }
 
+void hostsim_verify_batch_hs_w(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
+                               size_t n, uint8_t *out, int32_t *wins, const int32_t *wmin) {
+  verify_batch_hs_impl(pub, sig, msgs, off, n, out, wins, wmin, false);
+}
+
 void hostsim_verify_batch_hs(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
                              size_t n, uint8_t *out, int32_t *wins) {
-  hostsim_verify_batch_hs_w(pub, sig, msgs, off, n, out, wins, nullptr);
+  verify_batch_hs_impl(pub, sig, msgs, off, n, out, wins, nullptr, false);
+}
+
+void hostsim_verify_batch_hs16(const uint8_t *pub, const uint8_t *sig, const uint8_t *msgs, const uint32_t *off,
+                               size_t n, uint8_t *out, int32_t *wins) {
+  verify_batch_hs_impl(pub, sig, msgs, off, n, out, wins, nullptr, true);
 }
 
 // The lattice step alone: c, |d| (32-byte LE each), dneg, window count.

@@ -106,8 +106,11 @@ def test_decode_matches_go_rule(hostsim):
 def _verify(l, pubs, sigs, msgs, offs, group=16):
     n = len(pubs)
     out = np.zeros(n, np.uint8)
-    if group == "hs":  # main variant 6 (default): half-size scalars, verify_hs.h
+    if group == "hs":  # main variant 6 (default): half-size scalars, verify_hs.h, radix-2^26 B windows
         l.hostsim_verify_batch_hs(_p(pubs), _p(sigs), _p(msgs), _p(offs), ctypes.c_size_t(n), _p(out), None)
+        return out
+    if group == "hs16":  # the same with the radix-2^16 B windows (no 8.6-GB tables)
+        l.hostsim_verify_batch_hs16(_p(pubs), _p(sigs), _p(msgs), _p(offs), ctypes.c_size_t(n), _p(out), None)
         return out
     if group == "b16":  # main-kernel variant 5: radix-2^16 B windows from the 32769-entry table
         l.hostsim_verify_batch_b16(_p(pubs), _p(sigs), _p(msgs), _p(offs), ctypes.c_size_t(n), _p(out))
@@ -117,7 +120,7 @@ def _verify(l, pubs, sigs, msgs, offs, group=16):
     return out
 
 
-@pytest.mark.parametrize("group", [0, 1, 5, 16, "b16", "hs"])
+@pytest.mark.parametrize("group", [0, 1, 5, 16, "b16", "hs", "hs16"])
 def test_golden_vectors_hostsim(hostsim, golden, group):
     """Every golden tuple, with per-signature encoding (group 0) and through the batched
     finish (Montgomery inversion over groups of 1, 5 and 16 signatures, partial last group);

@@ -460,6 +460,23 @@ def main():
     parts.append(emit_fused_multi(
         "TMED_HD void fe_sq2_sq1_fused(int64_t H0[10], int64_t H1[10], %s, %s)" % (psig % (("a",) * 5), psig % (("b",) * 5)),
         [(s2, used_inputs(s2, sortk), "a_"), (s1, used_inputs(s1, sortk), "b_")], "// 2 a^2 (a carried) and b^2"))
+    parts.append('''
+// ---- squares of CARRIED inputs (one carried value, not a sum: every squaring chain of the
+// exponentiations and the X^2, Y^2 of a doubling): with inputs half the size of a 2-sum the 19
+// and the factors 2 fit on fewer premultiplied copies — x2 of limbs 0, 1, 2, 3, 5, 7, x19 of 6, 8
+// and x38 of 5..9 (13 copies, 5 of them v_mul_lo_u32, against 19 for up-to-3-sum inputs).''')
+    s1c = sq_products_fused(1, 1)
+    check_bounds(s1c, 1, 1)
+    csig = "const int32_t %s_x[10], const int32_t %s_x2[10], const int32_t %s_x19[10], const int32_t %s_x38[10]"
+    used_c = used_inputs(s1c, sortk)
+    assert all(o[0] in ("x", "x2", "x19", "x38") for o in used_c), used_c
+    parts.append(emit_fused("TMED_HD void fe_sq1c_fused(int64_t H[10], const int32_t x[10], const int32_t x2[10], "
+                            "const int32_t x19[10], const int32_t x38[10])", s1c, used_c,
+                            "// f^2, f carried: 55 mads, 9 carries, 5 adds; premuls used: %s"
+                            % " ".join("%s[%d]" % o for o in used_c if o[0] != "x")))
+    parts.append(emit_fused_multi(
+        "TMED_HD void fe_sq1c_fused_x2(int64_t H0[10], int64_t H1[10], %s, %s)" % (csig % (("a",) * 4), csig % (("b",) * 4)),
+        [(s1c, used_c, "a_"), (s1c, used_c, "b_")], "// two independent squares of carried values"))
     with open(OUT, "w") as fh:
         fh.write("\n".join(parts))
     print("wrote", OUT)
