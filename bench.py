@@ -67,14 +67,15 @@ MAIN_KERNEL = "verify_main_kernel"
 if MAIN_VARIANT == 6:
     # half-size scalars (verify_hs.h, the default): W = 33 radix-16 windows (the usual wave
     # maximum; some waves run 34) of 4 dbl (16 S + 13 M) and two cached adds with their
-    # conversions (15 M), 8 B steps of two niels adds (+14 M each), two tables (-A, -sign(d) R)
+    # conversions (15 M), 5 B steps of two niels adds (+14 M each; radix-2^26 tables, 8 steps at
+    # radix 2^16 — mads_main_hs), two tables (-A, -sign(d) R)
     # and T = XY of A and R; no finish.  Outside the main kernel: decode of A and strict decode
     # of R, the mod-L work (Barrett + |d| S).  The lattice step (fp64 quotient estimates,
     # ~130 Euclid steps) is not counted in mads.
     # tables by build_table_affine: 2d*xy (1 M) + 7 x (mixed add 3 M + p1p1->p3 4 M + 2dT 1 M)
     MADS_TABLE_HS = 57 * MUL
     HS_W = 33
-    MADS_MAIN = (HS_W - 1) * (16 * SQ + 13 * MUL) + HS_W * 15 * MUL + 8 * 14 * MUL + 2 * MADS_TABLE_HS + 2 * MUL
+    MADS_MAIN = (HS_W - 1) * (16 * SQ + 13 * MUL) + HS_W * 15 * MUL + 5 * 14 * MUL + 2 * MADS_TABLE_HS + 2 * MUL
     MADS_PER_VERIFY_GENERIC = MADS_MAIN + 2 * MADS_DECODE + MADS_SCALAR + 64 + 188
     MAIN_KERNEL = "verify_main_hs_kernel"
 # key-cached main kernel (C2 variant, kernels.hip keyset_straus_pf): 48 comb rows (32 of the key's
@@ -120,9 +121,11 @@ def spawn_ranks(n: int) -> int:
     return subprocess.call(cmd)
 
 
-def mads_main_hs(w: float) -> float:
-    """v_mad_i64_i32 of verify_main_hs_kernel per signature at a wave loop length of w windows."""
-    return (w - 1) * (16 * SQ + 13 * MUL) + w * 15 * MUL + 8 * 14 * MUL + 2 * 57 * MUL + 2 * MUL
+def mads_main_hs(w: float, b_bits: int = 26) -> float:
+    """v_mad_i64_i32 of verify_main_hs_kernel per signature at a wave loop length of w windows:
+    B steps of two niels adds (+14 M each) — five with the radix-2^26 tables, eight with radix 2^16."""
+    b_steps = 5 if b_bits == 26 else 8
+    return (w - 1) * (16 * SQ + 13 * MUL) + w * 15 * MUL + b_steps * 14 * MUL + 2 * 57 * MUL + 2 * MUL
 
 
 def window_summary(eng):
@@ -244,7 +247,11 @@ def main():
             torch.cuda.synchronize(dev)
             (prep_ms, main_ms, fin_ms), (prep_launches, launches, fin_launches) = eng.kernel_times()
             eng.set_kernel_timing(False)
-            mads_main = MADS_MAIN if wstats is None else mads_main_hs(wstats["wave_W_mean"])
+            try:
+                b_bits = eng.b_window_bits()
+            except AttributeError:  # an older library build (A/B runs through TMED_LIB)
+                b_bits = 16
+            mads_main = MADS_MAIN if wstats is None else mads_main_hs(wstats["wave_W_mean"], b_bits)
             achieved = n * mads_main / (main_ms * 1e-3) / 1e12
             traffic, traffic_src = pmc_traffic(n / max(1, launches))
             roof = {"bound": "valu", "kernel": MAIN_KERNEL, "achieved": round(achieved, 3),
@@ -254,8 +261,8 @@ def main():
                     "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                     "traffic_source": traffic_src,
                     "mads_per_verify_main": round(mads_main), "mads_per_verify_total": MADS_PER_VERIFY_GENERIC,
-                    "mads_basis": ("wave-mean window count %.3f (tmed_window_stats)" % wstats["wave_W_mean"])
-                                  if wstats else "formula",
+                    "mads_basis": ("wave-mean window count %.3f (tmed_window_stats), radix-2^%d B windows"
+                                   % (wstats["wave_W_mean"], b_bits)) if wstats else "formula",
                     "kernel_avg_ms": round(main_ms / max(1, launches), 4), "launches_per_step": launches,
                     "prep_kernels_ms": round(prep_ms / max(1, launches), 4), "prep_launches": prep_launches,
                     "finish_kernel_ms": round(fin_ms, 4), "finish_launches": fin_launches,

@@ -97,6 +97,14 @@ int tmed_sign_batch_device(tmed_ctx *ctx, const uint8_t *d_seeds, const uint8_t 
  */
 int tmed_window_stats(tmed_ctx *ctx, uint32_t lane_hist[65], uint32_t wave_hist[65]);
 
+/*
+ * Radix (in bits) of the fixed-base B windows of the default path on this context: 26 (two
+ * tables of 2^25 + 1 affine multiples of B and 2^128 B, 8.6 GB per device, ten B additions per
+ * signature) or 16 (windows of the context's radix-2^16 comb, sixteen additions: TMED_B26=0 or
+ * when the large tables could not be allocated).  Diagnostic; decisions are identical.
+ */
+int tmed_b_window_bits(const tmed_ctx *ctx);
+
 /* Device time (ms) of the last verify/sign launch on this context (HIP events).  A commit batch
  * small enough for the zero-copy latency mode (a single commit), or a tmed_verify_batch of at most
  * 1024 signatures, reports 0 unless kernel timing is on (tmed_set_kernel_timing): its events would

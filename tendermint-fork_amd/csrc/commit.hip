@@ -713,28 +713,44 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
   memcpy(st.tmpl, tmpl, n * tmed::kVoteTmplBytes);
   std::atomic<bool> key_ok{true};
   const uint32_t nkeys = keyed ? (uint32_t)st.ks->n : 0u;
+  // Runs of candidates of one request with consecutive signature indexes (a Light / blocksync
+  // commit's candidates are one run) are staged one memcpy per array; the key index, the
+  // template index and short signatures stay per vote.
   auto fill = [&](size_t lo, size_t hi, unsigned) {
     bool ok = true;
-    for (size_t j = lo; j < hi; j++) {
+    for (size_t j = lo; j < hi;) {
       const Cand &cd = cands[ix ? ix[j] : j];
       const tmed_commit_request &r = reqs[cd.req];
       const tmed_commit &c = *r.commit;
       const size_t i = (size_t)cd.sig_idx;
-      if (keyed) {
-        const uint32_t v = r.vals->keyset_index ? r.vals->keyset_index[cd.val_idx] : (uint32_t)cd.val_idx;
-        ok = ok && v < nkeys;
-        memcpy(st.key + j * 4, &v, 4);
-      } else {
-        memcpy(st.key + j * 32, r.vals->pubkeys + 32 * (size_t)cd.val_idx, 32);
+      size_t len = 1;
+      while (j + len < hi) {
+        const Cand &nx = cands[ix ? ix[j + len] : j + len];
+        if (nx.req != cd.req || (size_t)nx.sig_idx != i + len || nx.val_idx != cd.val_idx + (int32_t)len) break;
+        len++;
       }
-      const uint32_t sl = c.sig_lens ? c.sig_lens[i] : 64;
-      uint8_t *sd = st.sig + j * 64;
-      if (sl >= 64) memcpy(sd, c.sigs + 64 * i, 64);
-      else { memset(sd, 0, 64); memcpy(sd, c.sigs + 64 * i, sl); }
-      st.tidx[j] = (uint32_t)cd.req;
-      st.flag[j] = c.flags[i];
-      st.sec[j] = c.ts_seconds[i];
-      st.nan[j] = c.ts_nanos[i];
+      if (keyed) {
+        uint32_t *kd = reinterpret_cast<uint32_t *>(st.key) + j;
+        const uint32_t *kix = r.vals->keyset_index;
+        for (size_t u = 0; u < len; u++) {
+          const uint32_t v = kix ? kix[cd.val_idx + u] : (uint32_t)(cd.val_idx + u);
+          ok = ok && v < nkeys;
+          kd[u] = v;
+        }
+      } else {
+        memcpy(st.key + j * 32, r.vals->pubkeys + 32 * (size_t)cd.val_idx, 32 * len);
+      }
+      memcpy(st.sig + j * 64, c.sigs + 64 * i, 64 * len);
+      if (c.sig_lens)
+        for (size_t u = 0; u < len; u++) {
+          const uint32_t sl = c.sig_lens[i + u];
+          if (sl < 64) memset(st.sig + (j + u) * 64 + sl, 0, 64 - sl);
+        }
+      for (size_t u = 0; u < len; u++) st.tidx[j + u] = (uint32_t)cd.req;
+      memcpy(st.flag + j, c.flags + i, len);
+      memcpy(st.sec + j, c.ts_seconds + i, 8 * len);
+      memcpy(st.nan + j, c.ts_nanos + i, 4 * len);
+      j += len;
     }
     if (!ok) key_ok = false;
   };

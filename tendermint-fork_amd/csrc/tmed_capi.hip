@@ -250,6 +250,8 @@ int tmed_verify_batch_device(tmed_ctx *c, const uint8_t *d_pub, const uint8_t *d
   return map_err(e);
 }
 
+int tmed_b_window_bits(const tmed_ctx *c) { return c && c->d_b26 ? 26 : 16; }
+
 int tmed_window_stats(tmed_ctx *c, uint32_t lane_hist[65], uint32_t wave_hist[65]) {
   if (!c || !lane_hist || !wave_hist) return TMED_EINVAL;
   std::lock_guard<std::mutex> lk(c->mu);

@@ -218,5 +218,9 @@ class Engine:
             raise TmedError(rc, "tmed_window_stats")
         return lh, wh
 
+    def b_window_bits(self) -> int:
+        """Radix (bits) of the default path's fixed-base B windows: 26 or 16 (tmed_b_window_bits)."""
+        return int(lib().tmed_b_window_bits(self._h))
+
     def last_kernel_ms(self) -> float:
         return float(lib().tmed_last_kernel_ms(self._h))
