@@ -80,6 +80,80 @@ TMED_HD void sha512_init(uint64_t st[8]) {
   st[6] = 0x1f83d9abfb41bd6bull; st[7] = 0x5be0cd19137e2179ull;
 }
 
+// The round functions on the device as 32-bit halves: a 64-bit rotate is two v_alignbit_b32
+// (LLVM's lowering of rotr64 is a 64-bit shift, a 32-bit shift and an or: three instructions),
+// three-way xors and Maj are one v_bitop3_b32 per half (gfx950; LUT 0x96 = a ^ b ^ c, 0xE8 =
+// majority — both symmetric, so the operand order is immaterial).  Host builds use the plain
+// 64-bit expressions below.
+#ifndef TMED_SHA_BITOP3
+#define TMED_SHA_BITOP3 1  // A/B knob: 0 = the plain 64-bit expressions on the device too
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && TMED_SHA_BITOP3
+__device__ __forceinline__ uint32_t sha_xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ uint32_t sha_maj(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+// (lo, hi) -> uint64 as a register pair (a shift / or lets LLVM split the value into two
+// zero-extended 64-bit adds downstream)
+typedef uint32_t sha_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint64_t sha_pack(uint32_t lo, uint32_t hi) {
+  const sha_u32x2 v = {lo, hi};
+  return __builtin_bit_cast(uint64_t, v);
+}
+// rotr64(x, n) as (lo, hi) halves, n a compile-time constant in 1..63, n != 32
+template <int N>
+__device__ __forceinline__ void sha_rotr(uint32_t &lo, uint32_t &hi, uint32_t xl, uint32_t xh) {
+  if (N < 32) {
+    lo = __builtin_amdgcn_alignbit(xh, xl, N);
+    hi = __builtin_amdgcn_alignbit(xl, xh, N);
+  } else {
+    lo = __builtin_amdgcn_alignbit(xl, xh, N - 32);
+    hi = __builtin_amdgcn_alignbit(xh, xl, N - 32);
+  }
+}
+// rotr(x, A) ^ rotr(x, B) ^ rotr(x, C)      (Sigma0 / Sigma1)
+template <int A, int B, int C>
+__device__ __forceinline__ uint64_t sha_Sig(uint64_t x) {
+  const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+  uint32_t l0, h0, l1, h1, l2, h2;
+  sha_rotr<A>(l0, h0, xl, xh);
+  sha_rotr<B>(l1, h1, xl, xh);
+  sha_rotr<C>(l2, h2, xl, xh);
+  return sha_pack(sha_xor3(l0, l1, l2), sha_xor3(h0, h1, h2));
+}
+// rotr(x, A) ^ rotr(x, B) ^ (x >> C)       (sigma0 / sigma1 of the message schedule, C < 32)
+template <int A, int B, int C>
+__device__ __forceinline__ uint64_t sha_sig(uint64_t x) {
+  const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+  uint32_t l0, h0, l1, h1;
+  sha_rotr<A>(l0, h0, xl, xh);
+  sha_rotr<B>(l1, h1, xl, xh);
+  const uint32_t l2 = __builtin_amdgcn_alignbit(xh, xl, C), h2 = xh >> C;
+  return sha_pack(sha_xor3(l0, l1, l2), sha_xor3(h0, h1, h2));
+}
+__device__ __forceinline__ uint64_t sha_Maj(uint64_t a, uint64_t b, uint64_t c) {
+  return sha_pack(sha_maj((uint32_t)a, (uint32_t)b, (uint32_t)c),
+                  sha_maj((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)));
+}
+#define TMED_SHA_S0(a) sha_Sig<28, 34, 39>(a)
+#define TMED_SHA_S1(e) sha_Sig<14, 18, 41>(e)
+#define TMED_SHA_s0(w) sha_sig<1, 8, 7>(w)
+#define TMED_SHA_s1(w) sha_sig<19, 61, 6>(w)
+#define TMED_SHA_MAJ(a, b, c) sha_Maj(a, b, c)
+#else
+#define TMED_SHA_S0(a) (TMED_ROTR64(a, 28) ^ TMED_ROTR64(a, 34) ^ TMED_ROTR64(a, 39))
+#define TMED_SHA_S1(e) (TMED_ROTR64(e, 14) ^ TMED_ROTR64(e, 18) ^ TMED_ROTR64(e, 41))
+#define TMED_SHA_s0(w) (TMED_ROTR64(w, 1) ^ TMED_ROTR64(w, 8) ^ ((w) >> 7))
+#define TMED_SHA_s1(w) (TMED_ROTR64(w, 19) ^ TMED_ROTR64(w, 61) ^ ((w) >> 6))
+#define TMED_SHA_MAJ(a, b, c) (((a) & (b)) ^ ((c) & ((a) ^ (b))))
+#endif
+
 // 80 rounds as 5 x 16 (the message-schedule window w[i & 15] stays register-indexed);
 // the round constants come from a uniform table (scalar loads on the device), so the
 // rolled outer loop keeps the live set at state + window (~50 VGPRs).
@@ -91,15 +165,15 @@ TMED_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
     for (int j = 0; j < 16; j++) {
       if (r > 0) {
         const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
-        const uint64_t s0 = TMED_ROTR64(w15, 1) ^ TMED_ROTR64(w15, 8) ^ (w15 >> 7);
-        const uint64_t s1 = TMED_ROTR64(w2, 19) ^ TMED_ROTR64(w2, 61) ^ (w2 >> 6);
+        const uint64_t s0 = TMED_SHA_s0(w15);
+        const uint64_t s1 = TMED_SHA_s1(w2);
         w[j] += s0 + w[(j + 9) & 15] + s1;
       }
-      const uint64_t S1 = TMED_ROTR64(e, 14) ^ TMED_ROTR64(e, 18) ^ TMED_ROTR64(e, 41);
+      const uint64_t S1 = TMED_SHA_S1(e);
       const uint64_t ch = (e & f) ^ (~e & g);
       const uint64_t t1 = h + S1 + ch + sha512_k(r + j) + w[j];
-      const uint64_t S0 = TMED_ROTR64(a, 28) ^ TMED_ROTR64(a, 34) ^ TMED_ROTR64(a, 39);
-      const uint64_t mj = (a & b) ^ (c & (a ^ b));
+      const uint64_t S0 = TMED_SHA_S0(a);
+      const uint64_t mj = TMED_SHA_MAJ(a, b, c);
       h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
     }
   }

@@ -17,12 +17,12 @@ for v in "$@"; do
   tag=$(echo "$v" | tr ':=,' '___')
   env ${envs//,/ } TMED_LIB=$PWD/$lib timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU_INT64 SQ_WAVES GRBM_GUI_ACTIVE \
     --kernel-trace --output-format csv -d $PWD/$OUT/$tag -o run -- python3 $PWD/bench.py --steps 3 --warmup 1 \
-    --no-cpu-baseline --no-peak --no-c1 --no-keyset --no-c4 --no-c5 --no-zip215 > $OUT/$tag.log 2>&1 || exit $?
+    --no-cpu-baseline --no-peak --no-c1 ${PMC_BENCH_ARGS:---no-keyset} --no-c4 --no-c5 --no-zip215 > $OUT/$tag.log 2>&1 || exit $?
   python3 tools/pmc_summary.py $OUT/$tag.json $OUT/$tag > /dev/null 2>&1
   python3 - "$OUT/$tag.json" "$v" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))
-for k in ("verify_main_hs_kernel", "verify_prep_kernel", "verify_prep_r_kernel"):
+for k in ("verify_main_hs_kernel", "verify_prep_kernel", "verify_prep_r_kernel", "verify_keyset_prep_kernel", "verify_keyset_main_kernel"):
     r = d.get(k)
     if r:
         print(sys.argv[2], k, "gpu_cycles/8 %.0f" % (r["GRBM_GUI_ACTIVE"] / 8), "valu/wave %.0f" % r["valu_insts_per_wave"],
