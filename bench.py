@@ -78,10 +78,18 @@ if MAIN_VARIANT == 6:
     MADS_MAIN = (HS_W - 1) * (16 * SQ + 13 * MUL) + HS_W * 15 * MUL + 5 * 14 * MUL + 2 * MADS_TABLE_HS + 2 * MUL
     MADS_PER_VERIFY_GENERIC = MADS_MAIN + 2 * MADS_DECODE + MADS_SCALAR + 64 + 188
     MAIN_KERNEL = "verify_main_hs_kernel"
-# key-cached main kernel (C2 variant, kernels.hip keyset_straus_pf): 48 comb rows (32 of the key's
-# radix-256 comb, 16 of the radix-2^16 comb of B); the first is converted niels -> extended (1 M),
-# the next 46 are mixed additions (3 M) + p1p1 -> p3 (4 M), the last stops at projective (3 M + 3 M)
-MADS_KEYSET_MAIN = (1 + 46 * 7 + 6) * MUL
+# key-cached main kernel (C2 variant, kernels.hip keyset_straus_b24 / keyset_straus_pf): 32 rows of the
+# key's radix-256 comb and 11 of the shared radix-2^24 comb of B (16 of the radix-2^16 comb without
+# it); the first row is converted niels -> extended (1 M), the middle ones are mixed additions (3 M)
+# + p1p1 -> p3 (4 M), the last stops at projective (3 M + 3 M)
+
+
+def mads_keyset_main(b_bits: int = 24) -> int:
+    rows = 32 + (11 if b_bits == 24 else 16)
+    return (1 + (rows - 2) * 7 + 6) * MUL
+
+
+MADS_KEYSET_MAIN = mads_keyset_main(16)
 
 
 def parse():
@@ -373,7 +381,12 @@ def c2_keyset(eng, dev, torch_stream, n, steps, warmup, peak):
     (prep_ms, main_ms, fin_ms), (pl, ml, fl) = eng.kernel_times()
     eng.set_kernel_timing(False)
     eng.keyset_free(ks)
-    achieved = n * MADS_KEYSET_MAIN / (main_ms * 1e-3) / 1e12 if main_ms > 0 else None
+    try:
+        kb = eng.keyset_b_window_bits()
+    except AttributeError:  # an older library build (A/B runs through TMED_LIB)
+        kb = 16
+    mads_ks = mads_keyset_main(kb)
+    achieved = n * mads_ks / (main_ms * 1e-3) / 1e12 if main_ms > 0 else None
     traffic, traffic_src = pmc_traffic(n / max(1, ml), "verify_keyset_main_kernel")
     return {"metric": "ed25519 verifies/sec at 1/8 MI355X, key cache on (C2 variant: 10k reused keys)",
             "value": round(n * steps / dt, 1), "unit": "verifies/s", "steps": steps,
@@ -385,7 +398,7 @@ def c2_keyset(eng, dev, torch_stream, n, steps, warmup, peak):
                          "frac": round(achieved / peak, 4) if (achieved and peak) else None,
                          "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                          "traffic_source": traffic_src,
-                         "mads_per_verify_main": MADS_KEYSET_MAIN,
+                         "mads_per_verify_main": mads_ks, "b_window_bits": kb,
                          "visiting_order": "key-grouped (launch_key_order, charged to prep_kernel_ms)",
                          "kernel_avg_ms": round(main_ms / max(1, ml), 4), "launches_per_step": ml,
                          "prep_kernel_ms": round(prep_ms, 4), "finish_kernel_ms": round(fin_ms, 4)},

@@ -104,6 +104,13 @@ int tmed_window_stats(tmed_ctx *ctx, uint32_t lane_hist[65], uint32_t wave_hist[
  * when the large tables could not be allocated).  Diagnostic; decisions are identical.
  */
 int tmed_b_window_bits(const tmed_ctx *ctx);
+/*
+ * The same for the key-cached throughput path: 24 (a shared radix-2^24 comb of B, 11 windows of
+ * 2^23 + 1 multiples, 11.8 GB per device, acquired at the context's first tmed_keyset_load:
+ * eleven B additions per signature) or 16 (the context's radix-2^16 comb, sixteen: before any
+ * key-set load, with TMED_B24=0, or when the allocation failed).  Diagnostic; same decisions.
+ */
+int tmed_keyset_b_window_bits(const tmed_ctx *ctx);
 
 /* Device time (ms) of the last verify/sign launch on this context (HIP events).  A commit batch
  * small enough for the zero-copy latency mode (a single commit), or a tmed_verify_batch of at most

@@ -105,6 +105,8 @@ constexpr size_t kVoteZeroCopyMax = 256u << 10;
 // Raw host batches of at most this many signatures record no kernel-time events by default.
 constexpr size_t kLatencyUntimedMax = 1024;
 int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st, int slot = 0);
+// The shared radix-2^24 B comb (tmed_capi.hip), acquired on the first call; null: radix 2^16.
+const int4 *ctx_bcomb24(tmed_ctx *c);
 int votes_enqueue(tmed_ctx *c, VoteStage &st);
 int votes_collect(tmed_ctx *c, const VoteStage &st, uint8_t *out);
 int votes_launch(tmed_ctx *c, VoteStage &st, uint8_t *out);
@@ -135,6 +137,8 @@ struct tmed_ctx {
   int4 *d_b16 = nullptr;    // j*B, j = 0..32768 (main-kernel variant 5), built at init
   int4 *d_bcomb16 = nullptr;  // radix-2^16 comb of +B (key-cached throughput kernel), 67 MB
   int4 *d_b26 = nullptr;      // radix-2^26 B tables of the half-size main kernel (8.6 GB, shared per device)
+  int4 *d_b24 = nullptr;      // radix-2^24 B comb of the key-cached main kernel (11.8 GB, shared per device)
+  bool b24_tried = false;     // d_b24 acquired (or given up) at the first key-set load
   int4 *d_slab = nullptr;
   int4 *d_prep = nullptr;
   int4 *d_fin = nullptr;      // batched-finish hand-off (kFinBytes)

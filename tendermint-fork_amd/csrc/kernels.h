@@ -53,6 +53,13 @@ struct BTabs {
 constexpr uint32_t kB26Entries = (1u << 25) + 1;
 constexpr size_t kB26Bytes = 2 * (size_t)kB26Entries * 128;
 hipError_t launch_build_b26(const int4 *comb16, int4 *tab, hipStream_t stream);
+// Signed radix-2^24 comb of +B for the key-cached throughput kernel: window w holds j * 2^(24w) B
+// for j = 0..2^23 (11 windows, 11.8 GB, built once per device at the first key-set load:
+// keyset.hip b24_acquire): eleven B additions per signature instead of sixteen.
+constexpr int kB24Windows = 11;
+constexpr uint32_t kB24Entries = (1u << 23) + 1;
+constexpr size_t kB24Bytes = (size_t)kB24Windows * kB24Entries * 128;
+hipError_t launch_build_b24(const int4 *comb16, int4 *tab, hipStream_t stream);
 constexpr uint32_t kB16Entries = 32769;
 constexpr size_t kB16Bytes = (size_t)kB16Entries * 128;
 hipError_t launch_build_b16(int4 *tab, hipStream_t stream);
@@ -109,7 +116,7 @@ hipError_t launch_verify_keyset(const uint32_t *val_idx, uint32_t nkeys, const u
                                 const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
                                 int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots = false,
                                 KernelTimer *timer = nullptr, uint32_t *perm = nullptr,
-                                uint32_t *order_scratch = nullptr);
+                                uint32_t *order_scratch = nullptr, const int4 *bcomb24 = nullptr);
 // Key-grouped visiting order of a key-cached batch (counting sort of val_idx by groups of
 // consecutive keys, indices >= nkeys last): perm[0..n) = signature indices grouped by key.
 // scratch: key_order_scratch_words(n, nkeys) u32.  The comb rows of the lanes in flight then

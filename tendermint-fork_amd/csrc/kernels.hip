@@ -867,6 +867,49 @@ hipError_t launch_build_b26(const int4 *comb16, int4 *tab, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// Entry (w, j) of the radix-2^24 comb: j * 2^(24w) B for j = 0..2^23.  24w = 16v + r (r = 0 or 8):
+// J = j 2^r < 2^31 as two signed 16-bit digits at windows v, v + 1 of the radix-2^16 comb (two mixed
+// additions), then affine niels with one inversion.  Window 10 (bits 240..263) only ever needs
+// j <= 2^16 (S < 2^256); its entries whose second digit would fall past the comb's last window are
+// left as the identity.
+__global__ __launch_bounds__(256) void b24_fill_kernel(const int4 *__restrict__ comb16, int4 *__restrict__ tab) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (uint32_t)kB24Windows * kB24Entries) return;
+  const uint32_t w = g / kB24Entries, j = g % kB24Entries;
+  const uint32_t v = (24u * w) >> 4, r = (24u * w) & 15u;
+  const uint32_t J = j << r;
+  int d0 = (int)(J & 0xffffu);
+  uint32_t d1 = J >> 16;
+  if (d0 >= 32768) { d0 -= 65536; d1++; }
+  ge_niels e;
+  if (j == 0 || (v + 1 >= 16 && d1 != 0)) {
+    ge_niels_0(e);
+  } else {
+    const GlobalComb16 bc{comb16};
+    ge_p3 P;
+    ge_p1p1 q;
+    ge_niels n;
+    ge_p3_0(P);
+    bc.load((int)v, d0 < 0 ? -d0 : d0, n);
+    niels_apply_sign(n, d0 < 0);
+    ge_madd_niels(q, P, n, false);
+    ge_p1p1_to_p3(P, q);
+    if (d1) {
+      bc.load((int)v + 1, (int)d1, n);
+      ge_madd_niels(q, P, n, false);
+      ge_p1p1_to_p3(P, q);
+    }
+    ge_p3_to_niels(e, P);
+  }
+  niels_store(tab + (size_t)g * kCombEntryInt4, e);
+}
+
+hipError_t launch_build_b24(const int4 *comb16, int4 *tab, hipStream_t stream) {
+  const uint32_t n = (uint32_t)kB24Windows * kB24Entries;
+  hipLaunchKernelGGL(b24_fill_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, comb16, tab);
+  return hipGetLastError();
+}
+
 __device__ void comb_sign_one(uint32_t sg[16], uint32_t pb[8], const uint32_t seed[8], const uint8_t *m,
                               uint32_t mlen, const int4 *bcomb) {
   const GlobalComb bc{bcomb};
@@ -1042,7 +1085,70 @@ __device__ __forceinline__ void keyset_straus_pf(ge_p2 &out, const uint32_t k[8]
   }
 }
 
-template <int WAVES>
+// out (X : Y : Z) = [k](-A) + [s]B with the radix-2^24 comb of B: the key's 32 radix-256 rows, then
+// eleven B rows, d_m = bits [24m, 24m + 24) of s + bit (24m - 1) - 2^24 bit (24m + 23), read off a
+// copy of s shifted right by 24 bits per row (no carry chain); 43 mixed additions, the row of
+// addition t + 1 loaded while addition t runs.
+__device__ __forceinline__ const int4 *ks_b24row(const int4 *bc, int w, int d, bool &neg) {
+  neg = d < 0;
+  return bc + ((size_t)w * kB24Entries + (uint32_t)(neg ? -d : d)) * kCombEntryInt4;
+}
+__device__ __forceinline__ void keyset_straus_b24(ge_p2 &out, const uint32_t k[8], const uint32_t s[8],
+                                                  const int4 *ak, const int4 *bc) {
+  uint32_t kr[8], sw[8];
+  sc_recode256(kr, k);
+#pragma unroll
+  for (int i = 0; i < 8; i++) sw[i] = s[i];
+  CombRowPf pf;
+  bool ng;
+  pf.fetch(ks_arow(ak, 0, kr[0] & 0xffu, ng), ng);
+  ge_p3 acc;
+  ge_p1p1 t;
+  ge_niels e;
+  // the key's 32 rows, four per word of the recoding
+#pragma unroll 1
+  for (int q = 0; q < 8; q++) {
+    const uint32_t kc = kr[0];
+#pragma unroll
+    for (int m = 0; m < 7; m++) kr[m] = kr[m + 1];
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      pf.take(e);
+      if (b < 3) {
+        pf.fetch(ks_arow(ak, 4 * q + b + 1, (kc >> (8 * (b + 1))) & 0xffu, ng), ng);
+      } else if (q < 7) {
+        pf.fetch(ks_arow(ak, 4 * q + 4, kr[0] & 0xffu, ng), ng);
+      } else {  // the first B row: digit 0
+        const uint32_t u = sw[0] & 0xffffffu;
+        pf.fetch(ks_b24row(bc, 0, (int)u - (int)((u >> 23) << 24), ng), ng);
+      }
+      if (q == 0 && b == 0) {
+        ge_niels_to_p3(acc, e);
+      } else {
+        ge_madd_niels(t, acc, e, false);
+        ge_p1p1_to_p3(acc, t);
+      }
+    }
+  }
+  // the eleven B rows; row m + 1's digit is read off s shifted right by 24 (m + 1) bits
+#pragma unroll 1
+  for (int m = 0; m < kB24Windows; m++) {
+    pf.take(e);
+    if (m + 1 < kB24Windows) {
+      const uint32_t below = (sw[0] >> 23) & 1u;  // bit 24(m + 1) - 1
+#pragma unroll
+      for (int i = 0; i < 7; i++) sw[i] = __builtin_amdgcn_alignbit(sw[i + 1], sw[i], 24);
+      sw[7] >>= 24;
+      const uint32_t u = sw[0] & 0xffffffu;
+      pf.fetch(ks_b24row(bc, m + 1, (int)(u + below) - (int)((u >> 23) << 24), ng), ng);
+    }
+    ge_madd_niels(t, acc, e, false);
+    if (m + 1 == kB24Windows) ge_p1p1_to_p2(out, t);
+    else ge_p1p1_to_p3(acc, t);
+  }
+}
+
+template <int WAVES, bool B24 = false>
 __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_keyset_main_kernel(
     const uint32_t *__restrict__ val_idx, uint32_t nkeys, const int4 *__restrict__ acomb,
     const int4 *__restrict__ bcomb, uint32_t base, uint32_t count, const int4 *__restrict__ prep, uint32_t stride,
@@ -1068,7 +1174,8 @@ __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_keyset_main_ke
   for (int j = 0; j < 8; j++) { k[j] = (uint32_t)w[j]; s[j] = (uint32_t)w[8 + j]; }
 #if TMED_KS_PF
   ge_p2 R;
-  keyset_straus_pf(R, k, s, acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4, bcomb);
+  if (B24) keyset_straus_b24(R, k, s, acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4, bcomb);
+  else keyset_straus_pf(R, k, s, acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4, bcomb);
 #else
   const GlobalComb ac{acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4};
   const GlobalComb16 bc{bcomb};
@@ -1344,7 +1451,7 @@ hipError_t launch_verify_keyset(const uint32_t *val_idx, uint32_t nkeys, const u
                                 const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                 const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
                                 int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots, KernelTimer *timer,
-                                uint32_t *perm, uint32_t *order_scratch) {
+                                uint32_t *perm, uint32_t *order_scratch, const int4 *bcomb24) {
   const MsgSrc ms{msgs, off, msg_slots};
   if (stride > kFinCap) stride = kFinCap;
   if (timer) timer->mark(stream, -1);
@@ -1364,7 +1471,10 @@ hipError_t launch_verify_keyset(const uint32_t *val_idx, uint32_t nkeys, const u
         const char *v = getenv("TMED_KS_WAVES");
         return v ? atoi(v) : 2;
       }();
-      if (ks_waves >= 3)
+      if (bcomb24)
+        hipLaunchKernelGGL((verify_keyset_main_kernel<2, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream,
+                           val_idx, nkeys, acomb, bcomb24, base, count, prep, stride, fin, fbase, out, perm);
+      else if (ks_waves >= 3)
         hipLaunchKernelGGL(verify_keyset_main_kernel<3>, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx,
                            nkeys, acomb, bcomb, base, count, prep, stride, fin, fbase, out, perm);
       else

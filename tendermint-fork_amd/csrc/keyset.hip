@@ -69,7 +69,7 @@ static hipError_t keyset_verify(tmed_ctx *c, const Keyset &k, const uint32_t *d_
   // (the key order runs in front of each chunk's prep and is charged to prep by the timer)
   return launch_verify_keyset(d_idx, (uint32_t)k.n, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb16, d_sig, d_msgs, d_off, n,
                               d_out, c->d_prep, c->slab_slots, c->d_fin, c->d_fin_pre, s, msg_slots, timer, perm,
-                              scratch);
+                              scratch, c->d_b24);
 }
 
 int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st, int slot) {
@@ -242,6 +242,7 @@ int tmed_keyset_load(tmed_ctx *c, const uint8_t *pubkeys, size_t n, uint64_t *ha
   if (e == hipSuccess && n) e = hipMemcpyAsync(k.d_pub, pubkeys, n * 32, hipMemcpyHostToDevice, c->stream);
   int rc = map_err(e);
   if (rc == TMED_OK && n) rc = build_comb(c, k.d_pub, n, /*negate=*/1, k.d_ok, k.d_comb);
+  if (rc == TMED_OK) (void)ctx_bcomb24(c);  // the shared radix-2^24 B comb (null: radix 2^16)
   if (rc != TMED_OK) {
     free_keyset(k);
     return rc;

@@ -41,33 +41,36 @@ const char *tmed_strerror(int code) {
   }
 }
 
-// The radix-2^26 B tables (kernels.h kB26Bytes) are the same for every context of a device: built
-// by the first context, shared, freed with the last.  TMED_B26=0, or an allocation that fails,
-// leaves the main kernel on the radix-2^16 windows of the context's own comb.
+// The fixed-base tables of B too large to keep per context, the same for every context of a device:
+// built by the first context that needs them, shared, freed with the last.
+//   kind 0: the radix-2^26 tables of the default path (kernels.h kB26Bytes, 8.6 GB), at tmed_init;
+//   kind 1: the radix-2^24 comb of the key-cached throughput kernel (kB24Bytes, 11.8 GB), at the
+//           context's first tmed_keyset_load.
+// TMED_B26=0 / TMED_B24=0, or an allocation that fails, leaves that path on the context's own
+// radix-2^16 comb (same decisions).
 namespace {
-struct B26Share {
+struct BShare {
   int4 *p = nullptr;
   int refs = 0;
 };
-std::mutex g_b26_mu;
-B26Share g_b26[64];
+std::mutex g_bshare_mu;
+BShare g_bshare[2][64];
 }  // namespace
 
-static int4 *b26_acquire(int device, const int4 *comb16, hipStream_t s) {
-  static const bool on = [] {
-    const char *v = getenv("TMED_B26");
-    return !(v && v[0] == '0');
-  }();
-  if (!on || device < 0 || device >= 64) return nullptr;
-  std::lock_guard<std::mutex> lk(g_b26_mu);
-  B26Share &b = g_b26[device];
+static int4 *bshare_acquire(int kind, int device, const int4 *comb16, hipStream_t s) {
+  static const bool on[2] = {!(getenv("TMED_B26") && getenv("TMED_B26")[0] == '0'),
+                             !(getenv("TMED_B24") && getenv("TMED_B24")[0] == '0')};
+  if (!on[kind] || device < 0 || device >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(g_bshare_mu);
+  BShare &b = g_bshare[kind][device];
   if (!b.p) {
     int4 *p = nullptr;
-    if (hipMalloc((void **)&p, kB26Bytes) != hipSuccess) {
+    if (hipMalloc((void **)&p, kind == 0 ? kB26Bytes : kB24Bytes) != hipSuccess) {
       (void)hipGetLastError();
       return nullptr;
     }
-    if (launch_build_b26(comb16, p, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+    const hipError_t e = kind == 0 ? launch_build_b26(comb16, p, s) : launch_build_b24(comb16, p, s);
+    if (e != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
       (void)hipFree(p);
       return nullptr;
     }
@@ -77,15 +80,27 @@ static int4 *b26_acquire(int device, const int4 *comb16, hipStream_t s) {
   return b.p;
 }
 
-static void b26_release(int device, int4 *p) {
+static void bshare_release(int kind, int device, int4 *p) {
   if (!p) return;
-  std::lock_guard<std::mutex> lk(g_b26_mu);
-  B26Share &b = g_b26[device];
+  std::lock_guard<std::mutex> lk(g_bshare_mu);
+  BShare &b = g_bshare[kind][device];
   if (b.p == p && --b.refs == 0) {
     (void)hipFree(b.p);
     b.p = nullptr;
   }
 }
+
+extern "C++" {
+namespace tmed {
+const int4 *ctx_bcomb24(tmed_ctx *c) {
+  if (!c->b24_tried) {
+    c->b24_tried = true;
+    c->d_b24 = bshare_acquire(1, c->device, c->d_bcomb16, c->stream);
+  }
+  return c->d_b24;
+}
+}  // namespace tmed
+}  // extern "C++"
 
 int tmed_init(int device, tmed_ctx **out) {
   if (!out) return TMED_EINVAL;
@@ -149,7 +164,7 @@ int tmed_init(int device, tmed_ctx **out) {
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (d_bases) (void)hipFree(d_bases);
   }
-  if (e == hipSuccess) c->d_b26 = b26_acquire(device, c->d_bcomb16, c->stream);
+  if (e == hipSuccess) c->d_b26 = bshare_acquire(0, device, c->d_bcomb16, c->stream);
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_bcomb, kCombBytesPerKey);
   if (e == hipSuccess) e = hipMalloc((void **)&d_bpub, 32);
   if (e == hipSuccess) e = hipMalloc((void **)&d_bok, 1);
@@ -190,7 +205,8 @@ void tmed_destroy(tmed_ctx *c) {
   if (c->d_bcomb) hipFree(c->d_bcomb);
   if (c->d_b16) hipFree(c->d_b16);
   if (c->d_bcomb16) hipFree(c->d_bcomb16);
-  b26_release(c->device, c->d_b26);
+  bshare_release(0, c->device, c->d_b26);
+  bshare_release(1, c->device, c->d_b24);
   if (c->d_slab) hipFree(c->d_slab);
   if (c->d_prep) hipFree(c->d_prep);
   if (c->d_fin) hipFree(c->d_fin);
@@ -251,6 +267,7 @@ int tmed_verify_batch_device(tmed_ctx *c, const uint8_t *d_pub, const uint8_t *d
 }
 
 int tmed_b_window_bits(const tmed_ctx *c) { return c && c->d_b26 ? 26 : 16; }
+int tmed_keyset_b_window_bits(const tmed_ctx *c) { return c && c->d_b24 ? 24 : 16; }
 
 int tmed_window_stats(tmed_ctx *c, uint32_t lane_hist[65], uint32_t wave_hist[65]) {
   if (!c || !lane_hist || !wave_hist) return TMED_EINVAL;

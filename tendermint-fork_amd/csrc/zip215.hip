@@ -913,7 +913,7 @@ int zip215_verify_device(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, co
       const uint32_t lo = base + g.first;
       const uint8_t *gm = msg_slots ? msgs + (size_t)lo * kVoteSlot : msgs;
       e = launch_verify(pub + 32 * (size_t)lo, sig + 64 * (size_t)lo, gm, off + lo, g.second, out + lo, c->d_slab,
-                        c->slab_slots, BTabs{c->d_b16, c->d_bcomb16}, c->d_prep, c->d_fin, c->d_fin_pre, s, c->chunk,
+                        c->slab_slots, BTabs{c->d_b16, c->d_bcomb16, c->d_b26}, c->d_prep, c->d_fin, c->d_fin_pre, s, c->chunk,
                         6, msg_slots, nullptr, /*zip215=*/true);
       if (e != hipSuccess) return map_err(e);
     }

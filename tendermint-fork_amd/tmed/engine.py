@@ -222,5 +222,9 @@ class Engine:
         """Radix (bits) of the default path's fixed-base B windows: 26 or 16 (tmed_b_window_bits)."""
         return int(lib().tmed_b_window_bits(self._h))
 
+    def keyset_b_window_bits(self) -> int:
+        """Radix (bits) of the key-cached throughput path's B windows: 24 or 16 (tmed_keyset_b_window_bits)."""
+        return int(lib().tmed_keyset_b_window_bits(self._h))
+
     def last_kernel_ms(self) -> float:
         return float(lib().tmed_last_kernel_ms(self._h))
