@@ -18,9 +18,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "tendermint-fork_amd"))
 
 MUL, SQ = 100, 55
-# key-cached main kernel (kernels.hip keyset_straus_pf): first row niels -> extended (1 M), 46 mixed
-# additions + p1p1 -> p3 (7 M), the last to projective (6 M)
-MADS_KEYSET_MAIN = (1 + 46 * 7 + 6) * MUL
+sys.path.insert(0, ROOT)
+from bench import mads_keyset_main  # noqa: E402  (rows of the key-cached main kernel -> mads)
 
 
 def main():
@@ -85,6 +84,7 @@ def main():
     torch.cuda.synchronize(dev)
     (prep_ms, main_ms, fin_ms), (pl, ml, fl) = eng.kernel_times()
     eng.set_kernel_timing(False)
+    kbits = eng.keyset_b_window_bits()
     eng.keyset_free(ks)
     eng.close()
     if rank == 0:
@@ -93,7 +93,7 @@ def main():
             "unit": "verifies/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
             "all_valid": valid == n and ok_first == n, "keyset_build_s": round(t_ks, 3), "setup_s": round(t_gen, 2),
-            "mads_per_verify_main": MADS_KEYSET_MAIN,
+            "mads_per_verify_main": mads_keyset_main(kbits), "b_window_bits": kbits,
             "kernel_ms": {"prep": round(prep_ms, 4), "main": round(main_ms, 4), "finish": round(fin_ms, 4)},
             "sorted": args.sorted,
             "data": "synthetic (10k seeded keys, CanonicalVote sign-bytes, GPU RFC 8032 signer)",
