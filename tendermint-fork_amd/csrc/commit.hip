@@ -884,7 +884,8 @@ struct BsBatch {
 // before it, which is then collected and replayed (f4).  Same results as one run_seam over all
 // requests; the caller has checked every request (check_request) beforehand.
 // TMED_PIPE_SLOTS=3 keeps a third batch in flight (the host plans b+1 while b-1 and b are on the
-// device).  On
+// device).  Neither it nor a ramp of small first / last batches paid off (ramp: 188-195 against
+// 194-202 M/s, profiles/r03/c4_pipe/).  On
 // the GPU box's 16-CPU share it was SLOWER: the host staging of batch b then overlaps the copy
 // engine reading batch b-1 out of pinned memory and takes twice as long (C4 166-172 against
 // 181-191 M verifies/s, profiles/r03/c4_pipe/), so two slots stay the default.
@@ -897,17 +898,6 @@ static int pipe_slots() {
     return v && v[0] == '3' ? 3 : 2;
   }();
   return n;
-}
-
-// The first two batches of a call are a quarter and half of bsz (the device starts after a quarter
-// of the plan + staging + copy-in of a full batch) and the last one a quarter (the host waits out
-// a quarter batch's copy-in and kernels at the end); TMED_PIPE_RAMP=0: every batch bsz.
-static bool pipe_ramp() {
-  static const bool on = [] {
-    const char *v = getenv("TMED_PIPE_RAMP");
-    return !(v && v[0] == '0');
-  }();
-  return on;
 }
 
 static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t nb, size_t bsz, uint64_t keyset,
@@ -947,12 +937,8 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
     BsBatch &b = slots[idx % ns];
     BsBatch &mid = slots[(idx + ns - 1) % ns];  // batch idx-1 (in flight; with two slots the same as old)
     BsBatch &old = slots[(idx + 1) % ns];       // batch idx-ns+1: collected once batch idx is queued
-    size_t want = !pipe_ramp() ? bsz : idx == 0 ? std::max<size_t>(1, bsz / 4) : idx == 1 ? std::max<size_t>(1, bsz / 2) : bsz;
-    const size_t rem = nb - lo;
-    if (pipe_ramp() && idx >= 2 && rem <= bsz && rem > bsz / 4)
-      want = rem - std::max<size_t>(1, bsz / 4);  // a quarter batch last: less copy + kernels after the host is done
     b.lo = lo;
-    b.n = std::min(want, nb - lo);
+    b.n = std::min(bsz, nb - lo);
     lo += b.n;
     const tmed_commit_request *rq = reqs + b.lo;
     const auto tp = clock::now();

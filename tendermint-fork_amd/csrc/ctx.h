@@ -139,6 +139,7 @@ struct tmed_ctx {
   int4 *d_b26 = nullptr;      // radix-2^26 B tables of the half-size main kernel (8.6 GB, shared per device)
   int4 *d_b24 = nullptr;      // radix-2^24 B comb of the key-cached main kernel (11.8 GB, shared per device)
   bool b24_tried = false;     // d_b24 acquired (or given up) at the first key-set load
+  bool b24_on = true;         // TMED_B24 at tmed_init
   int4 *d_slab = nullptr;
   int4 *d_prep = nullptr;
   int4 *d_fin = nullptr;      // batched-finish hand-off (kFinBytes)

@@ -57,10 +57,13 @@ std::mutex g_bshare_mu;
 BShare g_bshare[2][64];
 }  // namespace
 
+static bool env_off(const char *name) {
+  const char *v = getenv(name);
+  return v && v[0] == '0';
+}
+
 static int4 *bshare_acquire(int kind, int device, const int4 *comb16, hipStream_t s) {
-  static const bool on[2] = {!(getenv("TMED_B26") && getenv("TMED_B26")[0] == '0'),
-                             !(getenv("TMED_B24") && getenv("TMED_B24")[0] == '0')};
-  if (!on[kind] || device < 0 || device >= 64) return nullptr;
+  if (device < 0 || device >= 64) return nullptr;
   std::lock_guard<std::mutex> lk(g_bshare_mu);
   BShare &b = g_bshare[kind][device];
   if (!b.p) {
@@ -93,7 +96,7 @@ static void bshare_release(int kind, int device, int4 *p) {
 extern "C++" {
 namespace tmed {
 const int4 *ctx_bcomb24(tmed_ctx *c) {
-  if (!c->b24_tried) {
+  if (!c->b24_tried && c->b24_on) {
     c->b24_tried = true;
     c->d_b24 = bshare_acquire(1, c->device, c->d_bcomb16, c->stream);
   }
@@ -164,7 +167,9 @@ int tmed_init(int device, tmed_ctx **out) {
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (d_bases) (void)hipFree(d_bases);
   }
-  if (e == hipSuccess) c->d_b26 = bshare_acquire(0, device, c->d_bcomb16, c->stream);
+  // TMED_B26 / TMED_B24 are read here, per context (a process may hold contexts of both kinds)
+  if (e == hipSuccess && !env_off("TMED_B26")) c->d_b26 = bshare_acquire(0, device, c->d_bcomb16, c->stream);
+  c->b24_on = !env_off("TMED_B24");
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_bcomb, kCombBytesPerKey);
   if (e == hipSuccess) e = hipMalloc((void **)&d_bpub, 32);
   if (e == hipSuccess) e = hipMalloc((void **)&d_bok, 1);
