@@ -173,7 +173,7 @@ __device__ __forceinline__ bool prep_load(const int4 *prep, uint32_t stride, uin
 // Phase 1: SHA-512(R||A||M) mod L, S < L, A = Point.SetBytes(pub)  (one lane per signature
 // of the chunk [base, base + count)).
 #ifndef TMED_PREP_WAVES
-#define TMED_PREP_WAVES 3  // 168 VGPRs, 59 spilled: -20 us per 2^20 against 2 waves (kernel-trace A/B)
+#define TMED_PREP_WAVES 3  // 152 VGPRs, no spills (4 waves with a leaner decode: no faster, profiles/r03/prep_joint)
 #endif
 __global__ __launch_bounds__(kThreadsPerBlock, TMED_PREP_WAVES) void verify_prep_kernel(
     const uint8_t *__restrict__ pub, const uint8_t *__restrict__ sig, MsgSrc ms, uint32_t base, uint32_t count,
@@ -314,7 +314,7 @@ constexpr int kHsWSmall = 32;
 static_assert((kPrepInt4 + kPrepHsInt4) * 16 <= kPrepSlotBytes, "prep slot too small for the half-size hand-off");
 
 #ifndef TMED_PREP_R_WAVES
-#define TMED_PREP_R_WAVES 3  // 168 VGPRs, 20 spilled: -0.06 ms per 2^20 against 2 waves (the Euclid loop hides its memory waits)
+#define TMED_PREP_R_WAVES 3  // 168 VGPRs, 6 spilled: -0.06 ms per 2^20 against 2 waves (the Euclid loop hides its memory waits)
 #endif
 __global__ __launch_bounds__(kThreadsPerBlock, TMED_PREP_R_WAVES) void verify_prep_r_kernel(
     const uint8_t *__restrict__ sig, uint32_t base, uint32_t count, const int4 *__restrict__ prep,
@@ -1467,16 +1467,9 @@ hipError_t launch_verify_keyset(const uint32_t *val_idx, uint32_t nkeys, const u
       hipLaunchKernelGGL(verify_keyset_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx,
                          nkeys, key_pub, key_ok, sig, ms, base, count, prep, stride);
       if (timer) timer->mark(stream, 0);
-      static const int ks_waves = [] {  // A/B: waves/SIMD the key-cached main kernel is compiled for
-        const char *v = getenv("TMED_KS_WAVES");
-        return v ? atoi(v) : 2;
-      }();
       if (bcomb24)
         hipLaunchKernelGGL((verify_keyset_main_kernel<2, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream,
                            val_idx, nkeys, acomb, bcomb24, base, count, prep, stride, fin, fbase, out, perm);
-      else if (ks_waves >= 3)
-        hipLaunchKernelGGL(verify_keyset_main_kernel<3>, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx,
-                           nkeys, acomb, bcomb, base, count, prep, stride, fin, fbase, out, perm);
       else
         hipLaunchKernelGGL(verify_keyset_main_kernel<2>, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx,
                            nkeys, acomb, bcomb, base, count, prep, stride, fin, fbase, out, perm);

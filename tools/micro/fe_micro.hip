@@ -103,6 +103,20 @@ int main() {
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
+  for (int wv = 1; wv <= 4; wv++)  // waves per SIMD resident (the kernels need few VGPRs)
+  for (auto &k : ks) {
+    const uint32_t nw = 65536u * wv;  // wv waves/SIMD: 256 CUs x 4 SIMDs x 64 lanes x wv
+    if (k.k == k_dbl) continue;
+    hipLaunchKernelGGL(k.k, dim3(nw / 256), dim3(256), 0, 0, d, nw, 10);
+    hipEventRecord(a, 0);
+    hipLaunchKernelGGL(k.k, dim3(nw / 256), dim3(256), 0, 0, d, nw, iters);
+    hipEventRecord(b, 0);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.3f, \"lane_Gop_s\": %.2f}\n", k.name, wv, ms,
+           (double)nw * iters * k.ops / (ms * 1e-3) / 1e9);
+  }
   for (auto &k : ks) {
     hipLaunchKernelGGL(k.k, dim3(n / 256), dim3(256), 0, 0, d, n, 10);
     hipEventRecord(a, 0);
