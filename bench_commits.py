@@ -263,7 +263,7 @@ def _c4_corrupt(commits, b0: int, every: int, upto: int):
 
 
 def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, batch: int, corrupt_every: int = 0,
-       pregen: bool = False):
+       pregen: bool = False, pinned: bool = True):
     """Blocksync replay (BASELINE C4): VerifyCommitLight for every block of a contiguous shard
     of the chain per rank, through the pipelined blocksync seam (tmed_blocksync_verify, f4),
     key-cached.  Blocks are generated window by window on the GPU (untimed) and verified
@@ -272,10 +272,14 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
     corrupt_every > 0: known-answer bad signatures in some blocks (_c4_corrupt); every block's
     outcome (code, error index, signatures verified) is checked against the expected one.
     pregen: generate every window of the shard before the timed part and start the ranks' timed
-    parts together (the host rehearsal: no rank's generation competes with another's seam)."""
+    parts together (the host rehearsal: no rank's generation competes with another's seam).
+    pinned: the commits' signatures are marshalled (untimed) into page-locked arenas
+    (tmed.PinnedBuffer, one per window held at once), as a Go shim that flattens its commits into
+    tmed_host_alloc memory would: the seam then DMAs them straight to the device."""
     import torch
     import torch.distributed as dist
     import tmed.types as T
+    from tmed import PinnedBuffer
     from tmed.workload import make_valset, pubkeys_of, seeds_from_tag, sign_commits
     seeds = seeds_from_tag(b"tmed-c4-key", 0, nvals)
     pubs = pubkeys_of(eng, seeds)
@@ -294,9 +298,24 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
     from tmed.types import seam_phase_us
     if world > 1:
         dist.barrier()
-    def gen(w0, w1):
+    arenas = []
+
+    def to_arena(commits, k):
+        if k == len(arenas):
+            arenas.append(PinnedBuffer(window * nvals * 64))
+        a = arenas[k].array((window * nvals, 64), np.uint8)
+        o = 0
+        for c in commits:
+            n = c.sigs.shape[0]
+            a[o:o + n] = c.sigs
+            c.sigs = a[o:o + n]
+            o += n
+
+    def gen(w0, w1, k=0):
         specs = [(seeds[order], addrs, b + 1, 0, block_id(b"c4-%d" % (b + 1)), T2023 + b, None) for b in range(w0, w1)]
         commits = sign_commits(eng, "test_chain_id", specs, sign_upto=upto)
+        if pinned:
+            to_arena(commits, k)
         exp = _c4_corrupt(commits, w0, corrupt_every, upto)
         win = T.BlocksyncWindow(vals, "test_chain_id", [c.block_id for c in commits], [c.height for c in commits],
                                 commits)
@@ -320,7 +339,7 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
         tg = time.perf_counter()
         for w0 in range(lo, hi, window):
             w1 = min(hi, w0 + window)
-            wins.append((w0, w1) + gen(w0, w1))
+            wins.append((w0, w1) + gen(w0, w1, len(wins)))
         t_gen += time.perf_counter() - tg
         if world > 1:
             dist.barrier()
@@ -355,6 +374,8 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
     ok, nb, ver, mism = (int(x) for x in tally.tolist())
     dt = float(tm.item())
     eng.keyset_free(vals.keyset)
+    for a in arenas:
+        a.free()
     n_bad = sum(1 for b in range(lo, hi) if corrupt_every and b % corrupt_every == 13)
     return {"metric": "blocksync replay verifies/s (VerifyCommitLight per block)", "value": round(ver / dt, 1),
             "unit": "verifies/s", "blocks_per_s": round(nb / dt, 1), "blocks": nb,
@@ -373,6 +394,8 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
                                    "blocks sharded over %d GPU(s) (contiguous heights), %d-block windows, "
                                    "%d-block device batches" % (blocks, nvals, world, window, batch),
                        "signed_per_commit": upto,
+                       "commit_memory": "pinned arenas (tmed_host_alloc): signatures DMA'd from them" if pinned
+                       else "pageable: signatures through the seam's staging copy",
                        "unsigned_note": "validators past the 2/3 crossing carry random (invalid) signatures "
                                         "the Light loop never reaches",
                        "keyset_build_s": round(t_ks, 3), "generate_s": round(t_gen, 2)}}
@@ -394,6 +417,8 @@ def main():
     ap.add_argument("--no-keyset", action="store_true")
     ap.add_argument("--corrupt-every", type=int, default=97, help="C4: known-answer bad signatures every N blocks (0: none)")
     ap.add_argument("--pregen", action="store_true", help="C4: generate the whole shard before timing (host rehearsal)")
+    ap.add_argument("--no-pinned", action="store_true",
+                    help="C4: commits in ordinary (pageable) memory: signatures go through the seam's staging copy")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -408,7 +433,7 @@ def main():
             r = c3(eng, args.headers, args.gap, not args.no_keyset, args.runs, args.bisect_gap)
         elif cfg == "c4":
             r = c4(eng, args.blocks, args.validators, rank, world, coll, args.window, args.batch, args.corrupt_every,
-                       args.pregen)
+                       args.pregen, not args.no_pinned)
         else:
             continue
         if rank == 0:

@@ -416,6 +416,22 @@ typedef struct {
 int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t batch_blocks,
                           tmed_commit_result *out);
 
+/*
+ * Pinned (page-locked) host memory for the commit arrays a caller marshals its commits into
+ * (the Go shim flattens every Commit into sigs / flags / timestamps arrays anyway).  When a
+ * candidate run's signatures lie in such memory, a large seam batch (tmed_blocksync_verify,
+ * tmed_verify_commits) DMAs them straight from the caller's array to the device instead of
+ * copying them through the library's pinned staging area first: one pass over host memory
+ * instead of three (read, staging write, DMA read) for 64 of the 85 bytes staged per vote.
+ * Decisions are identical either way.  tmed_host_alloc: hipHostMalloc'd memory (*p, freed with
+ * tmed_host_free); tmed_host_register: page-lock existing memory (hipHostRegister; undo with
+ * tmed_host_unregister before freeing it).  Process-wide, any context.
+ */
+int tmed_host_alloc(size_t bytes, void **p);
+int tmed_host_free(void *p);
+int tmed_host_register(void *p, size_t bytes);
+int tmed_host_unregister(void *p);
+
 /* ------------------------------------------ several GPUs in ONE process (§8e) */
 
 /*

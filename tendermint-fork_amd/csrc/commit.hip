@@ -713,11 +713,21 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
   memcpy(st.tmpl, tmpl, n * tmed::kVoteTmplBytes);
   std::atomic<bool> key_ok{true};
   const uint32_t nkeys = keyed ? (uint32_t)st.ks->n : 0u;
+  // Signature runs in pinned caller memory go to the device by their own DMA (votes_enqueue)
+  // instead of through the staging area: only batches copied on the copy stream.
+  static const bool direct_on = [] {
+    const char *v = getenv("TMED_DIRECT_DMA");
+    return !(v && v[0] == '0');
+  }();
+  const bool direct = direct_on && st.total >= tmed::kVoteCopyStreamMin;
+  const unsigned nt = host_threads(m);
+  std::vector<std::vector<tmed::VoteStage::Dma>> tdma(direct ? nt : 0u);
+  std::atomic<bool> all_direct{direct};
   // Runs of candidates of one request with consecutive signature indexes (a Light / blocksync
   // commit's candidates are one run) are staged one memcpy per array; the key index, the
   // template index and short signatures stay per vote.
-  auto fill = [&](size_t lo, size_t hi, unsigned) {
-    bool ok = true;
+  auto fill = [&](size_t lo, size_t hi, unsigned tid) {
+    bool ok = true, staged_sig = false;
     for (size_t j = lo; j < hi;) {
       const Cand &cd = cands[ix ? ix[j] : j];
       const tmed_commit_request &r = reqs[cd.req];
@@ -740,12 +750,20 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
       } else {
         memcpy(st.key + j * 32, r.vals->pubkeys + 32 * (size_t)cd.val_idx, 32 * len);
       }
-      memcpy(st.sig + j * 64, c.sigs + 64 * i, 64 * len);
-      if (c.sig_lens)
-        for (size_t u = 0; u < len; u++) {
-          const uint32_t sl = c.sig_lens[i + u];
-          if (sl < 64) memset(st.sig + (j + u) * 64 + sl, 0, 64 - sl);
-        }
+      bool dma = direct && tid < tdma.size() && tmed::host_pinned(c.sigs + 64 * i, 64 * len);
+      if (dma && c.sig_lens)  // short signatures are zero-padded in staging
+        for (size_t u = 0; u < len && dma; u++) dma = c.sig_lens[i + u] >= 64;
+      if (dma) {
+        tdma[tid].push_back({j * 64, c.sigs + 64 * i, 64 * len});
+      } else {
+        staged_sig = true;
+        memcpy(st.sig + j * 64, c.sigs + 64 * i, 64 * len);
+        if (c.sig_lens)
+          for (size_t u = 0; u < len; u++) {
+            const uint32_t sl = c.sig_lens[i + u];
+            if (sl < 64) memset(st.sig + (j + u) * 64 + sl, 0, 64 - sl);
+          }
+      }
       for (size_t u = 0; u < len; u++) st.tidx[j + u] = (uint32_t)cd.req;
       memcpy(st.flag + j, c.flags + i, len);
       memcpy(st.sec + j, c.ts_seconds + i, 8 * len);
@@ -753,9 +771,19 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
       j += len;
     }
     if (!ok) key_ok = false;
+    if (staged_sig) all_direct = false;
   };
-  parallel_ranges(m, host_threads(m), fill);
+  parallel_ranges(m, nt, fill);
   if (!key_ok) return TMED_EINVAL;  // a key-set index past the key set (votes_enqueue's check)
+  for (auto &v : tdma)  // thread ranges in order; a run cut at a thread boundary is joined again
+    for (const tmed::VoteStage::Dma &r : v) {
+      tmed::VoteStage::Dma *b = st.dma.empty() ? nullptr : &st.dma.back();
+      if (b && b->dst + b->bytes == r.dst && (const uint8_t *)b->src + b->bytes == (const uint8_t *)r.src)
+        b->bytes += r.bytes;
+      else
+        st.dma.push_back(r);
+    }
+  st.sig_direct = all_direct && m > 0;
   st.keys_checked = keyed;
   return TMED_OK;
 }
@@ -876,6 +904,7 @@ struct BsBatch {
   std::vector<uint8_t> tmpl, bits, valid;
   tmed::VoteStage st;
   bool device = false;  // queued on a vote slot (else verified synchronously / nothing to verify)
+  std::chrono::steady_clock::time_point enq;  // when it was queued (TMED_TRACE timeline)
 };
 }  // namespace
 
@@ -931,6 +960,11 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
     return r;
   };
   std::unique_lock<std::mutex> lk(ctx->mu);
+  if (trace_on()) {  // origin of the per-batch device timeline in the trace
+    if (!ctx->trace_t0) (void)hipEventCreate(&ctx->trace_t0);
+    if (ctx->trace_t0) (void)hipEventRecord(ctx->trace_t0, ctx->stream);
+  }
+  const auto t_origin = clock::now();
   size_t idx = 0;
   for (size_t lo = 0; lo < nb && rc == TMED_OK; idx++) {
     PhaseClock clk;
@@ -956,6 +990,7 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
         const auto te = clock::now();
         ph[0] += us(tp, te);
         if (rc == TMED_OK) rc = tmed::votes_enqueue(ctx, b.st);
+        b.enq = clock::now();
         clk.lap("enqueue");
         ph[1] += us(te, clock::now());  // queueing copies / launches can block behind a busy device
         b.device = rc == TMED_OK;
@@ -972,8 +1007,12 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
     if (rc == TMED_OK) rc = finish(old);  // overlaps the device work of batches idx-1 and idx
     clk.lap("finish_old");
     if (traced)
-      fprintf(stderr, "[tmed] blocksync collected batch: kernels %.0fus copy-in %.0fus copy end -> kernels %.0fus\n",
-              1000.0 * ctx->last_ms, 1000.0 * ctx->last_copy_ms, 1000.0 * ctx->last_copy_gap_ms);
+      fprintf(stderr,
+              "[tmed] blocksync collected batch: kernels %.0fus copy-in %.0fus copy end -> kernels %.0fus"
+              " | device us: copy %.0f-%.0f kernels %.0f-%.0f | host us: enqueued %.0f collected %.0f\n",
+              1000.0 * ctx->last_ms, 1000.0 * ctx->last_copy_ms, 1000.0 * ctx->last_copy_gap_ms,
+              1000.0 * ctx->last_at[0], 1000.0 * ctx->last_at[1], 1000.0 * ctx->last_at[2], 1000.0 * ctx->last_at[3],
+              us(t_origin, old.enq), us(t_origin, clock::now()));
     clk.emit("pipelined batch", b.n, m);
   }
   for (int k = 0; k < ns; k++)  // oldest first

@@ -4,6 +4,7 @@
 
 #include <mutex>
 #include <unordered_map>
+#include <vector>
 
 #include "../../include/tmed25519.h"
 #include "kernels.h"
@@ -99,7 +100,21 @@ struct VoteStage {
   bool timed = true;  // kernel-time events recorded (tmed_last_kernel_ms)
   bool keys_checked = false;  // every key-set index < the key set's size (checked while staging)
   bool copy_timed = false;    // cp0 / cp1 recorded around the copy-in (TMED_TRACE)
+  // Signature runs DMA'd straight from pinned caller memory (tmed_host_alloc / _register) into
+  // the device copy of the sig array at dst (bytes from the sig array's start); the staging area
+  // holds the rest.  sig_direct: every signature arrives that way (the staged sig region is not copied).
+  struct Dma {
+    size_t dst;
+    const void *src;
+    size_t bytes;
+  };
+  std::vector<Dma> dma;
+  bool sig_direct = false;
 };
+// Batches of at least this many staged bytes are copied on the context's copy stream (and may take
+// their signatures straight from pinned caller memory): votes_enqueue.
+constexpr size_t kVoteCopyStreamMin = 1u << 20;
+bool host_pinned(const void *p, size_t bytes);  // inside one tmed_host_alloc / _register range
 // staged-vote batches up to this size skip the copies (kernels read / write pinned host memory)
 constexpr size_t kVoteZeroCopyMax = 256u << 10;
 // Raw host batches of at most this many signatures record no kernel-time events by default.
@@ -132,6 +147,8 @@ struct tmed_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
   float last_copy_ms = 0.f, last_copy_gap_ms = 0.f;  // TMED_TRACE: copy-in of the last collected batch, copy end -> kernels
+  hipEvent_t trace_t0 = nullptr;  // TMED_TRACE: origin of last_at (recorded by the pipelined seam)
+  float last_at[4] = {0, 0, 0, 0};  // copy start, copy end, kernels start, kernels end (ms after trace_t0)
   std::mutex mu;
   int4 *d_bcomb = nullptr;  // signed radix-256 comb of +B (shared)
   int4 *d_b16 = nullptr;    // j*B, j = 0..32768 (main-kernel variant 5), built at init

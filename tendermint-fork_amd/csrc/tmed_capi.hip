@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <map>
 #include <mutex>
 #include <string>
 
@@ -56,6 +57,26 @@ struct BShare {
 std::mutex g_bshare_mu;
 BShare g_bshare[2][64];
 }  // namespace
+
+// Pinned caller memory (tmed_host_alloc / tmed_host_register): [start, end) ranges, looked up per
+// candidate run while a large seam batch is staged (host_pinned, ctx.h).
+namespace {
+std::mutex g_pin_mu;
+std::map<uintptr_t, uintptr_t> g_pinned;  // start -> end
+}  // namespace
+
+extern "C++" {
+namespace tmed {
+bool host_pinned(const void *p, size_t bytes) {
+  const uintptr_t a = (uintptr_t)p, b = a + bytes;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  auto it = g_pinned.upper_bound(a);
+  if (it == g_pinned.begin()) return false;
+  --it;
+  return a >= it->first && b <= it->second;
+}
+}  // namespace tmed
+}
 
 static bool env_off(const char *name) {
   const char *v = getenv(name);
@@ -269,6 +290,40 @@ int tmed_verify_batch_device(tmed_ctx *c, const uint8_t *d_pub, const uint8_t *d
     e = generic_verify(c, d_pub, d_sig, d_msgs, d_off, (uint32_t)n, d_out, s, false, c->timing ? &c->timer : nullptr);
   if (e == hipSuccess) e = scratch_release(c, s);
   return map_err(e);
+}
+
+int tmed_host_alloc(size_t bytes, void **p) {
+  if (!p || bytes == 0) return TMED_EINVAL;
+  *p = nullptr;
+  if (hipHostMalloc(p, bytes, hipHostMallocDefault) != hipSuccess || !*p) return TMED_ENOMEM;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pinned[(uintptr_t)*p] = (uintptr_t)*p + bytes;
+  return TMED_OK;
+}
+
+int tmed_host_free(void *p) {
+  if (!p) return TMED_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    if (!g_pinned.erase((uintptr_t)p)) return TMED_EINVAL;
+  }
+  return hipHostFree(p) == hipSuccess ? TMED_OK : TMED_EHIP;
+}
+
+int tmed_host_register(void *p, size_t bytes) {
+  if (!p || bytes == 0) return TMED_EINVAL;
+  if (hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) return TMED_EHIP;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pinned[(uintptr_t)p] = (uintptr_t)p + bytes;
+  return TMED_OK;
+}
+
+int tmed_host_unregister(void *p) {
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    if (!p || !g_pinned.erase((uintptr_t)p)) return TMED_EINVAL;
+  }
+  return hipHostUnregister(p) == hipSuccess ? TMED_OK : TMED_EHIP;
 }
 
 int tmed_b_window_bits(const tmed_ctx *c) { return c && c->d_b26 ? 26 : 16; }

@@ -28,7 +28,31 @@ import (
 
 // Engine wraps one tmed_ctx (one per GPU; safe for concurrent use: the
 // library serialises calls on a context).
-type Engine struct{ ctx *C.tmed_ctx }
+type Engine struct {
+	ctx *C.tmed_ctx
+	// page-locked arena the blocksync signatures are marshalled into (grow-only, kept across
+	// calls): the library DMAs them from it instead of copying them through its staging area
+	pinMu  sync.Mutex
+	pin    unsafe.Pointer
+	pinCap int
+}
+
+// pinnedSigs returns the engine's pinned arena grown to at least n bytes (nil if
+// tmed_host_alloc fails: the caller then marshals into ordinary C memory).  Holds pinMu.
+func (e *Engine) pinnedSigs(n int) unsafe.Pointer {
+	if n > e.pinCap {
+		if e.pin != nil {
+			C.tmed_host_free(e.pin)
+			e.pin, e.pinCap = nil, 0
+		}
+		var p unsafe.Pointer
+		if C.tmed_host_alloc(C.size_t(n+n/4), &p) != 0 {
+			return nil
+		}
+		e.pin, e.pinCap = p, n+n/4
+	}
+	return e.pin
+}
 
 var (
 	once    sync.Once
@@ -279,10 +303,27 @@ func (e *Engine) BlocksyncVerify(w *BlocksyncWindow, batchBlocks int) ([]Result,
 		keyset: C.uint64_t(w.Vals.Keyset), keyset_index: a.u32(w.Vals.KeysetIndex)}
 	cs := (*[1 << 26]C.tmed_commit)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_commit{})))[:n:n]
 	bids := (*[1 << 26]C.tmed_block_id)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_block_id{})))[:n:n]
+	// signatures into the pinned arena (direct DMA, include/tmed25519.h tmed_host_alloc)
+	total := 0
+	for _, c := range w.Commits {
+		total += len(c.Sigs)
+	}
+	e.pinMu.Lock()
+	defer e.pinMu.Unlock()
+	arenaBase := e.pinnedSigs(total)
+	off := 0
 	for i, c := range w.Commits {
+		sigs := (*C.uint8_t)(nil)
+		if arenaBase != nil && len(c.Sigs) > 0 {
+			p := unsafe.Add(arenaBase, off)
+			copy(unsafe.Slice((*byte)(p), len(c.Sigs)), c.Sigs)
+			sigs, off = (*C.uint8_t)(p), off+len(c.Sigs)
+		} else {
+			sigs = a.bytes(c.Sigs)
+		}
 		cs[i] = C.tmed_commit{height: C.int64_t(c.Height), round: C.int32_t(c.Round), block_id: a.blockID(&c.BlockID),
 			n_sigs: C.size_t(len(c.Flags)), flags: a.bytes(c.Flags), addresses: a.bytes(c.Addresses),
-			ts_seconds: a.i64(c.TsSeconds), ts_nanos: a.i32(c.TsNanos), sigs: a.bytes(c.Sigs), sig_lens: a.u32(c.SigLens),
+			ts_seconds: a.i64(c.TsSeconds), ts_nanos: a.i32(c.TsNanos), sigs: sigs, sig_lens: a.u32(c.SigLens),
 			address_lens: a.u32(c.AddrLens)}
 		bids[i] = a.blockID(&w.BlockIDs[i])
 	}

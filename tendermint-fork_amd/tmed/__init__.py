@@ -5,4 +5,4 @@ Host-side mirror of the reference interfaces on the hot path
 over the gfx950 C ABI in ``include/tmed25519.h``.
 """
 from ._native import LIB_PATH, TmedError, lib  # noqa: F401
-from .engine import Engine, pack_messages  # noqa: F401
+from .engine import Engine, PinnedBuffer, pack_messages  # noqa: F401

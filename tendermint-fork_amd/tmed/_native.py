@@ -82,6 +82,14 @@ def lib() -> ctypes.CDLL:
     l.tmed_b_window_bits.argtypes = [P]
     l.tmed_keyset_b_window_bits.restype = I
     l.tmed_keyset_b_window_bits.argtypes = [P]
+    l.tmed_host_alloc.restype = I
+    l.tmed_host_alloc.argtypes = [SZ, ctypes.POINTER(ctypes.c_void_p)]
+    l.tmed_host_free.restype = I
+    l.tmed_host_free.argtypes = [P]
+    l.tmed_host_register.restype = I
+    l.tmed_host_register.argtypes = [P, SZ]
+    l.tmed_host_unregister.restype = I
+    l.tmed_host_unregister.argtypes = [P]
     l.tmed_verify_batch_zip215.argtypes = [P, P, P, P, P, P, SZ, P]
     l.tmed_verify_batch_zip215_device.argtypes = [P, P, P, P, P, SZ, P, P]
     l.tmed_zip215_set_seed.argtypes = [P]
@@ -101,4 +109,5 @@ EXPORTED_SYMBOLS = [
     "tmed_merkle_roots", "tmed_valset_hashes", "tmed_header_hashes", "tmed_partset_roots",
     "tmed_verify_commits_multi", "tmed_blocksync_verify_multi", "tmed_window_stats", "tmed_b_window_bits", "tmed_keyset_b_window_bits", "tmed_seam_phase_us",
     "tmed_verify_batch_zip215", "tmed_verify_batch_zip215_device", "tmed_zip215_set_seed", "tmed_zip215_stats",
+    "tmed_host_alloc", "tmed_host_free", "tmed_host_register", "tmed_host_unregister",
 ]

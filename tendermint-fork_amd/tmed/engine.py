@@ -29,6 +29,33 @@ def pack_messages(msgs: Sequence[bytes]):
     return flat, off.astype(np.uint32)
 
 
+class PinnedBuffer:
+    """Page-locked host memory from tmed_host_alloc: commit arrays marshalled into it reach the
+    device by direct DMA in large seam batches (include/tmed25519.h).  Arrays from array() are
+    views: keep the buffer alive while they are used, free() it after."""
+
+    def __init__(self, nbytes: int):
+        p = ctypes.c_void_p()
+        rc = lib().tmed_host_alloc(int(nbytes), ctypes.byref(p))
+        if rc != TMED_OK:
+            raise TmedError(rc)
+        self.ptr, self.nbytes = p.value, int(nbytes)
+
+    def array(self, shape, dtype, offset: int = 0) -> np.ndarray:
+        count = int(np.prod(shape))
+        if offset + count * np.dtype(dtype).itemsize > self.nbytes:
+            raise ValueError("view past the pinned buffer")
+        raw = (ctypes.c_uint8 * self.nbytes).from_address(self.ptr)
+        return np.frombuffer(raw, dtype, count=count, offset=offset).reshape(shape)
+
+    def free(self) -> None:
+        if self.ptr:
+            rc = lib().tmed_host_free(self.ptr)
+            self.ptr = None
+            if rc != TMED_OK:
+                raise TmedError(rc)
+
+
 class Engine:
     """One context on one HIP device (one process per GPU)."""
 

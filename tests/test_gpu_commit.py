@@ -270,3 +270,63 @@ def test_edge_scenarios_gpu(engine):
     bad = [(q, got[q], exp[q]) for q in range(len(reqs)) if not same_outcome(got[q], exp[q])]
     assert not bad, bad[:5]
     assert any(isinstance(e, tuple) for e in exp)
+
+
+@pytest.mark.parametrize("pinned", ["all", "alternate"])
+@pytest.mark.parametrize("keyed", [False, True])
+def test_blocksync_pinned_signatures_gpu(engine, pinned, keyed):
+    """Signatures in tmed_host_alloc memory are DMA'd straight from the caller's arrays (batches of
+    >= 1 MB staged): every block's outcome (code, index, signatures verified) equals the run from
+    pageable memory — all commits pinned, and every other commit pinned (mixed runs: staged and
+    direct signatures in one batch) — with known-answer bad signatures before and after the
+    2/3 crossing and a short (63-byte) signature in a pinned run."""
+    import hashlib
+    import numpy as np
+    from tmed import PinnedBuffer
+    from tmed.workload import make_valset, pubkeys_of, seeds_from_tag, sign_commits
+    nvals, nblk = 2000, 30  # 12-block batches of ~16k candidates: 1.4 MB staged, the copy-stream path
+    seeds = seeds_from_tag(b"tmed-pin-key", 0, nvals)
+    vals, order = make_valset(pubkeys_of(engine, seeds), [10] * nvals)
+    addrs = np.array([np.frombuffer(v.address, np.uint8) for v in vals.validators])
+    upto = nvals * 2 // 3 + 1
+    bids = [T.BlockID(hashlib.sha256(b"pin%d" % b).digest(), 7, hashlib.sha256(b"psh%d" % b).digest())
+            for b in range(nblk)]
+    specs = [(seeds[order], addrs, 100 + b, 0, bids[b], 1672531200 + b, None) for b in range(nblk)]
+
+    def window(pin):
+        commits = sign_commits(engine, "pin-chain", specs, sign_upto=upto)
+        for b, c in enumerate(commits):
+            if b % 5 == 1:
+                c.sigs[(b * 31) % upto, 3] ^= 0x40      # before the crossing: wrong signature
+            if b % 5 == 2:
+                c.sigs[upto + 1, 9] ^= 0x01             # after it: never reached
+            if b % 7 == 3:
+                c.sig_lens[(b * 13) % upto] = 63        # a short signature: wrong length
+        buf = None
+        if pin:
+            buf = PinnedBuffer(nblk * nvals * 64)
+            a = buf.array((nblk * nvals, 64), np.uint8)
+            for b, c in enumerate(commits):
+                if pinned == "all" or b % 2 == 0:
+                    a[b * nvals:(b + 1) * nvals] = c.sigs
+                    c.sigs = a[b * nvals:(b + 1) * nvals]
+        return T.BlocksyncWindow(vals, "pin-chain", bids, [100 + b for b in range(nblk)], commits), buf
+
+    ks = 0
+    if keyed:
+        ks = engine.keyset_load(np.array([np.frombuffer(v.pub_key, np.uint8) for v in vals.validators]))
+        vals.keyset = ks
+    try:
+        w0, _ = window(False)
+        w0.run(engine, 12)
+        w1, buf = window(True)
+        w1.run(engine, 12)
+        assert (w0.codes() == w1.codes()).all()
+        assert (w0.verified() == w1.verified()).all()
+        assert [w0.res[h].idx for h in range(nblk)] == [w1.res[h].idx for h in range(nblk)]
+        assert (w0.codes() == 4).sum() >= 6 and (w0.codes() == 0).sum() >= 10
+        buf.free()
+    finally:
+        if ks:
+            engine.keyset_free(ks)
+            vals.keyset = 0
