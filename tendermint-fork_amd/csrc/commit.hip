@@ -912,19 +912,21 @@ struct BsBatch {
 // keys): batch b is planned, staged and queued while the device copies in and verifies the batch
 // before it, which is then collected and replayed (f4).  Same results as one run_seam over all
 // requests; the caller has checked every request (check_request) beforehand.
-// TMED_PIPE_SLOTS=3 keeps a third batch in flight (the host plans b+1 while b-1 and b are on the
-// device).  Neither it nor a ramp of small first / last batches paid off (ramp: 188-195 against
-// 194-202 M/s, profiles/r03/c4_pipe/).  On
-// the GPU box's 16-CPU share it was SLOWER: the host staging of batch b then overlaps the copy
-// engine reading batch b-1 out of pinned memory and takes twice as long (C4 166-172 against
-// 181-191 M verifies/s, profiles/r03/c4_pipe/), so two slots stay the default.
+// Pipeline depth.  With the signatures staged (pageable caller memory) two slots: a third
+// overlaps the host staging of batch b with the copy engine reading batch b-1 out of pinned
+// memory, and both slow down (C4 166-172 against 181-191 M verifies/s, profiles/r03/c4_pipe/).
+// With the signatures DMA'd from pinned caller memory the host's share per batch is ~1.5 ms
+// against ~2.2 ms of kernels, and a third slot keeps the kernel stream busy (C4 280-307 against
+// 258-282 M/s, profiles/r03/c4_direct/).  So the depth follows the first batch: three slots
+// when its signatures went direct (VoteStage::sig_direct), else two.  TMED_PIPE_SLOTS=2 / 3
+// forces either.  (A ramp of small first / last batches did not pay: profiles/r03/c4_pipe/.)
 constexpr int kPipeSlots = 3;
 static_assert(kPipeSlots <= (int)(sizeof(((tmed_ctx *)nullptr)->vslot) / sizeof(tmed::VoteSlot)),
               "one context vote slot per pipeline slot");
-static int pipe_slots() {
+static int pipe_slots_env() {  // 0: follow the first batch
   static const int n = [] {
-    const char *v = getenv("TMED_PIPE_SLOTS");  // 3: three batches in flight (see above)
-    return v && v[0] == '3' ? 3 : 2;
+    const char *v = getenv("TMED_PIPE_SLOTS");
+    return v && v[0] == '3' ? 3 : (v && v[0] == '2' ? 2 : 0);
   }();
   return n;
 }
@@ -932,7 +934,8 @@ static int pipe_slots() {
 static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t nb, size_t bsz, uint64_t keyset,
                          tmed_commit_result *out) {
   BsBatch slots[kPipeSlots];
-  const int ns = pipe_slots();
+  const int forced = pipe_slots_env();
+  int ns = forced ? forced : 2;  // raised to 3 after batch 0 when its signatures went direct
   int rc = TMED_OK;
   // tmed_seam_phase_us for a pipelined call: host plan + templates + staging, host time blocked on
   // the device (enqueueing the copies and kernels, votes_collect), host replay — the first and
@@ -991,6 +994,7 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
         ph[0] += us(tp, te);
         if (rc == TMED_OK) rc = tmed::votes_enqueue(ctx, b.st);
         b.enq = clock::now();
+        if (idx == 0 && !forced && b.st.sig_direct) ns = 3;
         clk.lap("enqueue");
         ph[1] += us(te, clock::now());  // queueing copies / launches can block behind a busy device
         b.device = rc == TMED_OK;

@@ -7,7 +7,10 @@
 // The reference has no such cache (it decodes A inside every Verify); callers
 // key the cache by ValidatorSet.Hash() (types/validator_set.go:347-353).
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <string.h>
+
+#include <chrono>
 
 #include "ctx.h"
 
@@ -118,7 +121,24 @@ int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteSta
   return TMED_OK;
 }
 
+namespace {
+// TMED_TRACE: names a queueing step of votes_enqueue that blocked the host for over 1 ms.
+struct SlowStep {
+  bool on;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void lap(const char *what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    const double us = std::chrono::duration<double, std::micro>(n - t).count();
+    if (us > 1000.0) fprintf(stderr, "[tmed] votes_enqueue: %s blocked %.0f us\n", what, us);
+    t = n;
+  }
+};
+}  // namespace
+
 int votes_enqueue(tmed_ctx *c, VoteStage &st) {
+  static const bool trace_steps = getenv("TMED_TRACE") != nullptr;
+  SlowStep slow{trace_steps};
   const uint32_t m = st.m;
   if (st.ks && !st.keys_checked)
     for (uint32_t j = 0; j < m; j++)
@@ -190,7 +210,9 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   } else {
     e = hipMemcpyAsync(d, vs.h_votes.p, st.total, hipMemcpyHostToDevice, s);
   }
+  slow.lap("copy-in");
   if (e == hipSuccess) e = scratch_acquire(c, s);
+  slow.lap("scratch_acquire");
   // Timing events cost ~8 us of a single commit's latency (C1 generic 249 -> 239 us, keyed
   // 97 -> 88 us): a zero-copy batch records them only under tmed_set_kernel_timing.
   st.timed = !st.zc || c->timing;
@@ -203,6 +225,7 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   if (e == hipSuccess && !fused)
     e = launch_assemble_votes(va.tmpl, va.tmpl_idx, va.flags, va.ts_sec, va.ts_nanos, m, (uint8_t *)vs.d_vmsg.p,
                               (uint32_t *)vs.d_off.p, s);
+  slow.lap("assemble");
   if (e == hipSuccess) {
     if (st.ks)
       e = keyset_verify(c, *st.ks, (const uint32_t *)(d + st.o_key), d + st.o_sig, (const uint8_t *)vs.d_vmsg.p,
@@ -211,10 +234,12 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
       e = generic_verify(c, d + st.o_key, d + st.o_sig, (const uint8_t *)vs.d_vmsg.p, (const uint32_t *)vs.d_off.p, m,
                          out_dev, s, /*msg_slots=*/true, nullptr, fused ? &va : nullptr);
   }
+  slow.lap("verify launches");
   if (e == hipSuccess && st.timed) e = hipEventRecord(vs.ev1, s);
   if (e == hipSuccess) e = scratch_release(c, s);
   if (e == hipSuccess && !st.zc) e = hipMemcpyAsync(vs.h_out.p, vs.d_out.p, m, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipEventRecord(vs.done, s);
+  slow.lap("copy-out");
   return map_err(e);
 }
 
