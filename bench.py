@@ -84,8 +84,12 @@ if MAIN_VARIANT == 6:
 # + p1p1 -> p3 (4 M), the last stops at projective (3 M + 3 M)
 
 
-def mads_keyset_main(b_bits: int = 24) -> int:
-    rows = 32 + (11 if b_bits == 24 else 16)
+def mads_keyset_main(b_bits: int = 24, a_bits: int = 8) -> int:
+    """Field products of the key-cached main kernel per signature, in mads: one comb row per
+    window (26 with the radix-2^10 -A comb, 32 with the radix-256 one; 11 B rows with the
+    radix-2^24 B comb, 16 with the radix-2^16 one); the first row is a conversion (1 M), the
+    last stops at projective (6 M), the rest are mixed additions (7 M)."""
+    rows = (26 if a_bits == 10 else 32) + (11 if b_bits == 24 else 16)
     return (1 + (rows - 2) * 7 + 6) * MUL
 
 
@@ -380,12 +384,16 @@ def c2_keyset(eng, dev, torch_stream, n, steps, warmup, peak):
     torch.cuda.synchronize(dev)
     (prep_ms, main_ms, fin_ms), (pl, ml, fl) = eng.kernel_times()
     eng.set_kernel_timing(False)
-    eng.keyset_free(ks)
     try:
         kb = eng.keyset_b_window_bits()
     except AttributeError:  # an older library build (A/B runs through TMED_LIB)
         kb = 16
-    mads_ks = mads_keyset_main(kb)
+    try:
+        ka = eng.keyset_a_window_bits(ks)
+    except AttributeError:
+        ka = 8
+    eng.keyset_free(ks)
+    mads_ks = mads_keyset_main(kb, ka)
     achieved = n * mads_ks / (main_ms * 1e-3) / 1e12 if main_ms > 0 else None
     traffic, traffic_src = pmc_traffic(n / max(1, ml), "verify_keyset_main_kernel")
     return {"metric": "ed25519 verifies/sec at 1/8 MI355X, key cache on (C2 variant: 10k reused keys)",
@@ -398,7 +406,7 @@ def c2_keyset(eng, dev, torch_stream, n, steps, warmup, peak):
                          "frac": round(achieved / peak, 4) if (achieved and peak) else None,
                          "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                          "traffic_source": traffic_src,
-                         "mads_per_verify_main": mads_ks, "b_window_bits": kb,
+                         "mads_per_verify_main": mads_ks, "b_window_bits": kb, "a_window_bits": ka,
                          "visiting_order": "key-grouped (launch_key_order, charged to prep_kernel_ms)",
                          "kernel_avg_ms": round(main_ms / max(1, ml), 4), "launches_per_step": ml,
                          "prep_kernel_ms": round(prep_ms, 4), "finish_kernel_ms": round(fin_ms, 4)},

@@ -85,6 +85,7 @@ def main():
     (prep_ms, main_ms, fin_ms), (pl, ml, fl) = eng.kernel_times()
     eng.set_kernel_timing(False)
     kbits = eng.keyset_b_window_bits()
+    abits = eng.keyset_a_window_bits(ks)
     eng.keyset_free(ks)
     eng.close()
     if rank == 0:
@@ -93,7 +94,7 @@ def main():
             "unit": "verifies/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
             "all_valid": valid == n and ok_first == n, "keyset_build_s": round(t_ks, 3), "setup_s": round(t_gen, 2),
-            "mads_per_verify_main": mads_keyset_main(kbits), "b_window_bits": kbits,
+            "mads_per_verify_main": mads_keyset_main(kbits, abits), "b_window_bits": kbits, "a_window_bits": abits,
             "kernel_ms": {"prep": round(prep_ms, 4), "main": round(main_ms, 4), "finish": round(fin_ms, 4)},
             "sorted": args.sorted,
             "data": "synthetic (10k seeded keys, CanonicalVote sign-bytes, GPU RFC 8032 signer)",

@@ -111,6 +111,14 @@ int tmed_b_window_bits(const tmed_ctx *ctx);
  * key-set load, with TMED_B24=0, or when the allocation failed).  Diagnostic; same decisions.
  */
 int tmed_keyset_b_window_bits(const tmed_ctx *ctx);
+/*
+ * Radix (in bits) of the -A comb the key-cached throughput kernel reads for key set `handle`: 10
+ * (26 windows of 513 multiples, 1.7 MB per key, built at the set's first throughput batch with the
+ * radix-2^24 B comb in use: 37 comb rows per signature) or 8 (the radix-256 comb every key set
+ * holds, also used by the latency kernels: TMED_KS_A10=0, before the first throughput batch, or
+ * no memory).  -1 for an unknown handle.  Diagnostic; decisions are identical.
+ */
+int tmed_keyset_a_window_bits(tmed_ctx *ctx, uint64_t handle);
 
 /* Device time (ms) of the last verify/sign launch on this context (HIP events).  A commit batch
  * small enough for the zero-copy latency mode (a single commit), or a tmed_verify_batch of at most

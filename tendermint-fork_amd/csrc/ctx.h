@@ -65,6 +65,11 @@ struct Keyset {
   uint8_t *d_pub = nullptr;   // n x 32 raw encodings (hashed into k)
   uint8_t *d_ok = nullptr;    // n: Point.SetBytes accepted the key
   int4 *d_comb = nullptr;     // n x kCombBytesPerKey: signed radix-256 comb of -A
+  // n x kComb10BytesPerKey: radix-2^10 comb of -A for the throughput kernel, built at the key
+  // set's first throughput batch (keyset.hip keyset_verify; null: not built / TMED_KS_A10=0 /
+  // no memory -> the radix-256 comb)
+  mutable int4 *d_comb10 = nullptr;
+  mutable bool comb10_tried = false;
 };
 
 int build_comb(tmed_ctx *c, const uint8_t *d_pubs, size_t n, int negate, uint8_t *d_ok, int4 *d_comb);
@@ -157,6 +162,7 @@ struct tmed_ctx {
   int4 *d_b24 = nullptr;      // radix-2^24 B comb of the key-cached main kernel (11.8 GB, shared per device)
   bool b24_tried = false;     // d_b24 acquired (or given up) at the first key-set load
   bool b24_on = true;         // TMED_B24 at tmed_init
+  bool a10_on = true;         // TMED_KS_A10 at tmed_init (radix-2^10 -A combs, keyset.hip comb10_build)
   int4 *d_slab = nullptr;
   int4 *d_prep = nullptr;
   int4 *d_fin = nullptr;      // batched-finish hand-off (kFinBytes)

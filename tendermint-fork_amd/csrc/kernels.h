@@ -107,6 +107,15 @@ hipError_t launch_comb_bases(const uint8_t *pubs, uint32_t n, int negate, uint8_
                              hipStream_t stream);
 // comb[key] from bases[key] (n * 32 workgroups of 128 lanes).
 hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStream_t stream);
+// Signed radix-2^10 comb of -A for the key-cached throughput kernel: entry [w][j] = j * 2^(10w) * (-A),
+// w = 0..25, j = 0..512; digit m of k is bits [10m, 10m + 10) + bit (10m - 1) - 2^10 * bit (10m + 9)
+// in [-512, 512] (no carry chain; k < 2^253 leaves digit 25 without a carry out): 26 rows per
+// signature instead of 32, 1.7 MB per key, built at a key set's first throughput batch.
+constexpr int kComb10Windows = 26;
+constexpr uint32_t kComb10Entries = 513;
+constexpr size_t kComb10BytesPerKey = (size_t)kComb10Windows * kComb10Entries * kCombEntryInt4 * 16;
+// comb10[key] of -A_key (bases: scratch of n * 26 * 40 int32).
+hipError_t launch_build_comb10(const uint8_t *pubs, uint32_t n, int32_t *bases, int4 *comb10, hipStream_t stream);
 // Key-cached verification: key index per signature into a keyset of nkeys keys (an index
 // >= nkeys rejects that signature).  perm (nullable, n entries of scratch) + order_scratch
 // (key_order_scratch_words): the main and finish kernels visit each chunk's signatures in
@@ -116,7 +125,8 @@ hipError_t launch_verify_keyset(const uint32_t *val_idx, uint32_t nkeys, const u
                                 const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
                                 int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots = false,
                                 KernelTimer *timer = nullptr, uint32_t *perm = nullptr,
-                                uint32_t *order_scratch = nullptr, const int4 *bcomb24 = nullptr);
+                                uint32_t *order_scratch = nullptr, const int4 *bcomb24 = nullptr,
+                                const int4 *acomb10 = nullptr);
 // Key-grouped visiting order of a key-cached batch (counting sort of val_idx by groups of
 // consecutive keys, indices >= nkeys last): perm[0..n) = signature indices grouped by key.
 // scratch: key_order_scratch_words(n, nkeys) u32.  The comb rows of the lanes in flight then

@@ -32,6 +32,7 @@ void free_keyset(Keyset &k) {
   if (k.d_pub) (void)hipFree(k.d_pub);
   if (k.d_ok) (void)hipFree(k.d_ok);
   if (k.d_comb) (void)hipFree(k.d_comb);
+  if (k.d_comb10) (void)hipFree(k.d_comb10);
   k = Keyset();
 }
 
@@ -50,6 +51,27 @@ static bool key_order_on(const Keyset &k, uint32_t n) {
   return on && n >= 4096 && k.n > 1 && k.n <= kKeyOrderMaxKeys;
 }
 
+// The key set's radix-2^10 comb (kernels.h kComb10*), once, on stream s (queued in front of the
+// batch that needs it; the bases scratch is freed after a sync of s).  TMED_KS_A10=0 (read at
+// tmed_init) keeps the radix-256 comb.
+static void comb10_build(tmed_ctx *c, const Keyset &k, hipStream_t s) {
+  k.comb10_tried = true;
+  if (!c->a10_on || k.n == 0) return;
+  int32_t *bases = nullptr;
+  int4 *comb = nullptr;
+  hipError_t e = hipMalloc((void **)&bases, k.n * kComb10Windows * 40 * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMalloc((void **)&comb, k.n * kComb10BytesPerKey);
+  if (e == hipSuccess) e = launch_build_comb10(k.d_pub, (uint32_t)k.n, bases, comb, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (bases) (void)hipFree(bases);
+  if (e == hipSuccess) {
+    k.d_comb10 = comb;
+  } else {
+    if (comb) (void)hipFree(comb);
+    (void)hipGetLastError();  // an allocation failure leaves the radix-256 comb in use
+  }
+}
+
 // Key-cached batch on the context's stream: latency kernels for small batches (C1: one
 // commit), the throughput kernels (prep / comb main / batched finish) above c->lat_max.
 static hipError_t keyset_verify(tmed_ctx *c, const Keyset &k, const uint32_t *d_idx, const uint8_t *d_sig,
@@ -60,6 +82,7 @@ static hipError_t keyset_verify(tmed_ctx *c, const Keyset &k, const uint32_t *d_
     return launch_verify_keyset_lat(d_idx, (uint32_t)k.n, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb, d_sig, d_msgs, d_off, n, d_out,
                                     c->d_fin, c->d_fin_pre, s, msg_slots, va);
   if (va) return hipErrorInvalidValue;
+  if (c->d_b24 && !k.comb10_tried) comb10_build(c, k, s);
   KernelTimer *timer = (c->timing && !msg_slots) ? &c->timer : nullptr;
   uint32_t *perm = nullptr, *scratch = nullptr;
   if (key_order_on(k, n)) {
@@ -72,7 +95,7 @@ static hipError_t keyset_verify(tmed_ctx *c, const Keyset &k, const uint32_t *d_
   // (the key order runs in front of each chunk's prep and is charged to prep by the timer)
   return launch_verify_keyset(d_idx, (uint32_t)k.n, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb16, d_sig, d_msgs, d_off, n,
                               d_out, c->d_prep, c->slab_slots, c->d_fin, c->d_fin_pre, s, msg_slots, timer, perm,
-                              scratch, c->d_b24);
+                              scratch, c->d_b24, c->d_b24 ? k.d_comb10 : nullptr);
 }
 
 int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st, int slot) {

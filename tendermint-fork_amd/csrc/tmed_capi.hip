@@ -191,6 +191,7 @@ int tmed_init(int device, tmed_ctx **out) {
   // TMED_B26 / TMED_B24 are read here, per context (a process may hold contexts of both kinds)
   if (e == hipSuccess && !env_off("TMED_B26")) c->d_b26 = bshare_acquire(0, device, c->d_bcomb16, c->stream);
   c->b24_on = !env_off("TMED_B24");
+  c->a10_on = !env_off("TMED_KS_A10");
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_bcomb, kCombBytesPerKey);
   if (e == hipSuccess) e = hipMalloc((void **)&d_bpub, 32);
   if (e == hipSuccess) e = hipMalloc((void **)&d_bok, 1);
@@ -328,6 +329,13 @@ int tmed_host_unregister(void *p) {
 
 int tmed_b_window_bits(const tmed_ctx *c) { return c && c->d_b26 ? 26 : 16; }
 int tmed_keyset_b_window_bits(const tmed_ctx *c) { return c && c->d_b24 ? 24 : 16; }
+int tmed_keyset_a_window_bits(tmed_ctx *c, uint64_t handle) {
+  if (!c) return -1;
+  std::lock_guard<std::mutex> lk(c->mu);
+  auto it = c->keysets.find(handle);
+  if (it == c->keysets.end()) return -1;
+  return it->second.d_comb10 && c->d_b24 ? 10 : 8;
+}
 
 int tmed_window_stats(tmed_ctx *c, uint32_t lane_hist[65], uint32_t wave_hist[65]) {
   if (!c || !lane_hist || !wave_hist) return TMED_EINVAL;

@@ -253,5 +253,10 @@ class Engine:
         """Radix (bits) of the key-cached throughput path's B windows: 24 or 16 (tmed_keyset_b_window_bits)."""
         return int(lib().tmed_keyset_b_window_bits(self._h))
 
+    def keyset_a_window_bits(self, handle: int) -> int:
+        """Radix (bits) of the -A comb the throughput kernel reads for a key set: 10 or 8
+        (tmed_keyset_a_window_bits; 10 once the set's first throughput batch built it)."""
+        return int(lib().tmed_keyset_a_window_bits(self._h, handle))
+
     def last_kernel_ms(self) -> float:
         return float(lib().tmed_last_kernel_ms(self._h))
