@@ -704,6 +704,7 @@ static int ctx_verify_host_msgs(tmed_ctx *ctx, const tmed_commit_request *reqs, 
 // only key references, signatures, flags and timestamps cross PCIe; they are written
 // straight from the request arrays into the pinned staging area (multi-threaded for
 // large batches).  The caller holds ctx->mu.
+constexpr size_t kDmaMinRun = 256;  // signatures (16 KB)
 static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands,
                        const uint32_t *ix, uint32_t m, uint64_t keyset, const uint8_t *tmpl, int slot,
                        tmed::VoteStage &st) {
@@ -719,7 +720,20 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
     const char *v = getenv("TMED_DIRECT_DMA");
     return !(v && v[0] == '0');
   }();
-  const bool direct = direct_on && st.total >= tmed::kVoteCopyStreamMin;
+  bool direct = direct_on && st.total >= tmed::kVoteCopyStreamMin;
+  // pinned-memory lookups once per request (a registry lookup per run took a global lock per
+  // vote where runs are single votes: Trusting candidates, C3)
+  std::vector<uint8_t> req_pinned;
+  if (direct) {
+    req_pinned.assign(n, 0);
+    bool any = false;
+    for (size_t q = 0; q < n; q++) {
+      const tmed_commit &c = *reqs[q].commit;
+      req_pinned[q] = c.n_sigs && tmed::host_pinned(c.sigs, 64 * c.n_sigs) ? 1 : 0;
+      any = any || req_pinned[q];
+    }
+    direct = any;
+  }
   const unsigned nt = host_threads(m);
   std::vector<std::vector<tmed::VoteStage::Dma>> tdma(direct ? nt : 0u);
   std::atomic<bool> all_direct{direct};
@@ -750,7 +764,8 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
       } else {
         memcpy(st.key + j * 32, r.vals->pubkeys + 32 * (size_t)cd.val_idx, 32 * len);
       }
-      bool dma = direct && tid < tdma.size() && tmed::host_pinned(c.sigs + 64 * i, 64 * len);
+      // runs of at least kDmaMinRun signatures: a DMA command costs ~10 us of the copy engine
+      bool dma = direct && len >= kDmaMinRun && tid < tdma.size() && req_pinned[cd.req];
       if (dma && c.sig_lens)  // short signatures are zero-padded in staging
         for (size_t u = 0; u < len && dma; u++) dma = c.sig_lens[i + u] >= 64;
       if (dma) {
