@@ -916,6 +916,10 @@ __device__ void comb_sign_one(uint32_t sg[16], uint32_t pb[8], const uint32_t se
   sign_one_bm(sg, pb, seed, m, mlen, [&](uint32_t enc[8], const uint32_t s[8]) { comb_base_mult(enc, s, bc); });
 }
 
+#ifndef TMED_SLOT_SHA
+#define TMED_SLOT_SHA 1  // A/B knob: sign-bytes slots hashed from dwordx4 loads (sha512_stream_slot)
+#endif
+constexpr bool kSlotSha = TMED_SLOT_SHA != 0;
 #ifndef TMED_KS_PREP_WAVES
 #define TMED_KS_PREP_WAVES 3  // 168 VGPRs, 27 spilled: keyed prep 0.445 -> 0.426 ms per 2^20 (A/B)
 #endif
@@ -935,7 +939,7 @@ __global__ __launch_bounds__(kThreadsPerBlock, TMED_KS_PREP_WAVES) void verify_k
   const uint8_t *m;
   uint32_t mlen;
   ms.get(i, m, mlen);
-  const bool ok = verify_prep_comb(pw, vin && key_ok[v] != 0, sw, m, mlen, k, s);
+  const bool ok = verify_prep_comb(pw, vin && key_ok[v] != 0, sw, m, mlen, k, s, ms.slots && kSlotSha);
   ge_p3 dummy;
   ge_p3_0(dummy);
   prep_store(prep, stride, slot, k, s, dummy, ok);

@@ -265,4 +265,76 @@ TMED_HD void sha512_stream(uint32_t out[16], const uint32_t p0[8], const uint32_
   }
 }
 
+// SHA-512(P0 || P1 || M) for M at the start of a 16-B aligned sign-bytes slot (kernels.h
+// kVoteSlot = 256 B, readable in full): each 128-B block's message bytes arrive as dwordx4 loads
+// (4 for block 0, 8 for block 1) instead of two dword loads per 8-byte word through MsgReader —
+// the key-cached prep kernel waited on those loads for about half of its wave time (PMC
+// wait_inst_any 0.49).  Bytes past M in the slot are masked exactly as sha512_stream_word does.
+// Messages needing a third block (|M| > 175) take sha512_stream.
+TMED_HD uint64_t sha512_slot_word(uint32_t a, uint32_t b, int32_t nv) {
+  uint64_t v = nv > 0 ? (((uint64_t)bswap32(a) << 32) | bswap32(b)) : 0ull;
+  if (nv < 8) {
+    if (nv > 0) v &= ~(~0ull >> (8 * nv));
+    if (nv >= 0) v |= 0x80ull << (56 - 8 * nv);
+  }
+  return v;
+}
+
+TMED_HD void sha512_stream_slot(uint32_t out[16], const uint32_t p0[8], const uint32_t p1[8], const uint8_t *m,
+                                uint32_t mlen) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t total = 64u + mlen;
+  const uint32_t nblocks = (total + 17u + 127u) >> 7;
+  if (nblocks > 2) {
+    sha512_stream(out, p0, p1, 64, m, mlen);
+    return;
+  }
+  const uint4 *q = reinterpret_cast<const uint4 *>(m);
+  uint64_t st[8];
+  sha512_init(st);
+  {
+    uint4 c[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) c[k] = q[k];  // M[0, 64)
+    uint64_t w[16];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {  // the 64-byte prefix: w[0..3] = P0, w[4..7] = P1
+      const uint64_t a = ((uint64_t)bswap32(p0[2 * t]) << 32) | bswap32(p0[2 * t + 1]);
+      const uint64_t b = ((uint64_t)bswap32(p1[2 * t]) << 32) | bswap32(p1[2 * t + 1]);
+      w[t] = a;
+      w[4 + t] = b;
+    }
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+      const uint4 cc = c[t >> 1];
+      const uint32_t x = (t & 1) ? cc.z : cc.x, y = (t & 1) ? cc.w : cc.y;
+      w[8 + t] = sha512_slot_word(x, y, (int32_t)mlen - 8 * t);
+    }
+    if (nblocks == 1) w[15] = (uint64_t)total * 8u;
+    sha512_compress(st, w);
+  }
+  if (nblocks == 2) {
+    uint4 c[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) c[k] = q[4 + k];  // M[64, 192)
+    uint64_t w[16];
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+      const uint4 cc = c[t >> 1];
+      const uint32_t x = (t & 1) ? cc.z : cc.x, y = (t & 1) ? cc.w : cc.y;
+      w[t] = sha512_slot_word(x, y, (int32_t)mlen - 64 - 8 * t);
+    }
+    w[15] = (uint64_t)total * 8u;
+    sha512_compress(st, w);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    out[2 * i] = bswap32((uint32_t)(st[i] >> 32));
+    out[2 * i + 1] = bswap32((uint32_t)st[i]);
+  }
+#else
+  sha512_stream(out, p0, p1, 64, m, mlen);
+#endif
+}
+
 }  // namespace tmed

@@ -414,11 +414,12 @@ TMED_HD void comb_entry(ge_niels &out, const ge_p3 &base, uint32_t j, int nbits 
 // Key-cached verification, phase 1: k = SHA-512(R||A||M) mod L and the S checks (A is
 // already decoded in the key set; key_ok carries Point.SetBytes' verdict).
 TMED_HD bool verify_prep_comb(const uint32_t pubw[8], bool key_ok, const uint32_t sigw[16], const uint8_t *msg,
-                              uint32_t mlen, uint32_t k[8], uint32_t s[8]) {
+                              uint32_t mlen, uint32_t k[8], uint32_t s[8], bool slot = false) {
   bool ok = key_ok && (sigw[15] & 0xE0000000u) == 0;
   ok = ok && sc_is_canonical(sigw + 8);
   uint32_t h[16];
-  sha512_stream(h, sigw, pubw, 64, msg, mlen);
+  if (slot) sha512_stream_slot(h, sigw, pubw, msg, mlen);  // msg: a 16-B aligned kVoteSlot slot
+  else sha512_stream(h, sigw, pubw, 64, msg, mlen);
   sc_reduce512(k, h);
 #pragma unroll
   for (int w = 0; w < 8; w++) s[w] = ok ? sigw[8 + w] : 0u;
