@@ -1365,6 +1365,26 @@ hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStr
   return hipGetLastError();
 }
 
+// ---- decisions out to pinned host memory (kernels.h launch_copy_out) ----------------------
+__global__ __launch_bounds__(256) void copy_out_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst,
+                                                      uint32_t n16, const uint8_t *__restrict__ src_b,
+                                                      uint8_t *__restrict__ dst_b, uint32_t n) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n16) dst[g] = src[g];
+  const uint32_t t = n16 * 16u + g;  // the tail bytes past the last whole 16-byte chunk
+  if (g < 16u && t < n) dst_b[t] = src_b[t];
+}
+
+hipError_t launch_copy_out(const uint8_t *src, uint8_t *dst_mapped, uint32_t n, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  if (((uintptr_t)src | (uintptr_t)dst_mapped) & 15u) return hipErrorInvalidValue;
+  const uint32_t n16 = n / 16u;
+  const uint32_t threads = n16 > 16u ? n16 : 16u;
+  hipLaunchKernelGGL(copy_out_kernel, dim3((threads + 255) / 256), dim3(256), 0, stream,
+                     reinterpret_cast<const uint4 *>(src), reinterpret_cast<uint4 *>(dst_mapped), n16, src, dst_mapped, n);
+  return hipGetLastError();
+}
+
 // ---- radix-2^10 comb of -A (kernels.h kComb10*) ------------------------------------------
 __global__ __launch_bounds__(64) void comb10_bases_kernel(const uint8_t *__restrict__ pubs, uint32_t n,
                                                          int32_t *__restrict__ bases) {

@@ -260,7 +260,21 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   slow.lap("verify launches");
   if (e == hipSuccess && st.timed) e = hipEventRecord(vs.ev1, s);
   if (e == hipSuccess) e = scratch_release(c, s);
-  if (e == hipSuccess && !st.zc) e = hipMemcpyAsync(vs.h_out.p, vs.d_out.p, m, hipMemcpyDeviceToHost, s);
+  // TMED_OUT_KERNEL=1 (experimental, off by default): the decisions of a large batch go out by a
+  // small kernel writing the pinned result buffer through its device mapping instead of a
+  // device-to-host copy command (the runtime blocked the host ~6 ms inside that call two or three
+  // times per C4 run, profiles/r03/c4_direct/).
+  static const bool out_kernel = [] {
+    const char *v = getenv("TMED_OUT_KERNEL");
+    return v && v[0] == '1';
+  }();
+  if (e == hipSuccess && !st.zc) {
+    void *hout = nullptr;
+    if (out_kernel && st.total >= kVoteCopyStreamMin && hipHostGetDevicePointer(&hout, vs.h_out.p, 0) == hipSuccess)
+      e = launch_copy_out((const uint8_t *)vs.d_out.p, (uint8_t *)hout, m, s);
+    else
+      e = hipMemcpyAsync(vs.h_out.p, vs.d_out.p, m, hipMemcpyDeviceToHost, s);
+  }
   if (e == hipSuccess) e = hipEventRecord(vs.done, s);
   slow.lap("copy-out");
   return map_err(e);
