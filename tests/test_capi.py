@@ -39,3 +39,22 @@ def test_strerror_and_no_fallback_without_gpu():
     assert lib().tmed_device_count() == 0
     with pytest.raises(TmedError):
         Engine(0)
+
+
+def test_pinned_memory_entry_points_reject_bad_arguments():
+    """tmed_host_alloc / _free / _register / _unregister (the pinned commit arenas the seam DMAs
+    signatures from): argument errors come back as TMED_EINVAL without touching the runtime, and a
+    pointer the registry never saw cannot be freed or unregistered."""
+    import ctypes
+    from tmed import lib
+    l = lib()
+    p = ctypes.c_void_p()
+    assert l.tmed_host_alloc(0, ctypes.byref(p)) == -1
+    assert l.tmed_host_alloc(16, None) == -1
+    assert l.tmed_host_free(None) == 0          # free(NULL) is a no-op
+    buf = ctypes.create_string_buffer(64)
+    assert l.tmed_host_free(ctypes.addressof(buf)) == -1
+    assert l.tmed_host_unregister(None) == -1
+    assert l.tmed_host_unregister(ctypes.addressof(buf)) == -1
+    assert l.tmed_host_register(None, 64) == -1
+    assert l.tmed_host_register(ctypes.addressof(buf), 0) == -1
