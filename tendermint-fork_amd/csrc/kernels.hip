@@ -567,7 +567,12 @@ __global__ __launch_bounds__(kThreadsPerBlock) void verify_finish_kernel(
 hipError_t launch_finish(const int4 *fin, int4 *pre, const uint8_t *sig, uint8_t *out, uint32_t fin_base, uint32_t m,
                          hipStream_t stream, const uint32_t *perm = nullptr) {
   if (m == 0) return hipSuccess;
-  uint32_t G = m / 65536;
+  static const uint32_t lanes = [] {  // A/B knob: lanes the finish spreads a batch over
+    const char *v = getenv("TMED_FIN_LANES");
+    const long x = v ? atol(v) : 65536;
+    return (uint32_t)(x >= 1024 && x <= (1 << 22) ? x : 65536);
+  }();
+  uint32_t G = m / lanes;
   if (G < 1) G = 1;
   if (G > kFinGroupMax) G = kFinGroupMax;
   const uint32_t L = (m + G - 1) / G;
