@@ -22,12 +22,19 @@ Extra JSON fields:
                 (anchor_openssl), an independent implementation, on the same sample.
   c2_keyset_variant    the second C2 variant: 10k reused keys, key cache on.
   c1_verifycommit_p50  the metric's second half: VerifyCommit p50 latency @175 validators
-                through the seam, generic and key-cached, with its 1-thread CPU baseline.
+                through the seam with the key-set cache as the drop-in uses it (steady state: cache
+                hit), the first call after a set change, the cache off, an explicit handle; 1-thread
+                CPU baseline beside it.
   c5_adversarial       C5: the C2 batch with 1% invalid signatures of every failure class
                 (tmed.workload.c5_mix), rate and mismatches against the port's bits.
-  c4_shard             C4 (blocksync, 12,500 blocks x 175 validators per rank = 100k blocks over 8 GPUs) through the commit
-                seam: commits/s and signatures/s, outcome mismatches against the oracle, and the
-                per-rank host phase split (plan+staging / enqueue+device wait / replay).
+  c4_shard             C4 (blocksync, 12,500 blocks x 10,000 validators per GPU = 100k blocks over 8 GPUs) through
+                the commit seam, on EVERY rank: contiguous block ranges per rank, the int64 tally
+                all-reduce and the per-block decision bitmap all-gather (RCCL at N > 1), MAX of the
+                ranks' seam times; verifies/s, outcome mismatches against known answers, the
+                per-rank host phase split and the window marshalling beside it.
+  c3_light_client      C3 (10k headers x 175 validators, the set changing one key per height) through the
+                seam with the key-set cache: headers/s direct (Trusting + Light per header) and by
+                bisection (verifySkipping), Got/Needed checked, marshalling beside it (rank 0, N = 1).
   zip215_batch_mode    the OPT-IN ZIP-215 rule (tmed_verify_batch_zip215): C2 all valid (one
                 randomized batch equation per 2^20 chunk) and the C5 mix (bisection + exact
                 single checks), each against the port's ZIP-215 bits, with the call's statistics.
@@ -114,6 +121,8 @@ def parse():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 one-GPU-shard blocksync leg")
     ap.add_argument("--no-zip215", action="store_true", help="skip the opt-in ZIP-215 batch-mode leg")
     ap.add_argument("--c4-blocks", type=int, default=12_500, help="C4 shard: blocks per GPU (100k blocks / 8 GPUs)")
+    ap.add_argument("--no-c3", action="store_true", help="skip the C3 light-client leg")
+    ap.add_argument("--c3-headers", type=int, default=10_000)
     ap.add_argument("--mix", choices=["c2", "c5"], default="c2",
                     help="c5: 1%% of the batch replaced by edge-case / invalid tuples (BASELINE C5)")
     return ap.parse_args()
@@ -240,6 +249,11 @@ def main():
     total = n_all * args.steps
     value = total / elapsed
 
+    # ---- C4 on every rank (weak scaling: c4_blocks per GPU, contiguous heights, RCCL tallies)
+    c4 = None
+    if not args.no_c4:
+        c4 = c4_shard(eng, coll, args.c4_blocks, rank, world)
+
     result = None
     if rank == 0:
         wstats = window_summary(eng) if MAIN_VARIANT != 5 else None
@@ -298,9 +312,9 @@ def main():
         zip_leg = None
         if not args.no_zip215 and world == 1 and args.mix == "c2":
             zip_leg = zip215_leg(eng, dev, torch_stream, d_pub, d_sig, d_msg, d_off, msgs, offs, n, args.steps // 10 + 1)
-        c4 = None
-        if not args.no_c4 and world == 1:
-            c4 = c4_shard(eng, dev, args.c4_blocks)
+        c3 = None
+        if not args.no_c3 and world == 1:
+            c3 = c3_leg(eng, args.c3_headers)
         result = {
             "metric": "ed25519 verifies/sec at %d/8 MI355X" % world,
             "value": round(value, 1),
@@ -329,6 +343,7 @@ def main():
             "c5": c5,
             "zip215_batch_mode": zip_leg,
             "c4_shard": c4,
+            "c3_light_client": c3,
             "setup_s": round(t_gen, 2),
         }
         print(json.dumps(result), flush=True)
@@ -492,16 +507,29 @@ def zip215_leg(eng, dev, torch_stream, d_pub, d_sig, d_msg, d_off, msgs, offs, n
     return res
 
 
-def c4_shard(eng, dev, blocks):
-    """One GPU's share of BASELINE C4 (100k blocks / 8 GPUs): `blocks` blocks x 10,000 validators,
-    VerifyCommitLight per block through the pipelined blocksync seam (tmed_blocksync_verify),
-    key-cached; known-answer bad signatures every 97 blocks (before and after the 2/3 crossing),
-    every block's outcome checked (bench_commits.c4); verifies/s and the seam's host phases."""
+def c4_shard(eng, coll, blocks, rank, world):
+    """BASELINE C4 (100k blocks / 8 GPUs): `blocks` blocks x 10,000 validators PER RANK, contiguous
+    heights, VerifyCommitLight per block through the pipelined blocksync seam (tmed_blocksync_verify)
+    with the set passed WITHOUT a key-set handle (the key-set cache builds its keys after the first,
+    untimed window); known-answer bad signatures every 97 blocks, every block's outcome checked
+    (bench_commits.c4).  At N ranks: int64 tallies all-reduced, the decision bitmaps all-gathered
+    (RCCL over xGMI; gloo with TMED_DIST_BACKEND=gloo), value = all verifies / the slowest rank's seam
+    time.  Called on every rank."""
     sys.path.insert(0, ROOT)
     import bench_commits
-    r = bench_commits.c4(eng, blocks, 10_000, 0, 1, dev, 1000, 128, corrupt_every=97)
-    r["metric"] = "blocksync replay verifies/s, one GPU's shard of C4 (VerifyCommitLight per block)"
+    r = bench_commits.c4(eng, blocks * world, 10_000, rank, world, coll, 1000, 128, corrupt_every=97)
+    r["metric"] = ("blocksync replay verifies/s, C4 sharded over %d GPU(s) (VerifyCommitLight per block)" % world
+                   if world > 1 else "blocksync replay verifies/s, one GPU's shard of C4 (VerifyCommitLight per block)")
+    if os.environ.get("TMED_DIST_BACKEND") == "gloo" and world > 1:
+        r["rehearsal"] = "gloo collectives, ranks sharing the GPUs present: not a scaling measurement"
     return r
+
+
+def c3_leg(eng, headers):
+    """BASELINE C3 through the seam with the key-set cache (bench_commits.c3, policy "cache")."""
+    sys.path.insert(0, ROOT)
+    import bench_commits
+    return bench_commits.c3(eng, headers, 2, "cache", runs=5, bisect_gap=150)
 
 
 def c1_latency(eng, reps, cpu):

@@ -148,6 +148,14 @@ int tmed_kernel_times(tmed_ctx *ctx, float ms[3], int launches[3]);
  */
 int tmed_keyset_load(tmed_ctx *ctx, const uint8_t *pubkeys, size_t n, uint64_t *handle);
 int tmed_keyset_free(tmed_ctx *ctx, uint64_t handle);
+/*
+ * Append n keys to a loaded key set (its comb tables are built before the call returns).  The keys
+ * already in the set keep their indexes; the new ones get first_index .. first_index + n - 1
+ * (*first_index = the set's size before the call; may be NULL).  One pooled set can then serve
+ * validator sets that change by a few keys per height (tmed_valset.keyset_index), as the light
+ * client's do (light/verifier.go:58,73-76).
+ */
+int tmed_keyset_extend(tmed_ctx *ctx, uint64_t handle, const uint8_t *pubkeys, size_t n, uint32_t *first_index);
 int tmed_verify_batch_keyset(tmed_ctx *ctx, uint64_t handle, const uint32_t *val_idx, const uint8_t *sigs,
                              const uint32_t *sig_lens, const uint8_t *msgs, const uint32_t *msg_off, size_t n,
                              uint8_t *out_valid);
@@ -173,7 +181,9 @@ int tmed_verify_batch_zip215(tmed_ctx *ctx, const uint8_t *pubkeys, const uint8_
 int tmed_verify_batch_zip215_device(tmed_ctx *ctx, const uint8_t *d_pubkeys, const uint8_t *d_sigs,
                                     const uint8_t *d_msgs, const uint32_t *d_msg_off, size_t n, uint8_t *d_out_valid,
                                     void *stream);
-/* Tests only: fix the batch weights' 32-byte seed for this thread's calls (NULL: getrandom again). */
+/* Tests only: fix the batch weights' 32-byte seed for this thread's calls (NULL: getrandom again).
+ * TMED_EINVAL unless the process environment has TMED_ZIP215_TEST_SEED=1 (known weights would let a
+ * forger build invalid signatures whose errors cancel in the batch equation). */
 int tmed_zip215_set_seed(const uint8_t *seed32);
 /* This thread's last ZIP-215 call: chunks, batch equations evaluated, groups decided signature by
  * signature, signatures decided singly. */
@@ -240,9 +250,13 @@ typedef struct {
                                Every validator address must be 20 bytes (Validator.ValidateBasic,
                                types/validator.go:49): a caller holding another length takes the Go path */
   int64_t total_power;      /* vals.TotalVotingPower() (its panics stay in Go, :298-321) */
-  uint64_t keyset;          /* 0, or a tmed_keyset_load handle holding these pubkeys (key-cached path) */
+  uint64_t keyset;          /* 0 (the context's key-set cache decides, see tmed_keycache_config), or a
+                               tmed_keyset_load handle holding these pubkeys (key-cached path) */
   const uint32_t *keyset_index; /* NULL: validator i is key i of the key set; else its index there
                                    (one key set can then serve many validator sets, e.g. the light client) */
+  const uint8_t *set_hash;  /* NULL, or ValidatorSet.Hash() of this set (32 bytes, types/validator_set.go:
+                               347-353): the key-set cache's key for it (else a digest of the key bytes).
+                               Either way a cached set is compared key by key before it is used. */
 } tmed_valset;
 
 /* Commit + CommitSigs (types/block.go:575-634, 737-752). */
@@ -277,6 +291,46 @@ typedef struct {
   const tmed_commit *commit;
   int64_t trust_num, trust_den;  /* LIGHT_TRUSTING: tmmath.Fraction (libs/math/fraction.go:11-18) */
 } tmed_commit_request;
+
+/* ------------------------------------------------- key-set cache of the commit seam (f2) */
+
+/*
+ * tmed_verify_commits / tmed_blocksync_verify (and their _multi forms) give every validator set
+ * that carries no handle (tmed_valset.keyset == 0) to the context's key-set cache, so the
+ * reference's callers reach the key-cached kernels without managing handles: LastCommit against
+ * LastValidators every block (state/validation.go:93-96), the blocksync window against
+ * state.Validators (blockchain/v0/reactor.go:366-367), the light client's trusted / untrusted sets
+ * (light/verifier.go:58,73-76).  The cache holds ONE pooled key set per context (a key held by many
+ * sets is built once) and an entry per validator set, keyed by set_hash when given, else by a digest
+ * of the ordered keys, and compared key by key on every hit.  On a miss: a set whose keys are all in
+ * the pool is keyed at once; a call whose own signatures pay for building the missing keys (>= 2048
+ * per key: a blocksync window, a light-client batch) builds them first and is keyed; otherwise the
+ * call runs the generic kernels and the missing keys are built right after it, so the next call
+ * against that set is keyed (C1: the first VerifyCommit after a set change is generic, the rest
+ * are cache hits).  Decisions are identical either way.
+ *   enabled: 1 on, 0 off (sets without a handle stay generic), -1 unchanged (default on; env
+ *            TMED_KEYCACHE=0 turns it off at tmed_init);
+ *   budget_bytes: 0 unchanged, else the pool's HBM budget (default 64 GiB, env TMED_KEYCACHE_GB;
+ *            ~2.2 MB per key with the radix-2^10 comb): a set that does not fit empties the pool
+ *            when no call is using it, else stays generic.
+ */
+int tmed_keycache_config(tmed_ctx *ctx, int enabled, size_t budget_bytes);
+typedef struct {
+  uint64_t enabled, budget_bytes;
+  uint64_t lookups, hits;                 /* validator-set lookups by seam calls; hits on a cached entry */
+  uint64_t keyed_sets, generic_sets;      /* lookups resolved to the key-cached / generic kernels */
+  uint64_t keyed_sigs, generic_sigs;      /* signatures of the requests resolved each way */
+  uint64_t keys_appended, keys_deferred;  /* keys built into the pool; of those, built after a generic call */
+  uint64_t pool_resets, sets_evicted;     /* pool emptied to fit a set; entries dropped (LRU bound) */
+  uint64_t pool_keys, pool_capacity_keys, pool_bytes, pool_a_window_bits;
+  uint64_t sets_cached, pending_keys;
+} tmed_keycache_counters;
+int tmed_keycache_stats(tmed_ctx *ctx, tmed_keycache_counters *out);
+/* Drop every cached set and the pool (TMED_EINVAL while a call is using it). */
+int tmed_keycache_flush(tmed_ctx *ctx);
+/* Build a set's missing keys now (e.g. at a validator-set change, before its first commit), so
+ * even its first call is keyed.  TMED_ENOMEM when it does not fit the budget. */
+int tmed_keycache_warm(tmed_ctx *ctx, const tmed_valset *vals);
 
 /* Outcome codes: the reference's return value, to be formatted by the caller exactly as Go does. */
 #define TMED_COMMIT_OK 0

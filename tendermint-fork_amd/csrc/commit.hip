@@ -27,6 +27,7 @@
 #include <thread>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/tmed25519.h"
@@ -879,6 +880,129 @@ static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, 
 static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t nb, size_t bsz, uint64_t keyset,
                          tmed_commit_result *out);
 
+// ---- key-set cache (keycache.h / keycache.hip) -------------------------------
+// The validator sets of one seam call that carry no handle, resolved through the context's cache:
+// the call then runs on copies of its requests whose sets point into the cache's pool (keyset =
+// the pool, keyset_index = the set's entry).  The call pins the pool from its first lookup until
+// this object dies, after the call's last batch was collected; then the keys that generic sets of
+// the call queued are built (asynchronously, in stream order: the next call finds them).
+struct KcCall {
+  tmed_ctx *c = nullptr;
+  std::vector<tmed_commit_request> reqs;
+  std::deque<tmed_valset> vals;  // stable addresses for reqs[q].vals
+  std::vector<std::shared_ptr<const tmed::KcSet>> holds;
+  ~KcCall() {
+    if (!c) return;
+    std::lock_guard<std::mutex> lk(c->mu);
+    tmed::keycache_unpin(c);
+    (void)tmed::keycache_drain(c);  // a failed build leaves those sets generic
+  }
+};
+
+static const tmed_commit_request *keycache_resolve(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
+                                                   KcCall &kc) {
+  if (!ctx->kc_on || n == 0 || !reqs) return reqs;
+  struct SetRef {
+    const uint8_t *pubs;
+    size_t n;
+    const uint8_t *hash;
+    size_t sigs = 0;
+    tmed::KcKey key;
+    std::shared_ptr<const tmed::KcSet> hold;
+    bool hit = false;
+    uint64_t handle = 0;
+  };
+  std::vector<SetRef> sets;
+  std::vector<int32_t> set_of(n, -1);
+  std::unordered_map<const uint8_t *, std::vector<int32_t>> by_pubs;  // distinct (keys, size, set_hash)
+  size_t keys = 0;
+  for (size_t q = 0; q < n; q++) {
+    const tmed_commit_request &r = reqs[q];
+    if (!r.vals || r.vals->keyset || r.vals->n == 0 || !r.vals->pubkeys || !r.commit) continue;
+    const tmed_valset &v = *r.vals;
+    std::vector<int32_t> &cand = by_pubs[v.pubkeys];
+    int32_t s = -1;
+    for (int32_t k : cand)
+      if (sets[k].n == v.n && sets[k].hash == v.set_hash) { s = k; break; }
+    if (s < 0) {
+      s = (int32_t)sets.size();
+      cand.push_back(s);
+      SetRef sr;
+      sr.pubs = v.pubkeys;
+      sr.n = v.n;
+      sr.hash = v.set_hash;
+      sets.push_back(sr);
+      keys += v.n;
+    }
+    sets[s].sigs += r.commit->n_sigs;
+    set_of[q] = s;
+  }
+  if (sets.empty()) return reqs;
+  const unsigned nt = host_threads(keys);
+  parallel_ranges(sets.size(), nt, [&](size_t lo, size_t hi, unsigned) {
+    for (size_t s = lo; s < hi; s++) sets[s].key = tmed::kc_key(sets[s].pubs, sets[s].n, sets[s].hash);
+  });
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    kc.c = ctx;
+    tmed::keycache_pin(ctx);
+    for (SetRef &sr : sets) sr.hold = tmed::keycache_find(ctx, sr.key);
+  }
+  // cached entries are compared with the sets' keys outside the lock (a light-client batch holds
+  // ~10k sets); the pinned pool keeps their indexes valid
+  parallel_ranges(sets.size(), nt, [&](size_t lo, size_t hi, unsigned) {
+    for (size_t s = lo; s < hi; s++)
+      sets[s].hit = sets[s].hold && tmed::kc_same_keys(*sets[s].hold, sets[s].pubs, sets[s].n);
+  });
+  bool any_keyed = false;
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    for (SetRef &sr : sets)
+      if (sr.hit) {
+        tmed::keycache_hit(ctx, sr.sigs);
+        sr.handle = tmed::keycache_pool_handle(ctx);
+        any_keyed = true;
+      }
+    // the call's signatures against every key it lacks: a window / batch that pays for them all
+    // builds them before its kernels (each set alone may carry too few signatures)
+    size_t call_sigs = 0, call_missing = 0;
+    std::unordered_set<tmed::Pub32, tmed::Pub32Hash> seen;
+    for (SetRef &sr : sets)
+      if (!sr.hit) {
+        call_sigs += sr.sigs;
+        call_missing += tmed::keycache_missing(ctx, sr.pubs, sr.n, &seen);
+      }
+    const bool build_all = call_missing && call_sigs >= tmed::kKcAmortizeSigsPerKey * call_missing;
+    for (SetRef &sr : sets) {
+      if (sr.hit) continue;
+      sr.hold.reset();
+      if (tmed::keycache_lookup(ctx, sr.pubs, sr.n, sr.key, sr.sigs, /*may_reset=*/!any_keyed, &sr.handle, sr.hold,
+                                build_all)) {
+        sr.hit = true;
+        any_keyed = true;
+      }
+    }
+  }
+  if (!any_keyed) return reqs;
+  kc.reqs.assign(reqs, reqs + n);
+  std::unordered_map<const tmed_valset *, tmed_valset *> copy_of;
+  for (size_t q = 0; q < n; q++) {
+    if (set_of[q] < 0 || !sets[set_of[q]].hit) continue;
+    const SetRef &sr = sets[set_of[q]];
+    tmed_valset *&cp = copy_of[reqs[q].vals];
+    if (!cp) {
+      kc.vals.push_back(*reqs[q].vals);
+      cp = &kc.vals.back();
+      cp->keyset = sr.handle;
+      cp->keyset_index = sr.hold->idx.data();
+    }
+    kc.reqs[q].vals = cp;
+  }
+  for (SetRef &sr : sets)
+    if (sr.hit) kc.holds.push_back(std::move(sr.hold));
+  return kc.reqs.data();
+}
+
 // A large call whose sets share one key set (a light-client or evidence backlog) goes through
 // the two-slot pipeline in batches of ~2^19 signatures (env TMED_PIPE_SIGS), so the host
 // planning, staging and replay of one batch overlap the device work of the next.
@@ -890,6 +1014,8 @@ static size_t pipe_batch_sigs() {
 extern "C" int tmed_verify_commits(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
                                    tmed_commit_result *out) {
   if (!ctx) return TMED_EINVAL;
+  KcCall kc;
+  reqs = keycache_resolve(ctx, reqs, n, kc);
   const size_t kPipeBatchSigs = pipe_batch_sigs();
   if (n > 1 && reqs && out) {
     bool ok = true;
@@ -933,24 +1059,15 @@ struct BsBatch {
 // With the signatures DMA'd from pinned caller memory the host's share per batch is ~1.5 ms
 // against ~2.2 ms of kernels, and a third slot keeps the kernel stream busy (C4 280-307 against
 // 258-282 M/s, profiles/r03/c4_direct/).  So the depth follows the first batch: three slots
-// when its signatures went direct (VoteStage::sig_direct), else two.  TMED_PIPE_SLOTS=2 / 3
-// forces either.  (A ramp of small first / last batches did not pay: profiles/r03/c4_pipe/.)
+// when its signatures went direct (VoteStage::sig_direct), else two.  (A ramp of small first / last
+// batches did not pay: profiles/r03/c4_pipe/.)
 constexpr int kPipeSlots = 3;
 static_assert(kPipeSlots <= (int)(sizeof(((tmed_ctx *)nullptr)->vslot) / sizeof(tmed::VoteSlot)),
               "one context vote slot per pipeline slot");
-static int pipe_slots_env() {  // 0: follow the first batch
-  static const int n = [] {
-    const char *v = getenv("TMED_PIPE_SLOTS");
-    return v && v[0] == '3' ? 3 : (v && v[0] == '2' ? 2 : 0);
-  }();
-  return n;
-}
-
 static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t nb, size_t bsz, uint64_t keyset,
                          tmed_commit_result *out) {
   BsBatch slots[kPipeSlots];
-  const int forced = pipe_slots_env();
-  int ns = forced ? forced : 2;  // raised to 3 after batch 0 when its signatures went direct
+  int ns = 2;  // raised to 3 after batch 0 when its signatures went direct
   int rc = TMED_OK;
   // tmed_seam_phase_us for a pipelined call: host plan + templates + staging, host time blocked on
   // the device (enqueueing the copies and kernels, votes_collect), host replay — the first and
@@ -1009,7 +1126,7 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
         ph[0] += us(tp, te);
         if (rc == TMED_OK) rc = tmed::votes_enqueue(ctx, b.st);
         b.enq = clock::now();
-        if (idx == 0 && !forced && b.st.sig_direct) ns = 3;
+        if (idx == 0 && b.st.sig_direct) ns = 3;
         clk.lap("enqueue");
         ph[1] += us(te, clock::now());  // queueing copies / launches can block behind a busy device
         b.device = rc == TMED_OK;
@@ -1036,7 +1153,10 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
   }
   for (int k = 0; k < ns; k++)  // oldest first
     if (rc == TMED_OK) rc = finish(slots[(idx + k) % ns]);
-  if (rc != TMED_OK) (void)hipStreamSynchronize(ctx->stream);
+  if (rc != TMED_OK) {  // nothing of this call may still read the caller's (pinned) buffers
+    (void)hipStreamSynchronize(ctx->copy_stream);
+    (void)hipStreamSynchronize(ctx->stream);
+  }
   for (int k = 0; k < 3; k++) g_seam_us[k] = ph[k];
   return rc;
 }
@@ -1060,7 +1180,9 @@ extern "C" int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window 
     r.commit = &w->commits[h];
     if (check_request(r) != TMED_OK) return TMED_EINVAL;
   }
-  return run_pipelined(ctx, reqs.data(), nb, batch_blocks ? batch_blocks : 128, w->vals->keyset, out);
+  KcCall kc;  // one set for the whole window
+  const tmed_commit_request *rq = keycache_resolve(ctx, reqs.data(), nb, kc);
+  return run_pipelined(ctx, rq, nb, batch_blocks ? batch_blocks : 128, rq[0].vals->keyset, out);
 }
 
 // ---- several GPUs in one process (§8e): contiguous shards balanced by signature count ----

@@ -8,6 +8,7 @@
 
 #include "../../include/tmed25519.h"
 #include "kernels.h"
+#include "keycache.h"
 
 struct tmed_ctx;
 
@@ -59,20 +60,45 @@ inline int map_err(hipError_t e) {
   return TMED_EHIP;
 }
 
-// A validator set's key material resident in HBM.
+// A validator set's key material resident in HBM.  Keys are appended
+// (tmed_keyset_extend, the key-set cache's pool): the buffers hold `cap` keys, keys [0, n) are
+// built, and the index of a key never changes.
 struct Keyset {
-  size_t n = 0;
-  uint8_t *d_pub = nullptr;   // n x 32 raw encodings (hashed into k)
-  uint8_t *d_ok = nullptr;    // n: Point.SetBytes accepted the key
-  int4 *d_comb = nullptr;     // n x kCombBytesPerKey: signed radix-256 comb of -A
-  // n x kComb10BytesPerKey: radix-2^10 comb of -A for the throughput kernel, built at the key
-  // set's first throughput batch (keyset.hip keyset_verify; null: not built / TMED_KS_A10=0 /
-  // no memory -> the radix-256 comb)
-  mutable int4 *d_comb10 = nullptr;
-  mutable bool comb10_tried = false;
+  size_t n = 0, cap = 0;
+  uint8_t *d_pub = nullptr;   // cap x 32 raw encodings (hashed into k)
+  uint8_t *d_ok = nullptr;    // cap: Point.SetBytes accepted the key
+  int4 *d_comb = nullptr;     // cap x kCombBytesPerKey: signed radix-256 comb of -A
+  // cap x kComb10BytesPerKey: radix-2^10 comb of -A for the throughput kernel, keys [0, comb10_n)
+  // built (at the set's first throughput batch and for keys appended after it: keyset.hip
+  // comb10_extend; null / comb10_failed: TMED_KS_A10=0 or no memory -> the radix-256 comb)
+  int4 *d_comb10 = nullptr;
+  size_t comb10_n = 0;
+  bool comb10_failed = false;
+  bool pooled = false;  // the context's key-set cache pool: not reachable through the public handles
 };
 
 int build_comb(tmed_ctx *c, const uint8_t *d_pubs, size_t n, int negate, uint8_t *d_ok, int4 *d_comb);
+// Append m keys (host pointer) to k on stream s: grows the buffers when needed (a copy of the built
+// keys and a synchronisation of s), uploads the keys through the context's pinned key staging and
+// queues their radix-256 combs; nothing waits for the build (later work on s is ordered behind it).
+// TMED_EINVAL past max_cap keys.
+int keyset_append(tmed_ctx *c, Keyset &k, const uint8_t *pubkeys, size_t m, hipStream_t s, size_t max_cap);
+// Device bytes one key of a key set can take (radix-256 comb + radix-2^10 comb + encoding + flag).
+size_t keyset_bytes_per_key(const tmed_ctx *c);
+// The public key set of `handle` (nullptr for unknown and pooled handles).
+Keyset *find_keyset(tmed_ctx *c, uint64_t handle);
+// The commit seam's key-set cache (keycache.hip, keycache.h); every call below holds ctx->mu.
+struct KeyCacheDev;
+void keycache_destroy(tmed_ctx *c);
+void keycache_pin(tmed_ctx *c);    // a seam call resolving sets: no pool reset until it unpins
+void keycache_unpin(tmed_ctx *c);
+uint64_t keycache_pool_handle(const tmed_ctx *c);  // 0 before the first key is built
+std::shared_ptr<const KcSet> keycache_find(tmed_ctx *c, const KcKey &key);  // KeyCache::find
+void keycache_hit(tmed_ctx *c, size_t sigs);                               // KeyCache::hit
+bool keycache_lookup(tmed_ctx *c, const uint8_t *pubs, size_t n, const KcKey &key, size_t sigs, bool may_reset,
+                     uint64_t *handle, std::shared_ptr<const KcSet> &hold, bool force_build = false);
+int keycache_drain(tmed_ctx *c);  // build the keys queued behind generic calls (asynchronously)
+size_t keycache_missing(tmed_ctx *c, const uint8_t *pubs, size_t n, std::unordered_set<Pub32, Pub32Hash> *seen);
 
 // Commit-seam device path (f1): stage votes (key refs, signatures, per-commit templates,
 // template index / flag / timestamp per vote), assemble sign-bytes on the device, verify
@@ -93,7 +119,7 @@ int verify_votes_device(tmed_ctx *c, uint64_t keyset, const uint8_t *keys, const
 // the device copies batch b in and runs batch b-1.  The caller holds ctx->mu across stage..collect.
 struct VoteStage {
   int slot = 0;
-  const Keyset *ks = nullptr;
+  Keyset *ks = nullptr;
   uint32_t m = 0;
   size_t n_tmpl = 0, total = 0;
   size_t o_key = 0, o_sig = 0, o_tmpl = 0, o_tidx = 0, o_flag = 0, o_sec = 0, o_nan = 0;
@@ -186,6 +212,12 @@ struct tmed_ctx {
   tmed::DevBuf d_zip;     // ZIP-215 batch mode scratch (zip215.hip zip_bufs: points, digits, sort, buckets)
   std::unordered_map<uint64_t, tmed::Keyset> keysets;
   uint64_t next_keyset = 1;
+  tmed::KeyCacheDev *kc = nullptr;  // key-set cache of the commit seam (keycache.hip), created at first use
+  bool kc_on = true;                // TMED_KEYCACHE at tmed_init / tmed_keycache_config
+  size_t kc_budget = (size_t)64 << 30;  // its pool's HBM budget
+  tmed::DevBuf d_kbases;            // comb-base scratch of keyset_append (ordered on the context stream)
+  tmed::HostBuf h_kup;              // pinned staging of keys keyset_append uploads
+  hipEvent_t kup_ev = nullptr;      // the last upload from h_kup (reused after it completes)
   // The verify scratch (slab, prep hand-off, finish buffers) is shared by every call on the
   // context, but the device-pointer entry points run on the CALLER's stream: each user of
   // the scratch first makes its stream wait for the previous user (scratch_ev, whatever its

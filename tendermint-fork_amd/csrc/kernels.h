@@ -179,9 +179,6 @@ hipError_t launch_verify_glat(const uint8_t *pub, const uint8_t *sig, const uint
 // messages that way (off = lengths).
 constexpr uint32_t kVoteTmplBytes = 256;
 constexpr uint32_t kVoteSlot = 256;
-// n bytes from device memory to pinned host memory (its device-mapped pointer) by a kernel on
-// `stream`: the decisions of a large seam batch without a device-to-host copy command.
-hipError_t launch_copy_out(const uint8_t *src, uint8_t *dst_mapped, uint32_t n, hipStream_t stream);
 hipError_t launch_assemble_votes(const uint8_t *tmpl, const uint32_t *tmpl_idx, const uint8_t *flags,
                                  const int64_t *ts_sec, const int32_t *ts_nanos, uint32_t n, uint8_t *out,
                                  uint32_t *out_len, hipStream_t stream);

@@ -567,12 +567,8 @@ __global__ __launch_bounds__(kThreadsPerBlock) void verify_finish_kernel(
 hipError_t launch_finish(const int4 *fin, int4 *pre, const uint8_t *sig, uint8_t *out, uint32_t fin_base, uint32_t m,
                          hipStream_t stream, const uint32_t *perm = nullptr) {
   if (m == 0) return hipSuccess;
-  static const uint32_t lanes = [] {  // A/B knob: lanes the finish spreads a batch over
-    const char *v = getenv("TMED_FIN_LANES");
-    const long x = v ? atol(v) : 65536;
-    return (uint32_t)(x >= 1024 && x <= (1 << 22) ? x : 65536);
-  }();
-  uint32_t G = m / lanes;
+  constexpr uint32_t kLanes = 65536;  // one inversion per lane and group; 65,536 lanes fill every SIMD
+  uint32_t G = m / kLanes;
   if (G < 1) G = 1;
   if (G > kFinGroupMax) G = kFinGroupMax;
   const uint32_t L = (m + G - 1) / G;
@@ -921,10 +917,6 @@ __device__ void comb_sign_one(uint32_t sg[16], uint32_t pb[8], const uint32_t se
   sign_one_bm(sg, pb, seed, m, mlen, [&](uint32_t enc[8], const uint32_t s[8]) { comb_base_mult(enc, s, bc); });
 }
 
-#ifndef TMED_SLOT_SHA
-#define TMED_SLOT_SHA 1  // A/B knob: sign-bytes slots hashed from dwordx4 loads (sha512_stream_slot)
-#endif
-constexpr bool kSlotSha = TMED_SLOT_SHA != 0;
 #ifndef TMED_KS_PREP_WAVES
 #define TMED_KS_PREP_WAVES 3  // 168 VGPRs, 27 spilled: keyed prep 0.445 -> 0.426 ms per 2^20 (A/B)
 #endif
@@ -944,7 +936,7 @@ __global__ __launch_bounds__(kThreadsPerBlock, TMED_KS_PREP_WAVES) void verify_k
   const uint8_t *m;
   uint32_t mlen;
   ms.get(i, m, mlen);
-  const bool ok = verify_prep_comb(pw, vin && key_ok[v] != 0, sw, m, mlen, k, s, ms.slots && kSlotSha);
+  const bool ok = verify_prep_comb(pw, vin && key_ok[v] != 0, sw, m, mlen, k, s, ms.slots);  // slots: hashed from dwordx4 loads (sha512_stream_slot)
   ge_p3 dummy;
   ge_p3_0(dummy);
   prep_store(prep, stride, slot, k, s, dummy, ok);
@@ -1370,25 +1362,6 @@ hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStr
   return hipGetLastError();
 }
 
-// ---- decisions out to pinned host memory (kernels.h launch_copy_out) ----------------------
-__global__ __launch_bounds__(256) void copy_out_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst,
-                                                      uint32_t n16, const uint8_t *__restrict__ src_b,
-                                                      uint8_t *__restrict__ dst_b, uint32_t n) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < n16) dst[g] = src[g];
-  const uint32_t t = n16 * 16u + g;  // the tail bytes past the last whole 16-byte chunk
-  if (g < 16u && t < n) dst_b[t] = src_b[t];
-}
-
-hipError_t launch_copy_out(const uint8_t *src, uint8_t *dst_mapped, uint32_t n, hipStream_t stream) {
-  if (n == 0) return hipSuccess;
-  if (((uintptr_t)src | (uintptr_t)dst_mapped) & 15u) return hipErrorInvalidValue;
-  const uint32_t n16 = n / 16u;
-  const uint32_t threads = n16 > 16u ? n16 : 16u;
-  hipLaunchKernelGGL(copy_out_kernel, dim3((threads + 255) / 256), dim3(256), 0, stream,
-                     reinterpret_cast<const uint4 *>(src), reinterpret_cast<uint4 *>(dst_mapped), n16, src, dst_mapped, n);
-  return hipGetLastError();
-}
 
 // ---- radix-2^10 comb of -A (kernels.h kComb10*) ------------------------------------------
 __global__ __launch_bounds__(64) void comb10_bases_kernel(const uint8_t *__restrict__ pubs, uint32_t n,

@@ -1,0 +1,351 @@
+// keycache.h — the per-context validator-set key cache behind the commit seam.
+//
+// The reference decodes A inside every Verify (crypto/ed25519/ed25519.go:148-155).  Its callers
+// verify commit after commit against the SAME validator set (state/validation.go:93-96 checks
+// LastCommit against LastValidators every block; blockchain/v0/reactor.go:366-367 checks every
+// buffered block against state.Validators; light/verifier.go:58,73-76 checks headers against sets
+// that change by a few keys per height).  This cache makes those callers reach the key-cached
+// kernels with no handle management on their side:
+//
+//   * ONE pool key set per context (a Keyset in ctx->keysets, grown by appending keys; indexes of
+//     keys already in it never change).  A pubkey is stored once however many sets hold it, so a
+//     light client's per-height sets share their keys.
+//   * set entries keyed by ValidatorSet.Hash() (types/validator_set.go:347-353) when the caller
+//     passes it (tmed_valset.set_hash), else by a digest of the ordered key bytes; an entry holds a
+//     copy of the set's keys (compared byte for byte on every hit: a stale or colliding key can
+//     only cost a miss, never a wrong index) and the set's index into the pool.
+//   * policy on a miss: if every key is already in the pool, the set is keyed at once; if the
+//     call's own signatures amortise building the new keys' combs (>= kAmortizeSigsPerKey per new
+//     key, a blocksync window or a large light-client batch), the keys are appended in stream
+//     order before this call's kernels and the set is keyed at once; otherwise (the first commit
+//     of a new set: C1) this call takes the generic kernels and the new keys are appended right
+//     after it (deferred), so the NEXT call against the set is keyed.
+//   * bounds: the pool holds at most capacity_keys() keys (the HBM budget); when a set does not
+//     fit, the pool is reset if no other call holds indexes into it, else the set stays generic.
+//     Set entries are bounded in count and host bytes (least recently used first out).
+//
+// Host-only logic, templated on a backend (the device pool in keycache.hip; a host stand-in in
+// tests/native/keycache_test.cpp, which checks the policy on the CPU).
+//   Backend::append(const uint8_t *pubs, size_t m) -> int   append m keys (TMED_OK or an error)
+//   Backend::capacity_keys() -> size_t                      pool keys the budget allows
+//   Backend::reset()                                        drop every key of the pool
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+namespace tmed {
+
+struct KcKey {
+  uint8_t d[32];
+  uint64_t n;
+  uint8_t from_hash;  // d is the caller's ValidatorSet.Hash(), not the key digest
+  bool operator==(const KcKey &o) const { return n == o.n && from_hash == o.from_hash && memcmp(d, o.d, 32) == 0; }
+};
+struct KcKeyHash {
+  size_t operator()(const KcKey &k) const {
+    uint64_t x;
+    memcpy(&x, k.d, 8);
+    return (size_t)((x ^ (k.n * 0x9E3779B97F4A7C15ull)) + k.from_hash);
+  }
+};
+
+struct Pub32 {
+  uint64_t w[4];
+  bool operator==(const Pub32 &o) const { return memcmp(w, o.w, 32) == 0; }
+};
+struct Pub32Hash {
+  size_t operator()(const Pub32 &p) const {  // keys are attacker-choosable: mix every word
+    uint64_t h = p.w[0] * 0x9E3779B97F4A7C15ull;
+    h = (h ^ (h >> 29) ^ p.w[1]) * 0xBF58476D1CE4E5B9ull;
+    h = (h ^ (h >> 31) ^ p.w[2]) * 0x94D049BB133111EBull;
+    h = (h ^ (h >> 30) ^ p.w[3]) * 0x9E3779B97F4A7C15ull;
+    return (size_t)(h ^ (h >> 32));
+  }
+};
+inline Pub32 pub32(const uint8_t *p) {
+  Pub32 k;
+  memcpy(k.w, p, 32);
+  return k;
+}
+
+// 256-bit digest of n ordered 32-byte keys: four independent multiply-xorshift lanes, one per
+// 8-byte word of a key, then a cross-lane finish.  Not cryptographic: an entry found by digest is
+// still compared byte for byte, so a collision only costs a miss.
+inline void kc_digest(const uint8_t *pubs, size_t n, uint8_t out[32]) {
+  uint64_t a[4] = {0x243F6A8885A308D3ull, 0x13198A2E03707344ull, 0xA4093822299F31D0ull, 0x082EFA98EC4E6C89ull};
+  for (size_t i = 0; i < n; i++) {
+    uint64_t w[4];
+    memcpy(w, pubs + 32 * i, 32);
+    for (int l = 0; l < 4; l++) {
+      uint64_t x = (a[l] ^ w[l]) * 0x9E3779B97F4A7C15ull;
+      a[l] = x ^ (x >> 31) ^ (uint64_t)i;
+    }
+  }
+  for (int r = 0; r < 2; r++)
+    for (int l = 0; l < 4; l++) {
+      uint64_t x = (a[l] + a[(l + 1) & 3] + (uint64_t)n) * 0xBF58476D1CE4E5B9ull;
+      a[l] = x ^ (x >> 27);
+    }
+  memcpy(out, a, 32);
+}
+
+inline KcKey kc_key(const uint8_t *pubs, size_t n, const uint8_t *set_hash) {
+  KcKey k;
+  k.n = n;
+  k.from_hash = set_hash ? 1 : 0;
+  if (set_hash)
+    memcpy(k.d, set_hash, 32);
+  else
+    kc_digest(pubs, n, k.d);
+  return k;
+}
+
+// One cached validator set: its keys (for the byte compare) and validator i -> pool index.
+struct KcSet {
+  std::vector<uint8_t> pubs;
+  std::vector<uint32_t> idx;
+  uint64_t tick = 0;
+  size_t bytes() const { return pubs.size() + 4 * idx.size() + 64; }
+};
+
+inline bool kc_same_keys(const KcSet &s, const uint8_t *pubs, size_t n) {
+  return s.pubs.size() == 32 * n && memcmp(s.pubs.data(), pubs, 32 * n) == 0;
+}
+
+// Counters (tmed_keycache_stats).
+struct KcCounters {
+  uint64_t lookups = 0, hits = 0;         // set lookups; hits on a cached entry
+  uint64_t keyed_sets = 0;                // lookups that gave the key-cached kernels
+  uint64_t generic_sets = 0;              // lookups that stayed generic this call
+  uint64_t keys_appended = 0;             // keys built into the pool (at once or deferred)
+  uint64_t keys_deferred = 0;             // of those, queued behind a generic call
+  uint64_t pool_resets = 0;               // the pool was emptied to fit a set
+  uint64_t sets_evicted = 0;              // entries dropped by the count / byte bound
+  uint64_t keyed_sigs = 0, generic_sigs = 0;  // signatures of requests resolved each way
+};
+
+// Signatures of a call per new key at which building the key's combs before the call pays: a key's
+// radix-256 + radix-2^10 combs cost ~22 us of device time, ~2.3k generic verifies at 105 M/s,
+// against a 7.5-ns saving per keyed verify (500 M/s); the latency-size batches never reach it (a
+// lone key's comb-base chain is ~0.5 ms serial, more than a generic commit).
+constexpr size_t kKcAmortizeSigsPerKey = 2048;
+
+template <class Backend>
+class KeyCache {
+ public:
+  static constexpr size_t kAmortizeSigsPerKey = kKcAmortizeSigsPerKey;
+
+  explicit KeyCache(Backend b) : be(std::move(b)) {}
+
+  Backend be;
+  size_t max_sets = 1u << 16;
+  size_t max_set_bytes = (size_t)512 << 20;
+  KcCounters st;
+
+  size_t pool_keys() const { return slot_.size(); }
+  size_t sets_cached() const { return sets_.size(); }
+  size_t pending_keys() const { return pending_.size() / 32; }
+  int users() const { return users_; }
+
+  // A seam call holds the pool (no reset while its resolved indexes are in use) from before its
+  // first lookup until it has collected its last batch.
+  void pin() { users_++; }
+  void unpin() {
+    if (users_ > 0) users_--;
+  }
+
+  // Fast path of a call resolving many sets: the cached entry under `key` (nullptr if none), to be
+  // compared with the set's keys outside the lock; a match is then recorded with hit().
+  std::shared_ptr<const KcSet> find(const KcKey &key) {
+    auto it = sets_.find(key);
+    if (it == sets_.end()) return nullptr;
+    it->second->tick = ++tick_;
+    return it->second;
+  }
+  void hit(size_t sigs) {
+    st.lookups++;
+    st.hits++;
+    st.keyed_sets++;
+    st.keyed_sigs += sigs;
+  }
+
+  // Resolve one set for a call that pinned the pool.  Returns true (keyed: *hold->idx are the
+  // pool indexes of validators 0..n-1, valid while hold lives and the call is pinned) or false
+  // (generic this call).  may_reset: the call has resolved no keyed set yet.
+  // force_build: build missing keys now whatever the call's size (tmed_keycache_warm).
+  bool lookup(const uint8_t *pubs, size_t n, const KcKey &key, size_t sigs, bool may_reset,
+              std::shared_ptr<const KcSet> &hold, bool force_build = false) {
+    st.lookups++;
+    auto it = sets_.find(key);
+    if (it != sets_.end()) {
+      KcSet &s = *it->second;
+      if (kc_same_keys(s, pubs, n)) {
+        s.tick = ++tick_;
+        st.hits++;
+        return keyed(it->second, sigs, hold);
+      }
+      drop_(it);  // same key, other keys (a stale or wrong set_hash, a digest collision)
+    }
+    auto e = std::make_shared<KcSet>();
+    e->pubs.assign(pubs, pubs + 32 * n);
+    e->idx.resize(n);
+    std::vector<size_t> fresh;  // first position of each key the pool lacks
+    if (!resolve_(*e, fresh)) return generic(sigs);  // more distinct new keys than the pool can hold
+    if (fresh.empty()) return insert_keyed(std::move(e), key, sigs, hold);
+    const size_t nf = fresh.size();
+    if (slot_.size() + nf > be.capacity_keys()) {
+      if (!(may_reset && users_ <= 1) || nf > be.capacity_keys()) return generic(sigs);
+      reset();
+      st.pool_resets++;
+      fresh.clear();
+      if (!resolve_(*e, fresh)) return generic(sigs);
+    }
+    if (!force_build && sigs < kAmortizeSigsPerKey * fresh.size()) {  // generic now, keys built after the call
+      for (size_t f : fresh) {
+        const Pub32 k = pub32(pubs + 32 * f);
+        if (pend_set_.insert(k).second) pending_.insert(pending_.end(), pubs + 32 * f, pubs + 32 * f + 32);
+      }
+      return generic(sigs);
+    }
+    std::vector<uint8_t> add(32 * fresh.size());
+    for (size_t j = 0; j < fresh.size(); j++) memcpy(&add[32 * j], pubs + 32 * fresh[j], 32);
+    if (!append_(add.data(), fresh.size())) return generic(sigs);
+    resolve_(*e, fresh);  // every key present now
+    return insert_keyed(std::move(e), key, sigs, hold);
+  }
+
+  // Distinct keys of a set that the pool lacks (not counting those already in *seen, which
+  // collects them across the sets of one call): a call builds every missing key at once when its
+  // signatures amortise them all (kAmortizeSigsPerKey each), as a blocksync window or a large
+  // light-client batch does.
+  size_t missing_keys(const uint8_t *pubs, size_t n, std::unordered_set<Pub32, Pub32Hash> *seen = nullptr) const {
+    std::unordered_set<Pub32, Pub32Hash> local;
+    if (!seen) seen = &local;
+    size_t m = 0;
+    for (size_t i = 0; i < n; i++) {
+      const Pub32 k = pub32(pubs + 32 * i);
+      if (!slot_.count(k) && seen->insert(k).second) m++;
+    }
+    return m;
+  }
+
+  // Build the keys queued by generic calls (after such a call has collected its results).
+  int drain_pending() {
+    if (pending_.empty()) return 0;
+    std::vector<uint8_t> add;
+    add.swap(pending_);
+    pend_set_.clear();
+    // keys another call appended meanwhile are skipped
+    size_t w = 0;
+    for (size_t r = 0; r < add.size() / 32; r++)
+      if (!slot_.count(pub32(&add[32 * r]))) {
+        if (w != r) memcpy(&add[32 * w], &add[32 * r], 32);
+        w++;
+      }
+    if (w == 0) return 0;
+    if (slot_.size() + w > be.capacity_keys()) {
+      if (users_ > 0 || w > be.capacity_keys()) return 0;  // dropped: the sets stay generic
+      reset();
+      st.pool_resets++;
+    }
+    st.keys_deferred += w;
+    return append_(add.data(), w) ? 0 : -1;
+  }
+
+  void reset() {
+    be.reset();
+    slot_.clear();
+    sets_.clear();
+    set_bytes_ = 0;
+    pending_.clear();
+    pend_set_.clear();
+  }
+
+ private:
+  bool keyed(const std::shared_ptr<KcSet> &e, size_t sigs, std::shared_ptr<const KcSet> &hold) {
+    hold = e;
+    st.keyed_sets++;
+    st.keyed_sigs += sigs;
+    return true;
+  }
+  bool generic(size_t sigs) {
+    st.generic_sets++;
+    st.generic_sigs += sigs;
+    return false;
+  }
+  // idx of every key already in the pool; `fresh` gets the first position of each key it lacks.
+  // False when there are more such keys than the pool could ever hold.
+  bool resolve_(KcSet &e, std::vector<size_t> &fresh) {
+    const size_t n = e.idx.size();
+    std::unordered_map<Pub32, uint32_t, Pub32Hash> local;  // new keys repeated inside the set
+    for (size_t i = 0; i < n; i++) {
+      const Pub32 k = pub32(&e.pubs[32 * i]);
+      auto s = slot_.find(k);
+      if (s != slot_.end()) {
+        e.idx[i] = s->second;
+        continue;
+      }
+      auto l = local.find(k);
+      if (l != local.end()) {
+        e.idx[i] = l->second;
+        continue;
+      }
+      const uint32_t provisional = (uint32_t)(slot_.size() + fresh.size());
+      local.emplace(k, provisional);
+      e.idx[i] = provisional;
+      fresh.push_back(i);
+      if (fresh.size() > be.capacity_keys()) return false;
+    }
+    return true;
+  }
+  bool append_(const uint8_t *keys, size_t m) {
+    if (be.append(keys, m) != 0) return false;
+    for (size_t j = 0; j < m; j++) slot_.emplace(pub32(keys + 32 * j), (uint32_t)slot_.size());
+    st.keys_appended += m;
+    return true;
+  }
+  bool insert_keyed(std::shared_ptr<KcSet> e, const KcKey &key, size_t sigs, std::shared_ptr<const KcSet> &hold) {
+    e->tick = ++tick_;
+    set_bytes_ += e->bytes();
+    sets_[key] = e;
+    if (sets_.size() > max_sets || set_bytes_ > max_set_bytes) evict_();
+    return keyed(e, sigs, hold);
+  }
+  void drop_(typename std::unordered_map<KcKey, std::shared_ptr<KcSet>, KcKeyHash>::iterator it) {
+    set_bytes_ -= it->second->bytes();
+    sets_.erase(it);
+  }
+  // Least recently used quarter out (calls in flight keep their entries through `hold`).
+  void evict_() {
+    std::vector<uint64_t> ticks;
+    ticks.reserve(sets_.size());
+    for (auto &kv : sets_) ticks.push_back(kv.second->tick);
+    const size_t k = std::max<size_t>(1, ticks.size() / 4);
+    std::nth_element(ticks.begin(), ticks.begin() + (k - 1), ticks.end());
+    const uint64_t cut = ticks[k - 1];
+    for (auto it = sets_.begin(); it != sets_.end();) {
+      auto nx = std::next(it);
+      if (it->second->tick <= cut) {
+        drop_(it);
+        st.sets_evicted++;
+      }
+      it = nx;
+    }
+  }
+
+  std::unordered_map<Pub32, uint32_t, Pub32Hash> slot_;  // pool index of every key in the pool
+  std::unordered_map<KcKey, std::shared_ptr<KcSet>, KcKeyHash> sets_;
+  std::vector<uint8_t> pending_;  // keys queued by generic calls
+  std::unordered_set<Pub32, Pub32Hash> pend_set_;
+  size_t set_bytes_ = 0;
+  uint64_t tick_ = 0;
+  int users_ = 0;
+};
+
+}  // namespace tmed

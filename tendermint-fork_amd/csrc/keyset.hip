@@ -10,6 +10,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 
 #include "ctx.h"
@@ -41,40 +42,118 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // Key-grouped visiting order for the throughput kernels (launch_key_order): the comb rows a
 // signature reads are random 128-B lines of its key's 528-KB comb; with the signatures of a
 // 10k-key set in random order the lanes in flight span the whole 5.3 GB and the main kernel
-// ran 3.27 ms per 2^20 against 2.02 ms with them in key order (profiles/r03/s3).  Env
-// TMED_KEY_ORDER=0 turns it off.
+// ran 3.27 ms per 2^20 against 2.02 ms with them in key order (profiles/r03/s3).
 static bool key_order_on(const Keyset &k, uint32_t n) {
-  static const bool on = [] {
-    const char *v = getenv("TMED_KEY_ORDER");
-    return !(v && v[0] == '0');
-  }();
-  return on && n >= 4096 && k.n > 1 && k.n <= kKeyOrderMaxKeys;
+  return n >= 4096 && k.n > 1 && k.n <= kKeyOrderMaxKeys;
 }
 
-// The key set's radix-2^10 comb (kernels.h kComb10*), once, on stream s (queued in front of the
-// batch that needs it; the bases scratch is freed after a sync of s).  TMED_KS_A10=0 (read at
-// tmed_init) keeps the radix-256 comb.
-static void comb10_build(tmed_ctx *c, const Keyset &k, hipStream_t s) {
-  k.comb10_tried = true;
-  if (!c->a10_on || k.n == 0) return;
+// The key set's radix-2^10 comb (kernels.h kComb10*) for keys [comb10_n, n), on stream s (queued
+// in front of the batch that needs it; the bases scratch is freed after a sync of s): at the set's
+// first throughput batch, then for keys appended after it.  TMED_KS_A10=0 (read at tmed_init) keeps
+// the radix-256 comb; so does a failed allocation (comb10_failed).
+static void comb10_extend(tmed_ctx *c, Keyset &k, hipStream_t s) {
+  if (!c->a10_on || k.comb10_failed || k.comb10_n >= k.n) return;
+  if (!k.d_comb10 && hipMalloc((void **)&k.d_comb10, k.cap * kComb10BytesPerKey) != hipSuccess) {
+    (void)hipGetLastError();
+    k.d_comb10 = nullptr;
+    k.comb10_failed = true;
+    return;
+  }
+  const size_t m = k.n - k.comb10_n;
   int32_t *bases = nullptr;
-  int4 *comb = nullptr;
-  hipError_t e = hipMalloc((void **)&bases, k.n * kComb10Windows * 40 * sizeof(int32_t));
-  if (e == hipSuccess) e = hipMalloc((void **)&comb, k.n * kComb10BytesPerKey);
-  if (e == hipSuccess) e = launch_build_comb10(k.d_pub, (uint32_t)k.n, bases, comb, s);
+  hipError_t e = hipMalloc((void **)&bases, m * kComb10Windows * 40 * sizeof(int32_t));
+  if (e == hipSuccess)
+    e = launch_build_comb10(k.d_pub + 32 * k.comb10_n, (uint32_t)m, bases,
+                            k.d_comb10 + k.comb10_n * (kComb10BytesPerKey / sizeof(int4)), s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (bases) (void)hipFree(bases);
   if (e == hipSuccess) {
-    k.d_comb10 = comb;
-  } else {
-    if (comb) (void)hipFree(comb);
-    (void)hipGetLastError();  // an allocation failure leaves the radix-256 comb in use
+    k.comb10_n = k.n;
+  } else {  // an allocation failure leaves the radix-256 comb in use
+    (void)hipGetLastError();
+    (void)hipFree(k.d_comb10);
+    k.d_comb10 = nullptr;
+    k.comb10_n = 0;
+    k.comb10_failed = true;
   }
+}
+
+size_t keyset_bytes_per_key(const tmed_ctx *c) {
+  return 33 + kCombBytesPerKey + (c->a10_on ? kComb10BytesPerKey : 0);
+}
+
+Keyset *find_keyset(tmed_ctx *c, uint64_t handle) {
+  auto it = c->keysets.find(handle);
+  return it == c->keysets.end() || it->second.pooled ? nullptr : &it->second;
+}
+
+// Room for `cap` keys: new buffers, the built keys (and their radix-2^10 combs) copied over on s,
+// a synchronisation of s, the old buffers freed.  A radix-2^10 comb that no longer fits is dropped
+// (rebuilt at the next throughput batch, or the radix-256 comb is used).
+static int keyset_reserve(tmed_ctx *c, Keyset &k, size_t cap, hipStream_t s) {
+  if (cap <= k.cap) return TMED_OK;
+  uint8_t *pub = nullptr, *ok = nullptr;
+  int4 *comb = nullptr, *comb10 = nullptr;
+  hipError_t e = hipMalloc((void **)&pub, cap * 32);
+  if (e == hipSuccess) e = hipMalloc((void **)&ok, cap);
+  if (e == hipSuccess) e = hipMalloc((void **)&comb, cap * kCombBytesPerKey);
+  if (e == hipSuccess && k.d_comb10 && hipMalloc((void **)&comb10, cap * kComb10BytesPerKey) != hipSuccess) {
+    (void)hipGetLastError();
+    comb10 = nullptr;
+  }
+  if (e == hipSuccess && k.n) {
+    e = hipMemcpyAsync(pub, k.d_pub, k.n * 32, hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(ok, k.d_ok, k.n, hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(comb, k.d_comb, k.n * kCombBytesPerKey, hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess && comb10 && k.comb10_n)
+      e = hipMemcpyAsync(comb10, k.d_comb10, k.comb10_n * kComb10BytesPerKey, hipMemcpyDeviceToDevice, s);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    for (void *p : {(void *)pub, (void *)ok, (void *)comb, (void *)comb10})
+      if (p) (void)hipFree(p);
+    return map_err(e);
+  }
+  for (void *p : {(void *)k.d_pub, (void *)k.d_ok, (void *)k.d_comb, (void *)k.d_comb10})
+    if (p) (void)hipFree(p);
+  k.d_pub = pub;
+  k.d_ok = ok;
+  k.d_comb = comb;
+  k.d_comb10 = comb10;
+  if (!comb10) k.comb10_n = 0;
+  k.cap = cap;
+  return TMED_OK;
+}
+
+int keyset_append(tmed_ctx *c, Keyset &k, const uint8_t *pubkeys, size_t m, hipStream_t s, size_t max_cap) {
+  if (m == 0) return TMED_OK;
+  max_cap = std::min<size_t>(max_cap, 0xffffffu);
+  if (k.n + m > max_cap) return TMED_EINVAL;
+  int rc = TMED_OK;
+  if (k.n + m > k.cap) rc = keyset_reserve(c, k, std::max(k.n + m, std::min(2 * k.cap, max_cap)), s);
+  if (rc != TMED_OK) return rc;
+  // the pinned key staging and the comb-base scratch are reused once the previous build is done
+  hipError_t e = hipSuccess;
+  if (c->kup_ev) e = hipEventSynchronize(c->kup_ev);
+  else e = hipEventCreateWithFlags(&c->kup_ev, hipEventDisableTiming);
+  const size_t bbytes = m * kCombWindows * 40 * sizeof(int32_t);
+  if (e == hipSuccess && bbytes > c->d_kbases.cap) e = c->d_kbases.ensure(bbytes);
+  if (e == hipSuccess) e = c->h_kup.ensure(m * 32);
+  if (e != hipSuccess) return map_err(e);
+  memcpy(c->h_kup.p, pubkeys, m * 32);
+  e = hipMemcpyAsync(k.d_pub + 32 * k.n, c->h_kup.p, m * 32, hipMemcpyHostToDevice, s);
+  int32_t *bases = (int32_t *)c->d_kbases.p;
+  if (e == hipSuccess) e = launch_comb_bases(k.d_pub + 32 * k.n, (uint32_t)m, /*negate=*/1, k.d_ok + k.n, bases, s);
+  if (e == hipSuccess) e = launch_comb_fill(bases, (uint32_t)m, k.d_comb + k.n * (kCombBytesPerKey / sizeof(int4)), s);
+  if (e == hipSuccess) e = hipEventRecord(c->kup_ev, s);
+  if (e != hipSuccess) return map_err(e);
+  k.n += m;
+  return TMED_OK;
 }
 
 // Key-cached batch on the context's stream: latency kernels for small batches (C1: one
 // commit), the throughput kernels (prep / comb main / batched finish) above c->lat_max.
-static hipError_t keyset_verify(tmed_ctx *c, const Keyset &k, const uint32_t *d_idx, const uint8_t *d_sig,
+static hipError_t keyset_verify(tmed_ctx *c, Keyset &k, const uint32_t *d_idx, const uint8_t *d_sig,
                                 const uint8_t *d_msgs, const uint32_t *d_off, uint32_t n, uint8_t *d_out,
                                 hipStream_t s, bool msg_slots, const VoteAsm *va = nullptr) {
   c->last_hs_count = 0;  // d_prep now holds another path's hand-off (tmed_window_stats)
@@ -82,7 +161,8 @@ static hipError_t keyset_verify(tmed_ctx *c, const Keyset &k, const uint32_t *d_
     return launch_verify_keyset_lat(d_idx, (uint32_t)k.n, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb, d_sig, d_msgs, d_off, n, d_out,
                                     c->d_fin, c->d_fin_pre, s, msg_slots, va);
   if (va) return hipErrorInvalidValue;
-  if (c->d_b24 && !k.comb10_tried) comb10_build(c, k, s);
+  if (c->d_b24) comb10_extend(c, k, s);
+  const int4 *comb10 = c->d_b24 && k.d_comb10 && k.comb10_n == k.n ? k.d_comb10 : nullptr;
   KernelTimer *timer = (c->timing && !msg_slots) ? &c->timer : nullptr;
   uint32_t *perm = nullptr, *scratch = nullptr;
   if (key_order_on(k, n)) {
@@ -95,7 +175,7 @@ static hipError_t keyset_verify(tmed_ctx *c, const Keyset &k, const uint32_t *d_
   // (the key order runs in front of each chunk's prep and is charged to prep by the timer)
   return launch_verify_keyset(d_idx, (uint32_t)k.n, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb16, d_sig, d_msgs, d_off, n,
                               d_out, c->d_prep, c->slab_slots, c->d_fin, c->d_fin_pre, s, msg_slots, timer, perm,
-                              scratch, c->d_b24, c->d_b24 ? k.d_comb10 : nullptr);
+                              scratch, c->d_b24, comb10);
 }
 
 int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st, int slot) {
@@ -177,12 +257,8 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   // A batch of up to kVoteZeroCopyMax staged bytes (a single commit: C1) is not copied at all:
   // the kernels read the pinned staging buffer over the bus and write the decisions into the
   // pinned result buffer, which saves the copy-in and copy-out latencies (~15 us of a 100-us
-  // commit).  TMED_VOTES_ZC=0 turns it off.
-  static const bool zc_on = [] {
-    const char *v = getenv("TMED_VOTES_ZC");
-    return !(v && v[0] == '0');
-  }();
-  st.zc = zc_on && st.total <= kVoteZeroCopyMax;
+  // commit).
+  st.zc = st.total <= kVoteZeroCopyMax;
   uint8_t *out_dev = (uint8_t *)vs.d_out.p;
   hipError_t e = hipSuccess;
   if (st.zc) {
@@ -218,6 +294,9 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
         while (k < nd && st.dma[k].bytes == a.bytes && st.dma[k].dst == a.dst + (k - r) * a.bytes &&
                (const uint8_t *)st.dma[k].src == s0 + (ptrdiff_t)(k - r) * pitch)
           k++;
+      // the 2-D source region spans the gaps between the runs: one copy only when it lies inside a
+      // single pinned range (runs in separate tmed_host_alloc / _register ranges go one by one)
+      if (k - r >= 2 && !host_pinned(s0, (size_t)pitch * (k - r - 1) + a.bytes)) k = r + 1;
       if (k - r >= 2) {
         e = hipMemcpy2DAsync(d + st.o_sig + a.dst, a.bytes, s0, (size_t)pitch, a.bytes, k - r, hipMemcpyHostToDevice,
                              c->copy_stream);
@@ -260,21 +339,7 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   slow.lap("verify launches");
   if (e == hipSuccess && st.timed) e = hipEventRecord(vs.ev1, s);
   if (e == hipSuccess) e = scratch_release(c, s);
-  // TMED_OUT_KERNEL=1 (experimental, off by default): the decisions of a large batch go out by a
-  // small kernel writing the pinned result buffer through its device mapping instead of a
-  // device-to-host copy command (the runtime blocked the host ~6 ms inside that call two or three
-  // times per C4 run, profiles/r03/c4_direct/).
-  static const bool out_kernel = [] {
-    const char *v = getenv("TMED_OUT_KERNEL");
-    return v && v[0] == '1';
-  }();
-  if (e == hipSuccess && !st.zc) {
-    void *hout = nullptr;
-    if (out_kernel && st.total >= kVoteCopyStreamMin && hipHostGetDevicePointer(&hout, vs.h_out.p, 0) == hipSuccess)
-      e = launch_copy_out((const uint8_t *)vs.d_out.p, (uint8_t *)hout, m, s);
-    else
-      e = hipMemcpyAsync(vs.h_out.p, vs.d_out.p, m, hipMemcpyDeviceToHost, s);
-  }
+  if (e == hipSuccess && !st.zc) e = hipMemcpyAsync(vs.h_out.p, vs.d_out.p, m, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipEventRecord(vs.done, s);
   slow.lap("copy-out");
   return map_err(e);
@@ -334,14 +399,9 @@ int tmed_keyset_load(tmed_ctx *c, const uint8_t *pubkeys, size_t n, uint64_t *ha
   std::lock_guard<std::mutex> lk(c->mu);
   (void)hipSetDevice(c->device);
   Keyset k;
-  k.n = n;
-  const size_t m = n ? n : 1;
-  hipError_t e = hipMalloc((void **)&k.d_pub, m * 32);
-  if (e == hipSuccess) e = hipMalloc((void **)&k.d_ok, m);
-  if (e == hipSuccess) e = hipMalloc((void **)&k.d_comb, m * kCombBytesPerKey);
-  if (e == hipSuccess && n) e = hipMemcpyAsync(k.d_pub, pubkeys, n * 32, hipMemcpyHostToDevice, c->stream);
-  int rc = map_err(e);
-  if (rc == TMED_OK && n) rc = build_comb(c, k.d_pub, n, /*negate=*/1, k.d_ok, k.d_comb);
+  int rc = keyset_reserve(c, k, n ? n : 1, c->stream);
+  if (rc == TMED_OK) rc = keyset_append(c, k, pubkeys, n, c->stream, n);
+  if (rc == TMED_OK) rc = map_err(hipStreamSynchronize(c->stream));
   if (rc == TMED_OK) (void)ctx_bcomb24(c);  // the shared radix-2^24 B comb (null: radix 2^16)
   if (rc != TMED_OK) {
     free_keyset(k);
@@ -353,15 +413,28 @@ int tmed_keyset_load(tmed_ctx *c, const uint8_t *pubkeys, size_t n, uint64_t *ha
   return TMED_OK;
 }
 
+int tmed_keyset_extend(tmed_ctx *c, uint64_t handle, const uint8_t *pubkeys, size_t n, uint32_t *first_index) {
+  if (!c || (n && !pubkeys)) return TMED_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  Keyset *k = find_keyset(c, handle);
+  if (!k) return TMED_ENOKEYSET;
+  if (first_index) *first_index = (uint32_t)k->n;
+  if (n == 0) return TMED_OK;
+  (void)hipSetDevice(c->device);
+  int rc = keyset_append(c, *k, pubkeys, n, c->stream, 0xffffffu);
+  if (rc == TMED_OK) rc = map_err(hipStreamSynchronize(c->stream));
+  return rc;
+}
+
 int tmed_keyset_free(tmed_ctx *c, uint64_t handle) {
   if (!c) return TMED_EINVAL;
   std::lock_guard<std::mutex> lk(c->mu);
-  auto it = c->keysets.find(handle);
-  if (it == c->keysets.end()) return TMED_ENOKEYSET;
+  Keyset *k = find_keyset(c, handle);
+  if (!k) return TMED_ENOKEYSET;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  free_keyset(it->second);
-  c->keysets.erase(it);
+  free_keyset(*k);
+  c->keysets.erase(handle);
   return TMED_OK;
 }
 
@@ -372,9 +445,9 @@ int tmed_verify_batch_keyset_device(tmed_ctx *c, uint64_t handle, const uint32_t
   if (n == 0) return TMED_OK;
   if (!d_val_idx || !d_sigs || !d_msgs || !d_msg_off || !d_out || n > 0xffffffffu) return TMED_EINVAL;
   std::lock_guard<std::mutex> lk(c->mu);
-  auto it = c->keysets.find(handle);
-  if (it == c->keysets.end()) return TMED_ENOKEYSET;
-  const Keyset &k = it->second;
+  Keyset *kp = find_keyset(c, handle);
+  if (!kp) return TMED_ENOKEYSET;
+  Keyset &k = *kp;
   (void)hipSetDevice(c->device);
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   if (c->timing) c->timer.n = 0;
@@ -395,9 +468,9 @@ int tmed_verify_batch_keyset(tmed_ctx *c, uint64_t handle, const uint32_t *val_i
   const size_t mbytes = off[n];
   if (mbytes && !msgs) return TMED_EINVAL;
   std::lock_guard<std::mutex> lk(c->mu);
-  auto it = c->keysets.find(handle);
-  if (it == c->keysets.end()) return TMED_ENOKEYSET;
-  const Keyset &k = it->second;
+  Keyset *kp = find_keyset(c, handle);
+  if (!kp) return TMED_ENOKEYSET;
+  Keyset &k = *kp;
   for (size_t i = 0; i < n; i++)
     if (val_idx[i] >= k.n) return TMED_EINVAL;
   (void)hipSetDevice(c->device);

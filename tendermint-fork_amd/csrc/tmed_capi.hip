@@ -192,6 +192,8 @@ int tmed_init(int device, tmed_ctx **out) {
   if (e == hipSuccess && !env_off("TMED_B26")) c->d_b26 = bshare_acquire(0, device, c->d_bcomb16, c->stream);
   c->b24_on = !env_off("TMED_B24");
   c->a10_on = !env_off("TMED_KS_A10");
+  c->kc_on = !env_off("TMED_KEYCACHE");
+  if (const char *v = getenv("TMED_KEYCACHE_GB")) c->kc_budget = (size_t)strtoull(v, nullptr, 10) << 30;
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_bcomb, kCombBytesPerKey);
   if (e == hipSuccess) e = hipMalloc((void **)&d_bpub, 32);
   if (e == hipSuccess) e = hipMalloc((void **)&d_bok, 1);
@@ -215,7 +217,11 @@ void tmed_destroy(tmed_ctx *c) {
   if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
   for (DevBuf *b : {&c->d_a, &c->d_b, &c->d_msg, &c->d_off, &c->d_out, &c->d_c}) b->release();
   for (HostBuf *b : {&c->h_a, &c->h_b, &c->h_msg, &c->h_off, &c->h_out, &c->h_c}) b->release();
-  for (DevBuf *b : {&c->d_merkle_a, &c->d_merkle_b, &c->d_merkle_idx}) b->release();
+  for (DevBuf *b : {&c->d_merkle_a, &c->d_merkle_b, &c->d_merkle_idx, &c->d_korder, &c->d_zip, &c->d_kbases})
+    b->release();
+  c->h_kup.release();
+  if (c->kup_ev) hipEventDestroy(c->kup_ev);
+  if (c->trace_t0) hipEventDestroy(c->trace_t0);
   for (VoteSlot &v : c->vslot) {
     for (DevBuf *b : {&v.d_votes, &v.d_vmsg, &v.d_off, &v.d_out}) b->release();
     for (HostBuf *b : {&v.h_votes, &v.h_out}) b->release();
@@ -226,6 +232,7 @@ void tmed_destroy(tmed_ctx *c) {
     if (v.cp0) hipEventDestroy(v.cp0);
     if (v.cp1) hipEventDestroy(v.cp1);
   }
+  keycache_destroy(c);
   for (auto &kv : c->keysets) free_keyset(kv.second);
   c->keysets.clear();
   if (c->scratch_ev) hipEventDestroy(c->scratch_ev);
@@ -332,9 +339,9 @@ int tmed_keyset_b_window_bits(const tmed_ctx *c) { return c && c->d_b24 ? 24 : 1
 int tmed_keyset_a_window_bits(tmed_ctx *c, uint64_t handle) {
   if (!c) return -1;
   std::lock_guard<std::mutex> lk(c->mu);
-  auto it = c->keysets.find(handle);
-  if (it == c->keysets.end()) return -1;
-  return it->second.d_comb10 && c->d_b24 ? 10 : 8;
+  const Keyset *k = find_keyset(c, handle);
+  if (!k) return -1;
+  return k->d_comb10 && k->comb10_n == k->n && c->d_b24 ? 10 : 8;
 }
 
 int tmed_window_stats(tmed_ctx *c, uint32_t lane_hist[65], uint32_t wave_hist[65]) {

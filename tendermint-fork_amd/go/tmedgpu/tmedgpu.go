@@ -105,8 +105,23 @@ type ValSet struct {
 	Powers      []int64 // n
 	Addresses   []byte  // n x 20 (every Validator.Address is 20 bytes; see verifyCommitGPU)
 	TotalPower  int64
-	Keyset      uint64   // 0 or a LoadKeyset handle (cache key: ValidatorSet.Hash())
+	Keyset      uint64   // 0: the engine's key-set cache decides (the default); or a LoadKeyset handle
 	KeysetIndex []uint32 // nil, or validator i -> index in the key set
+	// nil, or ValidatorSet.Hash() (types/validator_set.go:347-353) when the caller has it at no cost
+	// (a header's ValidatorsHash after its check): the key-set cache's key for this set.  Without it
+	// the library keys the set by a digest of PubKeys; a hit is compared key by key either way.
+	SetHash []byte
+}
+
+// valset builds the C struct of v (its slices copied into the arena).
+func (a *arena) valset(v *ValSet) C.tmed_valset {
+	var sh *C.uint8_t
+	if len(v.SetHash) == 32 {
+		sh = a.bytes(v.SetHash)
+	}
+	return C.tmed_valset{n: C.size_t(len(v.Powers)), pubkeys: a.bytes(v.PubKeys), powers: a.i64(v.Powers),
+		addresses: a.bytes(v.Addresses), total_power: C.int64_t(v.TotalPower), keyset: C.uint64_t(v.Keyset),
+		keyset_index: a.u32(v.KeysetIndex), set_hash: sh}
 }
 
 type BlockID struct {
@@ -219,6 +234,49 @@ func (e *Engine) LoadKeyset(pubKeys []byte) (uint64, error) {
 // FreeKeyset releases a key set.
 func (e *Engine) FreeKeyset(h uint64) { C.tmed_keyset_free(e.ctx, C.uint64_t(h)) }
 
+// ExtendKeyset appends keys to a key set; existing keys keep their indexes, the new ones start at
+// the returned index (tmed_keyset_extend).
+func (e *Engine) ExtendKeyset(h uint64, pubKeys []byte) (uint32, error) {
+	var a arena
+	defer a.free()
+	var first C.uint32_t
+	if rc := C.tmed_keyset_extend(e.ctx, C.uint64_t(h), a.bytes(pubKeys), C.size_t(len(pubKeys)/32), &first); rc != 0 {
+		return 0, errors.New(C.GoString(C.tmed_strerror(rc)))
+	}
+	return uint32(first), nil
+}
+
+// KeyCacheConfig turns the engine's key-set cache on or off (enabled < 0: unchanged) and sets its
+// HBM budget (0: unchanged).  It is on by default: sets passed without a handle reach the
+// key-cached kernels from their second call on (tmed_keycache_config).
+func (e *Engine) KeyCacheConfig(enabled int, budgetBytes uint64) error {
+	if rc := C.tmed_keycache_config(e.ctx, C.int(enabled), C.size_t(budgetBytes)); rc != 0 {
+		return errors.New(C.GoString(C.tmed_strerror(rc)))
+	}
+	return nil
+}
+
+// KeyCacheStats returns the cache's counters (tmed_keycache_counters).
+func (e *Engine) KeyCacheStats() (C.tmed_keycache_counters, error) {
+	var st C.tmed_keycache_counters
+	if rc := C.tmed_keycache_stats(e.ctx, &st); rc != 0 {
+		return st, errors.New(C.GoString(C.tmed_strerror(rc)))
+	}
+	return st, nil
+}
+
+// WarmKeyCache builds a set's missing keys now — e.g. when EndBlock changes the validator set —
+// so that even its first commit is keyed (tmed_keycache_warm).
+func (e *Engine) WarmKeyCache(v *ValSet) error {
+	var a arena
+	defer a.free()
+	cv := a.valset(v)
+	if rc := C.tmed_keycache_warm(e.ctx, &cv); rc != 0 {
+		return errors.New(C.GoString(C.tmed_strerror(rc)))
+	}
+	return nil
+}
+
 // VerifyCommits verifies many commits with ONE device batch.
 func (e *Engine) VerifyCommits(reqs []Request) ([]Result, error) {
 	return e.verifyCommitsWith(reqs, func(a *arena, creqs *C.tmed_commit_request, n C.size_t,
@@ -239,11 +297,17 @@ func (e *Engine) verifyCommitsWith(reqs []Request, call func(*arena, *C.tmed_com
 	vs := (*[1 << 26]C.tmed_valset)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_valset{})))[:n:n]
 	cs := (*[1 << 26]C.tmed_commit)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_commit{})))[:n:n]
 	bids := (*[1 << 26]C.tmed_block_id)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_block_id{})))[:n:n]
+	// one C copy per distinct *ValSet: requests on the same set share it (the library resolves each
+	// set once per call; a light-client batch holds each set twice)
+	seen := make(map[*ValSet]*C.tmed_valset, n)
 	for i := range reqs {
 		r := &reqs[i]
-		vs[i] = C.tmed_valset{n: C.size_t(len(r.Vals.Powers)), pubkeys: a.bytes(r.Vals.PubKeys),
-			powers: a.i64(r.Vals.Powers), addresses: a.bytes(r.Vals.Addresses), total_power: C.int64_t(r.Vals.TotalPower),
-			keyset: C.uint64_t(r.Vals.Keyset), keyset_index: a.u32(r.Vals.KeysetIndex)}
+		cv, ok := seen[r.Vals]
+		if !ok {
+			vs[i] = a.valset(r.Vals)
+			cv = &vs[i]
+			seen[r.Vals] = cv
+		}
 		c := r.Commit
 		cs[i] = C.tmed_commit{height: C.int64_t(c.Height), round: C.int32_t(c.Round), block_id: a.blockID(&c.BlockID),
 			n_sigs: C.size_t(len(c.Flags)), flags: a.bytes(c.Flags), addresses: a.bytes(c.Addresses),
@@ -256,7 +320,7 @@ func (e *Engine) verifyCommitsWith(reqs []Request, call func(*arena, *C.tmed_com
 		cid := C.CString(r.ChainID)
 		a.ptrs = append(a.ptrs, unsafe.Pointer(cid))
 		creqs[i] = C.tmed_commit_request{mode: C.int(r.Mode), chain_id: cid, chain_id_len: C.uint32_t(len(r.ChainID)),
-			vals: &vs[i], block_id: &bids[i], height: C.int64_t(r.Height), commit: &cs[i],
+			vals: cv, block_id: &bids[i], height: C.int64_t(r.Height), commit: &cs[i],
 			trust_num: C.int64_t(r.TrustNum), trust_den: C.int64_t(r.TrustDen)}
 	}
 	res := make([]C.tmed_commit_result, n)
@@ -298,9 +362,7 @@ func (e *Engine) BlocksyncVerify(w *BlocksyncWindow, batchBlocks int) ([]Result,
 	var a arena
 	defer a.free()
 	vs := (*C.tmed_valset)(a.alloc(unsafe.Sizeof(C.tmed_valset{})))
-	*vs = C.tmed_valset{n: C.size_t(len(w.Vals.Powers)), pubkeys: a.bytes(w.Vals.PubKeys),
-		powers: a.i64(w.Vals.Powers), addresses: a.bytes(w.Vals.Addresses), total_power: C.int64_t(w.Vals.TotalPower),
-		keyset: C.uint64_t(w.Vals.Keyset), keyset_index: a.u32(w.Vals.KeysetIndex)}
+	*vs = a.valset(w.Vals)
 	cs := (*[1 << 26]C.tmed_commit)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_commit{})))[:n:n]
 	bids := (*[1 << 26]C.tmed_block_id)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_block_id{})))[:n:n]
 	// signatures into the pinned arena (direct DMA, include/tmed25519.h tmed_host_alloc)
@@ -421,6 +483,9 @@ func (e *Engine) VerifyBatchZIP215(pubKeys []byte, msgs, sigs [][]byte) ([]bool,
 
 func (e *Engine) batch(pubKeys []byte, msgs, sigs [][]byte, zip215 bool) ([]bool, error) {
 	n := len(msgs)
+	if len(sigs) != n || len(pubKeys) != 32*n {
+		return nil, errors.New("tmedgpu: want one 32-byte key and one signature per message")
+	}
 	if n == 0 {
 		return nil, nil
 	}

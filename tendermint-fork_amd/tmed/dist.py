@@ -104,3 +104,46 @@ def verify_commit_sliced(engine, request: tuple, rank: int, world: int, device=N
 
     err = verify_commits(engine, [request], verifier=sliced)[0]
     return err, (seen[0] if seen else 0)
+
+
+def block_range(blocks: int, rank: int, world: int) -> tuple:
+    """Contiguous block heights [lo, hi) of `rank` for a blocksync replay (C4: 100k blocks / 8 GPUs)."""
+    return blocks * rank // world, blocks * (rank + 1) // world
+
+
+def aggregate_blocksync(ok_bits: np.ndarray, blocks: int, rank: int, world: int, verified: int, mismatches: int,
+                        seconds: float, extra_max=(), phases=(), device=None) -> dict:
+    """The only collectives of a sharded blocksync replay: ONE int64 all-reduce of
+    the tallies (blocks ok, blocks, signatures verified, outcome mismatches), a MAX of the ranks' seam
+    times (and of `extra_max`, e.g. marshalling times), ONE all-gather of the per-block decision
+    bitmaps (packed bits, every rank padded to the largest shard) and of the per-rank `phases`
+    (diagnostics).  ok_bits: this rank's blocks [lo, hi) of block_range.  Returns the same dict on
+    every rank; "ok_bits" is the whole chain's bitmap in height order."""
+    import torch
+    import torch.distributed as dist
+    dev = device if device is not None else torch.device("cpu")
+    lo, hi = block_range(blocks, rank, world)
+    assert ok_bits.shape[0] == hi - lo
+    tally = torch.tensor([int(ok_bits.sum()), hi - lo, int(verified), int(mismatches)], dtype=torch.int64, device=dev)
+    tmax = torch.tensor([float(seconds)] + [float(x) for x in extra_max], dtype=torch.float64, device=dev)
+    per = -(-blocks // world)  # the largest shard
+    bits = torch.from_numpy(np.packbits(np.pad(ok_bits.astype(np.uint8), (0, per - (hi - lo))))).to(dev)
+    ph = torch.tensor([float(x) for x in phases] + [float(seconds)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tally)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        gb = [torch.empty_like(bits) for _ in range(world)]
+        dist.all_gather(gb, bits)
+        gp = [torch.empty_like(ph) for _ in range(world)]
+        dist.all_gather(gp, ph)
+    else:
+        gb, gp = [bits], [ph]
+    full = []
+    for r in range(world):
+        a, b = block_range(blocks, r, world)
+        full.append(np.unpackbits(gb[r].cpu().numpy())[:b - a])
+    ok, nb, ver, mism = (int(x) for x in tally.tolist())
+    tm = tmax.tolist()
+    return {"blocks_ok": ok, "blocks": nb, "verified": ver, "mismatches": mism, "seconds": tm[0],
+            "extra_max": tm[1:], "ok_bits": np.concatenate(full) if full else np.zeros(0, np.uint8),
+            "phases": [g.tolist() for g in gp]}

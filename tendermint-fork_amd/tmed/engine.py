@@ -199,6 +199,47 @@ class Engine:
         if rc != TMED_OK:
             raise TmedError(rc, "tmed_keyset_free")
 
+    def keyset_extend(self, handle: int, pubs: np.ndarray) -> int:
+        """Append keys to a key set (tmed_keyset_extend); returns the first new key's index."""
+        pubs = np.ascontiguousarray(pubs, dtype=np.uint8).reshape(-1, 32)
+        first = ctypes.c_uint32(0)
+        rc = lib().tmed_keyset_extend(self._h, handle, _p(pubs), pubs.shape[0], ctypes.byref(first))
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_keyset_extend")
+        return first.value
+
+    # ---- the commit seam's key-set cache (tmed_keycache_*) -------------------
+    KEYCACHE_FIELDS = ("enabled", "budget_bytes", "lookups", "hits", "keyed_sets", "generic_sets", "keyed_sigs",
+                       "generic_sigs", "keys_appended", "keys_deferred", "pool_resets", "sets_evicted", "pool_keys",
+                       "pool_capacity_keys", "pool_bytes", "pool_a_window_bits", "sets_cached", "pending_keys")
+
+    def keycache_config(self, enabled: bool | None = None, budget_bytes: int = 0) -> None:
+        en = -1 if enabled is None else (1 if enabled else 0)
+        rc = lib().tmed_keycache_config(self._h, en, int(budget_bytes))
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_keycache_config")
+
+    def keycache_stats(self) -> dict:
+        out = (ctypes.c_uint64 * len(self.KEYCACHE_FIELDS))()
+        rc = lib().tmed_keycache_stats(self._h, out)
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_keycache_stats")
+        return {k: int(out[i]) for i, k in enumerate(self.KEYCACHE_FIELDS)}
+
+    def keycache_flush(self) -> None:
+        rc = lib().tmed_keycache_flush(self._h)
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_keycache_flush")
+
+    def keycache_warm(self, vals) -> None:
+        """Build a ValidatorSet's missing keys into the cache now (tmed_keycache_warm)."""
+        from .types import _valset_c
+        keep = []
+        vs = _valset_c(vals, keep)
+        rc = lib().tmed_keycache_warm(self._h, ctypes.byref(vs))
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_keycache_warm")
+
     def verify_keyset_arrays(self, handle: int, val_idx: np.ndarray, sigs: np.ndarray, msgs: np.ndarray,
                              offs: np.ndarray, sig_lens: np.ndarray | None = None) -> np.ndarray:
         n = val_idx.shape[0]

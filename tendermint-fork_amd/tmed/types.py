@@ -123,8 +123,9 @@ class ValidatorSet:
     validators: List[Validator]
     _total: int = field(default=0, repr=False)
     _packed: Optional[tuple] = field(default=None, repr=False)
-    keyset: int = field(default=0, repr=False)                       # tmed_keyset_load handle (0 = none)
+    keyset: int = field(default=0, repr=False)                       # tmed_keyset_load handle (0: the key-set cache)
     keyset_index: Optional[np.ndarray] = field(default=None, repr=False)  # validator -> key-set index (u32)
+    set_hash: Optional[bytes] = field(default=None, repr=False)      # ValidatorSet.Hash() (key-set cache key)
 
     def size(self) -> int:
         return len(self.validators)
@@ -226,7 +227,7 @@ class _BlockIDC(ctypes.Structure):
 class _ValsetC(ctypes.Structure):
     _fields_ = [("n", ctypes.c_size_t), ("pubkeys", ctypes.c_void_p), ("powers", ctypes.c_void_p),
                 ("addresses", ctypes.c_void_p), ("total_power", ctypes.c_int64), ("keyset", ctypes.c_uint64),
-                ("keyset_index", ctypes.c_void_p)]
+                ("keyset_index", ctypes.c_void_p), ("set_hash", ctypes.c_void_p)]
 
 
 class _CommitC(ctypes.Structure):
@@ -332,6 +333,20 @@ def _commit_c(c, keep):
                     _ptr(nan), _ptr(sigs), _ptr(lens), _ptr(alens))
 
 
+def _valset_c(vals: ValidatorSet, keep) -> _ValsetC:
+    """tmed_valset of a ValidatorSet (its packed arrays, handle, key-set index and set_hash)."""
+    pubs, powers, addrs = vals.packed()
+    kidx = getattr(vals, "keyset_index", None)
+    sh = getattr(vals, "set_hash", None)
+    if sh is not None and len(sh) != 32:
+        raise ValueError("set_hash must be ValidatorSet.Hash() (32 bytes)")
+    sh = None if sh is None else bytes(sh)
+    keep.extend([pubs, powers, addrs, kidx, sh])
+    return _ValsetC(len(vals.validators), _ptr(pubs), _ptr(powers), _ptr(addrs), vals.total_voting_power(),
+                    getattr(vals, "keyset", 0) or 0, None if kidx is None else _ptr(kidx),
+                    None if sh is None else ctypes.cast(ctypes.c_char_p(sh), ctypes.c_void_p))
+
+
 def _to_error(code, r: _ResultC, vals: ValidatorSet, block_id, commit: Commit):
     if code == 0:
         return None
@@ -366,15 +381,15 @@ class PreparedBatch:
         n = len(self.requests)
         self.n = n
         self.reqs = (_RequestC * max(n, 1))()
+        vcs = {}  # one tmed_valset per ValidatorSet object (the seam resolves each set once)
         for q, (mode, vals, chain_id, block_id, height, commit, num, den) in enumerate(self.requests):
-            pubs, powers, addrs = vals.packed()
-            kidx = getattr(vals, "keyset_index", None)
-            vs = _ValsetC(len(vals.validators), _ptr(pubs), _ptr(powers), _ptr(addrs), vals.total_voting_power(),
-                          getattr(vals, "keyset", 0) or 0, None if kidx is None else _ptr(kidx))
+            vs = vcs.get(id(vals))
+            if vs is None:
+                vs = vcs[id(vals)] = _valset_c(vals, self.keep)
             cc = _commit_c(commit, self.keep)
             cid = chain_id.encode()
             bid = _block_id_c(block_id, self.keep) if block_id is not None else None
-            self.keep.extend([vs, cc, cid, bid, kidx, pubs, powers, addrs])
+            self.keep.extend([vs, cc, cid, bid, vals])
             self.reqs[q] = _RequestC(mode, cid, len(cid), ctypes.pointer(vs),
                                      ctypes.pointer(bid) if bid is not None else None, height, ctypes.pointer(cc),
                                      num, den)
@@ -424,11 +439,7 @@ def verify_commits(engine, requests: Sequence[tuple], verifier=None, stats: Opti
     n = len(requests)
     reqs = (_RequestC * max(n, 1))()
     for q, (mode, vals, chain_id, block_id, height, commit, num, den) in enumerate(requests):
-        pubs, powers, addrs = vals.packed()
-        kidx = getattr(vals, "keyset_index", None)
-        vs = _ValsetC(len(vals.validators), _ptr(pubs), _ptr(powers), _ptr(addrs), vals.total_voting_power(),
-                      getattr(vals, "keyset", 0) or 0, None if kidx is None else _ptr(kidx))
-        keep.append(kidx)
+        vs = _valset_c(vals, keep)
         cc = _commit_c(commit, keep)
         cid = chain_id.encode()
         bid = _block_id_c(block_id, keep) if block_id is not None else None
@@ -477,11 +488,7 @@ class BlocksyncWindow:
         n = len(commits)
         self.n, self.vals, self.block_ids, self.commits = n, vals, list(block_ids), list(commits)
         self.keep = []
-        pubs, powers, addrs = vals.packed()
-        kidx = getattr(vals, "keyset_index", None)
-        self.vs = _ValsetC(len(vals.validators), _ptr(pubs), _ptr(powers), _ptr(addrs), vals.total_voting_power(),
-                           getattr(vals, "keyset", 0) or 0, None if kidx is None else _ptr(kidx))
-        self.keep.extend([pubs, powers, addrs, kidx])
+        self.vs = _valset_c(vals, self.keep)
         self.bids = (_BlockIDC * max(n, 1))()
         self.ccs = (_CommitC * max(n, 1))()
         for h in range(n):

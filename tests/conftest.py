@@ -11,6 +11,10 @@ for p in (ROOT, PKG):
         sys.path.insert(0, p)
 
 
+# the test suite fixes ZIP-215 batch weights (tmed_zip215_set_seed refuses otherwise)
+os.environ.setdefault("TMED_ZIP215_TEST_SEED", "1")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) device")
     config.addinivalue_line("markers", "slow: long-running CPU test")
@@ -34,15 +38,21 @@ def golden():
 
 @pytest.fixture(scope="session")
 def engine():
+    """The shared test context, with the seam's key-set cache OFF: a set without a handle takes the
+    generic kernels on every call, so each test exercises the path it names (the cache itself is
+    tested on its own contexts: tests/test_gpu_keycache.py)."""
     from tmed import Engine
     e = Engine(0)
+    e.keycache_config(False)
     yield e
     e.close()
 
 
 def engine_with_env(**env):
-    """A second context created with TMED_* overrides (read by tmed_init only)."""
+    """A second context created with TMED_* overrides (read by tmed_init only); the key-set cache
+    is off unless TMED_KEYCACHE is given."""
     from tmed import Engine
+    env.setdefault("TMED_KEYCACHE", 0)
     old = {k: os.environ.get(k) for k in env}
     os.environ.update({k: str(v) for k, v in env.items()})
     try:

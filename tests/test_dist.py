@@ -117,3 +117,60 @@ def test_index_sliced_commit_matches_reference_loop(world):
             assert got == want, (rank, got, want)
             kinds.add("ok" if e is None else type(e).__name__)
     assert len(kinds) >= 3, kinds  # ok, wrong-signature and not-enough-power cases all crossed slices
+
+
+def _blocksync_worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "tendermint-fork_amd"), os.path.join(ROOT, "tests")]
+    import torch.distributed as dist
+    from tmed.dist import aggregate_blocksync, block_range
+    from tmed.types import verify_commits
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    reqs = _light_blocks()
+    lo, hi = block_range(len(reqs), rank, world)
+    stats = []
+    errs = verify_commits(None, reqs[lo:hi], verifier=_verifier, stats=stats) if hi > lo else []
+    ok_bits = np.array([e is None for e in errs], np.uint8)
+    agg = aggregate_blocksync(ok_bits, len(reqs), rank, world, sum(stats), mismatches=rank,
+                              seconds=1.0 + rank, extra_max=[0.25 * (rank + 1)], phases=[10.0 * rank, 1.0, 2.0])
+    q.put((rank, agg["blocks_ok"], agg["blocks"], agg["verified"], agg["mismatches"], agg["seconds"],
+           agg["extra_max"], agg["ok_bits"].tolist(), agg["phases"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _light_blocks():
+    """Blocksync-shaped requests (VerifyCommitLight per block) from the seeded commit scenarios."""
+    import tmed.types as T
+    from commit_cases import pbid, scenarios
+    return [(T.MODE_LIGHT, pv, chain, pbid(bid), h, pc, num, den)
+            for mode, vs, pv, chain, bid, h, cm, pc, num, den in scenarios(seed=23, count=60) if mode == T.MODE_LIGHT]
+
+
+@pytest.mark.parametrize("world", [2])
+def test_blocksync_aggregation_matches_single_process(world):
+    """bench.py's C4 collectives (tmed.dist.aggregate_blocksync): contiguous block ranges per rank,
+    ONE int64 all-reduce of (blocks ok, blocks, verified, mismatches), a MAX of the seam (and
+    marshal) times, ONE all-gather of the packed decision bitmaps — equal to one process verifying
+    every block (stub verifier: the C port)."""
+    from tmed.types import verify_commits
+    reqs = _light_blocks()
+    assert len(reqs) >= 5
+    stats = []
+    single = np.array([e is None for e in verify_commits(None, reqs, verifier=_verifier, stats=stats)], np.uint8)
+    assert 0 < single.sum() < len(reqs)  # ok and failing blocks both present
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_blocksync_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok, nb, ver, mism, sec, extra, bits, phases in res:
+        assert (ok, nb, ver) == (int(single.sum()), len(reqs), sum(stats))
+        assert mism == sum(range(world)) and sec == 1.0 + (world - 1) and extra == [0.25 * world]
+        assert bits == single.tolist()
+        assert [p[0] for p in phases] == [10.0 * r for r in range(world)] and all(p[-1] == 1.0 + r for r, p in enumerate(phases))
