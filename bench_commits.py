@@ -117,8 +117,7 @@ def c1(eng, reps: int, cpu: bool, first_sets: int = 30):
         p2.run(eng)
         firsts.append(time.perf_counter() - t0)
         assert p2.codes()[0] == 0
-        torch.cuda.synchronize()  # the queued key build finishes before the next block's commit
-    time.sleep(0.05)
+        eng.keycache_wait()  # the queued key build finishes before the next block's commit
     out["first_call_after_set_change"] = summary(np.array(firsts) * 1e3)
     out["first_call_after_set_change"]["generic_calls"] = eng.keycache_stats()["generic_sets"] - gen_before
     eng.keycache_config(False)
@@ -249,6 +248,7 @@ def c3(eng, headers: int, gap: int, policy: str = "cache", runs: int = 7, bisect
     t0 = time.perf_counter()
     pb.run(eng)  # cold (cache: generic kernels, keys queued)
     t_cold = time.perf_counter() - t0
+    eng.keycache_wait()
     t0 = time.perf_counter()
     pb.run(eng)  # warm-up (cache: first keyed call, radix-2^10 combs built)
     t_warm = time.perf_counter() - t0
@@ -445,6 +445,7 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
             dist.barrier()
         for _ in range(2 if wins else 0):  # untimed warmup (see below)
             wins[0][2].run(eng, batch)
+            eng.keycache_wait()
         for w0, w1, win, exp, _ in wins:
             run(w0, w1, win, exp)
         del wins
@@ -459,6 +460,7 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
                 # first call runs generic and queues the keys, the second builds the radix-2^10 combs
                 for _ in range(2):
                     win.run(eng, batch)
+                    eng.keycache_wait()
             run(w0, w1, win, exp)
             del win, commits
     nbatch = -(-(hi - lo) // batch) if batch else 0

@@ -305,8 +305,8 @@ typedef struct {
  * of the ordered keys, and compared key by key on every hit.  On a miss: a set whose keys are all in
  * the pool is keyed at once; a call whose own signatures pay for building the missing keys (>= 2048
  * per key: a blocksync window, a light-client batch) builds them first and is keyed; otherwise the
- * call runs the generic kernels and the missing keys are built right after it, so the next call
- * against that set is keyed (C1: the first VerifyCommit after a set change is generic, the rest
+ * call runs the generic kernels and the missing keys are built right after it by a worker thread of
+ * the context (off the caller's critical path), so the next call against that set is keyed (C1: the first VerifyCommit after a set change is generic, the rest
  * are cache hits).  Decisions are identical either way.
  *   enabled: 1 on, 0 off (sets without a handle stay generic), -1 unchanged (default on; env
  *            TMED_KEYCACHE=0 turns it off at tmed_init);
@@ -326,6 +326,9 @@ typedef struct {
   uint64_t sets_cached, pending_keys;
 } tmed_keycache_counters;
 int tmed_keycache_stats(tmed_ctx *ctx, tmed_keycache_counters *out);
+/* Wait until the keys queued by generic calls are built (the context's build worker is idle and
+ * the device has finished): the next call against those sets is keyed.  Tests and benches. */
+int tmed_keycache_wait(tmed_ctx *ctx);
 /* Drop every cached set and the pool (TMED_EINVAL while a call is using it). */
 int tmed_keycache_flush(tmed_ctx *ctx);
 /* Build a set's missing keys now (e.g. at a validator-set change, before its first commit), so

@@ -617,15 +617,19 @@ static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_resul
   auto us = [](clock::time_point a, clock::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
   const auto t0 = clock::now();
   PhaseClock clk;
-  Plans plans;
-  std::vector<Cand> cands;
+  // per-thread planning buffers kept across calls: a light-client batch plans ~1.8M candidates
+  // (~60 MB of plans, parts and candidates), and fresh buffers cost a page fault per 4 KB on every
+  // call — the planner's threads then serialise on the kernel's page-table lock
+  thread_local Plans plans;
+  thread_local std::vector<Cand> cands;
+  thread_local std::vector<uint8_t> valid;
   int rc = seam_plan(reqs, n, out, plans, cands);
   if (rc != TMED_OK) return rc;
   clk.lap("plan");
   const auto t1 = clock::now();
   // ---- one device batch for every candidate of every request
   const size_t m = cands.size();
-  std::vector<uint8_t> valid(m, 0);
+  valid.assign(m, 0);
   if (m) {
     rc = verify(reqs, n, cands, valid.data());
     if (rc != TMED_OK) return rc;
@@ -885,121 +889,140 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
 // the call then runs on copies of its requests whose sets point into the cache's pool (keyset =
 // the pool, keyset_index = the set's entry).  The call pins the pool from its first lookup until
 // this object dies, after the call's last batch was collected; then the keys that generic sets of
-// the call queued are built (asynchronously, in stream order: the next call finds them).
+// the call queued are built by the context's key-build worker (keycache.hip), off this call's
+// critical path, in stream order ahead of later calls.
 struct KcCall {
   tmed_ctx *c = nullptr;
   std::vector<tmed_commit_request> reqs;
-  std::deque<tmed_valset> vals;  // stable addresses for reqs[q].vals
+  std::vector<tmed_valset> vals;  // copies of the resolved sets (reqs[q].vals points here)
   std::vector<std::shared_ptr<const tmed::KcSet>> holds;
   ~KcCall() {
     if (!c) return;
     std::lock_guard<std::mutex> lk(c->mu);
     tmed::keycache_unpin(c);
-    (void)tmed::keycache_drain(c);  // a failed build leaves those sets generic
+    tmed::keycache_after_call(c);  // the context's worker builds the queued keys
   }
 };
 
 static const tmed_commit_request *keycache_resolve(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
                                                    KcCall &kc) {
   if (!ctx->kc_on || n == 0 || !reqs) return reqs;
+  PhaseClock clk;
   struct SetRef {
-    const uint8_t *pubs;
-    size_t n;
-    const uint8_t *hash;
+    const tmed_valset *v;
     size_t sigs = 0;
     tmed::KcKey key;
     std::shared_ptr<const tmed::KcSet> hold;
     bool hit = false;
     uint64_t handle = 0;
   };
+  // distinct tmed_valset structs of the call (requests on one struct share its resolution), by a
+  // flat open-addressing table of pointers: a light-client batch has ~20k requests on ~10k sets
   std::vector<SetRef> sets;
   std::vector<int32_t> set_of(n, -1);
-  std::unordered_map<const uint8_t *, std::vector<int32_t>> by_pubs;  // distinct (keys, size, set_hash)
+  size_t cap = 16;
+  while (cap < 2 * n) cap <<= 1;
+  std::vector<const tmed_valset *> tkey(cap, nullptr);
+  std::vector<int32_t> tval(cap, -1);
   size_t keys = 0;
+  const tmed_valset *prev = nullptr;
+  int32_t prev_s = -1;
   for (size_t q = 0; q < n; q++) {
     const tmed_commit_request &r = reqs[q];
     if (!r.vals || r.vals->keyset || r.vals->n == 0 || !r.vals->pubkeys || !r.commit) continue;
-    const tmed_valset &v = *r.vals;
-    std::vector<int32_t> &cand = by_pubs[v.pubkeys];
-    int32_t s = -1;
-    for (int32_t k : cand)
-      if (sets[k].n == v.n && sets[k].hash == v.set_hash) { s = k; break; }
-    if (s < 0) {
-      s = (int32_t)sets.size();
-      cand.push_back(s);
-      SetRef sr;
-      sr.pubs = v.pubkeys;
-      sr.n = v.n;
-      sr.hash = v.set_hash;
-      sets.push_back(sr);
-      keys += v.n;
+    int32_t s = prev_s;
+    if (r.vals != prev) {
+      size_t h = (size_t)(((uintptr_t)r.vals >> 4) * 0x9E3779B97F4A7C15ull >> 20) & (cap - 1);
+      while (tkey[h] && tkey[h] != r.vals) h = (h + 1) & (cap - 1);
+      if (!tkey[h]) {
+        tkey[h] = r.vals;
+        tval[h] = (int32_t)sets.size();
+        SetRef sr;
+        sr.v = r.vals;
+        sets.push_back(sr);
+        keys += r.vals->n;
+      }
+      s = tval[h];
+      prev = r.vals;
+      prev_s = s;
     }
     sets[s].sigs += r.commit->n_sigs;
     set_of[q] = s;
   }
   if (sets.empty()) return reqs;
+  clk.lap("sets");
   const unsigned nt = host_threads(keys);
   parallel_ranges(sets.size(), nt, [&](size_t lo, size_t hi, unsigned) {
-    for (size_t s = lo; s < hi; s++) sets[s].key = tmed::kc_key(sets[s].pubs, sets[s].n, sets[s].hash);
+    for (size_t s = lo; s < hi; s++) sets[s].key = tmed::kc_key(sets[s].v->pubkeys, sets[s].v->n, sets[s].v->set_hash);
   });
+  clk.lap("digests");
   {
     std::lock_guard<std::mutex> lk(ctx->mu);
     kc.c = ctx;
     tmed::keycache_pin(ctx);
     for (SetRef &sr : sets) sr.hold = tmed::keycache_find(ctx, sr.key);
   }
+  clk.lap("find");
   // cached entries are compared with the sets' keys outside the lock (a light-client batch holds
   // ~10k sets); the pinned pool keeps their indexes valid
   parallel_ranges(sets.size(), nt, [&](size_t lo, size_t hi, unsigned) {
     for (size_t s = lo; s < hi; s++)
-      sets[s].hit = sets[s].hold && tmed::kc_same_keys(*sets[s].hold, sets[s].pubs, sets[s].n);
+      sets[s].hit = sets[s].hold && tmed::kc_same_keys(*sets[s].hold, sets[s].v->pubkeys, sets[s].v->n);
   });
+  clk.lap("compare");
   bool any_keyed = false;
+  size_t misses = 0;
   {
     std::lock_guard<std::mutex> lk(ctx->mu);
+    const uint64_t pool = tmed::keycache_pool_handle(ctx);
     for (SetRef &sr : sets)
       if (sr.hit) {
         tmed::keycache_hit(ctx, sr.sigs);
-        sr.handle = tmed::keycache_pool_handle(ctx);
+        sr.handle = pool;
         any_keyed = true;
+      } else {
+        misses++;
       }
-    // the call's signatures against every key it lacks: a window / batch that pays for them all
-    // builds them before its kernels (each set alone may carry too few signatures)
-    size_t call_sigs = 0, call_missing = 0;
-    std::unordered_set<tmed::Pub32, tmed::Pub32Hash> seen;
-    for (SetRef &sr : sets)
-      if (!sr.hit) {
-        call_sigs += sr.sigs;
-        call_missing += tmed::keycache_missing(ctx, sr.pubs, sr.n, &seen);
-      }
-    const bool build_all = call_missing && call_sigs >= tmed::kKcAmortizeSigsPerKey * call_missing;
-    for (SetRef &sr : sets) {
-      if (sr.hit) continue;
-      sr.hold.reset();
-      if (tmed::keycache_lookup(ctx, sr.pubs, sr.n, sr.key, sr.sigs, /*may_reset=*/!any_keyed, &sr.handle, sr.hold,
-                                build_all)) {
-        sr.hit = true;
-        any_keyed = true;
+    if (misses) {
+      // the call's signatures against every key it lacks: a window / batch that pays for them all
+      // builds them before its kernels (each set alone may carry too few signatures)
+      size_t call_sigs = 0, call_missing = 0;
+      std::unordered_set<tmed::Pub32, tmed::Pub32Hash> seen;
+      for (SetRef &sr : sets)
+        if (!sr.hit) {
+          call_sigs += sr.sigs;
+          call_missing += tmed::keycache_missing(ctx, sr.v->pubkeys, sr.v->n, &seen);
+        }
+      const bool build_all = call_missing && call_sigs >= tmed::kKcAmortizeSigsPerKey * call_missing;
+      for (SetRef &sr : sets) {
+        if (sr.hit) continue;
+        sr.hold.reset();
+        if (tmed::keycache_lookup(ctx, sr.v->pubkeys, sr.v->n, sr.key, sr.sigs, /*may_reset=*/!any_keyed, &sr.handle,
+                                  sr.hold, build_all)) {
+          sr.hit = true;
+          any_keyed = true;
+        }
       }
     }
   }
+  clk.lap("lookups");
   if (!any_keyed) return reqs;
-  kc.reqs.assign(reqs, reqs + n);
-  std::unordered_map<const tmed_valset *, tmed_valset *> copy_of;
-  for (size_t q = 0; q < n; q++) {
-    if (set_of[q] < 0 || !sets[set_of[q]].hit) continue;
-    const SetRef &sr = sets[set_of[q]];
-    tmed_valset *&cp = copy_of[reqs[q].vals];
-    if (!cp) {
-      kc.vals.push_back(*reqs[q].vals);
-      cp = &kc.vals.back();
-      cp->keyset = sr.handle;
-      cp->keyset_index = sr.hold->idx.data();
-    }
-    kc.reqs[q].vals = cp;
+  kc.vals.resize(sets.size());
+  for (size_t s = 0; s < sets.size(); s++) {
+    SetRef &sr = sets[s];
+    if (!sr.hit) continue;
+    kc.vals[s] = *sr.v;
+    kc.vals[s].keyset = sr.handle;
+    kc.vals[s].keyset_index = sr.hold->idx.data();
   }
+  kc.reqs.assign(reqs, reqs + n);
+  for (size_t q = 0; q < n; q++)
+    if (set_of[q] >= 0 && sets[set_of[q]].hit) kc.reqs[q].vals = &kc.vals[set_of[q]];
+  kc.holds.reserve(sets.size());
   for (SetRef &sr : sets)
     if (sr.hit) kc.holds.push_back(std::move(sr.hold));
+  clk.lap("rewrite");
+  clk.emit("keycache_resolve", n, sets.size());
   return kc.reqs.data();
 }
 
@@ -1064,9 +1087,24 @@ struct BsBatch {
 constexpr int kPipeSlots = 3;
 static_assert(kPipeSlots <= (int)(sizeof(((tmed_ctx *)nullptr)->vslot) / sizeof(tmed::VoteSlot)),
               "one context vote slot per pipeline slot");
+// Batch sizes of a pipelined call: the first batch's host planning and copy-in are exposed (the
+// device waits for them), so a call of at least four full batches ramps up with 1/8, 1/4 and 1/2
+// batches first — the device starts ~2.5 ms earlier on a C4 window and the copies of the larger
+// batches that follow overlap the small batches' kernels (tools/r04/c4_timeline.py).
+static size_t ramp_size(size_t idx, size_t bsz, size_t nb) {
+  if (nb < 4 * bsz || bsz < 64 || idx >= 3) return bsz;
+  return bsz >> (3 - idx);
+}
+
 static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t nb, size_t bsz, uint64_t keyset,
                          tmed_commit_result *out) {
-  BsBatch slots[kPipeSlots];
+  // kept per thread across calls, as run_seam's planning buffers (a blocksync window plans batch
+  // after batch into the same pages)
+  thread_local BsBatch slots[kPipeSlots];
+  for (BsBatch &b : slots) {
+    b.n = 0;
+    b.device = false;
+  }
   int ns = 2;  // raised to 3 after batch 0 when its signatures went direct
   int rc = TMED_OK;
   // tmed_seam_phase_us for a pipelined call: host plan + templates + staging, host time blocked on
@@ -1107,7 +1145,7 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
     BsBatch &mid = slots[(idx + ns - 1) % ns];  // batch idx-1 (in flight; with two slots the same as old)
     BsBatch &old = slots[(idx + 1) % ns];       // batch idx-ns+1: collected once batch idx is queued
     b.lo = lo;
-    b.n = std::min(bsz, nb - lo);
+    b.n = std::min(ramp_size(idx, bsz, nb), nb - lo);
     lo += b.n;
     const tmed_commit_request *rq = reqs + b.lo;
     const auto tp = clock::now();

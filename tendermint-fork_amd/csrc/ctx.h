@@ -98,6 +98,7 @@ void keycache_hit(tmed_ctx *c, size_t sigs);                               // Ke
 bool keycache_lookup(tmed_ctx *c, const uint8_t *pubs, size_t n, const KcKey &key, size_t sigs, bool may_reset,
                      uint64_t *handle, std::shared_ptr<const KcSet> &hold, bool force_build = false);
 int keycache_drain(tmed_ctx *c);  // build the keys queued behind generic calls (asynchronously)
+void keycache_after_call(tmed_ctx *c);  // wake the context's key-build worker when keys are queued
 size_t keycache_missing(tmed_ctx *c, const uint8_t *pubs, size_t n, std::unordered_set<Pub32, Pub32Hash> *seen);
 
 // Commit-seam device path (f1): stage votes (key refs, signatures, per-commit templates,
@@ -210,6 +211,7 @@ struct tmed_ctx {
   tmed::DevBuf d_merkle_a, d_merkle_b, d_merkle_idx;  // Merkle level digests (ping-pong) + level indexes
   tmed::DevBuf d_korder;  // key-grouped order of a key-cached batch: counts / cursors + permutation
   tmed::DevBuf d_zip;     // ZIP-215 batch mode scratch (zip215.hip zip_bufs: points, digits, sort, buckets)
+  bool zip_dense = false; // ZIP-215: the last chunk's failures were dense (zip215.hip: probe the next one first)
   std::unordered_map<uint64_t, tmed::Keyset> keysets;
   uint64_t next_keyset = 1;
   tmed::KeyCacheDev *kc = nullptr;  // key-set cache of the commit seam (keycache.hip), created at first use

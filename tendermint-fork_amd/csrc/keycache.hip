@@ -4,6 +4,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <thread>
 
 #include "ctx.h"
 #include "keycache.h"
@@ -41,9 +43,52 @@ struct KcBackendDev {
   }
 };
 
+// The keys a generic call queued are built by a worker thread of the context after the call has
+// returned, so the first call against a new set costs what a generic call costs (the build's
+// uploads and launches, ~30 us of host time, stay off the caller's critical path).  The worker
+// takes ctx->mu like any call; tmed_keycache_wait joins it.
 struct KeyCacheDev {
   KeyCache<KcBackendDev> kc;
-  explicit KeyCacheDev(tmed_ctx *c) : kc(KcBackendDev{c, 0}) {}
+  std::mutex wm;  // worker state (never held together with ctx->mu by the caller side)
+  std::condition_variable wcv;
+  bool want = false, busy = false, stop = false;
+  std::thread worker;
+  explicit KeyCacheDev(tmed_ctx *c) : kc(KcBackendDev{c, 0}) {
+    worker = std::thread([this, c] {
+      std::unique_lock<std::mutex> lk(wm);
+      for (;;) {
+        wcv.wait(lk, [&] { return want || stop; });
+        if (stop) return;
+        want = false;
+        busy = true;
+        lk.unlock();
+        {
+          std::lock_guard<std::mutex> g(c->mu);
+          (void)kc.drain_pending();  // a failed build leaves those sets generic
+        }
+        lk.lock();
+        busy = false;
+        wcv.notify_all();
+      }
+    });
+  }
+  void kick() {
+    std::lock_guard<std::mutex> lk(wm);
+    want = true;
+    wcv.notify_all();
+  }
+  void wait_idle() {
+    std::unique_lock<std::mutex> lk(wm);
+    wcv.wait(lk, [&] { return !want && !busy; });
+  }
+  ~KeyCacheDev() {
+    {
+      std::lock_guard<std::mutex> lk(wm);
+      stop = true;
+      wcv.notify_all();
+    }
+    worker.join();
+  }
 };
 
 static KeyCache<KcBackendDev> &cache_of(tmed_ctx *c) {
@@ -51,11 +96,16 @@ static KeyCache<KcBackendDev> &cache_of(tmed_ctx *c) {
   return c->kc->kc;
 }
 
-void keycache_destroy(tmed_ctx *c) {
+void keycache_destroy(tmed_ctx *c) {  // ctx->mu not held: the worker may be waiting for it
   if (!c->kc) return;
-  c->kc->kc.reset();
-  delete c->kc;
-  c->kc = nullptr;
+  KeyCacheDev *d = c->kc;
+  d->wait_idle();
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->kc = nullptr;
+  }
+  delete d;  // joins the worker
+  // the pool's Keyset is freed with the context's key sets
 }
 
 // ---- the seam's side (commit.hip keycache_resolve); the caller holds ctx->mu -----------------
@@ -77,6 +127,9 @@ size_t keycache_missing(tmed_ctx *c, const uint8_t *pubs, size_t n, std::unorder
   return cache_of(c).missing_keys(pubs, n, seen);
 }
 int keycache_drain(tmed_ctx *c) { return c->kc ? c->kc->kc.drain_pending() : TMED_OK; }
+void keycache_after_call(tmed_ctx *c) {
+  if (c->kc && c->kc->kc.pending_keys()) c->kc->kick();
+}
 
 }  // namespace tmed
 
@@ -129,8 +182,22 @@ int tmed_keycache_stats(tmed_ctx *c, tmed_keycache_counters *o) {
   return TMED_OK;
 }
 
+int tmed_keycache_wait(tmed_ctx *c) {
+  if (!c) return TMED_EINVAL;
+  KeyCacheDev *d;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    d = c->kc;
+  }
+  if (d) d->wait_idle();
+  std::lock_guard<std::mutex> lk(c->mu);
+  (void)hipSetDevice(c->device);
+  return map_err(hipStreamSynchronize(c->stream));
+}
+
 int tmed_keycache_flush(tmed_ctx *c) {
   if (!c) return TMED_EINVAL;
+  if (c->kc) c->kc->wait_idle();
   std::lock_guard<std::mutex> lk(c->mu);
   if (!c->kc) return TMED_OK;
   if (c->kc->kc.users() > 0) return TMED_EINVAL;  // a call in flight holds indexes into the pool

@@ -872,6 +872,36 @@ int zip215_verify_device(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, co
     e = hipMemcpyAsync(z.seed, seed, 32, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return map_err(e);
     g_zip_stats[0]++;
+    // Failure-density cut-off: after a chunk whose failures were dense (both halves of a failing
+    // equation failed again), the next chunk first checks a kZipProbe-signature sample (~1 ms: the
+    // MSM's fixed cost); if the sample fails too the chunk is decided signature by signature with no
+    // full-chunk prep or MSM (C5's 1 % failures put ~40 in every sample).  A passing sample resumes
+    // batch verification.  The decision of every signature is the single-check one either way.
+    constexpr uint32_t kZipProbe = 4096;
+    if (c->zip_dense && N >= 4 * kZipProbe) {
+      const uint32_t pb = (kZipProbe + kThreadsPerBlock - 1) / kThreadsPerBlock;
+      e = launch_verify_prep(pub, sig, msgs, off, msg_slots, base, kZipProbe, c->d_prep, c->slab_slots, s);
+      if (e != hipSuccess) return map_err(e);
+      hipLaunchKernelGGL(zip_prep_r_kernel, dim3(pb), dim3(kThreadsPerBlock), 0, s, sig, base, kZipProbe, c->d_prep,
+                         c->slab_slots, z.seed, (uint64_t)base, z.pts, z.dig, z.cs, kZipMax, out);
+      e = zip_msm(c, z, kZipProbe, 0, kZipProbe, s);
+      if (e != hipSuccess) return map_err(e);
+      bool ok = false;
+      int rc = zip_read_flag(c, z, s, &ok);
+      if (rc != TMED_OK) return rc;
+      g_zip_stats[1]++;
+      if (!ok) {  // still dense: the whole chunk singly
+        g_zip_stats[2]++;
+        g_zip_stats[3] += N;
+        const uint8_t *gm = msg_slots ? msgs + (size_t)base * kVoteSlot : msgs;
+        e = launch_verify(pub + 32 * (size_t)base, sig + 64 * (size_t)base, gm, off + base, N, out + base, c->d_slab,
+                          c->slab_slots, BTabs{c->d_b16, c->d_bcomb16, c->d_b26}, c->d_prep, c->d_fin, c->d_fin_pre, s,
+                          c->chunk, 6, msg_slots, nullptr, /*zip215=*/true);
+        if (e != hipSuccess) return map_err(e);
+        continue;
+      }
+      c->zip_dense = false;
+    }
     // k, S checks, decode of A (the generic throughput path's prep), then the ZIP-215 prep
     const uint32_t blocks = (N + kThreadsPerBlock - 1) / kThreadsPerBlock;
     e = launch_verify_prep(pub, sig, msgs, off, msg_slots, base, N, c->d_prep, c->slab_slots, s);
@@ -883,6 +913,7 @@ int zip215_verify_device(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, co
     // >= kZipMinGroup; the remaining failing groups are decided signature by signature.
     constexpr uint32_t kZipMinGroup = 1u << 14;
     std::vector<std::pair<uint32_t, uint32_t>> level{{0u, N}}, single;
+    bool chunk_dense = false;
     while (!level.empty()) {
       std::vector<std::pair<uint32_t, uint32_t>> failed;
       for (auto &g : level) {
@@ -895,6 +926,7 @@ int zip215_verify_device(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, co
         if (!ok) failed.push_back(g);
       }
       const bool dense = level.size() >= 2 && failed.size() * 2 > level.size();
+      chunk_dense = chunk_dense || dense;
       std::vector<std::pair<uint32_t, uint32_t>> next;
       for (auto &g : failed) {
         if (!dense && g.second >= 2 * kZipMinGroup) {
@@ -907,6 +939,7 @@ int zip215_verify_device(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, co
       }
       level.swap(next);
     }
+    c->zip_dense = chunk_dense;
     for (auto &g : single) {  // the exact ZIP-215 single check on the group's signatures
       g_zip_stats[2]++;
       g_zip_stats[3] += g.second;

@@ -226,6 +226,12 @@ class Engine:
             raise TmedError(rc, "tmed_keycache_stats")
         return {k: int(out[i]) for i, k in enumerate(self.KEYCACHE_FIELDS)}
 
+    def keycache_wait(self) -> None:
+        """Block until the keys queued by generic calls are built (tmed_keycache_wait)."""
+        rc = lib().tmed_keycache_wait(self._h)
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_keycache_wait")
+
     def keycache_flush(self) -> None:
         rc = lib().tmed_keycache_flush(self._h)
         if rc != TMED_OK:

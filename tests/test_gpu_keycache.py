@@ -65,6 +65,7 @@ def test_c1_first_call_generic_then_keyed(cached):
     reqs, exp = _c1_requests(vals, bid, base)
     s0 = cached.keycache_stats()
     first = T.verify_commits(cached, [reqs[0]])[0]
+    cached.keycache_wait()  # the context's worker builds the queued keys after the call
     d = _delta(s0, cached.keycache_stats())
     assert _same(first, exp[0])
     assert d["generic_sets"] == 1 and d["keyed_sets"] == 0 and d["keys_deferred"] == 175
@@ -129,6 +130,7 @@ def test_c3_changing_sets_without_handles(cached):
     for call in range(3):
         s0 = cached.keycache_stats()
         got = T.verify_commits(cached, reqs)
+        cached.keycache_wait()
         d = _delta(s0, cached.keycache_stats())
         bad = [(q, str(got[q]), str(exp[q])) for q in range(len(reqs)) if not _same(got[q], exp[q])]
         assert not bad, (call, bad[:4])
@@ -141,13 +143,24 @@ def test_c3_changing_sets_without_handles(cached):
     assert isinstance(exp[10], C.ErrNotEnoughVotingPowerSigned)
     assert (exp[10].got, exp[10].needed) == (10 * (nv - far - gap), 583)
     assert cached.keycache_stats()["pool_keys"] == len(distinct)  # each key built once
-    # slide by two heights: two new sets (one new key each) stay generic once, the rest are hits
+    # slide by two heights: two new sets, whose keys the pool already holds (the far set 127 covers
+    # keys 127..301): keyed at once by pooled-key misses, the rest are hits, nothing is built
     reqs2, exp2 = batch(2, H + 2)
     s0 = cached.keycache_stats()
     got = T.verify_commits(cached, reqs2)
     d = _delta(s0, cached.keycache_stats())
     assert all(_same(got[q], exp2[q]) for q in range(len(reqs2)))
-    assert d["generic_sets"] == 2 and d["keyed_sets"] == d["lookups"] - 2
+    assert d["keyed_sets"] == d["lookups"] and d["hits"] == d["lookups"] - 2 and d["keys_appended"] == 0
+    # two heights further the sets bring keys no set had: generic once, built after the call
+    far_keys = {pool_pubs[i].tobytes() for i in range(far + 5 + gap, far + 5 + gap + nv)}
+    reqs3, exp3 = batch(far + 5 + gap - nv + 1 - gap, far + 5 + gap - nv + 1 - gap + 4)
+    assert len(far_keys) == nv
+    s0 = cached.keycache_stats()
+    got = T.verify_commits(cached, reqs3)
+    cached.keycache_wait()
+    d = _delta(s0, cached.keycache_stats())
+    assert all(_same(got[q], exp3[q]) for q in range(len(reqs3)))
+    assert d["generic_sets"] >= 1 and d["keys_deferred"] >= 1
 
 
 def test_blocksync_window_builds_its_keys_first(cached, engine):
@@ -187,6 +200,7 @@ def test_blocksync_window_builds_its_keys_first(cached, engine):
     w2 = T.BlocksyncWindow(vals2, CHAIN, bids[:2], heights[:2], commits[:2])  # signed by other keys: fails
     s0 = cached.keycache_stats()
     w2.run(cached, 0)
+    cached.keycache_wait()
     assert _delta(s0, cached.keycache_stats())["generic_sets"] == 1
     w2.run(cached, 0)
     assert _delta(s0, cached.keycache_stats())["keyed_sets"] == 1
@@ -219,6 +233,7 @@ def test_budget_resets_and_wrong_set_hash(cached):
         for _ in range(2):
             for (reqs, exp) in ((ra, ea), (rb, eb)):
                 got = T.verify_commits(cached, reqs)
+                cached.keycache_wait()
                 assert all(_same(got[q], exp[q]) for q in range(len(reqs)))
     finally:
         a[0].set_hash = b[0].set_hash = None

@@ -134,3 +134,33 @@ def test_c5_mix_vs_port(engine):
     # the default (Go 1.18) path on the same tuples is unchanged and differs where the rules do
     go = engine.verify_arrays(pubs, sigs, msgs, offs)
     assert int((go != port.verify_batch(pubs, sigs, msgs, offs.astype(np.uint64), 16)).sum()) == 0
+
+
+def test_dense_failures_cut_off():
+    """Failure-density cut-off (zip215.hip kZipProbe): after a chunk whose failures were dense (the
+    C5 mix: the equation and both halves fail), the next chunk checks a 4,096-signature sample first
+    and, when it fails too, is decided singly without the full prep and MSM; a passing sample
+    resumes batch verification.  Decisions equal the port's ZIP-215 bits on every call."""
+    from conftest import engine_with_env
+    from tmed import Engine
+    from tmed.workload import c5_mix
+    eng = engine_with_env()
+    try:
+        rng, pubs, sigs, msgs, offs = _signed_batch(eng, 70_000, 0xC5)
+        good_p, good_s = pubs.copy(), sigs.copy()
+        c5_mix(pubs, sigs, seed=0xC5)
+        exp = port.verify_batch(pubs, sigs, msgs, offs.astype(np.uint64), 16, zip215=True)
+        stats = []
+        for _ in range(2):
+            out = eng.verify_zip215_arrays(pubs, sigs, msgs, offs)
+            stats.append(Engine.zip215_stats())
+            assert int((out != exp).sum()) == 0
+        assert stats[0]["equations"] == 3 and stats[0]["single_sigs"] == 70_000, stats
+        assert stats[1]["equations"] == 1 and stats[1]["single_sigs"] == 70_000, stats
+        out = eng.verify_zip215_arrays(good_p, good_s, msgs, offs)  # the sample passes: batch mode again
+        st = Engine.zip215_stats()
+        assert out.all() and st["equations"] == 2 and st["single_sigs"] == 0, st
+        eng.verify_zip215_arrays(good_p, good_s, msgs, offs)
+        assert Engine.zip215_stats()["equations"] == 1
+    finally:
+        eng.close()
