@@ -153,6 +153,17 @@ __device__ __forceinline__ void prep_store(int4 *prep, uint32_t stride, uint32_t
     prep[(size_t)q * stride + slot] = make_int4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
 
+// The key-cached hand-off: only what verify_keyset_main_kernel reads (k, s in int4 0..3, ok at
+// word 36 = int4 9): 80 B per signature instead of the generic prep's 160 B.
+__device__ __forceinline__ void prep_store_ks(int4 *prep, uint32_t stride, uint32_t slot, const uint32_t k[8],
+                                              const uint32_t s[8], bool ok) {
+  prep[slot] = make_int4((int)k[0], (int)k[1], (int)k[2], (int)k[3]);
+  prep[(size_t)stride + slot] = make_int4((int)k[4], (int)k[5], (int)k[6], (int)k[7]);
+  prep[(size_t)2 * stride + slot] = make_int4((int)s[0], (int)s[1], (int)s[2], (int)s[3]);
+  prep[(size_t)3 * stride + slot] = make_int4((int)s[4], (int)s[5], (int)s[6], (int)s[7]);
+  prep[(size_t)9 * stride + slot] = make_int4(ok ? 1 : 0, 0, 0, 0);
+}
+
 __device__ __forceinline__ bool prep_load(const int4 *prep, uint32_t stride, uint32_t slot, uint32_t k[8],
                                           uint32_t s[8], ge_p3 &A) {
   int32_t w[40];
@@ -321,21 +332,34 @@ __global__ __launch_bounds__(kThreadsPerBlock, TMED_PREP_R_WAVES) void verify_pr
     int4 *__restrict__ prep2, uint32_t stride, uint32_t *__restrict__ place, int zip215) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
   if (slot >= count) return;
+  // R's decode first (the sqrt-ratio chain), then k and s from the hand-off for the lattice step:
+  // nothing of the hand-off is live across the chain, so the kernel fits 3 waves/SIMD unspilled
+  uint32_t Rw[8];
+  load_row_words(Rw, sig + 64 * (size_t)(base + slot), 2);
+  fe Rx, Ry;
+  bool rok;
+  if (zip215) {
+    ge_p3 P;
+    rok = ge_frombytes_go(P, Rw);
+    fe_copy(Rx, P.X);
+    fe_copy(Ry, P.Y);
+  } else {
+    rok = r_decode_strict(Rx, Ry, Rw);
+  }
+  if (!rok) { fe_0(Rx); fe_1(Ry); }
   int32_t w[64];
 #pragma unroll
   for (int q = 0; q < 4; q++) {  // k (words 0-7), s (8-15)
     const int4 v = prep[(size_t)q * stride + slot];
     w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
   }
-  const bool ok = prep[(size_t)9 * stride + slot].x != 0;  // word 36
-  uint32_t k[8], s[8], Rw[8], cr[8], dr[8], er[8];
+  uint32_t k[8], s[8], cr[8], dr[8], er[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) { k[j] = (uint32_t)w[j]; s[j] = (uint32_t)w[8 + j]; }
-  load_row_words(Rw, sig + 64 * (size_t)(base + slot), 2);
-  fe Rx, Ry;
   bool dneg;
   int W;
-  const bool rok = hs_prep_r(k, s, Rw, cr, dr, er, dneg, Rx, Ry, W, zip215 != 0, /*raw_e=*/true);
+  hs_scalars(k, s, cr, dr, er, dneg, W, /*raw_e=*/true);  // (hs_prep_r's two phases, in this order)
+  const bool ok = prep[(size_t)9 * stride + slot].x != 0;  // word 36
 #pragma unroll
   for (int j = 0; j < 8; j++) { w[j] = (int32_t)cr[j]; w[13 + j] = (int32_t)er[j]; }
 #pragma unroll
@@ -937,9 +961,7 @@ __global__ __launch_bounds__(kThreadsPerBlock, TMED_KS_PREP_WAVES) void verify_k
   uint32_t mlen;
   ms.get(i, m, mlen);
   const bool ok = verify_prep_comb(pw, vin && key_ok[v] != 0, sw, m, mlen, k, s, ms.slots);  // slots: hashed from dwordx4 loads (sha512_stream_slot)
-  ge_p3 dummy;
-  ge_p3_0(dummy);
-  prep_store(prep, stride, slot, k, s, dummy, ok);
+  prep_store_ks(prep, stride, slot, k, s, ok);
 }
 
 // Key-cached Straus with the next comb row in flight (TMED_KS_PF): the 48 rows a signature
