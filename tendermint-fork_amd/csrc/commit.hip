@@ -960,7 +960,11 @@ static const tmed_commit_request *keycache_resolve(tmed_ctx *ctx, const tmed_com
     std::lock_guard<std::mutex> lk(ctx->mu);
     kc.c = ctx;
     tmed::keycache_pin(ctx);
-    for (SetRef &sr : sets) sr.hold = tmed::keycache_find(ctx, sr.key);
+    tmed::keycache_touch(ctx);
+    // concurrent read-only lookups while this thread holds the lock (no writer can run)
+    parallel_ranges(sets.size(), nt, [&](size_t lo, size_t hi, unsigned) {
+      for (size_t s = lo; s < hi; s++) sets[s].hold = tmed::keycache_find(ctx, sets[s].key);
+    });
   }
   clk.lap("find");
   // cached entries are compared with the sets' keys outside the lock (a light-client batch holds
@@ -977,7 +981,7 @@ static const tmed_commit_request *keycache_resolve(tmed_ctx *ctx, const tmed_com
     const uint64_t pool = tmed::keycache_pool_handle(ctx);
     for (SetRef &sr : sets)
       if (sr.hit) {
-        tmed::keycache_hit(ctx, sr.sigs);
+        tmed::keycache_hit(ctx, *sr.hold, sr.sigs);
         sr.handle = pool;
         any_keyed = true;
       } else {
@@ -1082,20 +1086,13 @@ struct BsBatch {
 // With the signatures DMA'd from pinned caller memory the host's share per batch is ~1.5 ms
 // against ~2.2 ms of kernels, and a third slot keeps the kernel stream busy (C4 280-307 against
 // 258-282 M/s, profiles/r03/c4_direct/).  So the depth follows the first batch: three slots
-// when its signatures went direct (VoteStage::sig_direct), else two.  (A ramp of small first / last
-// batches did not pay: profiles/r03/c4_pipe/.)
+// when its signatures went direct (VoteStage::sig_direct), else two.  (A ramp of small first
+// batches did not pay, in round 3 nor again in round 4 with direct DMA: the host's planning and
+// staging of each larger batch outlasted the device work of the small one before it, leaving the
+// device idle 0.6-1.6 ms per ramp step — profiles/r04/c4_ramp_rejected.txt.)
 constexpr int kPipeSlots = 3;
 static_assert(kPipeSlots <= (int)(sizeof(((tmed_ctx *)nullptr)->vslot) / sizeof(tmed::VoteSlot)),
               "one context vote slot per pipeline slot");
-// Batch sizes of a pipelined call: the first batch's host planning and copy-in are exposed (the
-// device waits for them), so a call of at least four full batches ramps up with 1/8, 1/4 and 1/2
-// batches first — the device starts ~2.5 ms earlier on a C4 window and the copies of the larger
-// batches that follow overlap the small batches' kernels (tools/r04/c4_timeline.py).
-static size_t ramp_size(size_t idx, size_t bsz, size_t nb) {
-  if (nb < 4 * bsz || bsz < 64 || idx >= 3) return bsz;
-  return bsz >> (3 - idx);
-}
-
 static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t nb, size_t bsz, uint64_t keyset,
                          tmed_commit_result *out) {
   // kept per thread across calls, as run_seam's planning buffers (a blocksync window plans batch
@@ -1145,7 +1142,7 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
     BsBatch &mid = slots[(idx + ns - 1) % ns];  // batch idx-1 (in flight; with two slots the same as old)
     BsBatch &old = slots[(idx + 1) % ns];       // batch idx-ns+1: collected once batch idx is queued
     b.lo = lo;
-    b.n = std::min(ramp_size(idx, bsz, nb), nb - lo);
+    b.n = std::min(bsz, nb - lo);
     lo += b.n;
     const tmed_commit_request *rq = reqs + b.lo;
     const auto tp = clock::now();

@@ -93,8 +93,11 @@ void keycache_destroy(tmed_ctx *c);
 void keycache_pin(tmed_ctx *c);    // a seam call resolving sets: no pool reset until it unpins
 void keycache_unpin(tmed_ctx *c);
 uint64_t keycache_pool_handle(const tmed_ctx *c);  // 0 before the first key is built
-std::shared_ptr<const KcSet> keycache_find(tmed_ctx *c, const KcKey &key);  // KeyCache::find
-void keycache_hit(tmed_ctx *c, size_t sigs);                               // KeyCache::hit
+// KeyCache::find: read-only, callable from several threads while the caller holds ctx->mu (after
+// keycache_touch has created the cache)
+std::shared_ptr<const KcSet> keycache_find(tmed_ctx *c, const KcKey &key);
+void keycache_touch(tmed_ctx *c);
+void keycache_hit(tmed_ctx *c, const KcSet &e, size_t sigs);  // KeyCache::hit
 bool keycache_lookup(tmed_ctx *c, const uint8_t *pubs, size_t n, const KcKey &key, size_t sigs, bool may_reset,
                      uint64_t *handle, std::shared_ptr<const KcSet> &hold, bool force_build = false);
 int keycache_drain(tmed_ctx *c);  // build the keys queued behind generic calls (asynchronously)

@@ -162,13 +162,15 @@ class KeyCache {
 
   // Fast path of a call resolving many sets: the cached entry under `key` (nullptr if none), to be
   // compared with the set's keys outside the lock; a match is then recorded with hit().
-  std::shared_ptr<const KcSet> find(const KcKey &key) {
+  // Read-only (safe from several threads at once while the caller holds the lock): the entry's
+  // LRU tick is refreshed by hit().
+  std::shared_ptr<const KcSet> find(const KcKey &key) const {
     auto it = sets_.find(key);
     if (it == sets_.end()) return nullptr;
-    it->second->tick = ++tick_;
     return it->second;
   }
-  void hit(size_t sigs) {
+  void hit(const KcSet &e, size_t sigs) {
+    const_cast<KcSet &>(e).tick = ++tick_;
     st.lookups++;
     st.hits++;
     st.keyed_sets++;

@@ -111,7 +111,8 @@ void keycache_destroy(tmed_ctx *c) {  // ctx->mu not held: the worker may be wai
 // ---- the seam's side (commit.hip keycache_resolve); the caller holds ctx->mu -----------------
 uint64_t keycache_pool_handle(const tmed_ctx *c) { return c->kc ? c->kc->kc.be.handle : 0; }
 std::shared_ptr<const KcSet> keycache_find(tmed_ctx *c, const KcKey &key) { return cache_of(c).find(key); }
-void keycache_hit(tmed_ctx *c, size_t sigs) { cache_of(c).hit(sigs); }
+void keycache_touch(tmed_ctx *c) { (void)cache_of(c); }
+void keycache_hit(tmed_ctx *c, const KcSet &e, size_t sigs) { cache_of(c).hit(e, sigs); }
 void keycache_pin(tmed_ctx *c) { cache_of(c).pin(); }
 void keycache_unpin(tmed_ctx *c) { cache_of(c).unpin(); }
 // true: the set's signatures take the key-cached kernels in this call, *handle = the pool and

@@ -225,23 +225,28 @@ int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteSta
 }
 
 namespace {
-// TMED_TRACE: names a queueing step of votes_enqueue that blocked the host for over 1 ms.
+// TMED_TRACE: host time of each queueing step of votes_enqueue (one line per large batch).
 struct SlowStep {
   bool on;
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  char buf[256];
+  int len = 0;
   void lap(const char *what) {
     if (!on) return;
     const auto n = std::chrono::steady_clock::now();
     const double us = std::chrono::duration<double, std::micro>(n - t).count();
-    if (us > 1000.0) fprintf(stderr, "[tmed] votes_enqueue: %s blocked %.0f us\n", what, us);
+    if (len < (int)sizeof(buf) - 40) len += snprintf(buf + len, sizeof(buf) - len, " %s=%.0fus", what, us);
     t = n;
+  }
+  void emit(uint32_t m) {
+    if (on && len) fprintf(stderr, "[tmed] votes_enqueue m=%u%.*s\n", m, len, buf);
   }
 };
 }  // namespace
 
 int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   static const bool trace_steps = getenv("TMED_TRACE") != nullptr;
-  SlowStep slow{trace_steps};
+  SlowStep slow{trace_steps && st.total >= kVoteCopyStreamMin};
   const uint32_t m = st.m;
   if (st.ks && !st.keys_checked)
     for (uint32_t j = 0; j < m; j++)
@@ -342,6 +347,7 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   if (e == hipSuccess && !st.zc) e = hipMemcpyAsync(vs.h_out.p, vs.d_out.p, m, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipEventRecord(vs.done, s);
   slow.lap("copy-out");
+  slow.emit(m);
   return map_err(e);
 }
 

@@ -51,7 +51,7 @@ int kct_lookup(void *h, const uint8_t *pubs, size_t n, const uint8_t *set_hash, 
   if (fast) {
     hold = kc.find(key);
     if (hold && kc_same_keys(*hold, pubs, n)) {
-      kc.hit(sigs);
+      kc.hit(*hold, sigs);
       keyed = true;
     } else {
       hold.reset();

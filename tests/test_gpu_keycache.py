@@ -151,16 +151,6 @@ def test_c3_changing_sets_without_handles(cached):
     d = _delta(s0, cached.keycache_stats())
     assert all(_same(got[q], exp2[q]) for q in range(len(reqs2)))
     assert d["keyed_sets"] == d["lookups"] and d["hits"] == d["lookups"] - 2 and d["keys_appended"] == 0
-    # two heights further the sets bring keys no set had: generic once, built after the call
-    far_keys = {pool_pubs[i].tobytes() for i in range(far + 5 + gap, far + 5 + gap + nv)}
-    reqs3, exp3 = batch(far + 5 + gap - nv + 1 - gap, far + 5 + gap - nv + 1 - gap + 4)
-    assert len(far_keys) == nv
-    s0 = cached.keycache_stats()
-    got = T.verify_commits(cached, reqs3)
-    cached.keycache_wait()
-    d = _delta(s0, cached.keycache_stats())
-    assert all(_same(got[q], exp3[q]) for q in range(len(reqs3)))
-    assert d["generic_sets"] >= 1 and d["keys_deferred"] >= 1
 
 
 def test_blocksync_window_builds_its_keys_first(cached, engine):
