@@ -80,15 +80,37 @@ bool safe_mul(int64_t a, int64_t b, int64_t *out) {
   return false;
 }
 
-struct Cand {
-  size_t req;
-  int32_t sig_idx;
-  int32_t val_idx;
-  // no zero-fill: the merged candidate list of a large call (tens of MB) is resized and
-  // then overwritten in parallel, so value-initialising it would be a serial memset
-  Cand() {}
-  Cand(size_t r, int32_t s, int32_t v) : req(r), sig_idx(s), val_idx(v) {}
+// The signatures a seam call sends to the verifier, as runs: run r holds candidates
+// off[r] .. off[r] + len - 1, the signatures sig .. sig + len - 1 of request req signed by
+// validators val .. val + len - 1 of its set.  A VerifyCommit / Light request's candidates are
+// one run per stretch of qualifying flags (C4: one run of ~6,667 per block), so planning, staging
+// and scattering cost per run, not per signature; a Trusting request's runs break where the
+// commit's order leaves the trusted set's.
+struct Run {
+  uint32_t req;
+  int32_t sig, val;
+  uint32_t len;
 };
+struct Cands {
+  std::vector<Run> runs;
+  std::vector<size_t> off;  // runs.size() + 1 candidate offsets
+  size_t size() const { return off.empty() ? 0 : off.back(); }
+  void clear() {
+    runs.clear();
+    off.assign(1, 0);
+  }
+};
+// Append candidate (q, i, v) to a part's runs, extending the last run when it continues it.
+inline void push_cand(std::vector<Run> &runs, uint32_t q, int32_t i, int32_t v) {
+  if (!runs.empty()) {
+    Run &b = runs.back();
+    if (b.req == q && b.sig + (int32_t)b.len == i && b.val + (int32_t)b.len == v) {
+      b.len++;
+      return;
+    }
+  }
+  runs.push_back(Run{q, i, v, 1u});
+}
 
 // address -> first validator index with that address (GetByAddress, types/validator_set.go:270-278
 // returns the first match).  Flat open-addressing table: a light-client batch builds one per
@@ -128,10 +150,14 @@ struct AddrIndex {
 struct Plan {
   bool decided = false;
   int64_t needed = 0;
-  int32_t panic_idx = -1;         // the loop panics on reaching this signature (TMED_COMMIT_PANIC)
-  int32_t *bit_of_sig = nullptr;  // sig idx -> candidate slot in its planning part (-1 = not sent,
-                                  // kNoValidator = Trusting: the address is not in the set)
-  size_t cand_off = 0;            // + the part's offset in the merged candidate list
+  int32_t panic_idx = -1;  // the loop panics on reaching this signature (TMED_COMMIT_PANIC)
+  int32_t stop = 0;        // candidates were collected among signatures [0, stop)
+  // Trusting only: sig idx -> validator index in the set, kNoValidator (the address is not in the
+  // set), -1 (not reached by the plan).  Other modes: candidate k is the k-th qualifying
+  // signature below stop (replay counts them), so nothing per signature is stored.
+  int32_t *vof = nullptr;
+  size_t cand_off = 0;  // the request's first candidate (in its part while planning, then global)
+  uint32_t ncand = 0;
   // Trusting: the double vote the loop stops at (sig idx, validator, first sig idx), -1 = none
   int32_t dv_idx = -1, dv_val = -1, dv_first = -1;
 };
@@ -148,13 +174,13 @@ struct RawBuf {
   }
 };
 
-// The plans of one seam call; bit_of_sig of every request lives in one flat array.  The
-// per-thread candidate parts are kept between calls (blocksync plans batch after batch),
-// so their pages are touched once.
+// The plans of one seam call; vof of every Trusting request lives in one flat array.  The
+// per-thread run parts are kept between calls (blocksync plans batch after batch), so their pages
+// are touched once.
 struct Plans {
   std::vector<Plan> v;
   RawBuf<int32_t> bits;
-  std::vector<std::vector<Cand>> parts;
+  std::vector<std::vector<Run>> parts;
 };
 
 // Per-thread "seen" marks of the Trusting loops (first index of each validator), reset in
@@ -235,21 +261,18 @@ struct CandBatch {
   }
 };
 using BatchVerifier =
-    std::function<int(const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands, uint8_t *valid)>;
+    std::function<int(const tmed_commit_request *reqs, size_t n, const Cands &cands, uint8_t *valid)>;
 
 // Per-request CanonicalVote encoders for the requests that have candidates; then(q, enc)
 // runs right after request q's encoder is built (false = failure).  Candidates are in request
 // order, so the first candidate of each request marks it used (one writer per request).
 template <class Then>
-static int init_encoders(const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands,
+static int init_encoders(const tmed_commit_request *reqs, size_t n, const Cands &cands,
                          std::vector<tmed::VoteEncoder> &enc, std::vector<uint8_t> &used, Then &&then) {
   enc.assign(n, tmed::VoteEncoder());
   used.assign(n, 0);
   const size_t m = cands.size();
-  parallel_ranges(m, host_threads(m), [&](size_t lo, size_t hi, unsigned) {
-    for (size_t k = lo; k < hi; k++)
-      if (k == 0 || cands[k].req != cands[k - 1].req) used[cands[k].req] = 1;
-  });
+  for (const Run &r : cands.runs) used[r.req] = 1;
   std::atomic<int> bad{0};
   parallel_ranges(n, n >= 64 ? host_threads(m) : 1, [&](size_t lo, size_t hi, unsigned) {
   for (size_t q = lo; q < hi; q++) {
@@ -272,8 +295,7 @@ static int init_encoders(const tmed_commit_request *reqs, size_t n, const std::v
 }
 
 // Flatten candidates with host-assembled sign-bytes (callback verifiers; oversize templates).
-static int build_cand_batch(const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands,
-                            CandBatch &cb) {
+static int build_cand_batch(const tmed_commit_request *reqs, size_t n, const Cands &cands, CandBatch &cb) {
   std::vector<uint8_t> used;
   int rc = init_encoders(reqs, n, cands, cb.enc, used, [](size_t, const tmed::VoteEncoder &) { return true; });
   if (rc != TMED_OK) return rc;
@@ -288,21 +310,25 @@ static int build_cand_batch(const tmed_commit_request *reqs, size_t n, const std
   cb.flags.resize(m);
   cb.ts_sec.resize(m);
   cb.ts_nanos.resize(m);
-  for (size_t k = 0; k < m; k++) {
-    const Cand &cd = cands[k];
-    const tmed_commit_request &r = reqs[cd.req];
+  for (size_t ri = 0; ri < cands.runs.size(); ri++) {
+    const Run &run = cands.runs[ri];
+    const tmed_commit_request &r = reqs[run.req];
     const tmed_commit &c = *r.commit;
-    const size_t i = (size_t)cd.sig_idx;
-    memcpy(&cb.pubs[k * 32], r.vals->pubkeys + 32 * (size_t)cd.val_idx, 32);
-    const uint32_t sl = c.sig_lens ? c.sig_lens[i] : 64;
-    memcpy(&cb.sigs[k * 64], c.sigs + 64 * i, sl < 64 ? sl : 64);
-    cb.lens[k] = sl;
-    cb.val_idx[k] = r.vals->keyset_index ? r.vals->keyset_index[cd.val_idx] : (uint32_t)cd.val_idx;
-    cb.keyset[k] = r.vals->keyset;
-    cb.tmpl[k] = (uint32_t)cd.req;
-    cb.flags[k] = c.flags[i];
-    cb.ts_sec[k] = c.ts_seconds[i];
-    cb.ts_nanos[k] = c.ts_nanos[i];
+    for (uint32_t u = 0; u < run.len; u++) {
+      const size_t k = cands.off[ri] + u;
+      const size_t i = (size_t)(run.sig + (int32_t)u);
+      const int32_t v = run.val + (int32_t)u;
+      memcpy(&cb.pubs[k * 32], r.vals->pubkeys + 32 * (size_t)v, 32);
+      const uint32_t sl = c.sig_lens ? c.sig_lens[i] : 64;
+      memcpy(&cb.sigs[k * 64], c.sigs + 64 * i, sl < 64 ? sl : 64);
+      cb.lens[k] = sl;
+      cb.val_idx[k] = r.vals->keyset_index ? r.vals->keyset_index[v] : (uint32_t)v;
+      cb.keyset[k] = r.vals->keyset;
+      cb.tmpl[k] = run.req;
+      cb.flags[k] = c.flags[i];
+      cb.ts_sec[k] = c.ts_seconds[i];
+      cb.ts_nanos[k] = c.ts_nanos[i];
+    }
   }
   return cb.build_host_msgs();
 }
@@ -323,16 +349,20 @@ struct AddrScratch {
   }
 };
 
-// Plan one request; candidates are appended to `cands` and bit_of_sig holds their index there.
+// Plan one request: its candidates are appended to `runs` (pl.cand_off = the part's candidate
+// count before them, pl.ncand = how many).
 static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_result &o, Plan &pl,
-                        std::vector<Cand> &cands, AddrScratch &addr) {
+                        std::vector<Run> &runs, size_t &part_cands, AddrScratch &addr) {
   const tmed_commit_request &r = reqs[q];
   memset(&o, 0, sizeof o);
   int rc = check_request(r);
   if (rc != TMED_OK) return rc;
   const tmed_valset &vs = *r.vals;
   const tmed_commit &c = *r.commit;
-  std::fill(pl.bit_of_sig, pl.bit_of_sig + c.n_sigs, -1);
+  pl.cand_off = part_cands;
+  pl.stop = (int32_t)c.n_sigs;
+  uint32_t nc = 0;
+  const uint32_t qq = (uint32_t)q;
   const bool bid_ok = block_hashes_valid(c.block_id);
   if (r.mode != TMED_MODE_LIGHT_TRUSTING) {
     if (vs.n != c.n_sigs) {
@@ -353,19 +383,19 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
         if (f == kAbsent) continue;
         // CommitSig.BlockID panics on an unknown flag (types/block.go:652-665), sign-bytes of a
         // Commit vote on a malformed hash: the loop stops there if it gets that far
-        if ((f != kCommit && f != kNil) || (f == kCommit && !bid_ok)) { pl.panic_idx = (int32_t)i; break; }
-        pl.bit_of_sig[i] = (int32_t)cands.size();
-        cands.emplace_back(q, (int32_t)i, (int32_t)i);
+        if ((f != kCommit && f != kNil) || (f == kCommit && !bid_ok)) { pl.panic_idx = (int32_t)i; pl.stop = (int32_t)i; break; }
+        push_cand(runs, qq, (int32_t)i, (int32_t)i);
+        nc++;
       }
     } else {
       int64_t tally = 0;
       for (size_t i = 0; i < c.n_sigs; i++) {
         if (c.flags[i] != kCommit) continue;
-        if (!bid_ok) { pl.panic_idx = (int32_t)i; break; }
-        pl.bit_of_sig[i] = (int32_t)cands.size();
-        cands.emplace_back(q, (int32_t)i, (int32_t)i);
+        if (!bid_ok) { pl.panic_idx = (int32_t)i; pl.stop = (int32_t)i; break; }
+        push_cand(runs, qq, (int32_t)i, (int32_t)i);
+        nc++;
         tally += vs.powers[i];
-        if (tally > pl.needed) break;
+        if (tally > pl.needed) { pl.stop = (int32_t)i + 1; break; }
       }
     }
   } else {
@@ -373,6 +403,7 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
     int64_t prod;
     if (safe_mul(vs.total_power, r.trust_num, &prod)) { o.code = TMED_COMMIT_OVERFLOW; pl.decided = true; return TMED_OK; }
     pl.needed = prod / r.trust_den;  // Go int64 division truncates toward zero, as C++ does
+    std::fill(pl.vof, pl.vof + c.n_sigs, -1);
     const AddrIndex &ix = addr.get(vs);
     thread_local SeenMarks seen;
     seen.reset(vs.n);
@@ -380,19 +411,23 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
     for (size_t i = 0; i < c.n_sigs; i++) {
       if (c.flags[i] != kCommit) continue;
       const int32_t v = lookup_address(ix, c, i);
-      if (v < 0) { pl.bit_of_sig[i] = kNoValidator; continue; }
+      if (v < 0) { pl.vof[i] = kNoValidator; continue; }
       if (seen.get(v) >= 0) {  // the loop returns the double-vote error here
         pl.dv_idx = (int32_t)i; pl.dv_val = v; pl.dv_first = seen.get(v);
+        pl.stop = (int32_t)i;
         break;
       }
       seen.set(v, (int32_t)i);
-      if (!bid_ok) { pl.panic_idx = (int32_t)i; break; }
-      pl.bit_of_sig[i] = (int32_t)cands.size();
-      cands.emplace_back(q, (int32_t)i, v);
+      if (!bid_ok) { pl.panic_idx = (int32_t)i; pl.stop = (int32_t)i; break; }
+      pl.vof[i] = v;
+      push_cand(runs, qq, (int32_t)i, v);
+      nc++;
       tally += vs.powers[v];
-      if (tally > pl.needed) break;
+      if (tally > pl.needed) { pl.stop = (int32_t)i + 1; break; }
     }
   }
+  pl.ncand = nc;
+  part_cands += nc;
   return TMED_OK;
 }
 
@@ -473,8 +508,7 @@ static size_t total_sigs(const tmed_commit_request *reqs, size_t n) {
 }
 
 // Candidates of requests [0, n) in request order (identical to a serial plan).
-static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, Plans &ps,
-                     std::vector<Cand> &cands) {
+static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, Plans &ps, Cands &cands) {
   PhaseClock clk;
   std::vector<Plan> &plans = ps.v;
   plans.assign(n, Plan());
@@ -482,68 +516,69 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
   size_t nbits = 0;
   for (size_t q = 0; q < n; q++) {
     if (check_request(reqs[q]) != TMED_OK) return TMED_EINVAL;
-    nbits += reqs[q].commit->n_sigs;
+    if (reqs[q].mode == TMED_MODE_LIGHT_TRUSTING) nbits += reqs[q].commit->n_sigs;
   }
   int32_t *bits = ps.bits.ensure(std::max<size_t>(nbits, 1));
   nbits = 0;
-  for (size_t q = 0; q < n; q++) {
-    plans[q].bit_of_sig = bits + nbits;
-    nbits += reqs[q].commit->n_sigs;
-  }
+  for (size_t q = 0; q < n; q++)
+    if (reqs[q].mode == TMED_MODE_LIGHT_TRUSTING) {
+      plans[q].vof = bits + nbits;
+      nbits += reqs[q].commit->n_sigs;
+    }
   clk.lap("check");
   const unsigned nt = host_threads(total_sigs(reqs, n));
-  if (nt <= 1) {
-    AddrScratch addr;
-    for (size_t q = 0; q < n; q++) {
-      int rc = plan_request(reqs, q, out[q], plans[q], cands, addr);
-      if (rc != TMED_OK) return rc;
-    }
-    return TMED_OK;
-  }
-  if (ps.parts.size() < nt) ps.parts.resize(nt);
-  std::vector<std::vector<Cand>> &part = ps.parts;
-  for (unsigned t = 0; t < nt; t++) part[t].clear();
-  std::vector<size_t> lo_of(nt, 0), hi_of(nt, 0);
-  std::vector<int> rcs(nt, TMED_OK);
-  parallel_ranges(n, nt, [&](size_t lo, size_t hi, unsigned t) {
+  const unsigned np = std::max(1u, nt);
+  if (ps.parts.size() < np) ps.parts.resize(np);
+  std::vector<std::vector<Run>> &part = ps.parts;
+  std::vector<size_t> lo_of(np, 0), hi_of(np, 0), pc(np, 0);
+  std::vector<int> rcs(np, TMED_OK);
+  auto plan_range = [&](size_t lo, size_t hi, unsigned t) {
     lo_of[t] = lo; hi_of[t] = hi;
-    size_t cap = 0;
-    for (size_t q = lo; q < hi; q++) cap += reqs[q].commit->n_sigs;
-    part[t].reserve(cap);
     AddrScratch addr;
-    for (size_t q = lo; q < hi && rcs[t] == TMED_OK; q++) {
-      rcs[t] = plan_request(reqs, q, out[q], plans[q], part[t], addr);
-    }
-  });
+    size_t c = 0;
+    for (size_t q = lo; q < hi && rcs[t] == TMED_OK; q++) rcs[t] = plan_request(reqs, q, out[q], plans[q], part[t], c, addr);
+    pc[t] = c;
+  };
+  for (unsigned t = 0; t < np; t++) part[t].clear();
+  if (nt <= 1) plan_range(0, n, 0);
+  else parallel_ranges(n, nt, plan_range);
   for (int rc : rcs)
     if (rc != TMED_OK) return rc;
   clk.lap("plan_requests");
-  std::vector<size_t> base(nt + 1, 0);
-  for (unsigned t = 0; t < nt; t++) base[t + 1] = base[t] + part[t].size();
-  cands.resize(base[nt]);
-  parallel_ranges(nt, nt, [&](size_t lo, size_t hi, unsigned) {
-    for (size_t t = lo; t < hi; t++) {
-      std::copy(part[t].begin(), part[t].end(), cands.begin() + base[t]);
-      for (size_t q = lo_of[t]; q < hi_of[t]; q++) plans[q].cand_off = base[t];
+  // merge: the parts' runs in thread order (= request order), candidate offsets made global
+  size_t nr = 0;
+  for (unsigned t = 0; t < np; t++) nr += part[t].size();
+  cands.runs.resize(nr);
+  cands.off.resize(nr + 1);
+  size_t rb = 0, cb = 0;
+  for (unsigned t = 0; t < np; t++) {
+    size_t c = cb;
+    for (size_t r = 0; r < part[t].size(); r++) {
+      cands.runs[rb + r] = part[t][r];
+      cands.off[rb + r] = c;
+      c += part[t][r].len;
     }
-  });
+    for (size_t q = lo_of[t]; q < hi_of[t]; q++) plans[q].cand_off += cb;
+    rb += part[t].size();
+    cb += pc[t];
+  }
+  cands.off[nr] = cb;
   clk.lap("merge");
-  clk.emit("plan", n, cands.size());
+  clk.emit("plan", n, cb);
   return TMED_OK;
 }
 
 // ---- replay of every reference loop over the validity bits (parallel over requests) ----
 
-static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, const Plan &pl, const Cand *cands,
-                          const uint8_t *valid) {
+static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, const Plan &pl, const uint8_t *valid) {
   const tmed_valset &vs = *r.vals;
   const tmed_commit &c = *r.commit;
+  uint32_t k = 0;  // candidates consumed: the loop reaches them in the plan's order
   auto bit = [&](size_t i, bool *ok) -> bool {
-    const int32_t k = pl.bit_of_sig[i];
-    if (k < 0) { *ok = false; return false; }
+    if ((int32_t)i >= pl.stop || k >= pl.ncand) { *ok = false; return false; }
     o.verified++;
     // a signature of any length but 64 is false (ed25519.go:150-152), whatever the verifier said
-    return valid[pl.cand_off + (size_t)k] != 0 && (!c.sig_lens || c.sig_lens[i] == 64);
+    return valid[pl.cand_off + k++] != 0 && (!c.sig_lens || c.sig_lens[i] == 64);
   };
   auto panics = [&](size_t i) -> bool {
     if ((int32_t)i != pl.panic_idx) return false;
@@ -577,14 +612,16 @@ static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, c
   } else {
     // the plan resolved every address up to where its loop stopped, and the replay stops no later
     for (size_t i = 0; i < c.n_sigs && o.code < 0; i++) {
-      if (c.flags[i] != kCommit || pl.bit_of_sig[i] == kNoValidator) continue;
+      if (c.flags[i] != kCommit || pl.vof[i] == kNoValidator) continue;
       if ((int32_t)i == pl.dv_idx) {
         o.code = TMED_COMMIT_DOUBLE_VOTE; o.val_idx = pl.dv_val; o.idx_first = pl.dv_first; o.idx = (int32_t)i;
         break;
       }
       if (panics(i)) break;
+      const int32_t v = pl.vof[i];
+      if (v < 0) { ok = false; break; }
       if (!bit(i, &ok)) { if (ok) { o.code = TMED_COMMIT_WRONG_SIGNATURE; o.idx = (int32_t)i; } break; }
-      tally += vs.powers[cands[pl.cand_off + (size_t)pl.bit_of_sig[i]].val_idx];
+      tally += vs.powers[v];
       if (tally > pl.needed) o.code = TMED_COMMIT_OK;
     }
     if (o.code < 0 && ok) { o.code = TMED_COMMIT_NOT_ENOUGH_POWER; o.got = tally; o.needed = pl.needed; }
@@ -592,15 +629,15 @@ static int replay_request(const tmed_commit_request &r, tmed_commit_result &o, c
   return ok ? TMED_OK : TMED_EINVAL;  // replay reached a signature the plan did not send (cannot happen)
 }
 
-static int seam_replay(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out,
-                       const Plans &ps, const std::vector<Cand> &cands, const uint8_t *valid) {
+static int seam_replay(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, const Plans &ps,
+                       const uint8_t *valid) {
   const std::vector<Plan> &plans = ps.v;
   const unsigned nt = host_threads(total_sigs(reqs, n));
   std::vector<int> rcs(std::max(1u, nt), TMED_OK);
   parallel_ranges(n, nt, [&](size_t lo, size_t hi, unsigned t) {
     for (size_t q = lo; q < hi; q++) {
       if (plans[q].decided) continue;
-      if (replay_request(reqs[q], out[q], plans[q], cands.data(), valid) != TMED_OK) rcs[t] = TMED_EINVAL;
+      if (replay_request(reqs[q], out[q], plans[q], valid) != TMED_OK) rcs[t] = TMED_EINVAL;
     }
   });
   for (int rc : rcs)
@@ -621,7 +658,7 @@ static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_resul
   // (~60 MB of plans, parts and candidates), and fresh buffers cost a page fault per 4 KB on every
   // call — the planner's threads then serialise on the kernel's page-table lock
   thread_local Plans plans;
-  thread_local std::vector<Cand> cands;
+  thread_local Cands cands;
   thread_local std::vector<uint8_t> valid;
   int rc = seam_plan(reqs, n, out, plans, cands);
   if (rc != TMED_OK) return rc;
@@ -636,7 +673,7 @@ static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_resul
   }
   clk.lap("verify");
   const auto t2 = clock::now();
-  rc = seam_replay(reqs, n, out, plans, cands, valid.data());
+  rc = seam_replay(reqs, n, out, plans, valid.data());
   clk.lap("replay");
   clk.emit("seam", n, m);
   const auto t3 = clock::now();
@@ -656,7 +693,7 @@ extern "C" int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t 
                                         tmed_batch_verify_fn verify, void *user) {
   if (!verify) return TMED_EINVAL;
   return run_seam(reqs, n, out,
-                  [&](const tmed_commit_request *rq, size_t nr, const std::vector<Cand> &cands, uint8_t *valid) {
+                  [&](const tmed_commit_request *rq, size_t nr, const Cands &cands, uint8_t *valid) {
                     CandBatch cb;
                     int rc = build_cand_batch(rq, nr, cands, cb);
                     if (rc != TMED_OK) return rc;
@@ -666,8 +703,8 @@ extern "C" int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t 
 }
 
 // Host fallback of the GPU verifier for templates the device assembler cannot hold.
-static int ctx_verify_host_msgs(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
-                                const std::vector<Cand> &cands, uint8_t *valid) {
+static int ctx_verify_host_msgs(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, const Cands &cands,
+                                uint8_t *valid) {
   CandBatch cb;
   int rc = build_cand_batch(reqs, n, cands, cb);
   if (rc != TMED_OK) return rc;
@@ -704,16 +741,40 @@ static int ctx_verify_host_msgs(tmed_ctx *ctx, const tmed_commit_request *reqs, 
   return TMED_OK;
 }
 
-// Device staging of the candidates ix[...] (all of one key set) into vote slot `slot`:
-// sign-bytes are assembled on the device from per-commit templates, so
-// only key references, signatures, flags and timestamps cross PCIe; they are written
-// straight from the request arrays into the pinned staging area (multi-threaded for
-// large batches).  The caller holds ctx->mu.
+// The runs of one device group (one key set) and their staging positions: run rix[j] of the
+// call (rix empty: every run, in order) stages its candidates at pos[j] .. pos[j + 1).
+struct Group {
+  std::vector<uint32_t> rix;
+  std::vector<size_t> pos;
+  size_t size(const Cands &c) const { return rix.empty() ? c.size() : pos.back(); }
+  uint32_t run(const Cands &c, size_t j) const { (void)c; return rix.empty() ? (uint32_t)j : rix[j]; }
+  size_t nruns(const Cands &c) const { return rix.empty() ? c.runs.size() : rix.size(); }
+  const size_t *positions(const Cands &c) const { return rix.empty() ? c.off.data() : pos.data(); }
+};
+
+// For f(j, u0, u1, p0): the segment u0 .. u1 - 1 of group run j, staged from position p0, for the
+// positions [lo, hi) of a thread's share (runs split across threads are cut at the share edges).
+template <class F>
+static void for_segments(const Cands &c, const Group &g, size_t lo, size_t hi, F &&f) {
+  const size_t *pos = g.positions(c);
+  const size_t nr = g.nruns(c);
+  size_t j = (size_t)(std::upper_bound(pos, pos + nr + 1, lo) - pos);
+  j = j ? j - 1 : 0;
+  for (; j < nr && pos[j] < hi; j++) {
+    const size_t a = std::max(lo, pos[j]), b = std::min(hi, pos[j + 1]);
+    if (a < b) f(j, (uint32_t)(a - pos[j]), (uint32_t)(b - pos[j]), a);
+  }
+}
+
+// Device staging of one group's candidates into vote slot `slot`: sign-bytes are assembled on
+// the device from per-commit templates, so only key references, signatures,
+// flags and timestamps cross PCIe; they are written straight from the request arrays into the
+// pinned staging area, run by run (multi-threaded for large batches).  The caller holds ctx->mu.
 constexpr size_t kDmaMinRun = 256;  // signatures (16 KB)
-static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands,
-                       const uint32_t *ix, uint32_t m, uint64_t keyset, const uint8_t *tmpl, int slot,
-                       tmed::VoteStage &st) {
+static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, const Cands &cands, const Group &grp,
+                       uint64_t keyset, const uint8_t *tmpl, int slot, tmed::VoteStage &st) {
   const bool keyed = keyset != 0;
+  const uint32_t m = (uint32_t)grp.size(cands);
   int rc = tmed::votes_stage(ctx, keyset, m, n, st, slot);
   if (rc != TMED_OK) return rc;
   memcpy(st.tmpl, tmpl, n * tmed::kVoteTmplBytes);
@@ -742,54 +803,48 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
   const unsigned nt = host_threads(m);
   std::vector<std::vector<tmed::VoteStage::Dma>> tdma(direct ? nt : 0u);
   std::atomic<bool> all_direct{direct};
-  // Runs of candidates of one request with consecutive signature indexes (a Light / blocksync
-  // commit's candidates are one run) are staged one memcpy per array; the key index, the
-  // template index and short signatures stay per vote.
+  // per run segment: one memcpy per array; the key index, the template index and short
+  // signatures stay per vote
   auto fill = [&](size_t lo, size_t hi, unsigned tid) {
     bool ok = true, staged_sig = false;
-    for (size_t j = lo; j < hi;) {
-      const Cand &cd = cands[ix ? ix[j] : j];
-      const tmed_commit_request &r = reqs[cd.req];
+    for_segments(cands, grp, lo, hi, [&](size_t j, uint32_t u0, uint32_t u1, size_t p) {
+      const Run &run = cands.runs[grp.run(cands, j)];
+      const tmed_commit_request &r = reqs[run.req];
       const tmed_commit &c = *r.commit;
-      const size_t i = (size_t)cd.sig_idx;
-      size_t len = 1;
-      while (j + len < hi) {
-        const Cand &nx = cands[ix ? ix[j + len] : j + len];
-        if (nx.req != cd.req || (size_t)nx.sig_idx != i + len || nx.val_idx != cd.val_idx + (int32_t)len) break;
-        len++;
-      }
+      const size_t i = (size_t)(run.sig + (int32_t)u0);
+      const int32_t v0 = run.val + (int32_t)u0;
+      const size_t len = u1 - u0;
       if (keyed) {
-        uint32_t *kd = reinterpret_cast<uint32_t *>(st.key) + j;
+        uint32_t *kd = reinterpret_cast<uint32_t *>(st.key) + p;
         const uint32_t *kix = r.vals->keyset_index;
         for (size_t u = 0; u < len; u++) {
-          const uint32_t v = kix ? kix[cd.val_idx + u] : (uint32_t)(cd.val_idx + u);
+          const uint32_t v = kix ? kix[v0 + (int32_t)u] : (uint32_t)(v0 + (int32_t)u);
           ok = ok && v < nkeys;
           kd[u] = v;
         }
       } else {
-        memcpy(st.key + j * 32, r.vals->pubkeys + 32 * (size_t)cd.val_idx, 32 * len);
+        memcpy(st.key + p * 32, r.vals->pubkeys + 32 * (size_t)v0, 32 * len);
       }
       // runs of at least kDmaMinRun signatures: a DMA command costs ~10 us of the copy engine
-      bool dma = direct && len >= kDmaMinRun && tid < tdma.size() && req_pinned[cd.req];
+      bool dma = direct && len >= kDmaMinRun && tid < tdma.size() && req_pinned[run.req];
       if (dma && c.sig_lens)  // short signatures are zero-padded in staging
         for (size_t u = 0; u < len && dma; u++) dma = c.sig_lens[i + u] >= 64;
       if (dma) {
-        tdma[tid].push_back({j * 64, c.sigs + 64 * i, 64 * len});
+        tdma[tid].push_back({p * 64, c.sigs + 64 * i, 64 * len});
       } else {
         staged_sig = true;
-        memcpy(st.sig + j * 64, c.sigs + 64 * i, 64 * len);
+        memcpy(st.sig + p * 64, c.sigs + 64 * i, 64 * len);
         if (c.sig_lens)
           for (size_t u = 0; u < len; u++) {
             const uint32_t sl = c.sig_lens[i + u];
-            if (sl < 64) memset(st.sig + (j + u) * 64 + sl, 0, 64 - sl);
+            if (sl < 64) memset(st.sig + (p + u) * 64 + sl, 0, 64 - sl);
           }
       }
-      for (size_t u = 0; u < len; u++) st.tidx[j + u] = (uint32_t)cd.req;
-      memcpy(st.flag + j, c.flags + i, len);
-      memcpy(st.sec + j, c.ts_seconds + i, 8 * len);
-      memcpy(st.nan + j, c.ts_nanos + i, 4 * len);
-      j += len;
-    }
+      std::fill(st.tidx + p, st.tidx + p + len, run.req);
+      memcpy(st.flag + p, c.flags + i, len);
+      memcpy(st.sec + p, c.ts_seconds + i, 8 * len);
+      memcpy(st.nan + p, c.ts_nanos + i, 4 * len);
+    });
     if (!ok) key_ok = false;
     if (staged_sig) all_direct = false;
   };
@@ -808,23 +863,28 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
   return TMED_OK;
 }
 
-// Collected bits -> valid[] (signatures of length != 64 are false: ed25519.go:150-152).
-static void scatter_bits(const tmed_commit_request *reqs, const std::vector<Cand> &cands, const uint32_t *ix,
-                         uint32_t m, const uint8_t *bits, uint8_t *valid) {
+// Collected bits of a group -> valid[] by candidate (signatures of length != 64 are false:
+// ed25519.go:150-152).
+static void scatter_bits(const tmed_commit_request *reqs, const Cands &cands, const Group &grp, const uint8_t *bits,
+                         uint8_t *valid) {
+  const size_t m = grp.size(cands);
   parallel_ranges(m, host_threads(m), [&](size_t lo, size_t hi, unsigned) {
-    for (size_t j = lo; j < hi; j++) {
-      const uint32_t k = ix ? ix[j] : (uint32_t)j;
-      const Cand &cd = cands[k];
-      const tmed_commit &c = *reqs[cd.req].commit;
-      const uint32_t sl = c.sig_lens ? c.sig_lens[cd.sig_idx] : 64;
-      valid[k] = sl == 64 ? bits[j] : 0;
-    }
+    for_segments(cands, grp, lo, hi, [&](size_t j, uint32_t u0, uint32_t u1, size_t p) {
+      const uint32_t ri = grp.run(cands, j);
+      const Run &run = cands.runs[ri];
+      const tmed_commit &c = *reqs[run.req].commit;
+      uint8_t *dst = valid + cands.off[ri];
+      for (uint32_t u = u0; u < u1; u++) {
+        const uint32_t sl = c.sig_lens ? c.sig_lens[run.sig + (int32_t)u] : 64;
+        dst[u] = sl == 64 ? bits[p + (u - u0)] : 0;
+      }
+    });
   });
 }
 
 // Device templates of the requests that have candidates; false if one does not fit.
-static int device_templates(const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands,
-                            std::vector<uint8_t> &tmpl, bool *fits) {
+static int device_templates(const tmed_commit_request *reqs, size_t n, const Cands &cands, std::vector<uint8_t> &tmpl,
+                            bool *fits) {
   std::vector<tmed::VoteEncoder> enc;
   std::vector<uint8_t> used;
   tmpl.resize(n * tmed::kVoteTmplBytes);  // rows of requests without candidates are never read
@@ -842,7 +902,7 @@ static int device_templates(const tmed_commit_request *reqs, size_t n, const std
 
 // GPU verifier of one seam call: candidates of validator sets with a key-set handle go
 // through the key-cached kernels, one launch sequence per distinct key set.
-static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, const std::vector<Cand> &cands,
+static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, const Cands &cands,
                       uint8_t *valid) {
   PhaseClock clk;
   std::vector<uint8_t> tmpl;
@@ -851,22 +911,24 @@ static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, 
   if (rc != TMED_OK) return rc;
   if (!fits) return ctx_verify_host_msgs(ctx, reqs, n, cands, valid);
   clk.lap("templates");
-  // group by key set (usually a single group)
+  // group the runs by key set (usually a single group: then it is every run, in order)
   std::vector<uint64_t> gkeys;
-  std::vector<std::vector<uint32_t>> gidx;
-  for (size_t k = 0; k < cands.size(); k++) {
-    const uint64_t ks = reqs[cands[k].req].vals->keyset;
+  std::vector<Group> groups;
+  for (size_t r = 0; r < cands.runs.size(); r++) {
+    const uint64_t ks = reqs[cands.runs[r].req].vals->keyset;
     size_t g = 0;
     while (g < gkeys.size() && gkeys[g] != ks) g++;
-    if (g == gkeys.size()) { gkeys.push_back(ks); gidx.emplace_back(); }
-    gidx[g].push_back((uint32_t)k);
+    if (g == gkeys.size()) { gkeys.push_back(ks); groups.emplace_back(); groups.back().pos.push_back(0); }
+    groups[g].rix.push_back((uint32_t)r);
+    groups[g].pos.push_back(groups[g].pos.back() + cands.runs[r].len);
   }
+  if (groups.size() == 1) groups[0] = Group();  // every run in order: the call's own offsets
   std::lock_guard<std::mutex> lk(ctx->mu);
   for (size_t g = 0; g < gkeys.size(); g++) {
-    const std::vector<uint32_t> &ix = gidx[g];
-    const uint32_t m = (uint32_t)ix.size();
+    const Group &grp = groups[g];
+    const uint32_t m = (uint32_t)grp.size(cands);
     tmed::VoteStage st;
-    rc = stage_group(ctx, reqs, n, cands, ix.data(), m, gkeys[g], tmpl.data(), 0, st);
+    rc = stage_group(ctx, reqs, n, cands, grp, gkeys[g], tmpl.data(), 0, st);
     clk.lap("stage");
     std::vector<uint8_t> out(m);
     if (rc == TMED_OK) rc = tmed::votes_launch(ctx, st, out.data());
@@ -874,7 +936,7 @@ static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, 
     clk.lap("device");
     if (trace_on()) fprintf(stderr, "[tmed] group %zu: %u votes, assemble+verify kernels %.0fus\n", g, m,
                             1000.0 * ctx->last_ms);
-    scatter_bits(reqs, cands, ix.data(), m, out.data(), valid);
+    scatter_bits(reqs, cands, grp, out.data(), valid);
     clk.lap("scatter");
   }
   clk.emit("ctx_verify", n, cands.size());
@@ -1058,7 +1120,7 @@ extern "C" int tmed_verify_commits(tmed_ctx *ctx, const tmed_commit_request *req
     }
   }
   return run_seam(reqs, n, out,
-                  [&](const tmed_commit_request *rq, size_t nr, const std::vector<Cand> &cands, uint8_t *valid) {
+                  [&](const tmed_commit_request *rq, size_t nr, const Cands &cands, uint8_t *valid) {
                     return ctx_verify(ctx, rq, nr, cands, valid);
                   });
 }
@@ -1068,7 +1130,7 @@ namespace {
 struct BsBatch {
   size_t lo = 0, n = 0;
   Plans plans;
-  std::vector<Cand> cands;
+  Cands cands;
   std::vector<uint8_t> tmpl, bits, valid;
   tmed::VoteStage st;
   bool device = false;  // queued on a vote slot (else verified synchronously / nothing to verify)
@@ -1123,7 +1185,7 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
     const auto t1 = clock::now();
     // the device bits are in candidate order: replay reads them directly (it applies the
     // signature-length rule itself)
-    int r = seam_replay(reqs + b.lo, b.n, out + b.lo, b.plans, b.cands, b.device ? b.bits.data() : b.valid.data());
+    int r = seam_replay(reqs + b.lo, b.n, out + b.lo, b.plans, b.device ? b.bits.data() : b.valid.data());
     ph[2] += us(t1, clock::now());
     b.n = 0;
     b.device = false;
@@ -1154,7 +1216,7 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
     clk.lap("templates");
     if (rc == TMED_OK && m) {
       if (fits && m <= 0xffffffffu) {
-        rc = stage_group(ctx, rq, b.n, b.cands, nullptr, (uint32_t)m, keyset, b.tmpl.data(), (int)(idx % ns),
+        rc = stage_group(ctx, rq, b.n, b.cands, Group(), keyset, b.tmpl.data(), (int)(idx % ns),
                          b.st);
         clk.lap("stage");
         const auto te = clock::now();

@@ -438,8 +438,12 @@ def verify_commits(engine, requests: Sequence[tuple], verifier=None, stats: Opti
     keep = []
     n = len(requests)
     reqs = (_RequestC * max(n, 1))()
+    vcs = {}  # one tmed_valset per ValidatorSet object: the seam resolves each set once per call
     for q, (mode, vals, chain_id, block_id, height, commit, num, den) in enumerate(requests):
-        vs = _valset_c(vals, keep)
+        vs = vcs.get(id(vals))
+        if vs is None:
+            vs = vcs[id(vals)] = _valset_c(vals, keep)
+            keep.append(vals)
         cc = _commit_c(commit, keep)
         cid = chain_id.encode()
         bid = _block_id_c(block_id, keep) if block_id is not None else None
