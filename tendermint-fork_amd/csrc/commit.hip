@@ -112,40 +112,7 @@ inline void push_cand(std::vector<Run> &runs, uint32_t q, int32_t i, int32_t v) 
   runs.push_back(Run{q, i, v, 1u});
 }
 
-// address -> first validator index with that address (GetByAddress, types/validator_set.go:270-278
-// returns the first match).  Flat open-addressing table: a light-client batch builds one per
-// trusted set (10k sets x 175 validators in C3), so construction cost matters.
-struct AddrIndex {
-  const uint8_t *addrs = nullptr;  // the set's n x 20 address array (owned by the request)
-  std::vector<int32_t> vals;       // validator index, -1 = empty
-  size_t mask = 0;
-  static size_t slot_of(const uint8_t *p) {  // addresses are SHA-256 truncations: 8 bytes mix well
-    uint64_t a;
-    memcpy(&a, p, 8);
-    return (size_t)((a * 0x9E3779B97F4A7C15ull) >> 20);
-  }
-  void build(const uint8_t *addresses, size_t n) {
-    addrs = addresses;
-    size_t cap = 16;
-    while (cap < 2 * n + 1) cap <<= 1;
-    mask = cap - 1;
-    vals.assign(cap, -1);
-    for (size_t v = 0; v < n; v++) {
-      const uint8_t *a = addresses + 20 * v;
-      size_t h = slot_of(a) & mask;
-      while (vals[h] >= 0 && memcmp(addrs + 20 * (size_t)vals[h], a, 20) != 0) h = (h + 1) & mask;
-      if (vals[h] < 0) vals[h] = (int32_t)v;  // keep the first match
-    }
-  }
-  int32_t find(const uint8_t *addr) const {
-    size_t h = slot_of(addr) & mask;
-    while (vals[h] >= 0) {
-      if (memcmp(addrs + 20 * (size_t)vals[h], addr, 20) == 0) return vals[h];
-      h = (h + 1) & mask;
-    }
-    return -1;
-  }
-};
+using tmed::AddrIndex;  // keycache.h
 
 struct Plan {
   bool decided = false;
@@ -340,10 +307,16 @@ static int build_cand_batch(const tmed_commit_request *reqs, size_t n, const Can
 // caller may rewrite its buffers between calls).  The plan records every lookup result the
 // replay needs (the candidate's validator, kNoValidator, the double vote), so the index is
 // never read after planning.
+// Sets resolved through the key-set cache (KcCall, below) carry their entry's address index.
+struct KcCall;
+static const AddrIndex *kc_addr_index(const KcCall *kc, const tmed_valset &vs);
 struct AddrScratch {
   AddrIndex ix;
   const tmed_valset *of = nullptr;
+  const KcCall *kc = nullptr;
   const AddrIndex &get(const tmed_valset &vs) {
+    if (kc)
+      if (const AddrIndex *c = kc_addr_index(kc, vs)) return *c;
     if (of != &vs) { ix.build(vs.addresses, vs.n); of = &vs; }
     return ix;
   }
@@ -508,7 +481,8 @@ static size_t total_sigs(const tmed_commit_request *reqs, size_t n) {
 }
 
 // Candidates of requests [0, n) in request order (identical to a serial plan).
-static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, Plans &ps, Cands &cands) {
+static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, Plans &ps, Cands &cands,
+                     const KcCall *kc = nullptr) {
   PhaseClock clk;
   std::vector<Plan> &plans = ps.v;
   plans.assign(n, Plan());
@@ -535,6 +509,7 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
   auto plan_range = [&](size_t lo, size_t hi, unsigned t) {
     lo_of[t] = lo; hi_of[t] = hi;
     AddrScratch addr;
+    addr.kc = kc;
     size_t c = 0;
     for (size_t q = lo; q < hi && rcs[t] == TMED_OK; q++) rcs[t] = plan_request(reqs, q, out[q], plans[q], part[t], c, addr);
     pc[t] = c;
@@ -648,7 +623,8 @@ static int seam_replay(const tmed_commit_request *reqs, size_t n, tmed_commit_re
 // Wall time of the three phases of the calling thread's last run_seam (tmed_seam_phase_us).
 static thread_local double g_seam_us[3] = {0, 0, 0};
 
-static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, const BatchVerifier &verify) {
+static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, const BatchVerifier &verify,
+                    const KcCall *kc = nullptr) {
   if (n && (!reqs || !out)) return TMED_EINVAL;
   using clock = std::chrono::steady_clock;
   auto us = [](clock::time_point a, clock::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
@@ -660,7 +636,7 @@ static int run_seam(const tmed_commit_request *reqs, size_t n, tmed_commit_resul
   thread_local Plans plans;
   thread_local Cands cands;
   thread_local std::vector<uint8_t> valid;
-  int rc = seam_plan(reqs, n, out, plans, cands);
+  int rc = seam_plan(reqs, n, out, plans, cands, kc);
   if (rc != TMED_OK) return rc;
   clk.lap("plan");
   const auto t1 = clock::now();
@@ -944,7 +920,7 @@ static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, 
 }
 
 static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t nb, size_t bsz, uint64_t keyset,
-                         tmed_commit_result *out);
+                         tmed_commit_result *out, const KcCall *kc);
 
 // ---- key-set cache (keycache.h / keycache.hip) -------------------------------
 // The validator sets of one seam call that carry no handle, resolved through the context's cache:
@@ -957,6 +933,7 @@ struct KcCall {
   tmed_ctx *c = nullptr;
   std::vector<tmed_commit_request> reqs;
   std::vector<tmed_valset> vals;  // copies of the resolved sets (reqs[q].vals points here)
+  std::vector<const tmed::KcSet *> entry;  // the cache entry of vals[s] (nullptr: not keyed)
   std::vector<std::shared_ptr<const tmed::KcSet>> holds;
   ~KcCall() {
     if (!c) return;
@@ -965,6 +942,15 @@ struct KcCall {
     tmed::keycache_after_call(c);  // the context's worker builds the queued keys
   }
 };
+
+// The cached address index of a set this call resolved through the cache (nullptr otherwise, or
+// when the request's addresses differ from the ones the entry's index was built from).
+static const AddrIndex *kc_addr_index(const KcCall *kc, const tmed_valset &vs) {
+  if (kc->vals.empty() || !vs.addresses || &vs < kc->vals.data() || &vs >= kc->vals.data() + kc->vals.size())
+    return nullptr;
+  const tmed::KcSet *e = kc->entry[(size_t)(&vs - kc->vals.data())];
+  return e ? e->addr_index(vs.addresses, vs.n) : nullptr;
+}
 
 static const tmed_commit_request *keycache_resolve(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
                                                    KcCall &kc) {
@@ -1074,9 +1060,11 @@ static const tmed_commit_request *keycache_resolve(tmed_ctx *ctx, const tmed_com
   clk.lap("lookups");
   if (!any_keyed) return reqs;
   kc.vals.resize(sets.size());
+  kc.entry.assign(sets.size(), nullptr);
   for (size_t s = 0; s < sets.size(); s++) {
     SetRef &sr = sets[s];
     if (!sr.hit) continue;
+    kc.entry[s] = sr.hold.get();
     kc.vals[s] = *sr.v;
     kc.vals[s].keyset = sr.handle;
     kc.vals[s].keyset_index = sr.hold->idx.data();
@@ -1116,13 +1104,15 @@ extern "C" int tmed_verify_commits(tmed_ctx *ctx, const tmed_commit_request *req
     }
     if (ok && sigs >= 2 * kPipeBatchSigs) {
       const size_t bsz = std::max<size_t>(16, kPipeBatchSigs / std::max<size_t>(1, sigs / n));
-      if (n > bsz) return run_pipelined(ctx, reqs, n, bsz, ks, out);
+      if (n > bsz) return run_pipelined(ctx, reqs, n, bsz, ks, out, &kc);
     }
   }
-  return run_seam(reqs, n, out,
-                  [&](const tmed_commit_request *rq, size_t nr, const Cands &cands, uint8_t *valid) {
-                    return ctx_verify(ctx, rq, nr, cands, valid);
-                  });
+  return run_seam(
+      reqs, n, out,
+      [&](const tmed_commit_request *rq, size_t nr, const Cands &cands, uint8_t *valid) {
+        return ctx_verify(ctx, rq, nr, cands, valid);
+      },
+      &kc);
 }
 
 // ---- blocksync replay window (f4): pipelined LIGHT batches --------------------------------
@@ -1156,7 +1146,7 @@ constexpr int kPipeSlots = 3;
 static_assert(kPipeSlots <= (int)(sizeof(((tmed_ctx *)nullptr)->vslot) / sizeof(tmed::VoteSlot)),
               "one context vote slot per pipeline slot");
 static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t nb, size_t bsz, uint64_t keyset,
-                         tmed_commit_result *out) {
+                         tmed_commit_result *out, const KcCall *kc) {
   // kept per thread across calls, as run_seam's planning buffers (a blocksync window plans batch
   // after batch into the same pages)
   thread_local BsBatch slots[kPipeSlots];
@@ -1208,7 +1198,7 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
     lo += b.n;
     const tmed_commit_request *rq = reqs + b.lo;
     const auto tp = clock::now();
-    rc = seam_plan(rq, b.n, out + b.lo, b.plans, b.cands);
+    rc = seam_plan(rq, b.n, out + b.lo, b.plans, b.cands, kc);
     clk.lap("plan");
     const size_t m = b.cands.size();
     bool fits = true;
@@ -1279,7 +1269,7 @@ extern "C" int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window 
   }
   KcCall kc;  // one set for the whole window
   const tmed_commit_request *rq = keycache_resolve(ctx, reqs.data(), nb, kc);
-  return run_pipelined(ctx, rq, nb, batch_blocks ? batch_blocks : 128, rq[0].vals->keyset, out);
+  return run_pipelined(ctx, rq, nb, batch_blocks ? batch_blocks : 128, rq[0].vals->keyset, out, &kc);
 }
 
 // ---- several GPUs in one process (§8e): contiguous shards balanced by signature count ----

@@ -35,6 +35,7 @@
 
 #include <algorithm>
 #include <memory>
+#include <mutex>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -106,12 +107,63 @@ inline KcKey kc_key(const uint8_t *pubs, size_t n, const uint8_t *set_hash) {
   return k;
 }
 
-// One cached validator set: its keys (for the byte compare) and validator i -> pool index.
+// address -> first validator index with that address (GetByAddress, types/validator_set.go:270-278
+// returns the first match).  Flat open-addressing table: a light-client batch looks up ~59
+// addresses per Trusting request, one request per trusted set (C3: 10k sets x 175 validators).
+struct AddrIndex {
+  const uint8_t *addrs = nullptr;  // the set's n x 20 address array
+  std::vector<int32_t> vals;       // validator index, -1 = empty
+  size_t mask = 0;
+  static size_t slot_of(const uint8_t *p) {  // addresses are SHA-256 truncations: 8 bytes mix well
+    uint64_t a;
+    memcpy(&a, p, 8);
+    return (size_t)((a * 0x9E3779B97F4A7C15ull) >> 20);
+  }
+  void build(const uint8_t *addresses, size_t n) {
+    addrs = addresses;
+    size_t cap = 16;
+    while (cap < 2 * n + 1) cap <<= 1;
+    mask = cap - 1;
+    vals.assign(cap, -1);
+    for (size_t v = 0; v < n; v++) {
+      const uint8_t *a = addresses + 20 * v;
+      size_t h = slot_of(a) & mask;
+      while (vals[h] >= 0 && memcmp(addrs + 20 * (size_t)vals[h], a, 20) != 0) h = (h + 1) & mask;
+      if (vals[h] < 0) vals[h] = (int32_t)v;  // keep the first match
+    }
+  }
+  int32_t find(const uint8_t *addr) const {
+    size_t h = slot_of(addr) & mask;
+    while (vals[h] >= 0) {
+      if (memcmp(addrs + 20 * (size_t)vals[h], addr, 20) == 0) return vals[h];
+      h = (h + 1) & mask;
+    }
+    return -1;
+  }
+};
+
+// One cached validator set: its keys (for the byte compare) and validator i -> pool index; and,
+// built at the first LightTrusting request against it, its address index over a private copy of
+// the addresses that request passed (a later request uses it only if its addresses are the same
+// bytes: tmed_valset.addresses is not part of the cache key).
 struct KcSet {
   std::vector<uint8_t> pubs;
   std::vector<uint32_t> idx;
   uint64_t tick = 0;
   size_t bytes() const { return pubs.size() + 4 * idx.size() + 64; }
+  // nullptr when `addrs` (n x 20) differ from the addresses the cached index was built from
+  const AddrIndex *addr_index(const uint8_t *addrs, size_t n) const {
+    std::call_once(addr_once_, [&] {
+      addr_copy_.assign(addrs, addrs + 20 * n);
+      addr_ix_.build(addr_copy_.data(), n);
+    });
+    return addr_copy_.size() == 20 * n && memcmp(addr_copy_.data(), addrs, 20 * n) == 0 ? &addr_ix_ : nullptr;
+  }
+
+ private:
+  mutable std::once_flag addr_once_;
+  mutable std::vector<uint8_t> addr_copy_;
+  mutable AddrIndex addr_ix_;
 };
 
 inline bool kc_same_keys(const KcSet &s, const uint8_t *pubs, size_t n) {

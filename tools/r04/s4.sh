@@ -12,3 +12,5 @@ rc=$?; echo "bench rc=$rc"
 case $rc in 124|134|137|139) exit $rc;; esac
 TMED_TRACE=1 timeout -k 10 300 python bench_commits.py --config c4 --blocks 3000 --no-cpu > $O/c4_trace.log 2>&1
 echo "c4 trace rc=$?"
+TMED_TRACE=1 timeout -k 10 300 python bench_commits.py --config c3 --runs 3 > $O/c3_trace.log 2>&1
+echo "c3 trace rc=$?"
