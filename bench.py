@@ -180,7 +180,7 @@ def main():
     from tmed import Engine, lib
     from tmed.workload import c2_messages, c2_seeds
 
-    from tmed.launch import dist_setup
+    from tmed.launch import dist_setup, gpu_count_fields
     world, rank, local_rank, dev, coll = dist_setup()
     eng = Engine(local_rank)
     n = args.sigs
@@ -319,7 +319,7 @@ def main():
             "metric": "ed25519 verifies/sec at %d/8 MI355X" % world,
             "value": round(value, 1),
             "unit": "verifies/s",
-            "n_gpus": world,
+            **gpu_count_fields(world),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),

@@ -352,8 +352,11 @@ def _c4_corrupt(commits, b0: int, every: int, upto: int):
     return exp
 
 
+STREAM_CHUNK_WINDOWS = 13  # C4 stream mode: windows generated (pinned) at once; 13 x 1000 blocks x 10k x 64 B = 8.3 GB
+
+
 def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, batch: int, corrupt_every: int = 0,
-       pregen: bool = False, pinned: bool = True, policy: str = "cache"):
+       pregen: bool = False, pinned: bool = True, policy: str = "cache", stream: bool = True):
     """Blocksync replay (BASELINE C4): VerifyCommitLight for every block of a contiguous shard
     of the chain per rank, through the pipelined blocksync seam (tmed_blocksync_verify, f4),
     key-cached.  Blocks are generated window by window on the GPU (untimed) and verified
@@ -375,6 +378,9 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
     import tmed.types as T
     from tmed import PinnedBuffer
     from tmed.dist import aggregate_blocksync, block_range
+    if stream:
+        pregen = True  # every window exists before the timed stream starts (nothing generated inside it)
+    from tmed.launch import gpu_count_fields
     from tmed.workload import make_valset, pubkeys_of, seeds_from_tag, sign_commits
     seeds = seeds_from_tag(b"tmed-c4-key", 0, nvals)
     pubs = pubkeys_of(eng, seeds)
@@ -421,34 +427,75 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
         t_marshal += time.perf_counter() - tm
         return win, exp, commits
 
+    def check(w0, w1, win, exp):
+        """(verifies, outcome mismatches) of a collected window; its ok bits into ok_bits"""
+        codes, vers = win.codes(), win.verified()
+        ok_bits[w0 - lo:w1 - lo] = codes == 0
+        bad = 0
+        for h, (ec, ei, ev) in enumerate(exp):
+            if codes[h] != ec or vers[h] != ev or (ec == 4 and win.res[h].idx != ei):
+                bad += 1
+        return int(vers.sum()), bad
+
     def run(w0, w1, win, exp):
-        nonlocal dt, ver, mism, phase
+        nonlocal dt, phase, ver, mism
         t0 = time.perf_counter()
         win.run(eng, batch)
         dt += time.perf_counter() - t0
         phase += np.asarray(seam_phase_us(), np.float64)
-        codes, vers = win.codes(), win.verified()
-        ok_bits[w0 - lo:w1 - lo] = codes == 0
-        ver += int(vers.sum())
-        for h, (ec, ei, ev) in enumerate(exp):
-            if codes[h] != ec or vers[h] != ev or (ec == 4 and win.res[h].idx != ei):
-                mism += 1
+        v, m = check(w0, w1, win, exp)
+        ver += v
+        mism += m
 
-    if pregen:  # every window of the shard generated first, then all ranks verify together
-        wins = []
-        tg = time.perf_counter()
-        for w0 in range(lo, hi, window):
-            w1 = min(hi, w0 + window)
-            wins.append((w0, w1) + gen(w0, w1, len(wins)))
-        t_gen += time.perf_counter() - tg
-        if world > 1:
-            dist.barrier()
-        for _ in range(2 if wins else 0):  # untimed warmup (see below)
-            wins[0][2].run(eng, batch)
-            eng.keycache_wait()
-        for w0, w1, win, exp, _ in wins:
-            run(w0, w1, win, exp)
-        del wins
+    sync_pass = [0.0, 0, 0]  # the per-window calls of stream mode: seconds, verifies, mismatches
+
+    if pregen:  # the windows generated first (in chunks of STREAM_CHUNK_WINDOWS), then all ranks verify together
+        starts = list(range(lo, hi, window))
+        chunk_w = STREAM_CHUNK_WINDOWS if stream else max(1, len(starts))
+        first = True
+        for c0 in range(0, len(starts), chunk_w):
+            wins = []
+            tg = time.perf_counter()
+            for k, w0 in enumerate(starts[c0:c0 + chunk_w]):
+                w1 = min(hi, w0 + window)
+                wins.append((w0, w1) + gen(w0, w1, k))
+            t_gen += time.perf_counter() - tg
+            if world > 1:
+                dist.barrier()
+            for _ in range(2 if first else 0):  # untimed warmup (see below)
+                wins[0][2].run(eng, batch)
+                eng.keycache_wait()
+            first = False
+            if not stream:
+                for w0, w1, win, exp, _ in wins:  # a call per window (tmed_blocksync_verify)
+                    run(w0, w1, win, exp)
+                del wins
+                continue
+            # a call per window first (reported beside), then the same windows as ONE stream
+            # (tmed_blocksync_submit each, then tmed_blocksync_wait): the device is not drained
+            # between windows; timed from the first submit to the wait
+            for w0, w1, win, exp, _ in wins:
+                t0 = time.perf_counter()
+                win.run(eng, batch)
+                sync_pass[0] += time.perf_counter() - t0
+                v, m = check(w0, w1, win, exp)
+                sync_pass[1] += v
+                sync_pass[2] += m
+                win.res = type(win.res)()  # fresh results for the stream
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            for w0, w1, win, exp, _ in wins:
+                win.submit(eng, batch)
+                phase += np.asarray(seam_phase_us(), np.float64)
+            T.blocksync_wait(eng)
+            phase += np.asarray(seam_phase_us(), np.float64)
+            dt += time.perf_counter() - t0
+            for w0, w1, win, exp, _ in wins:
+                v, m = check(w0, w1, win, exp)
+                ver += v
+                mism += m
+            del wins
     else:
         for w0 in range(lo, hi, window):
             w1 = min(hi, w0 + window)
@@ -464,10 +511,11 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
             run(w0, w1, win, exp)
             del win, commits
     nbatch = -(-(hi - lo) // batch) if batch else 0
-    agg = aggregate_blocksync(ok_bits, blocks, rank, world, ver, mism, dt, extra_max=[t_marshal],
+    sdt, sver, smism = sync_pass
+    agg = aggregate_blocksync(ok_bits, blocks, rank, world, ver, mism + smism, dt, extra_max=[t_marshal, sdt],
                               phases=list(phase) + [nbatch], device=dev)
     ok, nb, ver, mism, dt = agg["blocks_ok"], agg["blocks"], agg["verified"], agg["mismatches"], agg["seconds"]
-    t_marshal_max = agg["extra_max"][0]
+    t_marshal_max, sdt_max = agg["extra_max"]
     ph_all = [p[:3] + [p[4], p[3]] for p in agg["phases"]]  # plan, wait, replay, seconds, batches
     kc1 = eng.keycache_stats()
     if vals.keyset:
@@ -482,6 +530,13 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
             "marshal_note": "Python harness: the signature arena fill + the window's C structs (BlocksyncWindow), "
                             "timed per window beside the seam; the Go shim's flatten is the same work in Go",
             "key_policy": policy,
+            "windows": ("one stream: tmed_blocksync_submit per window, tmed_blocksync_wait at the end (the "
+                        "device is not drained between windows), in chunks of %d windows generated beforehand"
+                        % STREAM_CHUNK_WINDOWS if stream else "a tmed_blocksync_verify call per window"),
+            "per_window_calls": ({"value": round(ver / sdt_max, 1), "seconds": round(sdt_max, 4),
+                                  "note": "the same windows, a tmed_blocksync_verify call each (pipeline drained and "
+                                          "refilled at every window); outcome mismatches counted with the stream's"}
+                                 if stream else None),
             "keycache_rank0": {k: kc1[k] - kc0[k] for k in ("lookups", "hits", "keyed_sets", "generic_sets",
                                                             "keys_appended", "keys_deferred")},
             "all_ok": ok == nb if not corrupt_every else None,
@@ -494,7 +549,7 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
                                          "enqueue_and_wait_for_device": round(p[1] / 1e3 / max(1, p[4]), 3),
                                          "replay": round(p[2] / 1e3 / max(1, p[4]), 3),
                                          "batches": int(p[4]), "seconds": round(p[3], 3)} for r, p in enumerate(ph_all)],
-            "verifies": ver, "seconds": round(dt, 4), "n_gpus": world,
+            "verifies": ver, "seconds": round(dt, 4), **gpu_count_fields(world),
             "config": {"workload": "C4: %d blocks x %d validators, VerifyCommitLight per block, key-cached, "
                                    "blocks sharded over %d GPU(s) (contiguous heights), %d-block windows, "
                                    "%d-block device batches" % (blocks, nvals, world, window, batch),
@@ -527,13 +582,15 @@ def main():
     ap.add_argument("--pregen", action="store_true", help="C4: generate the whole shard before timing (host rehearsal)")
     ap.add_argument("--c4-policy", choices=["cache", "explicit"], default="cache",
                     help="C4 key handling: the seam's key-set cache (default) or an explicit key-set handle")
+    ap.add_argument("--no-stream", action="store_true",
+                    help="C4: a tmed_blocksync_verify call per window only (no submit/wait stream pass)")
     ap.add_argument("--no-pinned", action="store_true",
                     help="C4: commits in ordinary (pageable) memory: signatures go through the seam's staging copy")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
     from tmed import Engine
-    from tmed.launch import dist_setup
+    from tmed.launch import dist_setup, gpu_count_fields
     world, rank, local, dev, coll = dist_setup()
     eng = Engine(local)
     for cfg in args.config.split(","):
@@ -543,7 +600,7 @@ def main():
             r = c3(eng, args.headers, args.gap, args.c3_policy, args.runs, args.bisect_gap)
         elif cfg == "c4":
             r = c4(eng, args.blocks, args.validators, rank, world, coll, args.window, args.batch, args.corrupt_every,
-                       args.pregen, not args.no_pinned, args.c4_policy)
+                       args.pregen, not args.no_pinned, args.c4_policy, not args.no_stream)
         else:
             continue
         if rank == 0:

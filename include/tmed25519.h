@@ -225,7 +225,10 @@ int tmed_vote_sign_bytes(const tmed_vote_template *t, size_t n, const uint8_t *f
  * Integer-VALU peak probe for the roofline: runs a
  * dependency-free stream of `kind` instructions on every lane of the device
  * (0 v_mad_i64_i32, 1 v_mad_u64_u32, 2 v_add_u32, 3 v_mul_lo_u32, 4 v_ashrrev_i64,
- * 5 v_lshl_add_u64, 6 v_lshl_add_u32, 7 v_add_co_u32+v_addc_co_u32)
+ * 5 v_lshl_add_u64, 6 v_lshl_add_u32, 7 v_add_co_u32+v_addc_co_u32, 8 v_lshrrev_b64,
+ * 9 v_alignbit_b32, 10 v_and_b32, 11 v_bfe_i32, 12 v_and_or_b32, 13 v_cndmask_b32,
+ * 14 v_ashrrev_i32, 15 v_cndmask_b32_e64 with an SGPR lane mask, 16 / 17 v_cmp_gt_u32 +
+ * v_cndmask_b32 through vcc / an SGPR pair, counted as 2)
  * and returns the sustained rate in 1e9 instructions (lane-ops) per second.
  */
 int tmed_valu_peak(tmed_ctx *ctx, int kind, double *giga_ops_per_s);
@@ -475,11 +478,31 @@ typedef struct {
  * over TMED_MODE_LIGHT requests — computed speculatively for the whole window, so the
  * caller applies blocks in order and stops at the first non-OK one (the reactor then
  * redoes that request, reactor.go:368-388).  The window is processed in device batches
- * of batch_blocks blocks (0 = 128, the measured best) through a two-slot pipeline: while the device verifies
- * batch b, the host plans and stages batch b+1 and replays batch b-1.
+ * of batch_blocks blocks (0 = 128, the measured best) through a pipeline of up to three batches:
+ * while the device verifies batch b, the host plans and stages batch b+1 and replays batch b-2.
  */
 int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t batch_blocks,
                           tmed_commit_result *out);
+
+/*
+ * The same as a stream of windows: a replay that verifies its backlog window after window
+ * (blockchain/v0/reactor.go:349-418 over the pool's pending blocks, pool.go:31-34) submits window
+ * w+1 before it consumes window w.  tmed_blocksync_submit queues the window's batches behind the
+ * context's batches in flight and returns once the results of every EARLIER submitted window are
+ * final in their `out` arrays; the window's own last batches may still be in flight, so the device
+ * is never drained between windows (a call per window drains the pipeline and refills it: the
+ * first batch's planning and copy-in).  tmed_blocksync_wait collects everything submitted and
+ * returns the first error of any submitted window (or TMED_OK).  Until the window's results are
+ * final, `out` and the memory the window's structs point to (block hashes, the commits' arrays —
+ * signatures in pinned memory are DMA'd from there — and the set's keys, powers and addresses)
+ * must stay valid and unchanged; the structs themselves (the window, its block_ids / heights /
+ * commits arrays, the tmed_valset, the chain ID) are copied by submit.  Any other seam call on the context
+ * (tmed_verify_commits, tmed_blocksync_verify) first collects every submitted window.
+ * Results are identical to tmed_blocksync_verify on each window.
+ */
+int tmed_blocksync_submit(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t batch_blocks,
+                          tmed_commit_result *out);
+int tmed_blocksync_wait(tmed_ctx *ctx);
 
 /*
  * Pinned (page-locked) host memory for the commit arrays a caller marshals its commits into

@@ -94,10 +94,13 @@ struct Run {
 struct Cands {
   std::vector<Run> runs;
   std::vector<size_t> off;  // runs.size() + 1 candidate offsets
+  // (candidate, the candidate whose bit it takes), ascending: see find_aliases
+  std::vector<std::pair<uint32_t, uint32_t>> alias;
   size_t size() const { return off.empty() ? 0 : off.back(); }
   void clear() {
     runs.clear();
     off.assign(1, 0);
+    alias.clear();
   }
 };
 // Append candidate (q, i, v) to a part's runs, extending the last run when it continues it.
@@ -125,6 +128,7 @@ struct Plan {
   int32_t *vof = nullptr;
   size_t cand_off = 0;  // the request's first candidate (in its part while planning, then global)
   uint32_t ncand = 0;
+  size_t run_lo = 0, run_hi = 0;  // its runs (in its part while planning, then in the merged runs)
   // Trusting: the double vote the loop stops at (sig idx, validator, first sig idx), -1 = none
   int32_t dv_idx = -1, dv_val = -1, dv_first = -1;
 };
@@ -333,6 +337,7 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
   const tmed_valset &vs = *r.vals;
   const tmed_commit &c = *r.commit;
   pl.cand_off = part_cands;
+  pl.run_lo = runs.size();
   pl.stop = (int32_t)c.n_sigs;
   uint32_t nc = 0;
   const uint32_t qq = (uint32_t)q;
@@ -400,6 +405,7 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
     }
   }
   pl.ncand = nc;
+  pl.run_hi = runs.size();
   part_cands += nc;
   return TMED_OK;
 }
@@ -480,6 +486,9 @@ static size_t total_sigs(const tmed_commit_request *reqs, size_t n) {
   return s;
 }
 
+static void find_aliases(const tmed_commit_request *reqs, size_t n, const Plans &ps, const Cands &cands,
+                         std::vector<std::pair<uint32_t, uint32_t>> &alias);
+
 // Candidates of requests [0, n) in request order (identical to a serial plan).
 static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, Plans &ps, Cands &cands,
                      const KcCall *kc = nullptr) {
@@ -533,14 +542,75 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
       cands.off[rb + r] = c;
       c += part[t][r].len;
     }
-    for (size_t q = lo_of[t]; q < hi_of[t]; q++) plans[q].cand_off += cb;
+    for (size_t q = lo_of[t]; q < hi_of[t]; q++) {
+      plans[q].cand_off += cb;
+      plans[q].run_lo += rb;
+      plans[q].run_hi += rb;
+    }
     rb += part[t].size();
     cb += pc[t];
   }
   cands.off[nr] = cb;
   clk.lap("merge");
+  if (nbits && cb <= 0xffffffffu) find_aliases(reqs, n, ps, cands, cands.alias);
+  clk.lap("aliases");
   clk.emit("plan", n, cb);
   return TMED_OK;
+}
+
+// ---- candidates verified once for two requests ----------------------------------------
+// The light client checks one commit twice, LightTrusting against the trusted set and Light
+// against the untrusted one (light/verifier.go:58,73-76), and most validators sign for both
+// sets: a Trusting candidate (signature i of a commit, key K) is the same verification as the
+// Light / VerifyCommit candidate (signature i of the SAME commit, same chain ID, same key K) of
+// a neighbouring request.  Such a candidate is sent once; the other takes its bit (C3: ~59 of
+// the ~176 candidates of each header).  alias: (candidate, the candidate whose bit it takes).
+static bool same_key(const tmed_valset &a, int32_t va, const tmed_valset &b, int32_t vb) {
+  if (a.keyset != b.keyset) return false;
+  if (a.keyset) {
+    const uint32_t ka = a.keyset_index ? a.keyset_index[va] : (uint32_t)va;
+    const uint32_t kb = b.keyset_index ? b.keyset_index[vb] : (uint32_t)vb;
+    return ka == kb;
+  }
+  return memcmp(a.pubkeys + 32 * (size_t)va, b.pubkeys + 32 * (size_t)vb, 32) == 0;
+}
+
+static void find_aliases(const tmed_commit_request *reqs, size_t n, const Plans &ps, const Cands &cands,
+                         std::vector<std::pair<uint32_t, uint32_t>> &alias) {
+  alias.clear();
+  const std::vector<Plan> &plans = ps.v;
+  const unsigned nt = host_threads(cands.size());
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> part(std::max(1u, nt));
+  parallel_ranges(n, nt, [&](size_t lo, size_t hi, unsigned t) {
+    for (size_t q = lo; q < hi; q++) {
+      const tmed_commit_request &r = reqs[q];
+      const Plan &pl = plans[q];
+      if (r.mode != TMED_MODE_LIGHT_TRUSTING || pl.decided || pl.ncand == 0) continue;
+      for (size_t pq : {q + 1, q - 1}) {  // the pair is adjacent in the light client's batches
+        if (pq >= n) continue;
+        const tmed_commit_request &o = reqs[pq];
+        const Plan &po = plans[pq];
+        if (o.mode == TMED_MODE_LIGHT_TRUSTING || o.commit != r.commit || po.decided || po.ncand == 0 ||
+            o.chain_id_len != r.chain_id_len || memcmp(o.chain_id, r.chain_id, r.chain_id_len) != 0)
+          continue;
+        // o's candidates are its qualifying signatures in order, as runs sorted by signature
+        size_t ro = po.run_lo;
+        for (size_t ri = pl.run_lo; ri < pl.run_hi; ri++) {
+          const Run &run = cands.runs[ri];
+          for (uint32_t u = 0; u < run.len; u++) {
+            const int32_t i = run.sig + (int32_t)u;
+            while (ro < po.run_hi && cands.runs[ro].sig + (int32_t)cands.runs[ro].len <= i) ro++;
+            if (ro == po.run_hi) break;
+            const Run &orun = cands.runs[ro];
+            if (i < orun.sig || !same_key(*r.vals, run.val + (int32_t)u, *o.vals, orun.val + (i - orun.sig))) continue;
+            part[t].push_back({(uint32_t)(cands.off[ri] + u), (uint32_t)(cands.off[ro] + (size_t)(i - orun.sig))});
+          }
+        }
+        break;
+      }
+    }
+  });
+  for (auto &p : part) alias.insert(alias.end(), p.begin(), p.end());
 }
 
 // ---- replay of every reference loop over the validity bits (parallel over requests) ----
@@ -717,16 +787,44 @@ static int ctx_verify_host_msgs(tmed_ctx *ctx, const tmed_commit_request *reqs, 
   return TMED_OK;
 }
 
-// The runs of one device group (one key set) and their staging positions: run rix[j] of the
-// call (rix empty: every run, in order) stages its candidates at pos[j] .. pos[j + 1).
+// The run segments of one device group (one key set) and their staging positions: segment j is
+// run rix[j]'s candidates from ub[j] on, staged at pos[j] .. pos[j + 1) (rix empty: every run
+// whole, in order; ub empty: segments start at their run's first candidate).
 struct Group {
-  std::vector<uint32_t> rix;
+  std::vector<uint32_t> rix, ub;
   std::vector<size_t> pos;
   size_t size(const Cands &c) const { return rix.empty() ? c.size() : pos.back(); }
   uint32_t run(const Cands &c, size_t j) const { (void)c; return rix.empty() ? (uint32_t)j : rix[j]; }
+  uint32_t base(size_t j) const { return ub.empty() ? 0u : ub[j]; }
   size_t nruns(const Cands &c) const { return rix.empty() ? c.runs.size() : rix.size(); }
   const size_t *positions(const Cands &c) const { return rix.empty() ? c.off.data() : pos.data(); }
+  void start() {
+    rix.clear();
+    ub.clear();
+    pos.assign(1, 0);
+  }
+  // run r without its aliased candidates (alias[ap..] ascending; ap advances past run r's)
+  void add_run(const Cands &c, uint32_t r, size_t &ap) {
+    const size_t c0 = c.off[r], c1 = c.off[r + 1];
+    size_t k = c0;
+    auto seg = [&](size_t a, size_t b) {
+      if (a >= b) return;
+      rix.push_back(r);
+      ub.push_back((uint32_t)(a - c0));
+      pos.push_back(pos.back() + (b - a));
+    };
+    for (; ap < c.alias.size() && c.alias[ap].first < c1; ap++) {
+      seg(k, c.alias[ap].first);
+      k = (size_t)c.alias[ap].first + 1;
+    }
+    seg(k, c1);
+  }
 };
+
+// The verified bits of the aliased candidates (scatter_bits wrote their targets).
+static void copy_aliases(const Cands &c, uint8_t *valid) {
+  for (const auto &a : c.alias) valid[a.first] = valid[a.second];
+}
 
 // For f(j, u0, u1, p0): the segment u0 .. u1 - 1 of group run j, staged from position p0, for the
 // positions [lo, hi) of a thread's share (runs split across threads are cut at the share edges).
@@ -738,7 +836,8 @@ static void for_segments(const Cands &c, const Group &g, size_t lo, size_t hi, F
   j = j ? j - 1 : 0;
   for (; j < nr && pos[j] < hi; j++) {
     const size_t a = std::max(lo, pos[j]), b = std::min(hi, pos[j + 1]);
-    if (a < b) f(j, (uint32_t)(a - pos[j]), (uint32_t)(b - pos[j]), a);
+    const uint32_t u = g.base(j);
+    if (a < b) f(j, u + (uint32_t)(a - pos[j]), u + (uint32_t)(b - pos[j]), a);
   }
 }
 
@@ -858,6 +957,8 @@ static void scatter_bits(const tmed_commit_request *reqs, const Cands &cands, co
   });
 }
 
+static int bs_drain(tmed_ctx *ctx);
+
 // Device templates of the requests that have candidates; false if one does not fit.
 static int device_templates(const tmed_commit_request *reqs, size_t n, const Cands &cands, std::vector<uint8_t> &tmpl,
                             bool *fits) {
@@ -888,21 +989,25 @@ static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, 
   if (!fits) return ctx_verify_host_msgs(ctx, reqs, n, cands, valid);
   clk.lap("templates");
   // group the runs by key set (usually a single group: then it is every run, in order)
+  // (aliased candidates are left out: copy_aliases)
   std::vector<uint64_t> gkeys;
   std::vector<Group> groups;
+  size_t ap = 0;
   for (size_t r = 0; r < cands.runs.size(); r++) {
     const uint64_t ks = reqs[cands.runs[r].req].vals->keyset;
     size_t g = 0;
     while (g < gkeys.size() && gkeys[g] != ks) g++;
-    if (g == gkeys.size()) { gkeys.push_back(ks); groups.emplace_back(); groups.back().pos.push_back(0); }
-    groups[g].rix.push_back((uint32_t)r);
-    groups[g].pos.push_back(groups[g].pos.back() + cands.runs[r].len);
+    if (g == gkeys.size()) { gkeys.push_back(ks); groups.emplace_back(); groups.back().start(); }
+    groups[g].add_run(cands, (uint32_t)r, ap);
   }
-  if (groups.size() == 1) groups[0] = Group();  // every run in order: the call's own offsets
+  if (groups.size() == 1 && cands.alias.empty()) groups[0] = Group();  // every run in order: the call's own offsets
   std::lock_guard<std::mutex> lk(ctx->mu);
+  rc = bs_drain(ctx);  // batches of submitted blocksync windows hold the vote slots
+  if (rc != TMED_OK) return rc;
   for (size_t g = 0; g < gkeys.size(); g++) {
     const Group &grp = groups[g];
     const uint32_t m = (uint32_t)grp.size(cands);
+    if (m == 0) continue;
     tmed::VoteStage st;
     rc = stage_group(ctx, reqs, n, cands, grp, gkeys[g], tmpl.data(), 0, st);
     clk.lap("stage");
@@ -915,6 +1020,7 @@ static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, 
     scatter_bits(reqs, cands, grp, out.data(), valid);
     clk.lap("scatter");
   }
+  copy_aliases(cands, valid);
   clk.emit("ctx_verify", n, cands.size());
   return TMED_OK;
 }
@@ -929,26 +1035,49 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
 // this object dies, after the call's last batch was collected; then the keys that generic sets of
 // the call queued are built by the context's key-build worker (keycache.hip), off this call's
 // critical path, in stream order ahead of later calls.
+// Its buffers are the calling thread's, kept across calls: a light-client batch rewrites ~20k
+// requests onto ~10k sets, and fresh pages cost a fault per 4 KB on every call.
+struct KcStore {
+  std::vector<tmed_commit_request> reqs;
+  std::vector<tmed_valset> vals;           // copies of the resolved sets (reqs[q].vals points here)
+  std::vector<const tmed::KcSet *> entry;  // the cache entry of vals[s] (nullptr: not keyed)
+  // resolution scratch: distinct sets, request -> set, the pointer table
+  struct SetRef {
+    const tmed_valset *v;
+    size_t sigs;
+    const tmed::KcSet *e;
+    uint64_t handle;
+    bool hit, skip;
+    tmed::KcKey key;
+  };
+  std::vector<SetRef> sets;
+  std::vector<int32_t> set_of, tval;
+  std::vector<const tmed_valset *> tkey;
+  std::vector<uint32_t> nsig;
+};
 struct KcCall {
   tmed_ctx *c = nullptr;
-  std::vector<tmed_commit_request> reqs;
-  std::vector<tmed_valset> vals;  // copies of the resolved sets (reqs[q].vals points here)
-  std::vector<const tmed::KcSet *> entry;  // the cache entry of vals[s] (nullptr: not keyed)
-  std::vector<std::shared_ptr<const tmed::KcSet>> holds;
+  bool active = false;  // this call's requests were rewritten onto st.vals
+  KcStore &st;
+  KcCall() : st(store()) {}
   ~KcCall() {
     if (!c) return;
     std::lock_guard<std::mutex> lk(c->mu);
-    tmed::keycache_unpin(c);
+    tmed::keycache_unpin(c);  // entries dropped during the call are freed with the last pin
     tmed::keycache_after_call(c);  // the context's worker builds the queued keys
+  }
+  static KcStore &store() {
+    thread_local KcStore s;
+    return s;
   }
 };
 
 // The cached address index of a set this call resolved through the cache (nullptr otherwise, or
 // when the request's addresses differ from the ones the entry's index was built from).
 static const AddrIndex *kc_addr_index(const KcCall *kc, const tmed_valset &vs) {
-  if (kc->vals.empty() || !vs.addresses || &vs < kc->vals.data() || &vs >= kc->vals.data() + kc->vals.size())
-    return nullptr;
-  const tmed::KcSet *e = kc->entry[(size_t)(&vs - kc->vals.data())];
+  const std::vector<tmed_valset> &vals = kc->st.vals;
+  if (!kc->active || !vs.addresses || &vs < vals.data() || &vs >= vals.data() + vals.size()) return nullptr;
+  const tmed::KcSet *e = kc->st.entry[(size_t)(&vs - vals.data())];
   return e ? e->addr_index(vs.addresses, vs.n) : nullptr;
 }
 
@@ -956,101 +1085,108 @@ static const tmed_commit_request *keycache_resolve(tmed_ctx *ctx, const tmed_com
                                                    KcCall &kc) {
   if (!ctx->kc_on || n == 0 || !reqs) return reqs;
   PhaseClock clk;
-  struct SetRef {
-    const tmed_valset *v;
-    size_t sigs = 0;
-    tmed::KcKey key;
-    std::shared_ptr<const tmed::KcSet> hold;
-    bool hit = false;
-    uint64_t handle = 0;
-  };
+  KcStore &S = kc.st;
+  using SetRef = KcStore::SetRef;
   // distinct tmed_valset structs of the call (requests on one struct share its resolution), by a
-  // flat open-addressing table of pointers: a light-client batch has ~20k requests on ~10k sets
-  std::vector<SetRef> sets;
-  std::vector<int32_t> set_of(n, -1);
+  // flat open-addressing table of pointers; only the request array is read here (the structs and
+  // commits behind it are read by the parallel pass below)
+  std::vector<SetRef> &sets = S.sets;
+  sets.clear();
+  S.set_of.resize(n);
   size_t cap = 16;
   while (cap < 2 * n) cap <<= 1;
-  std::vector<const tmed_valset *> tkey(cap, nullptr);
-  std::vector<int32_t> tval(cap, -1);
-  size_t keys = 0;
+  S.tkey.assign(cap, nullptr);
+  S.tval.resize(cap);
+  const tmed_valset **tkey = S.tkey.data();
+  int32_t *tval = S.tval.data();
   const tmed_valset *prev = nullptr;
   int32_t prev_s = -1;
   for (size_t q = 0; q < n; q++) {
-    const tmed_commit_request &r = reqs[q];
-    if (!r.vals || r.vals->keyset || r.vals->n == 0 || !r.vals->pubkeys || !r.commit) continue;
-    int32_t s = prev_s;
-    if (r.vals != prev) {
-      size_t h = (size_t)(((uintptr_t)r.vals >> 4) * 0x9E3779B97F4A7C15ull >> 20) & (cap - 1);
-      while (tkey[h] && tkey[h] != r.vals) h = (h + 1) & (cap - 1);
-      if (!tkey[h]) {
-        tkey[h] = r.vals;
-        tval[h] = (int32_t)sets.size();
-        SetRef sr;
-        sr.v = r.vals;
-        sets.push_back(sr);
-        keys += r.vals->n;
-      }
-      s = tval[h];
-      prev = r.vals;
-      prev_s = s;
+    const tmed_valset *v = reqs[q].vals;
+    if (!v || !reqs[q].commit) {
+      S.set_of[q] = -1;
+      continue;
     }
-    sets[s].sigs += r.commit->n_sigs;
-    set_of[q] = s;
+    if (v != prev) {
+      size_t h = (size_t)(((uintptr_t)v >> 4) * 0x9E3779B97F4A7C15ull >> 20) & (cap - 1);
+      while (tkey[h] && tkey[h] != v) h = (h + 1) & (cap - 1);
+      if (!tkey[h]) {
+        tkey[h] = v;
+        tval[h] = (int32_t)sets.size();
+        sets.push_back(SetRef{v, 0, nullptr, 0, false, false, tmed::KcKey()});
+      }
+      prev = v;
+      prev_s = tval[h];
+    }
+    S.set_of[q] = prev_s;
   }
   if (sets.empty()) return reqs;
   clk.lap("sets");
-  const unsigned nt = host_threads(keys);
-  parallel_ranges(sets.size(), nt, [&](size_t lo, size_t hi, unsigned) {
-    for (size_t s = lo; s < hi; s++) sets[s].key = tmed::kc_key(sets[s].v->pubkeys, sets[s].v->n, sets[s].v->set_hash);
+  // signatures per set (the policy's amortisation and the counters)
+  S.nsig.resize(n);
+  const unsigned nt = host_threads(sets.size() * 128);
+  parallel_ranges(n, nt, [&](size_t lo, size_t hi, unsigned) {
+    for (size_t q = lo; q < hi; q++) S.nsig[q] = S.set_of[q] >= 0 ? reqs[q].commit->n_sigs : 0;
   });
-  clk.lap("digests");
+  for (size_t q = 0; q < n; q++)
+    if (S.set_of[q] >= 0) sets[S.set_of[q]].sigs += S.nsig[q];
+  clk.lap("sigs");
+  bool any_keyed = false;
+  size_t misses = 0;
   {
     std::lock_guard<std::mutex> lk(ctx->mu);
     kc.c = ctx;
     tmed::keycache_pin(ctx);
     tmed::keycache_touch(ctx);
-    // concurrent read-only lookups while this thread holds the lock (no writer can run)
-    parallel_ranges(sets.size(), nt, [&](size_t lo, size_t hi, unsigned) {
-      for (size_t s = lo; s < hi; s++) sets[s].hold = tmed::keycache_find(ctx, sets[s].key);
+    // one pass per set in parallel while this thread holds the lock (no writer can run): the
+    // digest (or set_hash), the read-only find, the byte compare while the set's keys are in this
+    // thread's cache, and the entry's LRU tick
+    const uint64_t tick = tmed::keycache_call_tick(ctx);
+    std::vector<size_t> thits(std::max(1u, nt), 0), tsigs(std::max(1u, nt), 0);
+    parallel_ranges(sets.size(), nt, [&](size_t lo, size_t hi, unsigned t) {
+      for (size_t s = lo; s < hi; s++) {
+        SetRef &sr = sets[s];
+        const tmed_valset &v = *sr.v;
+        sr.skip = v.keyset || v.n == 0 || !v.pubkeys;
+        if (sr.skip) continue;
+        sr.key = tmed::kc_key(v.pubkeys, v.n, v.set_hash);
+        sr.e = tmed::keycache_find(ctx, sr.key);
+        sr.hit = sr.e && tmed::kc_same_keys(*sr.e, v.pubkeys, v.n);
+        if (sr.hit) {
+          const_cast<tmed::KcSet *>(sr.e)->touch(tick);
+          thits[t]++;
+          tsigs[t] += sr.sigs;
+        }
+      }
     });
-  }
-  clk.lap("find");
-  // cached entries are compared with the sets' keys outside the lock (a light-client batch holds
-  // ~10k sets); the pinned pool keeps their indexes valid
-  parallel_ranges(sets.size(), nt, [&](size_t lo, size_t hi, unsigned) {
-    for (size_t s = lo; s < hi; s++)
-      sets[s].hit = sets[s].hold && tmed::kc_same_keys(*sets[s].hold, sets[s].v->pubkeys, sets[s].v->n);
-  });
-  clk.lap("compare");
-  bool any_keyed = false;
-  size_t misses = 0;
-  {
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    clk.lap("find_compare");
+    size_t nh = 0, ns = 0;
+    for (size_t t = 0; t < thits.size(); t++) {
+      nh += thits[t];
+      ns += tsigs[t];
+    }
+    tmed::keycache_hits(ctx, nh, ns);
+    any_keyed = nh > 0;
     const uint64_t pool = tmed::keycache_pool_handle(ctx);
     for (SetRef &sr : sets)
-      if (sr.hit) {
-        tmed::keycache_hit(ctx, *sr.hold, sr.sigs);
-        sr.handle = pool;
-        any_keyed = true;
-      } else {
-        misses++;
-      }
+      if (sr.hit) sr.handle = pool;
+      else if (!sr.skip) misses++;
     if (misses) {
       // the call's signatures against every key it lacks: a window / batch that pays for them all
       // builds them before its kernels (each set alone may carry too few signatures)
       size_t call_sigs = 0, call_missing = 0;
       std::unordered_set<tmed::Pub32, tmed::Pub32Hash> seen;
       for (SetRef &sr : sets)
-        if (!sr.hit) {
+        if (!sr.hit && !sr.skip) {
           call_sigs += sr.sigs;
           call_missing += tmed::keycache_missing(ctx, sr.v->pubkeys, sr.v->n, &seen);
         }
       const bool build_all = call_missing && call_sigs >= tmed::kKcAmortizeSigsPerKey * call_missing;
       for (SetRef &sr : sets) {
-        if (sr.hit) continue;
-        sr.hold.reset();
+        if (sr.hit || sr.skip) continue;
+        sr.e = nullptr;
         if (tmed::keycache_lookup(ctx, sr.v->pubkeys, sr.v->n, sr.key, sr.sigs, /*may_reset=*/!any_keyed, &sr.handle,
-                                  sr.hold, build_all)) {
+                                  sr.e, build_all)) {
           sr.hit = true;
           any_keyed = true;
         }
@@ -1059,25 +1195,31 @@ static const tmed_commit_request *keycache_resolve(tmed_ctx *ctx, const tmed_com
   }
   clk.lap("lookups");
   if (!any_keyed) return reqs;
-  kc.vals.resize(sets.size());
-  kc.entry.assign(sets.size(), nullptr);
-  for (size_t s = 0; s < sets.size(); s++) {
-    SetRef &sr = sets[s];
-    if (!sr.hit) continue;
-    kc.entry[s] = sr.hold.get();
-    kc.vals[s] = *sr.v;
-    kc.vals[s].keyset = sr.handle;
-    kc.vals[s].keyset_index = sr.hold->idx.data();
-  }
-  kc.reqs.assign(reqs, reqs + n);
-  for (size_t q = 0; q < n; q++)
-    if (set_of[q] >= 0 && sets[set_of[q]].hit) kc.reqs[q].vals = &kc.vals[set_of[q]];
-  kc.holds.reserve(sets.size());
-  for (SetRef &sr : sets)
-    if (sr.hit) kc.holds.push_back(std::move(sr.hold));
+  // the call's requests, rewritten onto copies of the sets that resolved keyed
+  S.vals.resize(sets.size());
+  S.entry.resize(sets.size());
+  S.reqs.resize(n);
+  parallel_ranges(sets.size(), nt, [&](size_t lo, size_t hi, unsigned) {
+    for (size_t s = lo; s < hi; s++) {
+      const SetRef &sr = sets[s];
+      S.entry[s] = sr.hit ? sr.e : nullptr;
+      if (!sr.hit) continue;
+      S.vals[s] = *sr.v;
+      S.vals[s].keyset = sr.handle;
+      S.vals[s].keyset_index = sr.e->idx.data();
+    }
+  });
+  parallel_ranges(n, nt, [&](size_t lo, size_t hi, unsigned) {
+    for (size_t q = lo; q < hi; q++) {
+      S.reqs[q] = reqs[q];
+      const int32_t s = S.set_of[q];
+      if (s >= 0 && sets[s].hit) S.reqs[q].vals = &S.vals[s];
+    }
+  });
+  kc.active = true;
   clk.lap("rewrite");
   clk.emit("keycache_resolve", n, sets.size());
-  return kc.reqs.data();
+  return S.reqs.data();
 }
 
 // A large call whose sets share one key set (a light-client or evidence backlog) goes through
@@ -1116,89 +1258,178 @@ extern "C" int tmed_verify_commits(tmed_ctx *ctx, const tmed_commit_request *req
 }
 
 // ---- blocksync replay window (f4): pipelined LIGHT batches --------------------------------
+// The context's batch stream: windows of requests whose sets share one key set (0 = generic keys)
+// are cut into batches of up to bsz requests; batch b is planned, staged and queued while the
+// device copies in and verifies the batches before it, which are then collected and replayed (f4).
+// Same results as one run_seam over all requests.  The stream outlives a call: a replay that
+// submits window w+1 before collecting window w (tmed_blocksync_submit) keeps the device busy
+// across the windows' boundaries, where a call per window drains the pipeline at its end and
+// refills it (the first batch's planning and copy-in) at the next start.
 namespace {
+struct BsWindow {
+  const tmed_commit_request *rq = nullptr;  // the window's requests (checked: check_request)
+  tmed_commit_result *out = nullptr;
+  size_t n = 0, bsz = 0, next = 0;          // requests; per batch; the next one to batch
+  uint64_t keyset = 0;
+  const KcCall *kc = nullptr;  // planning's cached address indexes (a call-scoped window only)
+  // a submitted window owns its requests, its resolved set and its key-set cache pin (held until
+  // its last batch is collected; released outside ctx->mu: ~KcCall takes it)
+  std::vector<tmed_commit_request> own_reqs;
+  std::vector<tmed_block_id> own_bids;
+  std::vector<tmed_commit> own_commits;
+  tmed_valset own_set{}, own_vals{};  // the caller's set; its resolved copy
+  std::string own_chain;
+  std::unique_ptr<KcCall> own_kc;
+  size_t inflight = 0;
+  bool done() const { return next >= n && inflight == 0; }
+};
 struct BsBatch {
+  BsWindow *win = nullptr;
   size_t lo = 0, n = 0;
   Plans plans;
   Cands cands;
   std::vector<uint8_t> tmpl, bits, valid;
+  Group grp;  // the staged segments when candidates are aliased (else every run, in order)
   tmed::VoteStage st;
   bool device = false;  // queued on a vote slot (else verified synchronously / nothing to verify)
   std::chrono::steady_clock::time_point enq;  // when it was queued (TMED_TRACE timeline)
 };
 }  // namespace
 
-// Pipeline over batches of up to bsz requests whose validator sets share one key set (0 = generic
-// keys): batch b is planned, staged and queued while the device copies in and verifies the batch
-// before it, which is then collected and replayed (f4).  Same results as one run_seam over all
-// requests; the caller has checked every request (check_request) beforehand.
 // Pipeline depth.  With the signatures staged (pageable caller memory) two slots: a third
 // overlaps the host staging of batch b with the copy engine reading batch b-1 out of pinned
 // memory, and both slow down (C4 166-172 against 181-191 M verifies/s, profiles/r03/c4_pipe/).
 // With the signatures DMA'd from pinned caller memory the host's share per batch is ~1.5 ms
 // against ~2.2 ms of kernels, and a third slot keeps the kernel stream busy (C4 280-307 against
-// 258-282 M/s, profiles/r03/c4_direct/).  So the depth follows the first batch: three slots
-// when its signatures went direct (VoteStage::sig_direct), else two.  (A ramp of small first
+// 258-282 M/s, profiles/r03/c4_direct/).  So the depth follows the stream's first batch: three
+// slots when its signatures went direct (VoteStage::sig_direct), else two.  (A ramp of small first
 // batches did not pay, in round 3 nor again in round 4 with direct DMA: the host's planning and
 // staging of each larger batch outlasted the device work of the small one before it, leaving the
 // device idle 0.6-1.6 ms per ramp step — profiles/r04/c4_ramp_rejected.txt.)
 constexpr int kPipeSlots = 3;
 static_assert(kPipeSlots <= (int)(sizeof(((tmed_ctx *)nullptr)->vslot) / sizeof(tmed::VoteSlot)),
               "one context vote slot per pipeline slot");
-static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t nb, size_t bsz, uint64_t keyset,
-                         tmed_commit_result *out, const KcCall *kc) {
-  // kept per thread across calls, as run_seam's planning buffers (a blocksync window plans batch
-  // after batch into the same pages)
-  thread_local BsBatch slots[kPipeSlots];
-  for (BsBatch &b : slots) {
-    b.n = 0;
-    b.device = false;
+
+struct BsStream {
+  BsBatch slots[kPipeSlots];
+  int ns = 2;
+  size_t idx = 0;    // batches queued since the stream was last empty (slot idx % ns)
+  int rc = TMED_OK;  // the first error of a submitted window, reported by tmed_blocksync_wait
+  std::deque<std::unique_ptr<BsWindow>> wins;
+  bool empty() const {
+    for (const BsBatch &b : slots)
+      if (b.n) return false;
+    return true;
   }
-  int ns = 2;  // raised to 3 after batch 0 when its signatures went direct
+};
+
+namespace tmed {
+void bs_destroy(tmed_ctx *c) {  // tmed_destroy: nothing may still read the windows' buffers
+  if (!c->bs) return;
+  (void)hipStreamSynchronize(c->copy_stream);
+  (void)hipStreamSynchronize(c->stream);
+  delete c->bs;  // the windows' cache pins go with them (the cache is destroyed after this)
+  c->bs = nullptr;
+}
+}  // namespace tmed
+
+using BsClock = std::chrono::steady_clock;
+static double bs_us(BsClock::time_point a, BsClock::time_point b) {
+  return std::chrono::duration<double, std::micro>(b - a).count();
+}
+
+// Collect batch b (ctx->mu held): its bits, the alias copies, the replay into its window's results.
+// ph: tmed_seam_phase_us — host plan + templates + staging, host time blocked on the device
+// (enqueueing the copies and kernels, votes_collect), host replay.
+static int bs_finish(tmed_ctx *ctx, BsBatch &b, double ph[3]) {
+  if (b.n == 0) return TMED_OK;
+  BsWindow &w = *b.win;
+  const size_t m = b.cands.size();
+  const bool aliased = b.device && !b.cands.alias.empty();
+  int r = TMED_OK;
+  if (b.device) {
+    b.bits.resize(b.grp.size(b.cands));
+    const auto t0 = BsClock::now();
+    r = tmed::votes_collect(ctx, b.st, b.bits.data());
+    ph[1] += bs_us(t0, BsClock::now());
+  }
+  const auto t1 = BsClock::now();
+  if (r == TMED_OK && aliased) {  // bits by staged segment -> by candidate
+    b.valid.assign(m, 0);
+    scatter_bits(w.rq + b.lo, b.cands, b.grp, b.bits.data(), b.valid.data());
+    copy_aliases(b.cands, b.valid.data());
+  }
+  // the device bits are in candidate order: replay reads them directly (it applies the
+  // signature-length rule itself)
+  if (r == TMED_OK)
+    r = seam_replay(w.rq + b.lo, b.n, w.out + b.lo, b.plans, b.device && !aliased ? b.bits.data() : b.valid.data());
+  ph[2] += bs_us(t1, BsClock::now());
+  b.n = 0;
+  b.device = false;
+  b.win = nullptr;
+  w.inflight--;
+  return r;
+}
+
+// Collect every batch in flight, oldest first, except those of window `keep` (nullptr: all).
+static int bs_collect(tmed_ctx *ctx, BsStream &S, const BsWindow *keep, double ph[3]) {
   int rc = TMED_OK;
-  // tmed_seam_phase_us for a pipelined call: host plan + templates + staging, host time blocked on
-  // the device (enqueueing the copies and kernels, votes_collect), host replay — the first and
-  // last overlap device work.
-  using clock = std::chrono::steady_clock;
-  auto us = [](clock::time_point a, clock::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-  double ph[3] = {0, 0, 0};
-  auto finish = [&](BsBatch &b) -> int {
-    if (b.n == 0) return TMED_OK;
-    const size_t m = b.cands.size();
-    if (b.device) {
-      b.bits.resize(m);
-      const auto t0 = clock::now();
-      int r = tmed::votes_collect(ctx, b.st, b.bits.data());
-      ph[1] += us(t0, clock::now());
-      if (r != TMED_OK) return r;
+  for (int k = 0; k < S.ns; k++) {
+    BsBatch &b = S.slots[(S.idx + k) % S.ns];
+    if (b.n && b.win != keep) {
+      const int r = bs_finish(ctx, b, ph);
+      if (rc == TMED_OK) rc = r;
     }
-    const auto t1 = clock::now();
-    // the device bits are in candidate order: replay reads them directly (it applies the
-    // signature-length rule itself)
-    int r = seam_replay(reqs + b.lo, b.n, out + b.lo, b.plans, b.device ? b.bits.data() : b.valid.data());
-    ph[2] += us(t1, clock::now());
-    b.n = 0;
-    b.device = false;
-    return r;
-  };
-  std::unique_lock<std::mutex> lk(ctx->mu);
+  }
+  return rc;
+}
+
+// After an error: nothing queued may still read the callers' (pinned) buffers; the batches in
+// flight are dropped (their windows' results are incomplete: the error is what the caller gets).
+static void bs_abort(tmed_ctx *ctx, BsStream &S, int rc) {
+  (void)hipStreamSynchronize(ctx->copy_stream);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (BsBatch &b : S.slots)
+    if (b.n) {
+      b.n = 0;
+      b.device = false;
+      if (b.win) b.win->inflight--;
+      b.win = nullptr;
+    }
+  for (auto &w : S.wins) w->next = w->n;
+  if (S.rc == TMED_OK) S.rc = rc;
+}
+
+// Queue window w's batches (ctx->mu held through lk), collecting older batches as their slots are
+// reused; returns with up to S.ns - 1 of them... in flight.
+static int bs_pump(tmed_ctx *ctx, BsStream &S, BsWindow &w, double ph[3], std::unique_lock<std::mutex> &lk) {
+  int rc = TMED_OK;
+  if (S.empty()) {
+    S.idx = 0;
+    S.ns = 2;  // raised to 3 after the stream's first batch when its signatures went direct
+  }
   if (trace_on()) {  // origin of the per-batch device timeline in the trace
     if (!ctx->trace_t0) (void)hipEventCreate(&ctx->trace_t0);
     if (ctx->trace_t0) (void)hipEventRecord(ctx->trace_t0, ctx->stream);
   }
-  const auto t_origin = clock::now();
-  size_t idx = 0;
-  for (size_t lo = 0; lo < nb && rc == TMED_OK; idx++) {
+  const auto t_origin = BsClock::now();
+  while (w.next < w.n && rc == TMED_OK) {
     PhaseClock clk;
-    BsBatch &b = slots[idx % ns];
-    BsBatch &mid = slots[(idx + ns - 1) % ns];  // batch idx-1 (in flight; with two slots the same as old)
-    BsBatch &old = slots[(idx + 1) % ns];       // batch idx-ns+1: collected once batch idx is queued
-    b.lo = lo;
-    b.n = std::min(bsz, nb - lo);
-    lo += b.n;
-    const tmed_commit_request *rq = reqs + b.lo;
-    const auto tp = clock::now();
-    rc = seam_plan(rq, b.n, out + b.lo, b.plans, b.cands, kc);
+    const size_t idx = S.idx++;
+    const int ns = S.ns;
+    BsBatch &b = S.slots[idx % ns];
+    BsBatch &mid = S.slots[(idx + ns - 1) % ns];  // batch idx-1 (in flight; with two slots the same as old)
+    BsBatch &old = S.slots[(idx + 1) % ns];       // batch idx-ns+1: collected once batch idx is queued
+    if (b.n) rc = bs_finish(ctx, b, ph);          // the slot's previous batch (the depth changed)
+    if (rc != TMED_OK) break;
+    b.win = &w;
+    b.lo = w.next;
+    b.n = std::min(w.bsz, w.n - w.next);
+    w.next += b.n;
+    w.inflight++;
+    const tmed_commit_request *rq = w.rq + b.lo;
+    const auto tp = BsClock::now();
+    rc = seam_plan(rq, b.n, w.out + b.lo, b.plans, b.cands, w.kc);
     clk.lap("plan");
     const size_t m = b.cands.size();
     bool fits = true;
@@ -1206,28 +1437,34 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
     clk.lap("templates");
     if (rc == TMED_OK && m) {
       if (fits && m <= 0xffffffffu) {
-        rc = stage_group(ctx, rq, b.n, b.cands, Group(), keyset, b.tmpl.data(), (int)(idx % ns),
-                         b.st);
+        if (b.cands.alias.empty()) {
+          b.grp = Group();
+        } else {
+          b.grp.start();
+          size_t ap = 0;
+          for (size_t r = 0; r < b.cands.runs.size(); r++) b.grp.add_run(b.cands, (uint32_t)r, ap);
+        }
+        rc = stage_group(ctx, rq, b.n, b.cands, b.grp, w.keyset, b.tmpl.data(), (int)(idx % ns), b.st);
         clk.lap("stage");
-        const auto te = clock::now();
-        ph[0] += us(tp, te);
+        const auto te = BsClock::now();
+        ph[0] += bs_us(tp, te);
         if (rc == TMED_OK) rc = tmed::votes_enqueue(ctx, b.st);
-        b.enq = clock::now();
-        if (idx == 0 && b.st.sig_direct) ns = 3;
+        b.enq = BsClock::now();
+        if (idx == 0 && b.st.sig_direct) S.ns = 3;
         clk.lap("enqueue");
-        ph[1] += us(te, clock::now());  // queueing copies / launches can block behind a busy device
+        ph[1] += bs_us(te, BsClock::now());  // queueing copies / launches can block behind a busy device
         b.device = rc == TMED_OK;
       } else {  // oversize template: host-assembled messages, synchronous (drain the pipeline first)
-        rc = finish(old);
-        if (rc == TMED_OK) rc = finish(mid);
+        if (old.n && &old != &b) rc = bs_finish(ctx, old, ph);
+        if (rc == TMED_OK && mid.n && &mid != &b) rc = bs_finish(ctx, mid, ph);
         lk.unlock();
         b.valid.assign(m, 0);
         if (rc == TMED_OK) rc = ctx_verify_host_msgs(ctx, rq, b.n, b.cands, b.valid.data());
         lk.lock();
       }
     }
-    const bool traced = trace_on() && old.n && old.st.m;
-    if (rc == TMED_OK) rc = finish(old);  // overlaps the device work of batches idx-1 and idx
+    const bool traced = trace_on() && old.n && old.st.m && &old != &b;
+    if (rc == TMED_OK && &old != &b) rc = bs_finish(ctx, old, ph);  // overlaps the device work of batches idx-1 and idx
     clk.lap("finish_old");
     if (traced)
       fprintf(stderr,
@@ -1235,41 +1472,168 @@ static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t 
               " | device us: copy %.0f-%.0f kernels %.0f-%.0f | host us: enqueued %.0f collected %.0f\n",
               1000.0 * ctx->last_ms, 1000.0 * ctx->last_copy_ms, 1000.0 * ctx->last_copy_gap_ms,
               1000.0 * ctx->last_at[0], 1000.0 * ctx->last_at[1], 1000.0 * ctx->last_at[2], 1000.0 * ctx->last_at[3],
-              us(t_origin, old.enq), us(t_origin, clock::now()));
+              bs_us(t_origin, b.enq), bs_us(t_origin, BsClock::now()));
     clk.emit("pipelined batch", b.n, m);
   }
-  for (int k = 0; k < ns; k++)  // oldest first
-    if (rc == TMED_OK) rc = finish(slots[(idx + k) % ns]);
-  if (rc != TMED_OK) {  // nothing of this call may still read the caller's (pinned) buffers
-    (void)hipStreamSynchronize(ctx->copy_stream);
-    (void)hipStreamSynchronize(ctx->stream);
+  return rc;
+}
+
+static BsStream &bs_stream(tmed_ctx *ctx) {
+  if (!ctx->bs) ctx->bs = new BsStream();
+  return *ctx->bs;
+}
+
+// Windows whose batches are all collected leave the stream (front first); they are destroyed by
+// the caller after it released ctx->mu.
+static void bs_pop_done(BsStream &S, std::vector<std::unique_ptr<BsWindow>> &gone) {
+  while (!S.wins.empty() && S.wins.front()->done()) {
+    gone.push_back(std::move(S.wins.front()));
+    S.wins.pop_front();
   }
-  for (int k = 0; k < 3; k++) g_seam_us[k] = ph[k];
+}
+
+// Every batch of the stream collected (ctx->mu held): before a seam call uses the vote slots.
+static int bs_drain(tmed_ctx *ctx) {
+  if (!ctx->bs || ctx->bs->empty()) return TMED_OK;
+  double ph[3] = {0, 0, 0};
+  int rc = bs_collect(ctx, *ctx->bs, nullptr, ph);
+  if (rc != TMED_OK) bs_abort(ctx, *ctx->bs, rc);
+  return rc;
+}
+
+// One window through the stream and back (every batch collected before returning).
+static int run_pipelined(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t nb, size_t bsz, uint64_t keyset,
+                         tmed_commit_result *out, const KcCall *kc) {
+  std::vector<std::unique_ptr<BsWindow>> gone;
+  int rc;
+  {
+    std::unique_lock<std::mutex> lk(ctx->mu);
+    BsStream &S = bs_stream(ctx);
+    double ph[3] = {0, 0, 0};
+    rc = bs_collect(ctx, S, nullptr, ph);  // earlier submitted windows finish first
+    if (rc != TMED_OK) bs_abort(ctx, S, rc);  // theirs: reported here and by tmed_blocksync_wait
+    const int prev = S.rc;
+    auto w = std::make_unique<BsWindow>();
+    w->rq = reqs;
+    w->out = out;
+    w->n = nb;
+    w->bsz = std::max<size_t>(1, bsz);
+    w->keyset = keyset;
+    w->kc = kc;
+    BsWindow *wp = w.get();
+    S.wins.push_back(std::move(w));
+    if (rc == TMED_OK) {
+      rc = bs_pump(ctx, S, *wp, ph, lk);
+      if (rc == TMED_OK) rc = bs_collect(ctx, S, nullptr, ph);
+      if (rc != TMED_OK) {
+        bs_abort(ctx, S, rc);
+        S.rc = prev;  // only this call's window was in flight: its error is reported here
+      }
+    }
+    wp->next = wp->n;
+    for (int k = 0; k < 3; k++) g_seam_us[k] = ph[k];
+    bs_pop_done(S, gone);
+    for (auto it = S.wins.begin(); it != S.wins.end(); ++it)  // this call's window (borrowed buffers) never stays
+      if (it->get() == wp) {
+        gone.push_back(std::move(*it));
+        S.wins.erase(it);
+        break;
+      }
+  }
+  return rc;
+}
+
+// A blocksync window as LIGHT requests (blockchain/v0/reactor.go:366-367), resolved through the
+// key-set cache, owned by the returned window.
+static int bs_window(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t batch_blocks, tmed_commit_result *out,
+                     std::unique_ptr<BsWindow> &win) {
+  if (!ctx || !w || (w->n_blocks && (!w->vals || !w->block_ids || !w->heights || !w->commits || !out)))
+    return TMED_EINVAL;
+  const size_t nb = w->n_blocks;
+  win = std::make_unique<BsWindow>();
+  BsWindow &W = *win;
+  // the structs are copied (the caller may reuse them once submit returns); what they point to
+  // (hashes, commit arrays, keys) is the caller's until the window's results are final
+  W.own_reqs.resize(nb);
+  W.own_bids.assign(w->block_ids, w->block_ids + nb);
+  W.own_commits.assign(w->commits, w->commits + nb);
+  if (nb) W.own_set = *w->vals;
+  if (w->chain_id_len) W.own_chain.assign(w->chain_id, w->chain_id_len);
+  for (size_t h = 0; h < nb; h++) {
+    tmed_commit_request &r = W.own_reqs[h];
+    memset(&r, 0, sizeof r);
+    r.mode = TMED_MODE_LIGHT;
+    r.chain_id = W.own_chain.data();
+    r.chain_id_len = w->chain_id_len;
+    r.vals = &W.own_set;
+    r.block_id = &W.own_bids[h];
+    r.height = w->heights[h];
+    r.commit = &W.own_commits[h];
+    if (check_request(r) != TMED_OK) return TMED_EINVAL;
+  }
+  W.own_kc = std::make_unique<KcCall>();  // one set for the whole window
+  if (nb) {
+    const tmed_commit_request *rq = keycache_resolve(ctx, W.own_reqs.data(), nb, *W.own_kc);
+    if (rq != W.own_reqs.data()) {  // resolved onto the cache's pool: the window keeps its own copy
+      W.own_vals = *rq[0].vals;
+      for (tmed_commit_request &r : W.own_reqs) r.vals = &W.own_vals;
+    }
+  }
+  W.rq = W.own_reqs.data();
+  W.out = out;
+  W.n = nb;
+  W.bsz = batch_blocks ? batch_blocks : 128;
+  W.keyset = nb ? W.own_reqs[0].vals->keyset : 0;
+  return TMED_OK;
+}
+
+extern "C" int tmed_blocksync_submit(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t batch_blocks,
+                                     tmed_commit_result *out) {
+  std::unique_ptr<BsWindow> win;
+  int rc = bs_window(ctx, w, batch_blocks, out, win);
+  if (rc != TMED_OK) return rc;
+  std::vector<std::unique_ptr<BsWindow>> gone;
+  {
+    std::unique_lock<std::mutex> lk(ctx->mu);
+    BsStream &S = bs_stream(ctx);
+    double ph[3] = {0, 0, 0};
+    BsWindow *wp = win.get();
+    S.wins.push_back(std::move(win));
+    rc = bs_pump(ctx, S, *wp, ph, lk);
+    // every EARLIER window's results final on return; this window's last batches stay in flight
+    if (rc == TMED_OK) rc = bs_collect(ctx, S, wp, ph);
+    if (rc != TMED_OK) bs_abort(ctx, S, rc);
+    for (int k = 0; k < 3; k++) g_seam_us[k] = ph[k];
+    bs_pop_done(S, gone);
+  }
+  return rc;
+}
+
+extern "C" int tmed_blocksync_wait(tmed_ctx *ctx) {
+  if (!ctx) return TMED_EINVAL;
+  std::vector<std::unique_ptr<BsWindow>> gone;
+  int rc;
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!ctx->bs) return TMED_OK;
+    BsStream &S = *ctx->bs;
+    double ph[3] = {0, 0, 0};
+    rc = bs_collect(ctx, S, nullptr, ph);
+    if (rc != TMED_OK) bs_abort(ctx, S, rc);
+    rc = S.rc;
+    S.rc = TMED_OK;
+    for (int k = 0; k < 3; k++) g_seam_us[k] = ph[k];
+    bs_pop_done(S, gone);
+  }
   return rc;
 }
 
 extern "C" int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t batch_blocks,
                                      tmed_commit_result *out) {
-  if (!ctx || !w || (w->n_blocks && (!w->vals || !w->block_ids || !w->heights || !w->commits || !out)))
-    return TMED_EINVAL;
-  const size_t nb = w->n_blocks;
-  if (nb == 0) return TMED_OK;
-  std::vector<tmed_commit_request> reqs(nb);
-  for (size_t h = 0; h < nb; h++) {
-    tmed_commit_request &r = reqs[h];
-    memset(&r, 0, sizeof r);
-    r.mode = TMED_MODE_LIGHT;
-    r.chain_id = w->chain_id;
-    r.chain_id_len = w->chain_id_len;
-    r.vals = w->vals;
-    r.block_id = &w->block_ids[h];
-    r.height = w->heights[h];
-    r.commit = &w->commits[h];
-    if (check_request(r) != TMED_OK) return TMED_EINVAL;
-  }
-  KcCall kc;  // one set for the whole window
-  const tmed_commit_request *rq = keycache_resolve(ctx, reqs.data(), nb, kc);
-  return run_pipelined(ctx, rq, nb, batch_blocks ? batch_blocks : 128, rq[0].vals->keyset, out, &kc);
+  std::unique_ptr<BsWindow> win;
+  int rc = bs_window(ctx, w, batch_blocks, out, win);
+  if (rc != TMED_OK || win->n == 0) return rc;
+  return run_pipelined(ctx, win->rq, win->n, win->bsz, win->keyset, out, nullptr);
 }
 
 // ---- several GPUs in one process (§8e): contiguous shards balanced by signature count ----

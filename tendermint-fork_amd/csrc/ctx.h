@@ -11,6 +11,7 @@
 #include "keycache.h"
 
 struct tmed_ctx;
+struct BsStream;  // commit.hip: the context's blocksync batch stream
 
 namespace tmed {
 
@@ -90,16 +91,19 @@ Keyset *find_keyset(tmed_ctx *c, uint64_t handle);
 // The commit seam's key-set cache (keycache.hip, keycache.h); every call below holds ctx->mu.
 struct KeyCacheDev;
 void keycache_destroy(tmed_ctx *c);
+void bs_destroy(tmed_ctx *c);  // commit.hip: the blocksync batch stream (before keycache_destroy)
 void keycache_pin(tmed_ctx *c);    // a seam call resolving sets: no pool reset until it unpins
 void keycache_unpin(tmed_ctx *c);
 uint64_t keycache_pool_handle(const tmed_ctx *c);  // 0 before the first key is built
 // KeyCache::find: read-only, callable from several threads while the caller holds ctx->mu (after
 // keycache_touch has created the cache)
-std::shared_ptr<const KcSet> keycache_find(tmed_ctx *c, const KcKey &key);
+const KcSet *keycache_find(tmed_ctx *c, const KcKey &key);
+uint64_t keycache_call_tick(tmed_ctx *c);                        // KeyCache::call_tick
+void keycache_hits(tmed_ctx *c, size_t sets, size_t sigs);       // KeyCache::hits
 void keycache_touch(tmed_ctx *c);
 void keycache_hit(tmed_ctx *c, const KcSet &e, size_t sigs);  // KeyCache::hit
 bool keycache_lookup(tmed_ctx *c, const uint8_t *pubs, size_t n, const KcKey &key, size_t sigs, bool may_reset,
-                     uint64_t *handle, std::shared_ptr<const KcSet> &hold, bool force_build = false);
+                     uint64_t *handle, const KcSet *&hold, bool force_build = false);
 int keycache_drain(tmed_ctx *c);  // build the keys queued behind generic calls (asynchronously)
 void keycache_after_call(tmed_ctx *c);  // wake the context's key-build worker when keys are queued
 size_t keycache_missing(tmed_ctx *c, const uint8_t *pubs, size_t n, std::unordered_set<Pub32, Pub32Hash> *seen);
@@ -210,7 +214,8 @@ struct tmed_ctx {
   tmed::KernelTimer timer;
   tmed::DevBuf d_a, d_b, d_msg, d_off, d_out, d_c;
   tmed::HostBuf h_a, h_b, h_msg, h_off, h_out, h_c;
-  tmed::VoteSlot vslot[3];  // the blocksync pipeline (commit.hip run_pipelined: two slots, three with TMED_PIPE_SLOTS=3)
+  tmed::VoteSlot vslot[3];  // the blocksync pipeline (commit.hip BsStream: two slots, three when the signatures go direct)
+  BsStream *bs = nullptr;   // batches of submitted blocksync windows in flight (tmed_blocksync_submit)
   tmed::DevBuf d_merkle_a, d_merkle_b, d_merkle_idx;  // Merkle level digests (ping-pong) + level indexes
   tmed::DevBuf d_korder;  // key-grouped order of a key-cached batch: counts / cursors + permutation
   tmed::DevBuf d_zip;     // ZIP-215 batch mode scratch (zip215.hip zip_bufs: points, digits, sort, buckets)

@@ -34,6 +34,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <unordered_map>
@@ -149,7 +150,8 @@ struct AddrIndex {
 struct KcSet {
   std::vector<uint8_t> pubs;
   std::vector<uint32_t> idx;
-  uint64_t tick = 0;
+  std::atomic<uint64_t> tick{0};  // LRU: the call that last used it (set from a call's threads)
+  void touch(uint64_t t) { tick.store(t, std::memory_order_relaxed); }
   size_t bytes() const { return pubs.size() + 4 * idx.size() + 64; }
   // nullptr when `addrs` (n x 20) differ from the addresses the cached index was built from
   const AddrIndex *addr_index(const uint8_t *addrs, size_t n) const {
@@ -204,29 +206,36 @@ class KeyCache {
   size_t sets_cached() const { return sets_.size(); }
   size_t pending_keys() const { return pending_.size() / 32; }
   int users() const { return users_; }
+  size_t retired() const { return retired_.size(); }
 
   // A seam call holds the pool (no reset while its resolved indexes are in use) from before its
-  // first lookup until it has collected its last batch.
+  // first lookup until it has collected its last batch.  Entries dropped meanwhile (LRU bound, a
+  // reset, a mismatching key) are retired, not freed, until no call is pinned: the entry pointers
+  // a call resolved (and their idx / address index) stay valid for the whole call without a
+  // reference count per entry (a light-client batch resolves ~10k sets).
   void pin() { users_++; }
   void unpin() {
     if (users_ > 0) users_--;
+    if (users_ == 0) retired_.clear();
   }
 
   // Fast path of a call resolving many sets: the cached entry under `key` (nullptr if none), to be
-  // compared with the set's keys outside the lock; a match is then recorded with hit().
-  // Read-only (safe from several threads at once while the caller holds the lock): the entry's
-  // LRU tick is refreshed by hit().
-  std::shared_ptr<const KcSet> find(const KcKey &key) const {
+  // compared with the set's keys; a match is then recorded with touch(call_tick()) + hits().
+  // Read-only (safe from several threads at once while the caller holds the lock).
+  const KcSet *find(const KcKey &key) const {
     auto it = sets_.find(key);
-    if (it == sets_.end()) return nullptr;
-    return it->second;
+    return it == sets_.end() ? nullptr : it->second.get();
+  }
+  uint64_t call_tick() { return ++tick_; }
+  void hits(size_t sets, size_t sigs) {
+    st.lookups += sets;
+    st.hits += sets;
+    st.keyed_sets += sets;
+    st.keyed_sigs += sigs;
   }
   void hit(const KcSet &e, size_t sigs) {
-    const_cast<KcSet &>(e).tick = ++tick_;
-    st.lookups++;
-    st.hits++;
-    st.keyed_sets++;
-    st.keyed_sigs += sigs;
+    const_cast<KcSet &>(e).touch(call_tick());
+    hits(1, sigs);
   }
 
   // Resolve one set for a call that pinned the pool.  Returns true (keyed: *hold->idx are the
@@ -234,19 +243,19 @@ class KeyCache {
   // (generic this call).  may_reset: the call has resolved no keyed set yet.
   // force_build: build missing keys now whatever the call's size (tmed_keycache_warm).
   bool lookup(const uint8_t *pubs, size_t n, const KcKey &key, size_t sigs, bool may_reset,
-              std::shared_ptr<const KcSet> &hold, bool force_build = false) {
+              const KcSet *&hold, bool force_build = false) {
     st.lookups++;
     auto it = sets_.find(key);
     if (it != sets_.end()) {
       KcSet &s = *it->second;
       if (kc_same_keys(s, pubs, n)) {
-        s.tick = ++tick_;
+        s.touch(++tick_);
         st.hits++;
-        return keyed(it->second, sigs, hold);
+        return keyed(it->second.get(), sigs, hold);
       }
       drop_(it);  // same key, other keys (a stale or wrong set_hash, a digest collision)
     }
-    auto e = std::make_shared<KcSet>();
+    auto e = std::make_unique<KcSet>();
     e->pubs.assign(pubs, pubs + 32 * n);
     e->idx.resize(n);
     std::vector<size_t> fresh;  // first position of each key the pool lacks
@@ -315,6 +324,8 @@ class KeyCache {
   void reset() {
     be.reset();
     slot_.clear();
+    if (users_ > 0)
+      for (auto &kv : sets_) retired_.push_back(std::move(kv.second));
     sets_.clear();
     set_bytes_ = 0;
     pending_.clear();
@@ -322,7 +333,7 @@ class KeyCache {
   }
 
  private:
-  bool keyed(const std::shared_ptr<KcSet> &e, size_t sigs, std::shared_ptr<const KcSet> &hold) {
+  bool keyed(const KcSet *e, size_t sigs, const KcSet *&hold) {
     hold = e;
     st.keyed_sets++;
     st.keyed_sigs += sigs;
@@ -364,28 +375,30 @@ class KeyCache {
     st.keys_appended += m;
     return true;
   }
-  bool insert_keyed(std::shared_ptr<KcSet> e, const KcKey &key, size_t sigs, std::shared_ptr<const KcSet> &hold) {
-    e->tick = ++tick_;
+  bool insert_keyed(std::unique_ptr<KcSet> e, const KcKey &key, size_t sigs, const KcSet *&hold) {
+    e->touch(++tick_);
     set_bytes_ += e->bytes();
-    sets_[key] = e;
+    const KcSet *p = e.get();
+    sets_[key] = std::move(e);
     if (sets_.size() > max_sets || set_bytes_ > max_set_bytes) evict_();
-    return keyed(e, sigs, hold);
+    return keyed(p, sigs, hold);
   }
-  void drop_(typename std::unordered_map<KcKey, std::shared_ptr<KcSet>, KcKeyHash>::iterator it) {
+  void drop_(typename std::unordered_map<KcKey, std::unique_ptr<KcSet>, KcKeyHash>::iterator it) {
     set_bytes_ -= it->second->bytes();
+    if (users_ > 0) retired_.push_back(std::move(it->second));
     sets_.erase(it);
   }
-  // Least recently used quarter out (calls in flight keep their entries through `hold`).
+  // Least recently used quarter out (calls in flight keep theirs: retired_).
   void evict_() {
     std::vector<uint64_t> ticks;
     ticks.reserve(sets_.size());
-    for (auto &kv : sets_) ticks.push_back(kv.second->tick);
+    for (auto &kv : sets_) ticks.push_back(kv.second->tick.load(std::memory_order_relaxed));
     const size_t k = std::max<size_t>(1, ticks.size() / 4);
     std::nth_element(ticks.begin(), ticks.begin() + (k - 1), ticks.end());
     const uint64_t cut = ticks[k - 1];
     for (auto it = sets_.begin(); it != sets_.end();) {
       auto nx = std::next(it);
-      if (it->second->tick <= cut) {
+      if (it->second->tick.load(std::memory_order_relaxed) <= cut) {
         drop_(it);
         st.sets_evicted++;
       }
@@ -394,7 +407,8 @@ class KeyCache {
   }
 
   std::unordered_map<Pub32, uint32_t, Pub32Hash> slot_;  // pool index of every key in the pool
-  std::unordered_map<KcKey, std::shared_ptr<KcSet>, KcKeyHash> sets_;
+  std::unordered_map<KcKey, std::unique_ptr<KcSet>, KcKeyHash> sets_;
+  std::vector<std::unique_ptr<KcSet>> retired_;  // dropped while a call was pinned
   std::vector<uint8_t> pending_;  // keys queued by generic calls
   std::unordered_set<Pub32, Pub32Hash> pend_set_;
   size_t set_bytes_ = 0;

@@ -110,7 +110,9 @@ void keycache_destroy(tmed_ctx *c) {  // ctx->mu not held: the worker may be wai
 
 // ---- the seam's side (commit.hip keycache_resolve); the caller holds ctx->mu -----------------
 uint64_t keycache_pool_handle(const tmed_ctx *c) { return c->kc ? c->kc->kc.be.handle : 0; }
-std::shared_ptr<const KcSet> keycache_find(tmed_ctx *c, const KcKey &key) { return cache_of(c).find(key); }
+const KcSet *keycache_find(tmed_ctx *c, const KcKey &key) { return cache_of(c).find(key); }
+uint64_t keycache_call_tick(tmed_ctx *c) { return cache_of(c).call_tick(); }
+void keycache_hits(tmed_ctx *c, size_t sets, size_t sigs) { cache_of(c).hits(sets, sigs); }
 void keycache_touch(tmed_ctx *c) { (void)cache_of(c); }
 void keycache_hit(tmed_ctx *c, const KcSet &e, size_t sigs) { cache_of(c).hit(e, sigs); }
 void keycache_pin(tmed_ctx *c) { cache_of(c).pin(); }
@@ -118,7 +120,7 @@ void keycache_unpin(tmed_ctx *c) { cache_of(c).unpin(); }
 // true: the set's signatures take the key-cached kernels in this call, *handle = the pool and
 // hold->idx its index there.
 bool keycache_lookup(tmed_ctx *c, const uint8_t *pubs, size_t n, const KcKey &key, size_t sigs, bool may_reset,
-                     uint64_t *handle, std::shared_ptr<const KcSet> &hold, bool force_build) {
+                     uint64_t *handle, const KcSet *&hold, bool force_build) {
   KeyCache<KcBackendDev> &kc = cache_of(c);
   if (!kc.lookup(pubs, n, key, sigs, may_reset, hold, force_build)) return false;
   *handle = kc.be.handle;
@@ -214,7 +216,7 @@ int tmed_keycache_warm(tmed_ctx *c, const tmed_valset *vals) {
   (void)hipSetDevice(c->device);
   int rc = keycache_drain(c);
   if (rc != TMED_OK) return rc;
-  std::shared_ptr<const KcSet> hold;
+  const KcSet *hold = nullptr;
   uint64_t h = 0;
   kc.pin();
   // the missing keys are built now, whatever a call's size would say

@@ -213,6 +213,7 @@ func (a *arena) free() {
 	for _, p := range a.ptrs {
 		C.free(p)
 	}
+	a.ptrs = nil
 }
 
 func (a *arena) blockID(b *BlockID) C.tmed_block_id {
@@ -399,6 +400,97 @@ func (e *Engine) BlocksyncVerify(w *BlocksyncWindow, batchBlocks int) ([]Result,
 		return nil, errors.New(C.GoString(C.tmed_strerror(rc)))
 	}
 	return toResults(res), nil
+}
+
+// PendingWindow is a window queued by BlocksyncSubmit.  Its results are final once a LATER
+// BlocksyncSubmit or BlocksyncWait on the same engine has returned; until then its C copies and
+// its pinned signature buffer stay allocated (the library DMAs from them and writes the results
+// into C memory: cgo forbids C retaining Go pointers after a call returns).
+type PendingWindow struct {
+	e   *Engine
+	a   arena
+	pin unsafe.Pointer
+	res *C.tmed_commit_result
+	n   int
+}
+
+// BlocksyncSubmit queues a window behind the engine's windows in flight (tmed_blocksync_submit):
+// the reactor's replay submits window w+1 before it applies window w, so the device is never
+// drained between windows.  When it returns, every earlier submitted window's Results are final.
+func (e *Engine) BlocksyncSubmit(w *BlocksyncWindow, batchBlocks int) (*PendingWindow, error) {
+	n := len(w.Commits)
+	p := &PendingWindow{e: e, n: n}
+	if n == 0 {
+		return p, nil
+	}
+	a := &p.a
+	vs := (*C.tmed_valset)(a.alloc(unsafe.Sizeof(C.tmed_valset{})))
+	*vs = a.valset(w.Vals)
+	cs := (*[1 << 26]C.tmed_commit)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_commit{})))[:n:n]
+	bids := (*[1 << 26]C.tmed_block_id)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_block_id{})))[:n:n]
+	total := 0
+	for _, c := range w.Commits {
+		total += len(c.Sigs)
+	}
+	// a pinned buffer per window in flight (the engine's shared arena serves synchronous calls)
+	if total > 0 && C.tmed_host_alloc(C.size_t(total), &p.pin) != 0 {
+		p.pin = nil
+	}
+	off := 0
+	for i, c := range w.Commits {
+		sigs := (*C.uint8_t)(nil)
+		if p.pin != nil && len(c.Sigs) > 0 {
+			q := unsafe.Add(p.pin, off)
+			copy(unsafe.Slice((*byte)(q), len(c.Sigs)), c.Sigs)
+			sigs, off = (*C.uint8_t)(q), off+len(c.Sigs)
+		} else {
+			sigs = a.bytes(c.Sigs)
+		}
+		cs[i] = C.tmed_commit{height: C.int64_t(c.Height), round: C.int32_t(c.Round), block_id: a.blockID(&c.BlockID),
+			n_sigs: C.size_t(len(c.Flags)), flags: a.bytes(c.Flags), addresses: a.bytes(c.Addresses),
+			ts_seconds: a.i64(c.TsSeconds), ts_nanos: a.i32(c.TsNanos), sigs: sigs, sig_lens: a.u32(c.SigLens),
+			address_lens: a.u32(c.AddrLens)}
+		bids[i] = a.blockID(&w.BlockIDs[i])
+	}
+	cid := C.CString(w.ChainID)
+	a.ptrs = append(a.ptrs, unsafe.Pointer(cid))
+	win := (*C.tmed_blocksync_window)(a.alloc(unsafe.Sizeof(C.tmed_blocksync_window{})))
+	*win = C.tmed_blocksync_window{chain_id: cid, chain_id_len: C.uint32_t(len(w.ChainID)), vals: vs,
+		n_blocks: C.size_t(n), block_ids: &bids[0], heights: a.i64(w.Heights), commits: &cs[0]}
+	p.res = (*C.tmed_commit_result)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_commit_result{})))
+	if rc := C.tmed_blocksync_submit(e.ctx, win, C.uint32_t(batchBlocks), p.res); rc != 0 {
+		p.free()
+		return nil, errors.New(C.GoString(C.tmed_strerror(rc)))
+	}
+	return p, nil
+}
+
+// BlocksyncWait collects every window submitted on the engine (tmed_blocksync_wait).
+func (e *Engine) BlocksyncWait() error {
+	if rc := C.tmed_blocksync_wait(e.ctx); rc != 0 {
+		return errors.New(C.GoString(C.tmed_strerror(rc)))
+	}
+	return nil
+}
+
+// Results returns the window's outcomes and releases its memory.  Call it only after a later
+// BlocksyncSubmit or BlocksyncWait returned without error.
+func (p *PendingWindow) Results() []Result {
+	if p.n == 0 {
+		return nil
+	}
+	out := toResults(unsafe.Slice(p.res, p.n))
+	p.free()
+	return out
+}
+
+func (p *PendingWindow) free() {
+	if p.pin != nil {
+		C.tmed_host_free(p.pin)
+		p.pin = nil
+	}
+	p.a.free()
+	p.n = 0
 }
 
 // ValsetHashes returns ValidatorSet.Hash() of every set: set s is validators

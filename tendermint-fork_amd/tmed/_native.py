@@ -120,7 +120,7 @@ EXPORTED_SYMBOLS = [
     "tmed_vote_sign_bytes", "tmed_valu_peak", "tmed_verify_commits", "tmed_verify_commits_with",
     "tmed_keyset_load", "tmed_keyset_free", "tmed_keyset_extend", "tmed_verify_batch_keyset",
     "tmed_keycache_config", "tmed_keycache_stats", "tmed_keycache_flush", "tmed_keycache_warm", "tmed_keycache_wait", "tmed_verify_batch_keyset_device",
-    "tmed_set_kernel_timing", "tmed_kernel_times", "tmed_blocksync_verify",
+    "tmed_set_kernel_timing", "tmed_kernel_times", "tmed_blocksync_verify", "tmed_blocksync_submit", "tmed_blocksync_wait",
     "tmed_merkle_roots", "tmed_valset_hashes", "tmed_header_hashes", "tmed_partset_roots",
     "tmed_verify_commits_multi", "tmed_blocksync_verify_multi", "tmed_window_stats", "tmed_b_window_bits", "tmed_keyset_b_window_bits", "tmed_keyset_a_window_bits", "tmed_seam_phase_us",
     "tmed_verify_batch_zip215", "tmed_verify_batch_zip215_device", "tmed_zip215_set_seed", "tmed_zip215_stats",

@@ -28,3 +28,14 @@ def dist_setup():
         else:
             dist.init_process_group("nccl", device_id=dev)
     return world, rank, local, dev, coll
+
+
+def gpu_count_fields(world):
+    """The JSON fields naming the GPU count of a run: {"n_gpus": world} for real ranks (one GPU
+    each); for a gloo rehearsal with fewer GPUs than ranks, {"n_gpus_simulated": world,
+    "n_gpus_physical": k} instead, so the line cannot be read as an N-GPU measurement."""
+    import torch
+    ndev = max(1, torch.cuda.device_count())
+    if os.environ.get("TMED_DIST_BACKEND") == "gloo" and world > ndev:
+        return {"n_gpus_simulated": world, "n_gpus_physical": ndev}
+    return {"n_gpus": world}

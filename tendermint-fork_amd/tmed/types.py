@@ -269,6 +269,10 @@ def _bind():
         l.tmed_blocksync_verify.restype = ctypes.c_int
         l.tmed_blocksync_verify.argtypes = [ctypes.c_void_p, ctypes.POINTER(_BlocksyncWindowC), ctypes.c_uint32,
                                             ctypes.POINTER(_ResultC)]
+        l.tmed_blocksync_submit.restype = ctypes.c_int
+        l.tmed_blocksync_submit.argtypes = l.tmed_blocksync_verify.argtypes
+        l.tmed_blocksync_wait.restype = ctypes.c_int
+        l.tmed_blocksync_wait.argtypes = [ctypes.c_void_p]
         l.tmed_verify_commits_with.restype = ctypes.c_int
         l.tmed_verify_commits_with.argtypes = [ctypes.POINTER(_RequestC), ctypes.c_size_t,
                                                ctypes.POINTER(_ResultC), VERIFY_FN, ctypes.c_void_p]
@@ -282,6 +286,13 @@ def _bind():
         l.tmed_seam_phase_us.restype = ctypes.c_int
         l.tmed_seam_phase_us.argtypes = [ctypes.POINTER(ctypes.c_double)]
     return l
+
+
+def blocksync_wait(engine):
+    """tmed_blocksync_wait: collect every window submitted on the engine (BlocksyncWindow.submit)."""
+    rc = _bind().tmed_blocksync_wait(engine._h)
+    if rc != TMED_OK:
+        raise TmedError(rc, "tmed_blocksync_wait")
 
 
 def _ctx_array(engines):
@@ -513,6 +524,15 @@ class BlocksyncWindow:
             rc = _bind().tmed_blocksync_verify(engine._h, ctypes.byref(self.win), batch_blocks, self.res)
         if rc != TMED_OK:
             raise TmedError(rc, "tmed_blocksync_verify")
+        return self.res
+
+    def submit(self, engine, batch_blocks: int = 0):
+        """tmed_blocksync_submit: queue this window behind the engine's windows in flight; returns
+        once every EARLIER submitted window's results are final (this one's are final after the
+        next submit or blocksync_wait).  The window's commit arrays must stay unchanged until then."""
+        rc = _bind().tmed_blocksync_submit(engine._h, ctypes.byref(self.win), batch_blocks, self.res)
+        if rc != TMED_OK:
+            raise TmedError(rc, "tmed_blocksync_submit")
         return self.res
 
     def codes(self):

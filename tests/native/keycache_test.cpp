@@ -46,7 +46,7 @@ int kct_lookup(void *h, const uint8_t *pubs, size_t n, const uint8_t *set_hash, 
                int force, int fast, uint32_t *idx_out) {
   KeyCache<HostPool> &kc = ((Kct *)h)->kc;
   const KcKey key = kc_key(pubs, n, set_hash);
-  std::shared_ptr<const KcSet> hold;
+  const KcSet *hold = nullptr;
   bool keyed = false;
   if (fast) {
     hold = kc.find(key);
@@ -54,7 +54,7 @@ int kct_lookup(void *h, const uint8_t *pubs, size_t n, const uint8_t *set_hash, 
       kc.hit(*hold, sigs);
       keyed = true;
     } else {
-      hold.reset();
+      hold = nullptr;
     }
   }
   if (!keyed) keyed = kc.lookup(pubs, n, key, sigs, may_reset != 0, hold, force != 0);
@@ -79,5 +79,6 @@ int kct_pool_key(void *h, uint32_t i, uint8_t out[32]) {
   memcpy(out, &p.keys[(size_t)i * 32], 32);
   return 0;
 }
+size_t kct_retired(void *h) { return ((Kct *)h)->kc.retired(); }
 void kct_digest(const uint8_t *pubs, size_t n, uint8_t out[32]) { kc_digest(pubs, n, out); }
 }

@@ -330,3 +330,79 @@ def test_blocksync_pinned_signatures_gpu(engine, pinned, keyed):
         if ks:
             engine.keyset_free(ks)
             vals.keyset = 0
+
+
+@pytest.mark.parametrize("keyed", [False, True])
+def test_blocksync_stream_of_windows_gpu(engine, keyed):
+    """tmed_blocksync_submit / tmed_blocksync_wait: windows submitted back to back (batches of one
+    window still in flight when the next is queued, windows of 1, 5 and 12 blocks, pinned and
+    pageable signatures) give exactly the per-window tmed_blocksync_verify results; every earlier
+    window is final when submit returns; a tmed_verify_commits call between submits first collects
+    the stream; the structs passed to submit may be rebuilt right after it returns."""
+    import hashlib
+    import numpy as np
+    from tmed import PinnedBuffer
+    from tmed.workload import make_valset, pubkeys_of, seeds_from_tag, sign_commits
+    nvals = 1500
+    seeds = seeds_from_tag(b"tmed-stream-key", 0, nvals)
+    vals, order = make_valset(pubkeys_of(engine, seeds), [10] * nvals)
+    addrs = np.array([np.frombuffer(v.address, np.uint8) for v in vals.validators])
+    upto = nvals * 2 // 3 + 1
+    sizes = [12, 1, 5, 12, 7]
+    bufs = []
+
+    def window(k, b0, n, pin):
+        bids = [T.BlockID(hashlib.sha256(b"st%d" % b).digest(), 3, hashlib.sha256(b"sp%d" % b).digest())
+                for b in range(b0, b0 + n)]
+        specs = [(seeds[order], addrs, 500 + b, 0, bids[b - b0], 1672531200 + b, None) for b in range(b0, b0 + n)]
+        commits = sign_commits(engine, "stream-chain", specs, sign_upto=upto)
+        for b, c in zip(range(b0, b0 + n), commits):
+            if b % 4 == 1:
+                c.sigs[(b * 37) % upto, 5] ^= 0x20      # before the crossing: wrong signature
+            if b % 6 == 2:
+                c.sigs[upto + 3, 1] ^= 0x02             # after it: never reached
+        if pin:
+            buf = PinnedBuffer(n * nvals * 64)
+            a = buf.array((n * nvals, 64), np.uint8)
+            for j, c in enumerate(commits):
+                a[j * nvals:(j + 1) * nvals] = c.sigs
+                c.sigs = a[j * nvals:(j + 1) * nvals]
+            bufs.append(buf)
+        return T.BlocksyncWindow(vals, "stream-chain", bids, [500 + b for b in range(b0, b0 + n)], commits)
+
+    ks = 0
+    if keyed:
+        ks = engine.keyset_load(np.array([np.frombuffer(v.pub_key, np.uint8) for v in vals.validators]))
+        vals.keyset = ks
+    try:
+        wins, b0 = [], 0
+        for k, n in enumerate(sizes):
+            wins.append(window(k, b0, n, pin=k % 2 == 0))
+            b0 += n
+        ref = []
+        for w in wins:  # a call per window
+            w.run(engine, 2)
+            ref.append((w.codes().copy(), w.verified().copy(), [w.res[h].idx for h in range(w.n)]))
+            w.res = type(w.res)()
+        for k, w in enumerate(wins):
+            w.submit(engine, 2)
+            if k:  # the previous window is final now
+                p = wins[k - 1]
+                assert (p.codes() == ref[k - 1][0]).all() and (p.verified() == ref[k - 1][1]).all()
+            if k == 2:  # another seam call collects the stream first
+                c = wins[0].commits[0]
+                got = T.verify_commits(engine, [(T.MODE_LIGHT, vals, "stream-chain", c.block_id, c.height, c, 0, 0)])
+                assert got == [None]
+            w.win = w.bids = w.ccs = w.vs = None  # the structs may go once submit returned
+        T.blocksync_wait(engine)
+        for w, (codes, vers, idx) in zip(wins, ref):
+            assert (w.codes() == codes).all() and (w.verified() == vers).all()
+            assert [w.res[h].idx for h in range(w.n)] == idx
+        assert sum(int((r[0] == 4).sum()) for r in ref) >= 8
+        T.blocksync_wait(engine)  # nothing in flight: a no-op
+    finally:
+        for b in bufs:
+            b.free()
+        if ks:
+            engine.keyset_free(ks)
+            vals.keyset = 0

@@ -46,6 +46,8 @@ def kct():
     l.kct_pool_key.restype = ctypes.c_int
     l.kct_pool_key.argtypes = [P, ctypes.c_uint32, P]
     l.kct_digest.argtypes = [P, SZ, P]
+    l.kct_retired.restype = SZ
+    l.kct_retired.argtypes = [P]
     return l
 
 
@@ -225,6 +227,27 @@ def test_entry_bounds_lru(kct):
     assert c.lookup(sets[-1], 8)[0] and c.stats()["hits"] == 1  # the most recent entry survives
     assert c.lookup(sets[0], 8)[0]  # evicted entry: keys still pooled, keyed again (not a hit)
     assert c.stats()["hits"] == 1
+
+
+def test_entries_dropped_while_pinned_are_retired(kct):
+    """A call resolves raw entry pointers (no reference count per set): entries the LRU bound, a
+    key mismatch or a reset drop while any call is pinned are retired and freed at the last unpin."""
+    c = Cache(kct, 10_000)
+    kct.kct_limits(c.h, 2, 1 << 30)
+    sets = [keys(b"ret%d" % i, 0, 8) for i in range(5)]
+    kct.kct_pin(c.h)
+    for s in sets:
+        assert c.lookup(s, AMORTIZE * 8, force=True)[0]
+    assert c.stats()["sets_evicted"] >= 2 and kct.kct_retired(c.h) == c.stats()["sets_evicted"]
+    kct.kct_pin(c.h)    # a second call
+    kct.kct_unpin(c.h)
+    assert kct.kct_retired(c.h) > 0  # the first call is still pinned
+    kct.kct_unpin(c.h)
+    assert kct.kct_retired(c.h) == 0
+    # unpinned: dropped entries are freed at once
+    for s in sets:
+        assert c.lookup(s, AMORTIZE * 8, force=True)[0]
+    assert kct.kct_retired(c.h) == 0
 
 
 def test_digest_depends_on_order_and_size(kct):
