@@ -121,6 +121,22 @@ def c1(eng, reps: int, cpu: bool, first_sets: int = 30):
     out["first_call_after_set_change"] = summary(np.array(firsts) * 1e3)
     out["first_call_after_set_change"]["generic_calls"] = eng.keycache_stats()["generic_sets"] - gen_before
     eng.keycache_config(False)
+    # the same first calls with the cache off (fresh sets, a fresh batch each, the device idle
+    # before each): what a first call costs without the cache's resolution and queued build
+    firsts_off, specs = [], []
+    for k in range(first_sets):
+        sd, v2, o2, a2 = c1_set(b"tmed-c1-first-off-%d" % k)
+        specs.append((sd[o2], a2, 3, 0, bid, T2023, None, v2))
+    fc = sign_commits(eng, "test_chain_id", [s[:7] for s in specs])
+    for (spec, c2) in zip(specs, fc):
+        p2 = T.PreparedBatch([(T.MODE_COMMIT, spec[7], "test_chain_id", bid, 3, c2, 0, 0)])
+        torch.cuda.synchronize()
+        time.sleep(0.002)
+        t0 = time.perf_counter()
+        p2.run(eng)
+        firsts_off.append(time.perf_counter() - t0)
+        assert p2.codes()[0] == 0
+    out["first_call_cache_off"] = summary(np.array(firsts_off) * 1e3)
     for _ in range(20):
         pb.run(eng)
     out["generic_cache_off"] = summary(timed(pb, reps), marshal_timed(max(50, reps // 4)))
@@ -186,6 +202,13 @@ def _c3_world(eng, headers: int, reach: int, use_keyset: bool):
         sets.append(vals)
         addrs = np.array([np.frombuffer(v.address, np.uint8) for v in vals.validators])
         specs.append((pool_seeds[h:h + nv][order], addrs, h + 1, 0, block_id(b"c3-%d" % (h + 1)), T2023 + h, None))
+    if not ks:
+        # the light client holds every set's ValidatorSet.Hash() (header.ValidatorsHash /
+        # NextValidatorsHash, checked against the set by light/verifier.go): the drop-in passes it as
+        # the cache key (tmed_valset.set_hash), computed here by the f3 kernels (tmed_valset_hashes)
+        from tmed.merkle import valset_hashes
+        for vals, hsh in zip(sets, valset_hashes(eng, sets)):
+            vals.set_hash = hsh
     t_sign = time.perf_counter()
     commits = sign_commits(eng, "test_chain_id", specs)
     return sets, commits, ks, time.perf_counter() - t_sign
@@ -234,7 +257,10 @@ def c3(eng, headers: int, gap: int, policy: str = "cache", runs: int = 7, bisect
     res = {"metric": "light-client headers/s (VerifyCommitLightTrusting + VerifyCommitLight per header)",
            "unit": "headers/s", "host": _host_threads(),
            "config": {"workload": "C3: %d headers x 175 validators, trust 1/3, set changes 1 key/height" % headers,
-                      "key_policy": policy, "sign_s": round(t_sign, 2), "timed_runs": runs}}
+                      "key_policy": policy, "sign_s": round(t_sign, 2), "timed_runs": runs,
+                      "set_hash": ("each set's ValidatorSet.Hash() passed as the cache key (the light client's "
+                                   "header.ValidatorsHash; the cache still compares the keys byte for byte)"
+                                   if policy == "cache" else None)}}
     # ---- direct (gap) ----
     reqs = []
     for h in range(headers):

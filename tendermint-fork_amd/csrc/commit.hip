@@ -96,11 +96,16 @@ struct Cands {
   std::vector<size_t> off;  // runs.size() + 1 candidate offsets
   // (candidate, the candidate whose bit it takes), ascending: see find_aliases
   std::vector<std::pair<uint32_t, uint32_t>> alias;
+  // request -> the request whose device template its candidates use (empty: its own); a
+  // Trusting request shares the template of the Light request of the same commit (find_aliases)
+  std::vector<uint32_t> tmpl_of;
   size_t size() const { return off.empty() ? 0 : off.back(); }
+  uint32_t tmpl_row(uint32_t q) const { return tmpl_of.empty() ? q : tmpl_of[q]; }
   void clear() {
     runs.clear();
     off.assign(1, 0);
     alias.clear();
+    tmpl_of.clear();
   }
 };
 // Append candidate (q, i, v) to a part's runs, extending the last run when it continues it.
@@ -239,11 +244,14 @@ using BatchVerifier =
 // order, so the first candidate of each request marks it used (one writer per request).
 template <class Then>
 static int init_encoders(const tmed_commit_request *reqs, size_t n, const Cands &cands,
-                         std::vector<tmed::VoteEncoder> &enc, std::vector<uint8_t> &used, Then &&then) {
+                         std::vector<tmed::VoteEncoder> &enc, std::vector<uint8_t> &used, Then &&then,
+                         bool shared_rows = false) {
   enc.assign(n, tmed::VoteEncoder());
   used.assign(n, 0);
   const size_t m = cands.size();
-  for (const Run &r : cands.runs) used[r.req] = 1;
+  // shared_rows: a request whose candidates use another request's template (Cands::tmpl_of) needs
+  // no encoder of its own
+  for (const Run &r : cands.runs) used[shared_rows ? cands.tmpl_row(r.req) : r.req] = 1;
   std::atomic<int> bad{0};
   parallel_ranges(n, n >= 64 ? host_threads(m) : 1, [&](size_t lo, size_t hi, unsigned) {
   for (size_t q = lo; q < hi; q++) {
@@ -386,7 +394,10 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
     thread_local SeenMarks seen;
     seen.reset(vs.n);
     int64_t tally = 0;
+    constexpr size_t kAhead = 8;
     for (size_t i = 0; i < c.n_sigs; i++) {
+      if (i + kAhead < c.n_sigs) ix.prefetch_slot(c.addresses + 20 * (i + kAhead));
+      if (i + kAhead / 2 < c.n_sigs) ix.prefetch_entry(c.addresses + 20 * (i + kAhead / 2));
       if (c.flags[i] != kCommit) continue;
       const int32_t v = lookup_address(ix, c, i);
       if (v < 0) { pl.vof[i] = kNoValidator; continue; }
@@ -486,8 +497,7 @@ static size_t total_sigs(const tmed_commit_request *reqs, size_t n) {
   return s;
 }
 
-static void find_aliases(const tmed_commit_request *reqs, size_t n, const Plans &ps, const Cands &cands,
-                         std::vector<std::pair<uint32_t, uint32_t>> &alias);
+static void find_aliases(const tmed_commit_request *reqs, size_t n, const Plans &ps, Cands &cands);
 
 // Candidates of requests [0, n) in request order (identical to a serial plan).
 static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, Plans &ps, Cands &cands,
@@ -496,20 +506,40 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
   std::vector<Plan> &plans = ps.v;
   plans.assign(n, Plan());
   cands.clear();
+  // every request checked, and the signature count of each Trusting request (its vof), in parallel
+  // (the requests' sets and commits are cold in the cache)
+  // (the calling thread's buffer, taken by reference: a thread_local named inside the worker
+  // lambda would be each worker's own)
+  thread_local std::vector<size_t> tn_buf;
+  std::vector<size_t> &tn = tn_buf;
+  tn.resize(n);
+  std::atomic<bool> bad{false};
+  std::atomic<size_t> sigs_all{0};
+  parallel_ranges(n, n >= 256 ? host_threads(n * 64) : 1, [&](size_t lo, size_t hi, unsigned) {
+    size_t sg = 0;
+    for (size_t q = lo; q < hi; q++) {
+      tn[q] = 0;
+      if (check_request(reqs[q]) != TMED_OK) {
+        bad = true;
+        continue;
+      }
+      sg += reqs[q].commit->n_sigs;
+      if (reqs[q].mode == TMED_MODE_LIGHT_TRUSTING) tn[q] = reqs[q].commit->n_sigs;
+    }
+    sigs_all += sg;
+  });
+  if (bad) return TMED_EINVAL;
   size_t nbits = 0;
-  for (size_t q = 0; q < n; q++) {
-    if (check_request(reqs[q]) != TMED_OK) return TMED_EINVAL;
-    if (reqs[q].mode == TMED_MODE_LIGHT_TRUSTING) nbits += reqs[q].commit->n_sigs;
-  }
+  for (size_t q = 0; q < n; q++) nbits += tn[q];
   int32_t *bits = ps.bits.ensure(std::max<size_t>(nbits, 1));
   nbits = 0;
   for (size_t q = 0; q < n; q++)
-    if (reqs[q].mode == TMED_MODE_LIGHT_TRUSTING) {
+    if (tn[q]) {
       plans[q].vof = bits + nbits;
-      nbits += reqs[q].commit->n_sigs;
+      nbits += tn[q];
     }
   clk.lap("check");
-  const unsigned nt = host_threads(total_sigs(reqs, n));
+  const unsigned nt = host_threads(sigs_all.load());
   const unsigned np = std::max(1u, nt);
   if (ps.parts.size() < np) ps.parts.resize(np);
   std::vector<std::vector<Run>> &part = ps.parts;
@@ -530,29 +560,39 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
     if (rc != TMED_OK) return rc;
   clk.lap("plan_requests");
   // merge: the parts' runs in thread order (= request order), candidate offsets made global
-  size_t nr = 0;
-  for (unsigned t = 0; t < np; t++) nr += part[t].size();
+  std::vector<size_t> rbase(np + 1, 0), cbase(np + 1, 0);
+  for (unsigned t = 0; t < np; t++) {
+    rbase[t + 1] = rbase[t] + part[t].size();
+    cbase[t + 1] = cbase[t] + pc[t];
+  }
+  const size_t nr = rbase[np], cb = cbase[np];
   cands.runs.resize(nr);
   cands.off.resize(nr + 1);
-  size_t rb = 0, cb = 0;
-  for (unsigned t = 0; t < np; t++) {
-    size_t c = cb;
+  auto merge_part = [&](size_t t) {
+    size_t c = cbase[t];
+    Run *dst = cands.runs.data() + rbase[t];
+    size_t *off = cands.off.data() + rbase[t];
     for (size_t r = 0; r < part[t].size(); r++) {
-      cands.runs[rb + r] = part[t][r];
-      cands.off[rb + r] = c;
+      dst[r] = part[t][r];
+      off[r] = c;
       c += part[t][r].len;
     }
     for (size_t q = lo_of[t]; q < hi_of[t]; q++) {
-      plans[q].cand_off += cb;
-      plans[q].run_lo += rb;
-      plans[q].run_hi += rb;
+      plans[q].cand_off += cbase[t];
+      plans[q].run_lo += rbase[t];
+      plans[q].run_hi += rbase[t];
     }
-    rb += part[t].size();
-    cb += pc[t];
+  };
+  if (nt <= 1) {
+    for (unsigned t = 0; t < np; t++) merge_part(t);
+  } else {
+    parallel_ranges(np, np, [&](size_t lo, size_t hi, unsigned) {
+      for (size_t t = lo; t < hi; t++) merge_part(t);
+    });
   }
   cands.off[nr] = cb;
   clk.lap("merge");
-  if (nbits && cb <= 0xffffffffu) find_aliases(reqs, n, ps, cands, cands.alias);
+  if (nbits && cb <= 0xffffffffu) find_aliases(reqs, n, ps, cands);
   clk.lap("aliases");
   clk.emit("plan", n, cb);
   return TMED_OK;
@@ -575,9 +615,11 @@ static bool same_key(const tmed_valset &a, int32_t va, const tmed_valset &b, int
   return memcmp(a.pubkeys + 32 * (size_t)va, b.pubkeys + 32 * (size_t)vb, 32) == 0;
 }
 
-static void find_aliases(const tmed_commit_request *reqs, size_t n, const Plans &ps, const Cands &cands,
-                         std::vector<std::pair<uint32_t, uint32_t>> &alias) {
+static void find_aliases(const tmed_commit_request *reqs, size_t n, const Plans &ps, Cands &cands) {
+  std::vector<std::pair<uint32_t, uint32_t>> &alias = cands.alias;
   alias.clear();
+  cands.tmpl_of.resize(n);
+  for (size_t q = 0; q < n; q++) cands.tmpl_of[q] = (uint32_t)q;
   const std::vector<Plan> &plans = ps.v;
   const unsigned nt = host_threads(cands.size());
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> part(std::max(1u, nt));
@@ -593,6 +635,7 @@ static void find_aliases(const tmed_commit_request *reqs, size_t n, const Plans 
         if (o.mode == TMED_MODE_LIGHT_TRUSTING || o.commit != r.commit || po.decided || po.ncand == 0 ||
             o.chain_id_len != r.chain_id_len || memcmp(o.chain_id, r.chain_id, r.chain_id_len) != 0)
           continue;
+        cands.tmpl_of[q] = (uint32_t)pq;  // one commit, one chain ID: the same sign-bytes template
         // o's candidates are its qualifying signatures in order, as runs sorted by signature
         size_t ro = po.run_lo;
         for (size_t ri = pl.run_lo; ri < pl.run_hi; ri++) {
@@ -864,11 +907,17 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
   bool direct = direct_on && st.total >= tmed::kVoteCopyStreamMin;
   // pinned-memory lookups once per request (a registry lookup per run took a global lock per
   // vote where runs are single votes: Trusting candidates, C3)
+  // (only requests with a run long enough for its own DMA: a light-client batch has none)
   std::vector<uint8_t> req_pinned;
   if (direct) {
     req_pinned.assign(n, 0);
+    const size_t *pos = grp.positions(cands);
+    const size_t nr = grp.nruns(cands);
+    for (size_t j = 0; j < nr; j++)
+      if (pos[j + 1] - pos[j] >= kDmaMinRun) req_pinned[cands.runs[grp.run(cands, j)].req] = 2;
     bool any = false;
     for (size_t q = 0; q < n; q++) {
+      if (req_pinned[q] != 2) continue;
       const tmed_commit &c = *reqs[q].commit;
       req_pinned[q] = c.n_sigs && tmed::host_pinned(c.sigs, 64 * c.n_sigs) ? 1 : 0;
       any = any || req_pinned[q];
@@ -915,7 +964,7 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
             if (sl < 64) memset(st.sig + (p + u) * 64 + sl, 0, 64 - sl);
           }
       }
-      std::fill(st.tidx + p, st.tidx + p + len, run.req);
+      std::fill(st.tidx + p, st.tidx + p + len, cands.tmpl_row(run.req));
       memcpy(st.flag + p, c.flags + i, len);
       memcpy(st.sec + p, c.ts_seconds + i, 8 * len);
       memcpy(st.nan + p, c.ts_nanos + i, 4 * len);
@@ -971,7 +1020,7 @@ static int device_templates(const tmed_commit_request *reqs, size_t n, const Can
     memset(row, 0, tmed::kVoteTmplBytes);
     if (!e.device_template(row, tmed::kVoteTmplBytes, tmed::kVoteSlot)) ok = false;
     return true;
-  });
+  }, /*shared_rows=*/true);
   if (rc != TMED_OK) return rc;
   *fits = ok;
   return TMED_OK;

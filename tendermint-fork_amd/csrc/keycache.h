@@ -133,6 +133,13 @@ struct AddrIndex {
       if (vals[h] < 0) vals[h] = (int32_t)v;  // keep the first match
     }
   }
+  // software prefetch for a lookup a few signatures ahead (the index and the set's address copy
+  // are cold at a light-client batch's ~10k sets): the slot, then the address it holds
+  void prefetch_slot(const uint8_t *addr) const { __builtin_prefetch(&vals[slot_of(addr) & mask]); }
+  void prefetch_entry(const uint8_t *addr) const {
+    const int32_t v = vals[slot_of(addr) & mask];
+    if (v >= 0) __builtin_prefetch(addrs + 20 * (size_t)v);
+  }
   int32_t find(const uint8_t *addr) const {
     size_t h = slot_of(addr) & mask;
     while (vals[h] >= 0) {

@@ -263,32 +263,50 @@ template <class Acc>
 TMED_HD void finish_group(Acc &a) {
   const int cnt = a.count();
   if (cnt <= 0) return;
-  fe acc, z;
+  // Each row is loaded one signature ahead of its use: a finish lane runs alone on its SIMD (one
+  // wave per SIMD at 65,536 lanes), so a load issued right before its use exposes the whole memory
+  // latency at every signature.
+  fe acc, z, zn;
   uint32_t bad = 0;
+  a.load_z(0, zn);
 #pragma unroll 1
   for (int j = 0; j < cnt; j++) {
-    a.load_z(j, z);
+    fe_copy(z, zn);
+    if (j + 1 < cnt) a.load_z(j + 1, zn);
     if (fe_iszero(z)) { fe_1(z); bad |= 1u << j; }
     if (j == 0) fe_copy(acc, z); else fe_mul(acc, acc, z);
     a.store_pre(j, acc);
   }
   fe inv;
   fe_invert(inv, acc);  // 1 / (Z_0 ... Z_{cnt-1})
+  fe pre, X, Y, pren, Xn, Yn;
+  uint32_t Rw[8], Rn[8];
+  auto load_row = [&](int j, fe &p, fe &zr, fe &x, fe &y, uint32_t r[8]) {
+    if (j > 0) {
+      a.load_pre(j - 1, p);
+      a.load_z(j, zr);
+    }
+    a.load_xy(j, x, y);
+    a.load_r(j, r);
+  };
+  load_row(cnt - 1, pren, zn, Xn, Yn, Rn);
 #pragma unroll 1
   for (int j = cnt - 1; j >= 0; j--) {
-    fe zi, X, Y;
+    fe_copy(pre, pren);
+    fe_copy(z, zn);
+    fe_copy(X, Xn);
+    fe_copy(Y, Yn);
+#pragma unroll
+    for (int i = 0; i < 8; i++) Rw[i] = Rn[i];
+    if (j > 0) load_row(j - 1, pren, zn, Xn, Yn, Rn);
+    fe zi;
     if (j > 0) {
-      a.load_pre(j - 1, zi);
-      fe_mul(zi, zi, inv);  // 1 / Z_j
-      a.load_z(j, z);
+      fe_mul(zi, pre, inv);  // 1 / Z_j
       if ((bad >> j) & 1u) fe_1(z);
       fe_mul(inv, inv, z);  // 1 / (Z_0 ... Z_{j-1})
     } else {
       fe_copy(zi, inv);
     }
-    a.load_xy(j, X, Y);
-    uint32_t Rw[8];
-    a.load_r(j, Rw);
     a.result(j, encoding_matches(X, Y, zi, Rw) && !((bad >> j) & 1u));
   }
 }

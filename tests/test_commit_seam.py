@@ -47,11 +47,14 @@ def test_light_verifies_only_the_prefix():
 
 
 def test_parallel_plan_and_replay_equal_serial():
-    """Batches above 65,536 signatures are planned and replayed on host threads; the result
-    of every request must equal its result as a single (serial) call.  The verifier is a
-    deterministic stand-in (bit = low bit of sig[1]) so the test needs no signing."""
+    """Batches above 65,536 signatures are planned and replayed on host threads (and calls of
+    more than 1,024 requests check them on host threads); the result of every request must equal
+    its result as a single (serial) call.  Each Trusting request shares the commit of the Light
+    request before it (the light client's pair: the seam's candidate aliasing and shared
+    templates run).  The verifier is a deterministic stand-in (bit = low bit of sig[1]) so the
+    test needs no signing."""
     rng = np.random.default_rng(3)
-    n_vals, n_req = 150, 480
+    n_vals, n_req = 150, 1100
     pubs = rng.integers(0, 256, (n_vals, 32), dtype=np.uint8)
     vals = T.ValidatorSet([T.Validator(bytes(p), int(w), 0) for p, w in zip(pubs, rng.integers(1, 50, n_vals))])
     addrs = np.array([np.frombuffer(v.address, np.uint8) for v in vals.validators])
@@ -68,6 +71,8 @@ def test_parallel_plan_and_replay_equal_serial():
         pc = T.PackedCommit(10 + q, 0, bid, flags, ad, np.full(n_vals, 1700000000 + q, np.int64),
                             np.zeros(n_vals, np.int32), sigs, np.full(n_vals, 64, np.uint32))
         mode = q % 3
+        if mode == 2:  # Trusting on the Light request's commit
+            pc, bid = reqs[-1][5], reqs[-1][3]
         reqs.append((mode, vals, "par", bid if mode != 2 else None, 10 + q, pc, 1, 3))
 
     def bitfn(pubs_, sigs_, lens, msgs, offs):
@@ -75,7 +80,7 @@ def test_parallel_plan_and_replay_equal_serial():
 
     got = T.verify_commits(None, reqs, verifier=bitfn)
     assert sum(int(reqs[q][5].flags.shape[0]) for q in range(n_req)) >= 65536
-    for q in range(0, n_req, 3):
+    for q in list(range(0, n_req, 7)) + list(range(2, n_req, 9)):
         one = T.verify_commits(None, [reqs[q]], verifier=bitfn)[0]
         assert same(got[q], one), (q, got[q], one)
     assert len({type(e).__name__ for e in got}) >= 2

@@ -272,14 +272,16 @@ def test_edge_scenarios_gpu(engine):
     assert any(isinstance(e, tuple) for e in exp)
 
 
-@pytest.mark.parametrize("pinned", ["all", "alternate"])
+@pytest.mark.parametrize("pinned", ["all", "alternate", "separate"])
 @pytest.mark.parametrize("keyed", [False, True])
 def test_blocksync_pinned_signatures_gpu(engine, pinned, keyed):
     """Signatures in tmed_host_alloc memory are DMA'd straight from the caller's arrays (batches of
     >= 1 MB staged): every block's outcome (code, index, signatures verified) equals the run from
-    pageable memory — all commits pinned, and every other commit pinned (mixed runs: staged and
-    direct signatures in one batch) — with known-answer bad signatures before and after the
-    2/3 crossing and a short (63-byte) signature in a pinned run."""
+    pageable memory — all commits pinned, every other commit pinned (mixed runs: staged and
+    direct signatures in one batch), and one pinned allocation per commit (equal-length runs in
+    different allocations are not merged into one 2-D copy: keyset.hip votes_enqueue) — with
+    known-answer bad signatures before and after the 2/3 crossing and a short (63-byte) signature
+    in a pinned run."""
     import hashlib
     import numpy as np
     from tmed import PinnedBuffer
@@ -302,10 +304,16 @@ def test_blocksync_pinned_signatures_gpu(engine, pinned, keyed):
                 c.sigs[upto + 1, 9] ^= 0x01             # after it: never reached
             if b % 7 == 3:
                 c.sig_lens[(b * 13) % upto] = 63        # a short signature: wrong length
-        buf = None
-        if pin:
-            buf = PinnedBuffer(nblk * nvals * 64)
-            a = buf.array((nblk * nvals, 64), np.uint8)
+        buf = []
+        if pin and pinned == "separate":
+            for c in commits:
+                buf.append(PinnedBuffer(nvals * 64))
+                a = buf[-1].array((nvals, 64), np.uint8)
+                a[:] = c.sigs
+                c.sigs = a
+        elif pin:
+            buf.append(PinnedBuffer(nblk * nvals * 64))
+            a = buf[0].array((nblk * nvals, 64), np.uint8)
             for b, c in enumerate(commits):
                 if pinned == "all" or b % 2 == 0:
                     a[b * nvals:(b + 1) * nvals] = c.sigs
@@ -325,7 +333,8 @@ def test_blocksync_pinned_signatures_gpu(engine, pinned, keyed):
         assert (w0.verified() == w1.verified()).all()
         assert [w0.res[h].idx for h in range(nblk)] == [w1.res[h].idx for h in range(nblk)]
         assert (w0.codes() == 4).sum() >= 6 and (w0.codes() == 0).sum() >= 10
-        buf.free()
+        for b in buf:
+            b.free()
     finally:
         if ks:
             engine.keyset_free(ks)
