@@ -602,8 +602,8 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
 // The light client checks one commit twice, LightTrusting against the trusted set and Light
 // against the untrusted one (light/verifier.go:58,73-76), and most validators sign for both
 // sets: a Trusting candidate (signature i of a commit, key K) is the same verification as the
-// Light / VerifyCommit candidate (signature i of the SAME commit, same chain ID, same key K) of
-// a neighbouring request.  Such a candidate is sent once; the other takes its bit (C3: ~59 of
+// Light / VerifyCommit candidate (signature i of the SAME commit — same_commit — same chain ID,
+// same key K) of a neighbouring request.  Such a candidate is sent once; the other takes its bit (C3: ~59 of
 // the ~176 candidates of each header).  alias: (candidate, the candidate whose bit it takes).
 static bool same_key(const tmed_valset &a, int32_t va, const tmed_valset &b, int32_t vb) {
   if (a.keyset != b.keyset) return false;
@@ -613,6 +613,16 @@ static bool same_key(const tmed_valset &a, int32_t va, const tmed_valset &b, int
     return ka == kb;
   }
   return memcmp(a.pubkeys + 32 * (size_t)va, b.pubkeys + 32 * (size_t)vb, 32) == 0;
+}
+
+// One commit for both requests: the same struct, or structs over the same signature, flag and
+// timestamp arrays with equal height, round and BlockID (marshallers that copy the struct per
+// request).  Then signature i has the same sign-bytes and signature bytes in both.
+static bool same_commit(const tmed_commit &a, const tmed_commit &b) {
+  if (&a == &b) return true;
+  return a.n_sigs == b.n_sigs && a.sigs == b.sigs && a.flags == b.flags && a.ts_seconds == b.ts_seconds &&
+         a.ts_nanos == b.ts_nanos && a.sig_lens == b.sig_lens && a.height == b.height && a.round == b.round &&
+         block_id_equal(a.block_id, b.block_id);
 }
 
 static void find_aliases(const tmed_commit_request *reqs, size_t n, const Plans &ps, Cands &cands) {
@@ -632,7 +642,7 @@ static void find_aliases(const tmed_commit_request *reqs, size_t n, const Plans 
         if (pq >= n) continue;
         const tmed_commit_request &o = reqs[pq];
         const Plan &po = plans[pq];
-        if (o.mode == TMED_MODE_LIGHT_TRUSTING || o.commit != r.commit || po.decided || po.ncand == 0 ||
+        if (o.mode == TMED_MODE_LIGHT_TRUSTING || !same_commit(*o.commit, *r.commit) || po.decided || po.ncand == 0 ||
             o.chain_id_len != r.chain_id_len || memcmp(o.chain_id, r.chain_id, r.chain_id_len) != 0)
           continue;
         cands.tmpl_of[q] = (uint32_t)pq;  // one commit, one chain ID: the same sign-bytes template

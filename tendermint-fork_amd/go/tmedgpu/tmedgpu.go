@@ -301,6 +301,9 @@ func (e *Engine) verifyCommitsWith(reqs []Request, call func(*arena, *C.tmed_com
 	// one C copy per distinct *ValSet: requests on the same set share it (the library resolves each
 	// set once per call; a light-client batch holds each set twice)
 	seen := make(map[*ValSet]*C.tmed_valset, n)
+	// one C copy per distinct *CommitData as well: the light client's Trusting + Light pair checks
+	// one commit twice, and the library verifies a signature the two share once (same commit)
+	seenC := make(map[*CommitData]*C.tmed_commit, n)
 	for i := range reqs {
 		r := &reqs[i]
 		cv, ok := seen[r.Vals]
@@ -310,10 +313,15 @@ func (e *Engine) verifyCommitsWith(reqs []Request, call func(*arena, *C.tmed_com
 			seen[r.Vals] = cv
 		}
 		c := r.Commit
-		cs[i] = C.tmed_commit{height: C.int64_t(c.Height), round: C.int32_t(c.Round), block_id: a.blockID(&c.BlockID),
-			n_sigs: C.size_t(len(c.Flags)), flags: a.bytes(c.Flags), addresses: a.bytes(c.Addresses),
-			ts_seconds: a.i64(c.TsSeconds), ts_nanos: a.i32(c.TsNanos), sigs: a.bytes(c.Sigs), sig_lens: a.u32(c.SigLens),
-			address_lens: a.u32(c.AddrLens)}
+		cc, ok := seenC[c]
+		if !ok {
+			cs[i] = C.tmed_commit{height: C.int64_t(c.Height), round: C.int32_t(c.Round), block_id: a.blockID(&c.BlockID),
+				n_sigs: C.size_t(len(c.Flags)), flags: a.bytes(c.Flags), addresses: a.bytes(c.Addresses),
+				ts_seconds: a.i64(c.TsSeconds), ts_nanos: a.i32(c.TsNanos), sigs: a.bytes(c.Sigs), sig_lens: a.u32(c.SigLens),
+				address_lens: a.u32(c.AddrLens)}
+			cc = &cs[i]
+			seenC[c] = cc
+		}
 		bids[i] = C.tmed_block_id{}
 		if r.BlockID != nil {
 			bids[i] = a.blockID(r.BlockID)
@@ -321,7 +329,7 @@ func (e *Engine) verifyCommitsWith(reqs []Request, call func(*arena, *C.tmed_com
 		cid := C.CString(r.ChainID)
 		a.ptrs = append(a.ptrs, unsafe.Pointer(cid))
 		creqs[i] = C.tmed_commit_request{mode: C.int(r.Mode), chain_id: cid, chain_id_len: C.uint32_t(len(r.ChainID)),
-			vals: cv, block_id: &bids[i], height: C.int64_t(r.Height), commit: &cs[i],
+			vals: cv, block_id: &bids[i], height: C.int64_t(r.Height), commit: cc,
 			trust_num: C.int64_t(r.TrustNum), trust_den: C.int64_t(r.TrustDen)}
 	}
 	res := make([]C.tmed_commit_result, n)

@@ -393,11 +393,14 @@ class PreparedBatch:
         self.n = n
         self.reqs = (_RequestC * max(n, 1))()
         vcs = {}  # one tmed_valset per ValidatorSet object (the seam resolves each set once)
+        ccs = {}  # one tmed_commit per Commit object (the light client's Trusting + Light pair)
         for q, (mode, vals, chain_id, block_id, height, commit, num, den) in enumerate(self.requests):
             vs = vcs.get(id(vals))
             if vs is None:
                 vs = vcs[id(vals)] = _valset_c(vals, self.keep)
-            cc = _commit_c(commit, self.keep)
+            cc = ccs.get(id(commit))
+            if cc is None:
+                cc = ccs[id(commit)] = _commit_c(commit, self.keep)
             cid = chain_id.encode()
             bid = _block_id_c(block_id, self.keep) if block_id is not None else None
             self.keep.extend([vs, cc, cid, bid, vals])
@@ -449,13 +452,16 @@ def verify_commits(engine, requests: Sequence[tuple], verifier=None, stats: Opti
     keep = []
     n = len(requests)
     reqs = (_RequestC * max(n, 1))()
+    ccs = {}  # one tmed_commit per Commit object (the light client's Trusting + Light pair)
     vcs = {}  # one tmed_valset per ValidatorSet object: the seam resolves each set once per call
     for q, (mode, vals, chain_id, block_id, height, commit, num, den) in enumerate(requests):
         vs = vcs.get(id(vals))
         if vs is None:
             vs = vcs[id(vals)] = _valset_c(vals, keep)
             keep.append(vals)
-        cc = _commit_c(commit, keep)
+        cc = ccs.get(id(commit))
+        if cc is None:
+            cc = ccs[id(commit)] = _commit_c(commit, keep)
         cid = chain_id.encode()
         bid = _block_id_c(block_id, keep) if block_id is not None else None
         keep.extend([vs, cc, cid, bid])
