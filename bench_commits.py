@@ -202,7 +202,7 @@ def _c3_world(eng, headers: int, reach: int, use_keyset: bool):
         sets.append(vals)
         addrs = np.array([np.frombuffer(v.address, np.uint8) for v in vals.validators])
         specs.append((pool_seeds[h:h + nv][order], addrs, h + 1, 0, block_id(b"c3-%d" % (h + 1)), T2023 + h, None))
-    if not ks:
+    if not ks and hasattr(eng, "_h"):  # (a GPU engine: tools/c3_host_profile.py passes a stand-in)
         # the light client holds every set's ValidatorSet.Hash() (header.ValidatorsHash /
         # NextValidatorsHash, checked against the set by light/verifier.go): the drop-in passes it as
         # the cache key (tmed_valset.set_hash), computed here by the f3 kernels (tmed_valset_hashes)

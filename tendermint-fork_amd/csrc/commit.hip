@@ -545,12 +545,20 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
   std::vector<std::vector<Run>> &part = ps.parts;
   std::vector<size_t> lo_of(np, 0), hi_of(np, 0), pc(np, 0);
   std::vector<int> rcs(np, TMED_OK);
+  // (each worker plans into a vector header on its own stack and a local status: the per-thread
+  // slots of part / rcs share cache lines, and a push_back per Trusting candidate into them
+  // bounced those lines between the workers)
   auto plan_range = [&](size_t lo, size_t hi, unsigned t) {
     lo_of[t] = lo; hi_of[t] = hi;
     AddrScratch addr;
     addr.kc = kc;
     size_t c = 0;
-    for (size_t q = lo; q < hi && rcs[t] == TMED_OK; q++) rcs[t] = plan_request(reqs, q, out[q], plans[q], part[t], c, addr);
+    std::vector<Run> mine;
+    mine.swap(part[t]);
+    int rc = TMED_OK;
+    for (size_t q = lo; q < hi && rc == TMED_OK; q++) rc = plan_request(reqs, q, out[q], plans[q], mine, c, addr);
+    mine.swap(part[t]);
+    rcs[t] = rc;
     pc[t] = c;
   };
   for (unsigned t = 0; t < np; t++) part[t].clear();
@@ -626,6 +634,7 @@ static bool same_commit(const tmed_commit &a, const tmed_commit &b) {
 }
 
 static void find_aliases(const tmed_commit_request *reqs, size_t n, const Plans &ps, Cands &cands) {
+  PhaseClock clk;
   std::vector<std::pair<uint32_t, uint32_t>> &alias = cands.alias;
   alias.clear();
   cands.tmpl_of.resize(n);
@@ -634,6 +643,7 @@ static void find_aliases(const tmed_commit_request *reqs, size_t n, const Plans 
   const unsigned nt = host_threads(cands.size());
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> part(std::max(1u, nt));
   parallel_ranges(n, nt, [&](size_t lo, size_t hi, unsigned t) {
+    std::vector<std::pair<uint32_t, uint32_t>> mine;  // (a header of its own: see seam_plan)
     for (size_t q = lo; q < hi; q++) {
       const tmed_commit_request &r = reqs[q];
       const Plan &pl = plans[q];
@@ -646,6 +656,14 @@ static void find_aliases(const tmed_commit_request *reqs, size_t n, const Plans 
             o.chain_id_len != r.chain_id_len || memcmp(o.chain_id, r.chain_id, r.chain_id_len) != 0)
           continue;
         cands.tmpl_of[q] = (uint32_t)pq;  // one commit, one chain ID: the same sign-bytes template
+        // the two sets' key identities (pool indexes, or the keys) are cold: fetch them at once
+        // instead of one dependent miss per candidate
+        for (const tmed_valset *vs : {r.vals, o.vals}) {
+          const uint8_t *kp = vs->keyset ? (const uint8_t *)vs->keyset_index : vs->pubkeys;
+          const size_t kb = vs->keyset ? 4 * vs->n : 32 * vs->n;
+          if (kp)
+            for (size_t b = 0; b < kb; b += 64) __builtin_prefetch(kp + b);
+        }
         // o's candidates are its qualifying signatures in order, as runs sorted by signature
         size_t ro = po.run_lo;
         for (size_t ri = pl.run_lo; ri < pl.run_hi; ri++) {
@@ -656,14 +674,18 @@ static void find_aliases(const tmed_commit_request *reqs, size_t n, const Plans 
             if (ro == po.run_hi) break;
             const Run &orun = cands.runs[ro];
             if (i < orun.sig || !same_key(*r.vals, run.val + (int32_t)u, *o.vals, orun.val + (i - orun.sig))) continue;
-            part[t].push_back({(uint32_t)(cands.off[ri] + u), (uint32_t)(cands.off[ro] + (size_t)(i - orun.sig))});
+            mine.push_back({(uint32_t)(cands.off[ri] + u), (uint32_t)(cands.off[ro] + (size_t)(i - orun.sig))});
           }
         }
         break;
       }
     }
+    part[t].swap(mine);
   });
+  clk.lap("pairs");
   for (auto &p : part) alias.insert(alias.end(), p.begin(), p.end());
+  clk.lap("concat");
+  clk.emit("aliases", n, alias.size());
 }
 
 // ---- replay of every reference loop over the validity bits (parallel over requests) ----
@@ -941,6 +963,7 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
   // signatures stay per vote
   auto fill = [&](size_t lo, size_t hi, unsigned tid) {
     bool ok = true, staged_sig = false;
+    std::vector<tmed::VoteStage::Dma> mine;  // (a header of its own: see seam_plan)
     for_segments(cands, grp, lo, hi, [&](size_t j, uint32_t u0, uint32_t u1, size_t p) {
       const Run &run = cands.runs[grp.run(cands, j)];
       const tmed_commit_request &r = reqs[run.req];
@@ -964,7 +987,7 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
       if (dma && c.sig_lens)  // short signatures are zero-padded in staging
         for (size_t u = 0; u < len && dma; u++) dma = c.sig_lens[i + u] >= 64;
       if (dma) {
-        tdma[tid].push_back({p * 64, c.sigs + 64 * i, 64 * len});
+        mine.push_back({p * 64, c.sigs + 64 * i, 64 * len});
       } else {
         staged_sig = true;
         memcpy(st.sig + p * 64, c.sigs + 64 * i, 64 * len);
@@ -981,6 +1004,7 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
     });
     if (!ok) key_ok = false;
     if (staged_sig) all_direct = false;
+    if (tid < tdma.size()) tdma[tid].swap(mine);
   };
   parallel_ranges(m, nt, fill);
   if (!key_ok) return TMED_EINVAL;  // a key-set index past the key set (votes_enqueue's check)
@@ -1203,6 +1227,7 @@ static const tmed_commit_request *keycache_resolve(tmed_ctx *ctx, const tmed_com
     const uint64_t tick = tmed::keycache_call_tick(ctx);
     std::vector<size_t> thits(std::max(1u, nt), 0), tsigs(std::max(1u, nt), 0);
     parallel_ranges(sets.size(), nt, [&](size_t lo, size_t hi, unsigned t) {
+      size_t h = 0, g = 0;  // this worker's hits and their signatures (stored once: shared lines)
       for (size_t s = lo; s < hi; s++) {
         SetRef &sr = sets[s];
         const tmed_valset &v = *sr.v;
@@ -1213,10 +1238,12 @@ static const tmed_commit_request *keycache_resolve(tmed_ctx *ctx, const tmed_com
         sr.hit = sr.e && tmed::kc_same_keys(*sr.e, v.pubkeys, v.n);
         if (sr.hit) {
           const_cast<tmed::KcSet *>(sr.e)->touch(tick);
-          thits[t]++;
-          tsigs[t] += sr.sigs;
+          h++;
+          g += sr.sigs;
         }
       }
+      thits[t] = h;
+      tsigs[t] = g;
     });
     clk.lap("find_compare");
     size_t nh = 0, ns = 0;
