@@ -1424,6 +1424,15 @@ static double bs_us(BsClock::time_point a, BsClock::time_point b) {
   return std::chrono::duration<double, std::micro>(b - a).count();
 }
 
+// TMED_LANES=1: every batch on the context stream (A/B of the second kernel lane)
+static bool lanes_on() {
+  static const bool on = [] {
+    const char *v = getenv("TMED_LANES");
+    return !(v && v[0] == '1');
+  }();
+  return on;
+}
+
 // Collect batch b (ctx->mu held): its bits, the alias copies, the replay into its window's results.
 // ph: tmed_seam_phase_us — host plan + templates + staging, host time blocked on the device
 // (enqueueing the copies and kernels, votes_collect), host replay.
@@ -1531,6 +1540,9 @@ static int bs_pump(tmed_ctx *ctx, BsStream &S, BsWindow &w, double ph[3], std::u
           for (size_t r = 0; r < b.cands.runs.size(); r++) b.grp.add_run(b.cands, (uint32_t)r, ap);
         }
         rc = stage_group(ctx, rq, b.n, b.cands, b.grp, w.keyset, b.tmpl.data(), (int)(idx % ns), b.st);
+        // key-cached batches alternate between the two kernel lanes, so one batch's small kernels
+        // (assembly, key order, prep, finish) run beside the other's main kernel
+        b.st.lane = w.keyset && (idx & 1) && lanes_on() ? 1 : 0;
         clk.lap("stage");
         const auto te = BsClock::now();
         ph[0] += bs_us(tp, te);

@@ -92,6 +92,8 @@ Keyset *find_keyset(tmed_ctx *c, uint64_t handle);
 struct KeyCacheDev;
 void keycache_destroy(tmed_ctx *c);
 void bs_destroy(tmed_ctx *c);  // commit.hip: the blocksync batch stream (before keycache_destroy)
+struct Lane;
+void lane_release(Lane &L);    // keyset.hip: the second kernel lane's stream and scratch
 void keycache_pin(tmed_ctx *c);    // a seam call resolving sets: no pool reset until it unpins
 void keycache_unpin(tmed_ctx *c);
 uint64_t keycache_pool_handle(const tmed_ctx *c);  // 0 before the first key is built
@@ -149,6 +151,10 @@ struct VoteStage {
   };
   std::vector<Dma> dma;
   bool sig_direct = false;
+  // Kernel lane: 0 = the context stream; 1 = the second kernel stream of the key-cached
+  // throughput batches (its own scratch, ctx.h Lane), so consecutive batches of the pipelined seam
+  // overlap on the device (one batch's small kernels beside the other's main kernel).
+  int lane = 0;
 };
 // Batches of at least this many staged bytes are copied on the context's copy stream (and may take
 // their signatures straight from pinned caller memory): votes_enqueue.
@@ -176,6 +182,19 @@ struct VoteSlot {
   hipEvent_t done = nullptr;                // after its copy-out
   hipEvent_t copied = nullptr;              // its staged votes are on the device (copy stream)
   hipEvent_t cp0 = nullptr, cp1 = nullptr;  // around its copy-in (TMED_TRACE only)
+};
+}  // namespace tmed
+
+namespace tmed {
+// The second kernel lane of the pipelined seam (VoteStage::lane 1): a stream and the scratch its
+// key-cached throughput kernels write (prep hand-off, batched-finish buffers, key order), allocated
+// at its first use.  Key-set pool buffers are shared read-only; pool growth (keyset_reserve)
+// synchronises both lanes before it frees anything.
+struct Lane {
+  hipStream_t s = nullptr;
+  int4 *d_prep = nullptr, *d_fin = nullptr, *d_fin_pre = nullptr;
+  DevBuf d_korder;
+  bool failed = false;  // no stream / memory: every batch stays on lane 0
 };
 }  // namespace tmed
 
@@ -216,6 +235,7 @@ struct tmed_ctx {
   tmed::HostBuf h_a, h_b, h_msg, h_off, h_out, h_c;
   tmed::VoteSlot vslot[3];  // the blocksync pipeline (commit.hip BsStream: two slots, three when the signatures go direct)
   BsStream *bs = nullptr;   // batches of submitted blocksync windows in flight (tmed_blocksync_submit)
+  tmed::Lane lane1;         // the pipelined seam's second kernel lane (VoteStage::lane)
   tmed::DevBuf d_merkle_a, d_merkle_b, d_merkle_idx;  // Merkle level digests (ping-pong) + level indexes
   tmed::DevBuf d_korder;  // key-grouped order of a key-cached batch: counts / cursors + permutation
   tmed::DevBuf d_zip;     // ZIP-215 batch mode scratch (zip215.hip zip_bufs: points, digits, sort, buckets)

@@ -82,22 +82,10 @@ TMED_HD void fe_neg(fe &h, const fe &f) {
 #pragma unroll
   for (int i = 0; i < 10; i++) h.v[i] = -f.v[i];
 }
-// h = b ? g : f   (lane-local select, no branch).  TMED_SEL_BALLOT: the device build takes the
-// lane mask from a ballot into an SGPR pair and selects with the VOP3 v_cndmask_b32_e64 (the VOP2
-// form reading VCC issued at 22.8 cycles per wave instruction in tools/probe_valu.py, the VOP3
-// form at 4.1).
-#ifndef TMED_SEL_BALLOT
-#define TMED_SEL_BALLOT 0
-#endif
+// h = b ? g : f   (lane-local select, no branch)
 TMED_HD void fe_select(fe &h, const fe &f, const fe &g, bool b) {
-#if TMED_SEL_BALLOT && defined(__HIP_DEVICE_COMPILE__)
-  const uint64_t m = __builtin_amdgcn_ballot_w64(b);
-#pragma unroll
-  for (int i = 0; i < 10; i++) asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(h.v[i]) : "v"(f.v[i]), "v"(g.v[i]), "s"(m));
-#else
 #pragma unroll
   for (int i = 0; i < 10; i++) h.v[i] = b ? g.v[i] : f.v[i];
-#endif
 }
 
 // Column biases: the accumulators start at B_k = 2^25 (even k) / 2^24 (odd k), so the

@@ -34,6 +34,7 @@ struct KcBackendDev {
     if (!handle) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    if (c->lane1.s) (void)hipStreamSynchronize(c->lane1.s);
     auto it = c->keysets.find(handle);
     if (it != c->keysets.end()) {
       free_keyset(it->second);

@@ -109,6 +109,7 @@ static int keyset_reserve(tmed_ctx *c, Keyset &k, size_t cap, hipStream_t s) {
       e = hipMemcpyAsync(comb10, k.d_comb10, k.comb10_n * kComb10BytesPerKey, hipMemcpyDeviceToDevice, s);
   }
   if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess && c->lane1.s) e = hipStreamSynchronize(c->lane1.s);  // its batches read the old buffers
   if (e != hipSuccess) {
     for (void *p : {(void *)pub, (void *)ok, (void *)comb, (void *)comb10})
       if (p) (void)hipFree(p);
@@ -155,7 +156,7 @@ int keyset_append(tmed_ctx *c, Keyset &k, const uint8_t *pubkeys, size_t m, hipS
 // commit), the throughput kernels (prep / comb main / batched finish) above c->lat_max.
 static hipError_t keyset_verify(tmed_ctx *c, Keyset &k, const uint32_t *d_idx, const uint8_t *d_sig,
                                 const uint8_t *d_msgs, const uint32_t *d_off, uint32_t n, uint8_t *d_out,
-                                hipStream_t s, bool msg_slots, const VoteAsm *va = nullptr) {
+                                hipStream_t s, bool msg_slots, const VoteAsm *va = nullptr, Lane *lane = nullptr) {
   c->last_hs_count = 0;  // d_prep now holds another path's hand-off (tmed_window_stats)
   if (n <= c->lat_max)
     return launch_verify_keyset_lat(d_idx, (uint32_t)k.n, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb, d_sig, d_msgs, d_off, n, d_out,
@@ -165,17 +166,19 @@ static hipError_t keyset_verify(tmed_ctx *c, Keyset &k, const uint32_t *d_idx, c
   const int4 *comb10 = c->d_b24 && k.d_comb10 && k.comb10_n == k.n ? k.d_comb10 : nullptr;
   KernelTimer *timer = (c->timing && !msg_slots) ? &c->timer : nullptr;
   uint32_t *perm = nullptr, *scratch = nullptr;
+  DevBuf &korder = lane ? lane->d_korder : c->d_korder;
   if (key_order_on(k, n)) {
     const size_t sw = key_order_scratch_words(n, (uint32_t)k.n);
-    hipError_t e = c->d_korder.ensure((sw + (size_t)n) * 4);
+    hipError_t e = korder.ensure((sw + (size_t)n) * 4);
     if (e != hipSuccess) return e;
-    scratch = (uint32_t *)c->d_korder.p;
+    scratch = (uint32_t *)korder.p;
     perm = scratch + sw;
   }
   // (the key order runs in front of each chunk's prep and is charged to prep by the timer)
   return launch_verify_keyset(d_idx, (uint32_t)k.n, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb16, d_sig, d_msgs, d_off, n,
-                              d_out, c->d_prep, c->slab_slots, c->d_fin, c->d_fin_pre, s, msg_slots, timer, perm,
-                              scratch, c->d_b24, comb10);
+                              d_out, lane ? lane->d_prep : c->d_prep, c->slab_slots, lane ? lane->d_fin : c->d_fin,
+                              lane ? lane->d_fin_pre : c->d_fin_pre, s, msg_slots, timer, perm, scratch, c->d_b24,
+                              comb10);
 }
 
 int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st, int slot) {
@@ -244,6 +247,36 @@ struct SlowStep {
 };
 }  // namespace
 
+// The second kernel lane, created at its first use (false: unavailable, the batch takes lane 0).
+static bool lane1_ready(tmed_ctx *c) {
+  Lane &L = c->lane1;
+  if (L.s) return true;
+  if (L.failed) return false;
+  hipError_t e = hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc((void **)&L.d_prep, (size_t)c->slab_slots * kPrepSlotBytes + kPrepTailBytes);
+  if (e == hipSuccess) e = hipMalloc((void **)&L.d_fin, kFinBytes);
+  if (e == hipSuccess) e = hipMalloc((void **)&L.d_fin_pre, kFinPreBytes);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    lane_release(L);
+    L.failed = true;
+    return false;
+  }
+  return true;
+}
+
+void lane_release(Lane &L) {
+  if (L.s) {
+    (void)hipStreamSynchronize(L.s);
+    (void)hipStreamDestroy(L.s);
+  }
+  for (int4 *p : {L.d_prep, L.d_fin, L.d_fin_pre})
+    if (p) (void)hipFree(p);
+  L.d_korder.release();
+  L.s = nullptr;
+  L.d_prep = L.d_fin = L.d_fin_pre = nullptr;
+}
+
 int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   static const bool trace_steps = getenv("TMED_TRACE") != nullptr;
   SlowStep slow{trace_steps && st.total >= kVoteCopyStreamMin};
@@ -254,7 +287,11 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   VoteSlot &vs = c->vslot[st.slot];
   uint8_t *d = (uint8_t *)vs.d_votes.p;
   c->last_hs_count = 0;  // the commit seam reuses d_prep (tmed_window_stats)
-  hipStream_t s = c->stream;
+  // lane 1: key-cached throughput batches only (the latency kernels and the generic path use the
+  // context's scratch on lane 0)
+  if (st.lane == 1 && (!st.ks || st.m <= c->lat_max || !lane1_ready(c))) st.lane = 0;
+  Lane *lane = st.lane == 1 ? &c->lane1 : nullptr;
+  hipStream_t s = lane ? lane->s : c->stream;
   // A large copy runs on the copy stream, so it overlaps the kernels of the batch queued
   // before (the other slot; this slot's previous batch was collected before it was
   // restaged).  A small one (a single commit) stays on the kernel stream: the cross-stream
@@ -318,7 +355,10 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
     e = hipMemcpyAsync(d, vs.h_votes.p, st.total, hipMemcpyHostToDevice, s);
   }
   slow.lap("copy-in");
-  if (e == hipSuccess) e = scratch_acquire(c, s);
+  // lane 0 orders itself with the context's other scratch users; lane 1 has its own scratch but
+  // reads the key-set pool, whose keys are appended on the context stream (keyset_append: kup_ev)
+  if (e == hipSuccess && !lane) e = scratch_acquire(c, s);
+  if (e == hipSuccess && lane && c->kup_ev) e = hipStreamWaitEvent(s, c->kup_ev, 0);
   slow.lap("scratch_acquire");
   // Timing events cost ~8 us of a single commit's latency (C1 generic 249 -> 239 us, keyed
   // 97 -> 88 us): a zero-copy batch records them only under tmed_set_kernel_timing.
@@ -336,14 +376,14 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
   if (e == hipSuccess) {
     if (st.ks)
       e = keyset_verify(c, *st.ks, (const uint32_t *)(d + st.o_key), d + st.o_sig, (const uint8_t *)vs.d_vmsg.p,
-                        (const uint32_t *)vs.d_off.p, m, out_dev, s, /*msg_slots=*/true, fused ? &va : nullptr);
+                        (const uint32_t *)vs.d_off.p, m, out_dev, s, /*msg_slots=*/true, fused ? &va : nullptr, lane);
     else
       e = generic_verify(c, d + st.o_key, d + st.o_sig, (const uint8_t *)vs.d_vmsg.p, (const uint32_t *)vs.d_off.p, m,
                          out_dev, s, /*msg_slots=*/true, nullptr, fused ? &va : nullptr);
   }
   slow.lap("verify launches");
   if (e == hipSuccess && st.timed) e = hipEventRecord(vs.ev1, s);
-  if (e == hipSuccess) e = scratch_release(c, s);
+  if (e == hipSuccess && !lane) e = scratch_release(c, s);
   if (e == hipSuccess && !st.zc) e = hipMemcpyAsync(vs.h_out.p, vs.d_out.p, m, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipEventRecord(vs.done, s);
   slow.lap("copy-out");
@@ -439,6 +479,7 @@ int tmed_keyset_free(tmed_ctx *c, uint64_t handle) {
   if (!k) return TMED_ENOKEYSET;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  if (c->lane1.s) (void)hipStreamSynchronize(c->lane1.s);
   free_keyset(*k);
   c->keysets.erase(handle);
   return TMED_OK;

@@ -216,6 +216,7 @@ void tmed_destroy(tmed_ctx *c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
   bs_destroy(c);  // submitted blocksync windows never waited for (their cache pins go with them)
+  lane_release(c->lane1);
   for (DevBuf *b : {&c->d_a, &c->d_b, &c->d_msg, &c->d_off, &c->d_out, &c->d_c}) b->release();
   for (HostBuf *b : {&c->h_a, &c->h_b, &c->h_msg, &c->h_off, &c->h_out, &c->h_c}) b->release();
   for (DevBuf *b : {&c->d_merkle_a, &c->d_merkle_b, &c->d_merkle_idx, &c->d_korder, &c->d_zip, &c->d_kbases})
