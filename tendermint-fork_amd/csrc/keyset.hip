@@ -253,6 +253,7 @@ static bool lane1_ready(tmed_ctx *c) {
   if (L.s) return true;
   if (L.failed) return false;
   hipError_t e = hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking);
+
   if (e == hipSuccess) e = hipMalloc((void **)&L.d_prep, (size_t)c->slab_slots * kPrepSlotBytes + kPrepTailBytes);
   if (e == hipSuccess) e = hipMalloc((void **)&L.d_fin, kFinBytes);
   if (e == hipSuccess) e = hipMalloc((void **)&L.d_fin_pre, kFinPreBytes);
@@ -498,6 +499,8 @@ int tmed_verify_batch_keyset_device(tmed_ctx *c, uint64_t handle, const uint32_t
   (void)hipSetDevice(c->device);
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
   if (c->timing) c->timer.n = 0;
+  // (one lane: split over both kernel lanes in halves, a 2^20 batch ran 3 % slower — the halves'
+  // key orders spread each kernel's comb reads — profiles/r04/s10/ab_keyed_lanes.jsonl)
   hipError_t e = scratch_acquire(c, s);
   if (e == hipSuccess) e = keyset_verify(c, k, d_val_idx, d_sigs, d_msgs, d_msg_off, (uint32_t)n, d_out, s, false);
   if (e == hipSuccess) e = scratch_release(c, s);

@@ -17,7 +17,8 @@ s = torch.cuda.Stream(dev)
 torch.cuda.set_stream(s)
 r = bench.c2_keyset(eng, dev, s, 1 << 20, 20, 3, None)
 rf = r["roofline"]
-print(json.dumps({"lib": os.environ.get("TMED_LIB", "default"), "value": r["value"], "all_valid": r["all_valid"],
+print(json.dumps({"lib": os.environ.get("TMED_LIB", "default"), "lanes": os.environ.get("TMED_LANES", "2"),
+                  "value": r["value"], "all_valid": r["all_valid"],
                   "prep_ms": rf["prep_kernel_ms"], "main_ms": rf["kernel_avg_ms"] * rf["launches_per_step"],
                   "finish_ms": rf["finish_kernel_ms"]}), flush=True)
 eng.close()
