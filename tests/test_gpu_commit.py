@@ -403,6 +403,11 @@ def test_blocksync_stream_of_windows_gpu(engine, keyed):
                 got = T.verify_commits(engine, [(T.MODE_LIGHT, vals, "stream-chain", c.block_id, c.height, c, 0, 0)])
                 assert got == [None]
             w.win = w.bids = w.ccs = w.vs = None  # the structs may go once submit returned
+            if k == 3:  # a malformed window is refused without touching the windows in flight
+                bad = window(9, 1000, 2, pin=False)
+                bad.ccs[1].sigs = None  # a commit without its signature array: TMED_EINVAL
+                with pytest.raises(T.TmedError):
+                    bad.submit(engine, 2)
         T.blocksync_wait(engine)
         for w, (codes, vers, idx) in zip(wins, ref):
             assert (w.codes() == codes).all() and (w.verified() == vers).all()
