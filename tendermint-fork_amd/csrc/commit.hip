@@ -1077,6 +1077,7 @@ static void scatter_bits(const tmed_commit_request *reqs, const Cands &cands, co
 }
 
 static int bs_drain(tmed_ctx *ctx);
+static void bs_reap(tmed_ctx *ctx);
 
 // Device templates of the requests that have candidates; false if one does not fit.
 static int device_templates(const tmed_commit_request *reqs, size_t n, const Cands &cands, std::vector<uint8_t> &tmpl,
@@ -1359,24 +1360,40 @@ extern "C" int tmed_verify_commits(tmed_ctx *ctx, const tmed_commit_request *req
   reqs = keycache_resolve(ctx, reqs, n, kc);
   const size_t kPipeBatchSigs = pipe_batch_sigs();
   if (n > 1 && reqs && out) {
-    bool ok = true;
-    size_t sigs = 0;
+    // every request checked, one key set, the signature total (in parallel: a light-client call's
+    // ~10k commit structs are cold in the cache)
     const uint64_t ks = reqs[0].vals ? reqs[0].vals->keyset : 0;
-    for (size_t q = 0; q < n && ok; q++) {
-      ok = check_request(reqs[q]) == TMED_OK && reqs[q].vals->keyset == ks;
-      if (ok) sigs += reqs[q].commit->n_sigs;
-    }
+    std::atomic<bool> all_ok{true};
+    std::atomic<size_t> sig_total{0};
+    parallel_ranges(n, n >= 4096 ? host_threads(n * 64) : 1, [&](size_t lo, size_t hi, unsigned) {
+      size_t sg = 0;
+      bool good = true;
+      for (size_t q = lo; q < hi && good; q++) {
+        good = check_request(reqs[q]) == TMED_OK && reqs[q].vals->keyset == ks;
+        if (good) sg += reqs[q].commit->n_sigs;
+      }
+      sig_total += sg;
+      if (!good) all_ok = false;
+    });
+    const bool ok = all_ok.load();
+    const size_t sigs = sig_total.load();
     if (ok && sigs >= 2 * kPipeBatchSigs) {
       const size_t bsz = std::max<size_t>(16, kPipeBatchSigs / std::max<size_t>(1, sigs / n));
-      if (n > bsz) return run_pipelined(ctx, reqs, n, bsz, ks, out, &kc);
+      if (n > bsz) {
+        const int rc = run_pipelined(ctx, reqs, n, bsz, ks, out, &kc);
+        bs_reap(ctx);
+        return rc;
+      }
     }
   }
-  return run_seam(
+  const int rc = run_seam(
       reqs, n, out,
       [&](const tmed_commit_request *rq, size_t nr, const Cands &cands, uint8_t *valid) {
         return ctx_verify(ctx, rq, nr, cands, valid);
       },
       &kc);
+  bs_reap(ctx);  // submitted windows this call collected (ctx_verify drained the stream) leave now
+  return rc;
 }
 
 // ---- blocksync replay window (f4): pipelined LIGHT batches --------------------------------
@@ -1623,6 +1640,16 @@ static void bs_pop_done(BsStream &S, std::vector<std::unique_ptr<BsWindow>> &gon
   while (!S.wins.empty() && S.wins.front()->done()) {
     gone.push_back(std::move(S.wins.front()));
     S.wins.pop_front();
+  }
+}
+
+// Windows whose batches were collected by another seam call (bs_drain) are released here, outside
+// ctx->mu (their key-set cache pins go with them: ~KcCall takes the lock).
+static void bs_reap(tmed_ctx *ctx) {
+  std::vector<std::unique_ptr<BsWindow>> gone;
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (ctx->bs) bs_pop_done(*ctx->bs, gone);
   }
 }
 
