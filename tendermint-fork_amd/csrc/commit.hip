@@ -452,7 +452,9 @@ struct HostPool {
   std::condition_variable cv;
   static thread_local bool in_worker;
   static thread_local bool in_region;  // the caller while it runs parts of its own region
-  static constexpr int kSpin = 20000;  // ~20-50 us of polling before a worker sleeps
+  // Polling before a worker sleeps: a short pause loop, then sched_yield (a worker that polls must not
+  // take the CPU from the threads doing the work when the host has fewer cores than threads).
+  static constexpr int kPause = 1000, kYield = 200;
 
   static uint64_t gen_of(uint64_t w) { return w >> 40; }
   static unsigned parts_of(uint64_t w) { return (unsigned)((w >> 24) & 0xffffu); }
@@ -476,8 +478,12 @@ struct HostPool {
         for (;;) {
           int spins = 0;
           while (gen_of(word.load(std::memory_order_acquire)) == seen) {
-            if (++spins < kSpin) {
+            if (++spins < kPause) {
               __builtin_ia32_pause();
+              continue;
+            }
+            if (spins < kPause + kYield) {
+              std::this_thread::yield();
               continue;
             }
             std::unique_lock<std::mutex> lk(m);
@@ -504,7 +510,7 @@ struct HostPool {
     in_region = false;
     int spins = 0;
     while (done.load(std::memory_order_acquire) < parts)
-      if (++spins < kSpin) __builtin_ia32_pause();
+      if (++spins < kPause) __builtin_ia32_pause();
       else std::this_thread::yield();
   }
   static HostPool &get() {
