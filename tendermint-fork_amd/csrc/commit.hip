@@ -1302,18 +1302,27 @@ static const tmed_commit_request *keycache_resolve(tmed_ctx *ctx, const tmed_com
       else if (!sr.skip) misses++;
     if (misses) {
       // the call's signatures against every key it lacks: a window / batch that pays for them all
-      // builds them before its kernels (each set alone may carry too few signatures)
+      // builds them before its kernels (each set alone may carry too few signatures).  A call too
+      // small to pay for even one key (a single commit: C1) counts nothing.
       size_t call_sigs = 0, call_missing = 0;
-      std::unordered_set<tmed::Pub32, tmed::Pub32Hash> seen;
       for (SetRef &sr : sets)
-        if (!sr.hit && !sr.skip) {
-          call_sigs += sr.sigs;
-          call_missing += tmed::keycache_missing(ctx, sr.v->pubkeys, sr.v->n, &seen);
-        }
+        if (!sr.hit && !sr.skip) call_sigs += sr.sigs;
+      if (call_sigs >= tmed::kKcAmortizeSigsPerKey) {
+        std::unordered_set<tmed::Pub32, tmed::Pub32Hash> seen;
+        for (SetRef &sr : sets)
+          if (!sr.hit && !sr.skip) call_missing += tmed::keycache_missing(ctx, sr.v->pubkeys, sr.v->n, &seen);
+      }
       const bool build_all = call_missing && call_sigs >= tmed::kKcAmortizeSigsPerKey * call_missing;
       for (SetRef &sr : sets) {
         if (sr.hit || sr.skip) continue;
         sr.e = nullptr;
+        // too few signatures for even one key and not every key pooled: generic now, the keys are
+        // sorted out by the worker after the call (the first commit of a new set)
+        if (!build_all && sr.sigs < tmed::kKcAmortizeSigsPerKey &&
+            !tmed::keycache_all_pooled(ctx, sr.v->pubkeys, sr.v->n)) {
+          tmed::keycache_defer(ctx, sr.v->pubkeys, sr.v->n, sr.sigs);
+          continue;
+        }
         if (tmed::keycache_lookup(ctx, sr.v->pubkeys, sr.v->n, sr.key, sr.sigs, /*may_reset=*/!any_keyed, &sr.handle,
                                   sr.e, build_all)) {
           sr.hit = true;
@@ -1323,7 +1332,10 @@ static const tmed_commit_request *keycache_resolve(tmed_ctx *ctx, const tmed_com
     }
   }
   clk.lap("lookups");
-  if (!any_keyed) return reqs;
+  if (!any_keyed) {
+    clk.emit("keycache_resolve (generic)", n, sets.size());
+    return reqs;
+  }
   // the call's requests, rewritten onto copies of the sets that resolved keyed
   S.vals.resize(sets.size());
   S.entry.resize(sets.size());

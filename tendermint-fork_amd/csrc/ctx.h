@@ -104,6 +104,8 @@ uint64_t keycache_call_tick(tmed_ctx *c);                        // KeyCache::ca
 void keycache_hits(tmed_ctx *c, size_t sets, size_t sigs);       // KeyCache::hits
 void keycache_touch(tmed_ctx *c);
 void keycache_hit(tmed_ctx *c, const KcSet &e, size_t sigs);  // KeyCache::hit
+bool keycache_all_pooled(tmed_ctx *c, const uint8_t *pubs, size_t n);  // KeyCache::all_pooled
+void keycache_defer(tmed_ctx *c, const uint8_t *pubs, size_t n, size_t sigs);  // KeyCache::defer
 bool keycache_lookup(tmed_ctx *c, const uint8_t *pubs, size_t n, const KcKey &key, size_t sigs, bool may_reset,
                      uint64_t *handle, const KcSet *&hold, bool force_build = false);
 int keycache_drain(tmed_ctx *c);  // build the keys queued behind generic calls (asynchronously)

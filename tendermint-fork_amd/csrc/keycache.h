@@ -212,6 +212,7 @@ class KeyCache {
   size_t pool_keys() const { return slot_.size(); }
   size_t sets_cached() const { return sets_.size(); }
   size_t pending_keys() const { return pending_.size() / 32; }
+  bool has_work() const { return !pending_.empty() || !deferred_.empty(); }
   int users() const { return users_; }
   size_t retired() const { return retired_.size(); }
 
@@ -290,6 +291,23 @@ class KeyCache {
     return insert_keyed(std::move(e), key, sigs, hold);
   }
 
+  // Every key of the set already in the pool (stops at the first missing one).
+  bool all_pooled(const uint8_t *pubs, size_t n) const {
+    for (size_t i = 0; i < n; i++)
+      if (!slot_.count(pub32(pubs + 32 * i))) return false;
+    return true;
+  }
+
+  // A set of a small call (too few signatures to pay for even one key) whose keys are not all
+  // pooled: the call runs generic, and its keys are only copied here — which of them the pool lacks
+  // is worked out by drain_pending, after the call (the first commit of a new set pays no
+  // per-key lookups).  Counted like lookup()'s deferred path.
+  void defer(const uint8_t *pubs, size_t n, size_t sigs) {
+    st.lookups++;
+    generic(sigs);
+    deferred_.insert(deferred_.end(), pubs, pubs + 32 * n);
+  }
+
   // Distinct keys of a set that the pool lacks (not counting those already in *seen, which
   // collects them across the sets of one call): a call builds every missing key at once when its
   // signatures amortise them all (kAmortizeSigsPerKey each), as a blocksync window or a large
@@ -307,6 +325,12 @@ class KeyCache {
 
   // Build the keys queued by generic calls (after such a call has collected its results).
   int drain_pending() {
+    for (size_t r = 0; r < deferred_.size() / 32; r++) {  // the deferred sets' keys the pool lacks
+      const Pub32 k = pub32(&deferred_[32 * r]);
+      if (!slot_.count(k) && pend_set_.insert(k).second)
+        pending_.insert(pending_.end(), &deferred_[32 * r], &deferred_[32 * r] + 32);
+    }
+    deferred_.clear();
     if (pending_.empty()) return 0;
     std::vector<uint8_t> add;
     add.swap(pending_);
@@ -337,6 +361,7 @@ class KeyCache {
     set_bytes_ = 0;
     pending_.clear();
     pend_set_.clear();
+    deferred_.clear();
   }
 
  private:
@@ -417,6 +442,7 @@ class KeyCache {
   std::unordered_map<KcKey, std::unique_ptr<KcSet>, KcKeyHash> sets_;
   std::vector<std::unique_ptr<KcSet>> retired_;  // dropped while a call was pinned
   std::vector<uint8_t> pending_;  // keys queued by generic calls
+  std::vector<uint8_t> deferred_;  // keys of deferred sets, not yet checked against the pool
   std::unordered_set<Pub32, Pub32Hash> pend_set_;
   size_t set_bytes_ = 0;
   uint64_t tick_ = 0;

@@ -132,8 +132,10 @@ size_t keycache_missing(tmed_ctx *c, const uint8_t *pubs, size_t n, std::unorder
 }
 int keycache_drain(tmed_ctx *c) { return c->kc ? c->kc->kc.drain_pending() : TMED_OK; }
 void keycache_after_call(tmed_ctx *c) {
-  if (c->kc && c->kc->kc.pending_keys()) c->kc->kick();
+  if (c->kc && c->kc->kc.has_work()) c->kc->kick();
 }
+bool keycache_all_pooled(tmed_ctx *c, const uint8_t *pubs, size_t n) { return cache_of(c).all_pooled(pubs, n); }
+void keycache_defer(tmed_ctx *c, const uint8_t *pubs, size_t n, size_t sigs) { cache_of(c).defer(pubs, n, sigs); }
 
 }  // namespace tmed
 

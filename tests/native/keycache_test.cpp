@@ -80,5 +80,7 @@ int kct_pool_key(void *h, uint32_t i, uint8_t out[32]) {
   return 0;
 }
 size_t kct_retired(void *h) { return ((Kct *)h)->kc.retired(); }
+int kct_all_pooled(void *h, const uint8_t *pubs, size_t n) { return ((Kct *)h)->kc.all_pooled(pubs, n) ? 1 : 0; }
+void kct_defer(void *h, const uint8_t *pubs, size_t n, size_t sigs) { ((Kct *)h)->kc.defer(pubs, n, sigs); }
 void kct_digest(const uint8_t *pubs, size_t n, uint8_t out[32]) { kc_digest(pubs, n, out); }
 }

@@ -48,6 +48,9 @@ def kct():
     l.kct_digest.argtypes = [P, SZ, P]
     l.kct_retired.restype = SZ
     l.kct_retired.argtypes = [P]
+    l.kct_all_pooled.restype = ctypes.c_int
+    l.kct_all_pooled.argtypes = [P, P, SZ]
+    l.kct_defer.argtypes = [P, P, SZ, SZ]
     return l
 
 
@@ -248,6 +251,32 @@ def test_entries_dropped_while_pinned_are_retired(kct):
     for s in sets:
         assert c.lookup(s, AMORTIZE * 8, force=True)[0]
     assert kct.kct_retired(c.h) == 0
+
+
+def test_deferred_first_commit_of_a_new_set(kct):
+    """The seam's fast path for a single commit on a new set (commit.hip keycache_resolve): one
+    pool probe (all_pooled stops at the first missing key), the keys copied (defer), the call
+    generic; the worker's drain then queues and builds exactly the missing keys, and the next
+    commit on the set is keyed.  Counted as the deferred lookup path counts."""
+    c = Cache(kct, 10_000)
+    a = keys(b"df", 0, 175)
+    assert c.call([(a[:100], AMORTIZE * 100)])[0][0]          # 100 of the keys pooled by a big call
+    pa = np.ascontiguousarray(a)
+    assert kct.kct_all_pooled(c.h, pa.ctypes.data, 175) == 0
+    assert kct.kct_all_pooled(c.h, np.ascontiguousarray(a[:100]).ctypes.data, 100) == 1
+    s0 = c.stats()
+    kct.kct_pin(c.h)
+    kct.kct_defer(c.h, pa.ctypes.data, 175, 175)
+    kct.kct_unpin(c.h)
+    s1 = c.stats()
+    assert s1["generic_sets"] == s0["generic_sets"] + 1 and s1["lookups"] == s0["lookups"] + 1
+    assert s1["pool_keys"] == 100                             # nothing looked up or built in the call
+    assert kct.kct_drain(c.h) == 0
+    s2 = c.stats()
+    assert s2["pool_keys"] == 175 and s2["keys_deferred"] == s0["keys_deferred"] + 75
+    k, idx = c.call([(a, 175)])[0]
+    assert k
+    check_idx(c, a, idx)
 
 
 def test_digest_depends_on_order_and_size(kct):
