@@ -244,14 +244,11 @@ using BatchVerifier =
 // order, so the first candidate of each request marks it used (one writer per request).
 template <class Then>
 static int init_encoders(const tmed_commit_request *reqs, size_t n, const Cands &cands,
-                         std::vector<tmed::VoteEncoder> &enc, std::vector<uint8_t> &used, Then &&then,
-                         bool shared_rows = false) {
+                         std::vector<tmed::VoteEncoder> &enc, std::vector<uint8_t> &used, Then &&then) {
   enc.assign(n, tmed::VoteEncoder());
   used.assign(n, 0);
   const size_t m = cands.size();
-  // shared_rows: a request whose candidates use another request's template (Cands::tmpl_of) needs
-  // no encoder of its own
-  for (const Run &r : cands.runs) used[shared_rows ? cands.tmpl_row(r.req) : r.req] = 1;
+  for (const Run &r : cands.runs) used[r.req] = 1;
   std::atomic<int> bad{0};
   parallel_ranges(n, n >= 64 ? host_threads(m) : 1, [&](size_t lo, size_t hi, unsigned) {
   for (size_t q = lo; q < hi; q++) {
@@ -958,18 +955,66 @@ static void for_segments(const Cands &c, const Group &g, size_t lo, size_t hi, F
   }
 }
 
+// Device templates, one row per request whose candidates use its own (Cands::tmpl_row), rows
+// packed in request order: row_of[q] is request q's row (kNoRow: none).
+constexpr uint32_t kNoRow = 0xffffffffu;
+struct Templates {
+  std::vector<uint8_t> rows;
+  std::vector<uint32_t> row_of;
+  size_t nrows = 0;
+  uint32_t row(const Cands &c, uint32_t q) const { return row_of[c.tmpl_row(q)]; }
+};
+static int device_templates(const tmed_commit_request *reqs, size_t n, const Cands &cands, Templates &tp,
+                            bool *fits) {
+  tp.row_of.assign(n, kNoRow);
+  for (const Run &r : cands.runs) tp.row_of[cands.tmpl_row(r.req)] = 0;
+  size_t k = 0;
+  for (size_t q = 0; q < n; q++)
+    if (tp.row_of[q] != kNoRow) tp.row_of[q] = (uint32_t)k++;
+  tp.nrows = k;
+  tp.rows.resize(std::max<size_t>(k, 1) * tmed::kVoteTmplBytes);
+  std::atomic<bool> ok{true}, bad{false};
+  parallel_ranges(n, n >= 64 ? host_threads(cands.size()) : 1, [&](size_t lo, size_t hi, unsigned) {
+    for (size_t q = lo; q < hi; q++) {
+      if (tp.row_of[q] == kNoRow) continue;
+      const tmed_commit &c = *reqs[q].commit;
+      tmed_vote_template t;
+      t.chain_id = reqs[q].chain_id;
+      t.chain_id_len = reqs[q].chain_id_len;
+      t.height = c.height;
+      t.round = c.round;
+      t.block_hash = c.block_id.hash;
+      t.block_hash_len = c.block_id.hash_len;
+      t.psh_total = c.block_id.psh_total;
+      t.psh_hash = c.block_id.psh_hash;
+      t.psh_hash_len = c.block_id.psh_hash_len;
+      tmed::VoteEncoder e;
+      if (e.init(&t) != TMED_OK) {
+        bad = true;
+        continue;
+      }
+      uint8_t *row = &tp.rows[(size_t)tp.row_of[q] * tmed::kVoteTmplBytes];
+      memset(row, 0, tmed::kVoteTmplBytes);
+      if (!e.device_template(row, tmed::kVoteTmplBytes, tmed::kVoteSlot)) ok = false;
+    }
+  });
+  if (bad) return TMED_EINVAL;
+  *fits = ok;
+  return TMED_OK;
+}
+
 // Device staging of one group's candidates into vote slot `slot`: sign-bytes are assembled on
 // the device from per-commit templates, so only key references, signatures,
 // flags and timestamps cross PCIe; they are written straight from the request arrays into the
 // pinned staging area, run by run (multi-threaded for large batches).  The caller holds ctx->mu.
 constexpr size_t kDmaMinRun = 256;  // signatures (16 KB)
 static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, const Cands &cands, const Group &grp,
-                       uint64_t keyset, const uint8_t *tmpl, int slot, tmed::VoteStage &st) {
+                       uint64_t keyset, const Templates &tp, int slot, tmed::VoteStage &st) {
   const bool keyed = keyset != 0;
   const uint32_t m = (uint32_t)grp.size(cands);
-  int rc = tmed::votes_stage(ctx, keyset, m, n, st, slot);
+  int rc = tmed::votes_stage(ctx, keyset, m, std::max<size_t>(tp.nrows, 1), st, slot);
   if (rc != TMED_OK) return rc;
-  memcpy(st.tmpl, tmpl, n * tmed::kVoteTmplBytes);
+  memcpy(st.tmpl, tp.rows.data(), std::max<size_t>(tp.nrows, 1) * tmed::kVoteTmplBytes);
   std::atomic<bool> key_ok{true};
   const uint32_t nkeys = keyed ? (uint32_t)st.ks->n : 0u;
   // Signature runs in pinned caller memory go to the device by their own DMA (votes_enqueue)
@@ -1039,7 +1084,7 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
             if (sl < 64) memset(st.sig + (p + u) * 64 + sl, 0, 64 - sl);
           }
       }
-      std::fill(st.tidx + p, st.tidx + p + len, cands.tmpl_row(run.req));
+      std::fill(st.tidx + p, st.tidx + p + len, tp.row(cands, run.req));
       memcpy(st.flag + p, c.flags + i, len);
       memcpy(st.sec + p, c.ts_seconds + i, 8 * len);
       memcpy(st.nan + p, c.ts_nanos + i, 4 * len);
@@ -1085,30 +1130,13 @@ static void scatter_bits(const tmed_commit_request *reqs, const Cands &cands, co
 static int bs_drain(tmed_ctx *ctx);
 static void bs_reap(tmed_ctx *ctx);
 
-// Device templates of the requests that have candidates; false if one does not fit.
-static int device_templates(const tmed_commit_request *reqs, size_t n, const Cands &cands, std::vector<uint8_t> &tmpl,
-                            bool *fits) {
-  std::vector<tmed::VoteEncoder> enc;
-  std::vector<uint8_t> used;
-  tmpl.resize(n * tmed::kVoteTmplBytes);  // rows of requests without candidates are never read
-  std::atomic<bool> ok{true};
-  int rc = init_encoders(reqs, n, cands, enc, used, [&](size_t q, const tmed::VoteEncoder &e) {
-    uint8_t *row = &tmpl[q * tmed::kVoteTmplBytes];
-    memset(row, 0, tmed::kVoteTmplBytes);
-    if (!e.device_template(row, tmed::kVoteTmplBytes, tmed::kVoteSlot)) ok = false;
-    return true;
-  }, /*shared_rows=*/true);
-  if (rc != TMED_OK) return rc;
-  *fits = ok;
-  return TMED_OK;
-}
 
 // GPU verifier of one seam call: candidates of validator sets with a key-set handle go
 // through the key-cached kernels, one launch sequence per distinct key set.
 static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, const Cands &cands,
                       uint8_t *valid) {
   PhaseClock clk;
-  std::vector<uint8_t> tmpl;
+  thread_local Templates tmpl;
   bool fits = true;
   int rc = device_templates(reqs, n, cands, tmpl, &fits);
   if (rc != TMED_OK) return rc;
@@ -1135,7 +1163,7 @@ static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, 
     const uint32_t m = (uint32_t)grp.size(cands);
     if (m == 0) continue;
     tmed::VoteStage st;
-    rc = stage_group(ctx, reqs, n, cands, grp, gkeys[g], tmpl.data(), 0, st);
+    rc = stage_group(ctx, reqs, n, cands, grp, gkeys[g], tmpl, 0, st);
     clk.lap("stage");
     std::vector<uint8_t> out(m);
     if (rc == TMED_OK) rc = tmed::votes_launch(ctx, st, out.data());
@@ -1445,7 +1473,8 @@ struct BsBatch {
   size_t lo = 0, n = 0;
   Plans plans;
   Cands cands;
-  std::vector<uint8_t> tmpl, bits, valid;
+  Templates tmpl;
+  std::vector<uint8_t> bits, valid;
   Group grp;  // the staged segments when candidates are aliased (else every run, in order)
   tmed::VoteStage st;
   bool device = false;  // queued on a vote slot (else verified synchronously / nothing to verify)
@@ -1610,7 +1639,7 @@ static int bs_pump(tmed_ctx *ctx, BsStream &S, BsWindow &w, double ph[3], std::u
           size_t ap = 0;
           for (size_t r = 0; r < b.cands.runs.size(); r++) b.grp.add_run(b.cands, (uint32_t)r, ap);
         }
-        rc = stage_group(ctx, rq, b.n, b.cands, b.grp, w.keyset, b.tmpl.data(), (int)(idx % ns), b.st);
+        rc = stage_group(ctx, rq, b.n, b.cands, b.grp, w.keyset, b.tmpl, (int)(idx % ns), b.st);
         // key-cached batches alternate between the two kernel lanes, so one batch's small kernels
         // (assembly, key order, prep, finish) run beside the other's main kernel
         b.st.lane = w.keyset && (idx & 1) && lanes_on() ? 1 : 0;
