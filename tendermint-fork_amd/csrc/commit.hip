@@ -1524,15 +1524,6 @@ static double bs_us(BsClock::time_point a, BsClock::time_point b) {
   return std::chrono::duration<double, std::micro>(b - a).count();
 }
 
-// TMED_LANES=1: every batch on the context stream (A/B of the second kernel lane)
-static bool lanes_on() {
-  static const bool on = [] {
-    const char *v = getenv("TMED_LANES");
-    return !(v && v[0] == '1');
-  }();
-  return on;
-}
-
 // Collect batch b (ctx->mu held): its bits, the alias copies, the replay into its window's results.
 // ph: tmed_seam_phase_us — host plan + templates + staging, host time blocked on the device
 // (enqueueing the copies and kernels, votes_collect), host replay.
@@ -1642,7 +1633,7 @@ static int bs_pump(tmed_ctx *ctx, BsStream &S, BsWindow &w, double ph[3], std::u
         rc = stage_group(ctx, rq, b.n, b.cands, b.grp, w.keyset, b.tmpl, (int)(idx % ns), b.st);
         // key-cached batches alternate between the two kernel lanes, so one batch's small kernels
         // (assembly, key order, prep, finish) run beside the other's main kernel
-        b.st.lane = w.keyset && (idx & 1) && lanes_on() ? 1 : 0;
+        b.st.lane = w.keyset && (idx & 1) && tmed::lanes_on() ? 1 : 0;
         clk.lap("stage");
         const auto te = BsClock::now();
         ph[0] += bs_us(tp, te);

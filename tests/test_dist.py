@@ -174,3 +174,16 @@ def test_blocksync_aggregation_matches_single_process(world):
         assert mism == sum(range(world)) and sec == 1.0 + (world - 1) and extra == [0.25 * world]
         assert bits == single.tolist()
         assert [p[0] for p in phases] == [10.0 * r for r in range(world)] and all(p[-1] == 1.0 + r for r, p in enumerate(phases))
+
+
+def test_rehearsal_lines_name_simulated_gpus(monkeypatch):
+    """A gloo rehearsal with more ranks than GPUs labels its JSON n_gpus_simulated /
+    n_gpus_physical (bench.py, bench_commits.py); a real run keeps n_gpus."""
+    import torch
+    from tmed.launch import gpu_count_fields
+    ndev = max(1, torch.cuda.device_count())
+    monkeypatch.setenv("TMED_DIST_BACKEND", "gloo")
+    assert gpu_count_fields(ndev + 1) == {"n_gpus_simulated": ndev + 1, "n_gpus_physical": ndev}
+    assert gpu_count_fields(1) == {"n_gpus": 1}
+    monkeypatch.delenv("TMED_DIST_BACKEND")
+    assert gpu_count_fields(ndev + 1) == {"n_gpus": ndev + 1}
