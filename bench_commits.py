@@ -378,7 +378,7 @@ def _c4_corrupt(commits, b0: int, every: int, upto: int):
     return exp
 
 
-STREAM_CHUNK_WINDOWS = 4  # C4 stream mode: windows generated (pinned) at once: 4 x 1000 blocks x 10k x 64 B = 2.6 GB per rank
+STREAM_CHUNK_WINDOWS = 13  # C4 stream mode: windows generated (pinned) at once: 13 x 1000 blocks x 10k x 64 B = 8.3 GB per rank
 
 
 def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, batch: int, corrupt_every: int = 0,

@@ -94,7 +94,6 @@ void keycache_destroy(tmed_ctx *c);
 void bs_destroy(tmed_ctx *c);  // commit.hip: the blocksync batch stream (before keycache_destroy)
 struct Lane;
 void lane_release(Lane &L);    // keyset.hip: the second kernel lane's stream and scratch
-bool lane1_generic_ready(tmed_ctx *c);  // keyset.hip: lane 1 with the generic path's slab and events
 bool lanes_on();               // keyset.hip: TMED_LANES != 1
 void keycache_pin(tmed_ctx *c);    // a seam call resolving sets: no pool reset until it unpins
 void keycache_unpin(tmed_ctx *c);
@@ -197,8 +196,6 @@ namespace tmed {
 struct Lane {
   hipStream_t s = nullptr;
   int4 *d_prep = nullptr, *d_fin = nullptr, *d_fin_pre = nullptr;
-  int4 *d_slab = nullptr;  // the generic path's per-lane tables (a device batch split over the lanes)
-  hipEvent_t ev_in = nullptr, ev_out = nullptr;  // fork / join of a split device batch
   DevBuf d_korder;
   bool failed = false;  // no stream / memory: every batch stays on lane 0
 };

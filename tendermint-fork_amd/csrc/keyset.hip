@@ -274,33 +274,13 @@ bool lanes_on() {
   return on;
 }
 
-bool lane1_generic_ready(tmed_ctx *c) {
-  if (!lanes_on() || !lane1_ready(c)) return false;
-  Lane &L = c->lane1;
-  if (L.d_slab && L.ev_in && L.ev_out) return true;
-  hipError_t e = hipSuccess;
-  if (!L.d_slab)
-    e = hipMalloc((void **)&L.d_slab, (size_t)c->slab_slots * kSlabSlotBytes * slab_tables(c->main_waves));
-  if (e == hipSuccess && !L.ev_in) e = hipEventCreateWithFlags(&L.ev_in, hipEventDisableTiming);
-  if (e == hipSuccess && !L.ev_out) e = hipEventCreateWithFlags(&L.ev_out, hipEventDisableTiming);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  return true;
-}
-
 void lane_release(Lane &L) {
   if (L.s) {
     (void)hipStreamSynchronize(L.s);
     (void)hipStreamDestroy(L.s);
   }
-  for (int4 *p : {L.d_prep, L.d_fin, L.d_fin_pre, L.d_slab})
+  for (int4 *p : {L.d_prep, L.d_fin, L.d_fin_pre})
     if (p) (void)hipFree(p);
-  for (hipEvent_t ev : {L.ev_in, L.ev_out})
-    if (ev) (void)hipEventDestroy(ev);
-  L.ev_in = L.ev_out = nullptr;
-  L.d_slab = nullptr;
   L.d_korder.release();
   L.s = nullptr;
   L.d_prep = L.d_fin = L.d_fin_pre = nullptr;

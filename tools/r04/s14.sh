@@ -5,9 +5,6 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/s14
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_verify.py -x -q -m gpu --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
-rc=$?; echo "gpu tests rc=$rc"; tail -2 $O/gpu_tests.log
-case $rc in 0) ;; *) exit $rc;; esac
 for r in 1 2 3; do
   for L in 2 1; do
     TMED_LANES=$L timeout -k 10 200 python bench.py --no-c1 --no-c3 --no-c4 --no-c5 --no-zip215 --no-keyset --no-cpu-baseline --steps 100 > $O/c2_lanes$L.$r.log 2>&1
