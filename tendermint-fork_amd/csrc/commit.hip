@@ -392,11 +392,18 @@ static int plan_request(const tmed_commit_request *reqs, size_t q, tmed_commit_r
     seen.reset(vs.n);
     int64_t tally = 0;
     constexpr size_t kAhead = 8;
+    bool hashed = false;  // the index is prefetched once a signature missed its position
     for (size_t i = 0; i < c.n_sigs; i++) {
-      if (i + kAhead < c.n_sigs) ix.prefetch_slot(c.addresses + 20 * (i + kAhead));
-      if (i + kAhead / 2 < c.n_sigs) ix.prefetch_entry(c.addresses + 20 * (i + kAhead / 2));
+      if (hashed) {
+        if (i + kAhead < c.n_sigs) ix.prefetch_slot(c.addresses + 20 * (i + kAhead));
+        if (i + kAhead / 2 < c.n_sigs) ix.prefetch_entry(c.addresses + 20 * (i + kAhead / 2));
+      }
       if (c.flags[i] != kCommit) continue;
-      const int32_t v = lookup_address(ix, c, i);
+      int32_t v = c.address_lens && c.address_lens[i] != 20 ? -1 : ix.at(c.addresses + 20 * i, i);
+      if (v == -2) {
+        hashed = true;
+        v = lookup_address(ix, c, i);
+      }
       if (v < 0) { pl.vof[i] = kNoValidator; continue; }
       if (seen.get(v) >= 0) {  // the loop returns the double-vote error here
         pl.dv_idx = (int32_t)i; pl.dv_val = v; pl.dv_first = seen.get(v);
@@ -722,7 +729,12 @@ static void find_aliases(const tmed_commit_request *reqs, size_t n, const Plans 
     part[t].swap(mine);
   });
   clk.lap("pairs");
-  for (auto &p : part) alias.insert(alias.end(), p.begin(), p.end());
+  std::vector<size_t> abase(part.size() + 1, 0);
+  for (size_t t = 0; t < part.size(); t++) abase[t + 1] = abase[t] + part[t].size();
+  alias.resize(abase.back());
+  parallel_ranges(part.size(), alias.size() >= 8192 ? (unsigned)part.size() : 1u, [&](size_t lo, size_t hi, unsigned) {
+    for (size_t t = lo; t < hi; t++) std::copy(part[t].begin(), part[t].end(), alias.begin() + abase[t]);
+  });
   clk.lap("concat");
   clk.emit("aliases", n, alias.size());
 }
@@ -935,9 +947,51 @@ struct Group {
   }
 };
 
+// The group of every run without its aliased candidates: run ranges built in parallel (a
+// light-client batch has ~90k aliases, one per Trusting vote), then joined.
+static void build_group(const Cands &c, Group &g) {
+  const size_t nr = c.runs.size();
+  const unsigned nt = c.alias.size() >= 8192 ? host_threads(c.size()) : 1u;
+  std::vector<Group> part(std::max(1u, std::min<unsigned>(nt, (unsigned)std::max<size_t>(nr, 1))));
+  parallel_ranges(nr, nt, [&](size_t lo, size_t hi, unsigned t) {
+    Group mine;  // (a header of its own: see seam_plan)
+    mine.start();
+    const auto a0 = std::lower_bound(c.alias.begin(), c.alias.end(), std::make_pair((uint32_t)c.off[lo], 0u));
+    size_t ap = (size_t)(a0 - c.alias.begin());
+    for (size_t r = lo; r < hi; r++) mine.add_run(c, (uint32_t)r, ap);
+    part[t].rix.swap(mine.rix);
+    part[t].ub.swap(mine.ub);
+    part[t].pos.swap(mine.pos);
+  });
+  size_t ns = 0;
+  std::vector<size_t> sbase(part.size() + 1, 0), pbase(part.size() + 1, 0);
+  for (size_t t = 0; t < part.size(); t++) {
+    const size_t k = part[t].rix.size();
+    sbase[t + 1] = sbase[t] + k;
+    pbase[t + 1] = pbase[t] + (k ? part[t].pos.back() : 0);
+    ns += k;
+  }
+  g.rix.resize(ns);
+  g.ub.resize(ns);
+  g.pos.resize(ns + 1);
+  g.pos[0] = 0;
+  parallel_ranges(part.size(), (unsigned)part.size(), [&](size_t lo, size_t hi, unsigned) {
+    for (size_t t = lo; t < hi; t++) {
+      const Group &p = part[t];
+      const size_t k = p.rix.size(), s = sbase[t], pb = pbase[t];
+      std::copy(p.rix.begin(), p.rix.end(), g.rix.begin() + s);
+      std::copy(p.ub.begin(), p.ub.end(), g.ub.begin() + s);
+      for (size_t j = 0; j < k; j++) g.pos[s + j + 1] = pb + p.pos[j + 1];
+    }
+  });
+}
+
 // The verified bits of the aliased candidates (scatter_bits wrote their targets).
 static void copy_aliases(const Cands &c, uint8_t *valid) {
-  for (const auto &a : c.alias) valid[a.first] = valid[a.second];
+  const size_t na = c.alias.size();
+  parallel_ranges(na, na >= 8192 ? host_threads(c.size()) : 1u, [&](size_t lo, size_t hi, unsigned) {
+    for (size_t k = lo; k < hi; k++) valid[c.alias[k].first] = valid[c.alias[k].second];
+  });
 }
 
 // For f(j, u0, u1, p0): the segment u0 .. u1 - 1 of group run j, staged from position p0, for the
@@ -1147,7 +1201,15 @@ static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, 
   std::vector<uint64_t> gkeys;
   std::vector<Group> groups;
   size_t ap = 0;
-  for (size_t r = 0; r < cands.runs.size(); r++) {
+  bool one_set = !cands.runs.empty();
+  for (size_t r = 1; r < cands.runs.size() && one_set; r++)
+    one_set = reqs[cands.runs[r].req].vals->keyset == reqs[cands.runs[0].req].vals->keyset;
+  if (one_set && !cands.alias.empty()) {
+    gkeys.push_back(reqs[cands.runs[0].req].vals->keyset);
+    groups.emplace_back();
+    build_group(cands, groups[0]);
+  }
+  for (size_t r = 0; r < cands.runs.size() && !(one_set && !cands.alias.empty()); r++) {
     const uint64_t ks = reqs[cands.runs[r].req].vals->keyset;
     size_t g = 0;
     while (g < gkeys.size() && gkeys[g] != ks) g++;
@@ -1540,15 +1602,20 @@ static int bs_finish(tmed_ctx *ctx, BsBatch &b, double ph[3]) {
     ph[1] += bs_us(t0, BsClock::now());
   }
   const auto t1 = BsClock::now();
+  PhaseClock clk;
   if (r == TMED_OK && aliased) {  // bits by staged segment -> by candidate
-    b.valid.assign(m, 0);
+    b.valid.resize(m);  // scatter_bits writes every staged candidate, copy_aliases the rest
     scatter_bits(w.rq + b.lo, b.cands, b.grp, b.bits.data(), b.valid.data());
+    clk.lap("scatter");
     copy_aliases(b.cands, b.valid.data());
+    clk.lap("aliases");
   }
   // the device bits are in candidate order: replay reads them directly (it applies the
   // signature-length rule itself)
   if (r == TMED_OK)
     r = seam_replay(w.rq + b.lo, b.n, w.out + b.lo, b.plans, b.device && !aliased ? b.bits.data() : b.valid.data());
+  clk.lap("replay");
+  if (b.device) clk.emit("blocksync finish", b.n, m);
   ph[2] += bs_us(t1, BsClock::now());
   b.n = 0;
   b.device = false;
@@ -1626,10 +1693,9 @@ static int bs_pump(tmed_ctx *ctx, BsStream &S, BsWindow &w, double ph[3], std::u
         if (b.cands.alias.empty()) {
           b.grp = Group();
         } else {
-          b.grp.start();
-          size_t ap = 0;
-          for (size_t r = 0; r < b.cands.runs.size(); r++) b.grp.add_run(b.cands, (uint32_t)r, ap);
+          build_group(b.cands, b.grp);
         }
+        clk.lap("group");
         rc = stage_group(ctx, rq, b.n, b.cands, b.grp, w.keyset, b.tmpl, (int)(idx % ns), b.st);
         // key-cached batches alternate between the two kernel lanes, so one batch's small kernels
         // (assembly, key order, prep, finish) run beside the other's main kernel

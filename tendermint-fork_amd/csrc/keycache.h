@@ -114,14 +114,17 @@ inline KcKey kc_key(const uint8_t *pubs, size_t n, const uint8_t *set_hash) {
 struct AddrIndex {
   const uint8_t *addrs = nullptr;  // the set's n x 20 address array
   std::vector<int32_t> vals;       // validator index, -1 = empty
-  size_t mask = 0;
+  size_t mask = 0, n = 0;
+  bool unique = true;              // no address occurs twice (then position i is its own first match)
   static size_t slot_of(const uint8_t *p) {  // addresses are SHA-256 truncations: 8 bytes mix well
     uint64_t a;
     memcpy(&a, p, 8);
     return (size_t)((a * 0x9E3779B97F4A7C15ull) >> 20);
   }
-  void build(const uint8_t *addresses, size_t n) {
+  void build(const uint8_t *addresses, size_t count) {
     addrs = addresses;
+    n = count;
+    unique = true;
     size_t cap = 16;
     while (cap < 2 * n + 1) cap <<= 1;
     mask = cap - 1;
@@ -131,7 +134,14 @@ struct AddrIndex {
       size_t h = slot_of(a) & mask;
       while (vals[h] >= 0 && memcmp(addrs + 20 * (size_t)vals[h], a, 20) != 0) h = (h + 1) & mask;
       if (vals[h] < 0) vals[h] = (int32_t)v;  // keep the first match
+      else unique = false;
     }
+  }
+  // validator i of the set when it has this address and addresses are unique (a commit's
+  // signature i is usually validator i of a neighbouring set: one sequential compare instead of
+  // two cold reads of the index), else -2 (ask find)
+  int32_t at(const uint8_t *addr, size_t i) const {
+    return unique && i < n && memcmp(addrs + 20 * i, addr, 20) == 0 ? (int32_t)i : -2;
   }
   // software prefetch for a lookup a few signatures ahead (the index and the set's address copy
   // are cold at a light-client batch's ~10k sets): the slot, then the address it holds

@@ -59,7 +59,14 @@ def scenarios(seed=1, count=60, chains=("test_chain_id", "Lalande21185", "")):
         tvs = vs
         if mode == 2 and rng.random() < 0.3:
             other, _ = make_valset([seed_of("oth%d" % k, i) for i in range(2)], [5, 5])
-            tvs = C.ValidatorSet(other.validators + vs.validators) if rng.random() < 0.5 else other
+            r2 = rng.random()
+            if r2 < 0.35:
+                tvs = C.ValidatorSet(other.validators + vs.validators)
+            elif r2 < 0.7 or n <= 2:
+                tvs = other
+            else:  # validator 2's address also at position 0: signature 2 matches its own
+                # position, but GetByAddress returns the first match (index 0)
+                tvs = C.ValidatorSet([vs.validators[2]] + vs.validators[1:])
         pv, pc = to_product(tvs, cm)
         yield mode, tvs, pv, chain, want_bid, want_h, cm, pc, num, den
 

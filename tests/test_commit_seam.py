@@ -46,6 +46,34 @@ def test_light_verifies_only_the_prefix():
     assert stats == [21, 30, 11]  # > 2/3 of 300 after 21 sigs; all 30; > 1/3 after 11
 
 
+def test_trusting_first_match_with_duplicate_addresses():
+    """GetByAddress returns the FIRST validator with the address (types/validator_set.go:270-277).
+    The planner tries signature i's own position first; in a set where validator 2's address also
+    sits at position 0, signature 2 must still map to validator 0 — a double vote when signature
+    0 carries the same address."""
+    from oracle import commit as C
+    from oracle.fixtures import make_block_id, make_commit, make_valset, resign, seed_of
+    from commit_cases import to_product
+    vs, seeds = make_valset([seed_of("dupa", i) for i in range(6)], [10, 20, 30, 40, 50, 60])
+    bid = make_block_id("dupa")
+    reqs, exp = [], []
+    for absent0 in (False, True):
+        flags = [C.FLAG_ABSENT if (absent0 and i == 0) else C.FLAG_COMMIT for i in range(6)]
+        cm = make_commit(vs, seeds, "c", 5, 0, bid, flags=flags)
+        if not absent0:  # signature 0 carries validator 2's address: both map to validator 0
+            cm.signatures[0].address = vs.validators[2].address
+            resign(cm, 0, seeds[2], "c")  # ... and validator 2's signature
+        tvs = C.ValidatorSet([vs.validators[2]] + vs.validators[1:])
+        for num, den in ((1, 3), (2, 3), (1, 1)):
+            exp.append(C.verify_commit_light_trusting(tvs, "c", cm, num, den))
+            pv, pc = to_product(tvs, cm)
+            reqs.append((T.MODE_LIGHT_TRUSTING, pv, "c", None, 0, pc, num, den))
+    got = T.verify_commits(None, reqs, verifier=oracle_verifier)
+    for q in range(len(reqs)):
+        assert same(got[q], exp[q]), (q, got[q], exp[q])
+    assert any(e is not None and "double vote" in str(e) for e in exp)
+
+
 def test_parallel_plan_and_replay_equal_serial():
     """Batches above 65,536 signatures are planned and replayed on host threads (and calls of
     more than 1,024 requests check them on host threads); the result of every request must equal
