@@ -242,7 +242,10 @@ struct tmed_ctx {
   tmed::DevBuf d_merkle_a, d_merkle_b, d_merkle_idx;  // Merkle level digests (ping-pong) + level indexes
   tmed::DevBuf d_korder;  // key-grouped order of a key-cached batch: counts / cursors + permutation
   tmed::DevBuf d_zip;     // ZIP-215 batch mode scratch (zip215.hip zip_bufs: points, digits, sort, buckets)
-  bool zip_dense = false; // ZIP-215: the last chunk's failures were dense (zip215.hip: probe the next one first)
+  bool zip_dense = false; // ZIP-215: the last large chunk had failures (zip215.hip: decide the next one singly first)
+  tmed::HostBuf h_zip;    // pinned word: failures counted in the last singly decided chunk
+  hipEvent_t zip_ev = nullptr;  // that count's copy (read at the next chunk)
+  bool zip_count_pending = false;
   std::unordered_map<uint64_t, tmed::Keyset> keysets;
   uint64_t next_keyset = 1;
   tmed::KeyCacheDev *kc = nullptr;  // key-set cache of the commit seam (keycache.hip), created at first use

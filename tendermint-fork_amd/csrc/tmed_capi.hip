@@ -223,6 +223,8 @@ void tmed_destroy(tmed_ctx *c) {
     b->release();
   c->h_kup.release();
   if (c->kup_ev) hipEventDestroy(c->kup_ev);
+  c->h_zip.release();
+  if (c->zip_ev) hipEventDestroy(c->zip_ev);
   if (c->trace_t0) hipEventDestroy(c->trace_t0);
   for (VoteSlot &v : c->vslot) {
     for (DevBuf *b : {&v.d_votes, &v.d_vmsg, &v.d_off, &v.d_out}) b->release();

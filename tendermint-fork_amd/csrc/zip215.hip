@@ -716,6 +716,25 @@ __global__ __launch_bounds__(64) void zip_final_kernel(ZipItems wins, const uint
   if (threadIdx.x == 0) flag[0] = (fe_iszero(X) && fe_equal(Y, Z) && !fe_iszero(Z)) ? 1u : 0u;
 }
 
+// Failed verdicts (zero bytes) among n: 16 per lane, a wave sum, one atomic per wave (~1 MB per
+// chunk, a few microseconds); the count steers the next chunk (zip215_verify_device).
+__global__ __launch_bounds__(256) void zip_count_fail_kernel(const uint8_t *__restrict__ out, uint32_t n,
+                                                             uint32_t *__restrict__ cnt) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x, i0 = 16 * t;
+  uint32_t c = 0;
+  if (i0 + 16 <= n && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+    const uint4 v = reinterpret_cast<const uint4 *>(out)[t];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 16; k++) c += ((w[k >> 2] >> (8 * (k & 3))) & 0xffu) == 0;
+  } else {
+    for (uint32_t i = i0; i < n && i < i0 + 16; i++) c += out[i] == 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, (unsigned)o);
+  if ((threadIdx.x & 63u) == 0 && c) atomicAdd(cnt, c);
+}
+
 }  // namespace tmed
 
 // ================================================================ host orchestration
@@ -872,35 +891,38 @@ int zip215_verify_device(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, co
     e = hipMemcpyAsync(z.seed, seed, 32, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return map_err(e);
     g_zip_stats[0]++;
-    // Failure-density cut-off: after a chunk whose failures were dense (both halves of a failing
-    // equation failed again), the next chunk first checks a kZipProbe-signature sample (~1 ms: the
-    // MSM's fixed cost); if the sample fails too the chunk is decided signature by signature with no
-    // full-chunk prep or MSM (C5's 1 % failures put ~40 in every sample).  A passing sample resumes
-    // batch verification.  The decision of every signature is the single-check one either way.
-    constexpr uint32_t kZipProbe = 4096;
-    if (c->zip_dense && N >= 4 * kZipProbe) {
-      const uint32_t pb = (kZipProbe + kThreadsPerBlock - 1) / kThreadsPerBlock;
-      e = launch_verify_prep(pub, sig, msgs, off, msg_slots, base, kZipProbe, c->d_prep, c->slab_slots, s);
+    // Failure cut-off: a chunk of at least kZipSinglyMin signatures whose predecessor had failures
+    // is decided signature by signature first, with no MSM: with even one invalid signature the
+    // equation, its halves and the bisection down to kZipMinGroup cost more than the single checks
+    // (~2x the full-chunk MSM, profiles/r04/s19).  The failures of such a chunk are counted on the
+    // device (zip_count_fail_kernel) and read when the next chunk starts: a chunk without any puts
+    // the next one back on the batch equation.  The decision of every signature is the
+    // single-check one either way.
+    constexpr uint32_t kZipSinglyMin = 1u << 14;
+    if (N >= kZipSinglyMin && c->zip_count_pending) {
+      e = hipEventSynchronize(c->zip_ev);
       if (e != hipSuccess) return map_err(e);
-      hipLaunchKernelGGL(zip_prep_r_kernel, dim3(pb), dim3(kThreadsPerBlock), 0, s, sig, base, kZipProbe, c->d_prep,
-                         c->slab_slots, z.seed, (uint64_t)base, z.pts, z.dig, z.cs, kZipMax, out);
-      e = zip_msm(c, z, kZipProbe, 0, kZipProbe, s);
+      c->zip_count_pending = false;
+      c->zip_dense = *static_cast<const uint32_t *>(c->h_zip.p) != 0;
+    }
+    if (c->zip_dense && N >= kZipSinglyMin) {
+      g_zip_stats[2]++;
+      g_zip_stats[3] += N;
+      const uint8_t *gm = msg_slots ? msgs + (size_t)base * kVoteSlot : msgs;
+      e = launch_verify(pub + 32 * (size_t)base, sig + 64 * (size_t)base, gm, off + base, N, out + base, c->d_slab,
+                        c->slab_slots, BTabs{c->d_b16, c->d_bcomb16, c->d_b26}, c->d_prep, c->d_fin, c->d_fin_pre, s,
+                        c->chunk, 6, msg_slots, nullptr, /*zip215=*/true);
+      if (e == hipSuccess && !c->zip_ev) e = hipEventCreateWithFlags(&c->zip_ev, hipEventDisableTiming);
+      if (e == hipSuccess) e = c->h_zip.ensure(4);
+      if (e == hipSuccess) e = hipMemsetAsync(z.flag, 0, 4, s);
+      if (e == hipSuccess)
+        hipLaunchKernelGGL(zip_count_fail_kernel, dim3((N + 4095) / 4096), dim3(256), 0, s, out + base, N, z.flag);
+      if (e == hipSuccess) e = hipGetLastError();
+      if (e == hipSuccess) e = hipMemcpyAsync(c->h_zip.p, z.flag, 4, hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipEventRecord(c->zip_ev, s);
       if (e != hipSuccess) return map_err(e);
-      bool ok = false;
-      int rc = zip_read_flag(c, z, s, &ok);
-      if (rc != TMED_OK) return rc;
-      g_zip_stats[1]++;
-      if (!ok) {  // still dense: the whole chunk singly
-        g_zip_stats[2]++;
-        g_zip_stats[3] += N;
-        const uint8_t *gm = msg_slots ? msgs + (size_t)base * kVoteSlot : msgs;
-        e = launch_verify(pub + 32 * (size_t)base, sig + 64 * (size_t)base, gm, off + base, N, out + base, c->d_slab,
-                          c->slab_slots, BTabs{c->d_b16, c->d_bcomb16, c->d_b26}, c->d_prep, c->d_fin, c->d_fin_pre, s,
-                          c->chunk, 6, msg_slots, nullptr, /*zip215=*/true);
-        if (e != hipSuccess) return map_err(e);
-        continue;
-      }
-      c->zip_dense = false;
+      c->zip_count_pending = true;
+      continue;
     }
     // k, S checks, decode of A (the generic throughput path's prep), then the ZIP-215 prep
     const uint32_t blocks = (N + kThreadsPerBlock - 1) / kThreadsPerBlock;
@@ -913,7 +935,6 @@ int zip215_verify_device(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, co
     // >= kZipMinGroup; the remaining failing groups are decided signature by signature.
     constexpr uint32_t kZipMinGroup = 1u << 14;
     std::vector<std::pair<uint32_t, uint32_t>> level{{0u, N}}, single;
-    bool chunk_dense = false;
     while (!level.empty()) {
       std::vector<std::pair<uint32_t, uint32_t>> failed;
       for (auto &g : level) {
@@ -926,7 +947,6 @@ int zip215_verify_device(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, co
         if (!ok) failed.push_back(g);
       }
       const bool dense = level.size() >= 2 && failed.size() * 2 > level.size();
-      chunk_dense = chunk_dense || dense;
       std::vector<std::pair<uint32_t, uint32_t>> next;
       for (auto &g : failed) {
         if (!dense && g.second >= 2 * kZipMinGroup) {
@@ -939,7 +959,7 @@ int zip215_verify_device(tmed_ctx *c, const uint8_t *pub, const uint8_t *sig, co
       }
       level.swap(next);
     }
-    c->zip_dense = chunk_dense;
+    if (N >= kZipSinglyMin) c->zip_dense = !single.empty();  // a failing group always ends in `single`
     for (auto &g : single) {  // the exact ZIP-215 single check on the group's signatures
       g_zip_stats[2]++;
       g_zip_stats[3] += g.second;

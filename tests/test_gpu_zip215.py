@@ -137,10 +137,10 @@ def test_c5_mix_vs_port(engine):
 
 
 def test_dense_failures_cut_off():
-    """Failure-density cut-off (zip215.hip kZipProbe): after a chunk whose failures were dense (the
-    C5 mix: the equation and both halves fail), the next chunk checks a 4,096-signature sample first
-    and, when it fails too, is decided singly without the full prep and MSM; a passing sample
-    resumes batch verification.  Decisions equal the port's ZIP-215 bits on every call."""
+    """Failure cut-off (zip215.hip kZipSinglyMin): after a chunk with failures (the C5 mix: the
+    equation and both halves fail), the next chunk is decided signature by signature with no MSM;
+    its failures are counted on the device and a chunk without any puts the next one back on the
+    batch equation.  Decisions equal the port's ZIP-215 bits on every call."""
     from conftest import engine_with_env
     from tmed import Engine
     from tmed.workload import c5_mix
@@ -156,11 +156,25 @@ def test_dense_failures_cut_off():
             stats.append(Engine.zip215_stats())
             assert int((out != exp).sum()) == 0
         assert stats[0]["equations"] == 3 and stats[0]["single_sigs"] == 70_000, stats
-        assert stats[1]["equations"] == 1 and stats[1]["single_sigs"] == 70_000, stats
-        out = eng.verify_zip215_arrays(good_p, good_s, msgs, offs)  # the sample passes: batch mode again
+        assert stats[1]["equations"] == 0 and stats[1]["single_sigs"] == 70_000, stats
+        out = eng.verify_zip215_arrays(good_p, good_s, msgs, offs)  # singly (its predecessor failed) ...
         st = Engine.zip215_stats()
-        assert out.all() and st["equations"] == 2 and st["single_sigs"] == 0, st
-        eng.verify_zip215_arrays(good_p, good_s, msgs, offs)
-        assert Engine.zip215_stats()["equations"] == 1
+        assert out.all() and st["equations"] == 0 and st["single_sigs"] == 70_000, st
+        out = eng.verify_zip215_arrays(good_p, good_s, msgs, offs)  # ... and no failure: batch mode again
+        st = Engine.zip215_stats()
+        assert out.all() and st["equations"] == 1 and st["single_sigs"] == 0, st
+        # one bad signature: bisection, then the next chunk singly, whose count (one) keeps it so
+        one = good_s.copy()
+        one[1234, 7] ^= 0x40
+        exp1 = np.ones(70_000, np.uint8)
+        exp1[1234] = 0
+        for want_eq in (None, 0, 0):
+            out = eng.verify_zip215_arrays(good_p, one, msgs, offs)
+            st = Engine.zip215_stats()
+            assert int((out != exp1).sum()) == 0
+            if want_eq is None:
+                assert st["equations"] >= 3 and st["single_sigs"] < 70_000, st
+            else:
+                assert st["equations"] == want_eq and st["single_sigs"] == 70_000, st
     finally:
         eng.close()
