@@ -1246,13 +1246,32 @@ static const tmed_commit_request *keycache_resolve(tmed_ctx *ctx, const tmed_com
     std::vector<size_t> thits(std::max(1u, nt), 0), tsigs(std::max(1u, nt), 0);
     parallel_ranges(sets.size(), nt, [&](size_t lo, size_t hi, unsigned t) {
       size_t h = 0, g = 0;  // this worker's hits and their signatures (stored once: shared lines)
-      for (size_t s = lo; s < hi; s++) {
+      for (size_t s = lo; s < hi; s++) {  // keys and finds first: the compares below prefetch ahead
         SetRef &sr = sets[s];
         const tmed_valset &v = *sr.v;
         sr.skip = v.keyset || v.n == 0 || !v.pubkeys;
         if (sr.skip) continue;
         sr.key = tmed::kc_key(v.pubkeys, v.n, v.set_hash);
         sr.e = tmed::keycache_find(ctx, sr.key);
+      }
+      // the byte compares (~5.6 KB per set from the caller and as many from the entry, both cold):
+      // the next set's two arrays are prefetched while this one is compared
+      auto prefetch_set = [&](size_t s) {
+        if (s >= hi || sets[s].skip || !sets[s].e) return;
+        const tmed_valset &v = *sets[s].v;
+        const uint8_t *a = v.pubkeys, *b = sets[s].e->pubs.data();
+        const size_t nb = std::min(32 * v.n, sets[s].e->pubs.size());
+        for (size_t o = 0; o < nb; o += 64) {
+          __builtin_prefetch(a + o, 0, 0);
+          __builtin_prefetch(b + o, 0, 0);
+        }
+      };
+      prefetch_set(lo);
+      for (size_t s = lo; s < hi; s++) {
+        SetRef &sr = sets[s];
+        prefetch_set(s + 1);
+        if (sr.skip) continue;
+        const tmed_valset &v = *sr.v;
         sr.hit = sr.e && tmed::kc_same_keys(*sr.e, v.pubkeys, v.n);
         if (sr.hit) {
           const_cast<tmed::KcSet *>(sr.e)->touch(tick);

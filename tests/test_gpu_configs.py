@@ -170,6 +170,41 @@ def test_c3_light_client_changing_sets(engine, monkeypatch, keyed, pipelined):
             engine.keyset_free(ks)
 
 
+def test_c3_many_sets_through_the_cache(engine):
+    """A light-client call of 4,100 requests on 2,052 validator sets (8 validators, one key changing
+    per height) passed WITHOUT key-set handles: the key-set cache resolves them (above 4,096 requests
+    the distinct sets are found by the host workers, commit.hip keycache_resolve).  Twice — the
+    first call generic (cold cache), the second on the cached key sets — both equal to the oracle
+    loops; bad signatures in three commits."""
+    nv, H, gap = 8, 2050, 2
+    seeds = seeds_from_tag(b"tmed-c3-many", 0, H + gap + nv)
+    pubs = pubkeys_of(engine, seeds)
+    sets, specs = {}, []
+    for h in range(H + gap):
+        vals, order = make_valset(pubs[h:h + nv], [10] * nv)
+        sets[h] = vals
+        addrs = np.array([np.frombuffer(v.address, np.uint8) for v in vals.validators])
+        specs.append((seeds[h:h + nv][order], addrs, h + 1, 0, _bid(b"c3m-%d" % (h + 1)), T2023 + h, None))
+    commits = dict(zip(range(H + gap), sign_commits(engine, CHAIN, specs)))
+    for h, i in ((7, 1), (1000, 5), (2049, 0)):
+        _corrupt(commits[h], i)
+    reqs, exp, osets = [], [], {h: _ovals(v) for h, v in sets.items()}
+    for h in range(H):
+        u = h + gap
+        pc = commits[u]
+        oc = _ocommit(pc)
+        for req, ovs in (((T.MODE_LIGHT_TRUSTING, sets[h], CHAIN, None, 0, pc, 1, 3), osets[h]),
+                         ((T.MODE_LIGHT, sets[u], CHAIN, pc.block_id, u + 1, pc, 0, 0), osets[u])):
+            reqs.append(req)
+            exp.append(_oracle(req, ovs, oc))
+    assert len(reqs) > 4096
+    for _ in range(2):
+        got = T.verify_commits(engine, reqs)
+        bad = [(q, str(got[q]), str(exp[q])) for q in range(len(reqs)) if not _same(got[q], exp[q])]
+        assert not bad, bad[:4]
+    assert sum(e is not None for e in exp) >= 2
+
+
 def test_c4_10k_validator_light_window(engine):
     """C4 shape: a blocksync window of 6 blocks x 10,000 validators (equal power 10: needed 66,666,
     crossed by the 6,667th signature, index 6,666), VerifyCommitLight per block through the pipelined
