@@ -942,7 +942,8 @@ __device__ void comb_sign_one(uint32_t sg[16], uint32_t pb[8], const uint32_t se
 }
 
 #ifndef TMED_KS_PREP_WAVES
-#define TMED_KS_PREP_WAVES 3  // 168 VGPRs, 27 spilled: keyed prep 0.445 -> 0.426 ms per 2^20 (A/B)
+#define TMED_KS_PREP_WAVES 4  // 128 VGPRs, 4 spilled: keyed prep 0.347 -> 0.337 ms per 2^20 against 3 waves
+                              // (130 VGPRs), three alternating runs each (profiles/r04/s22)
 #endif
 __global__ __launch_bounds__(kThreadsPerBlock, TMED_KS_PREP_WAVES) void verify_keyset_prep_kernel(
     const uint32_t *__restrict__ val_idx, uint32_t nkeys, const uint8_t *__restrict__ key_pub,
