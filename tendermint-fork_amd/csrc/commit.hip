@@ -487,7 +487,26 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
     std::vector<Run> mine;
     mine.swap(part[t]);
     int rc = TMED_OK;
-    for (size_t q = lo; q < hi && rc == TMED_OK; q++) rc = plan_request(reqs, q, out[q], plans[q], mine, c, addr);
+    // the next request's arrays are cold (a light-client batch touches ~5 KB of flags, powers and
+    // addresses per request, each request in arrays of its own): their first lines are fetched
+    // while this request is planned
+    auto prefetch_req = [&](size_t q) {
+      if (q >= hi) return;
+      const tmed_commit_request &r = reqs[q];
+      if (!r.commit || !r.vals) return;
+      const tmed_commit &cm = *r.commit;
+      const size_t ns = std::min<size_t>(cm.n_sigs, 128);
+      for (size_t o = 0; o < ns; o += 64) __builtin_prefetch(cm.flags + o, 0, 0);
+      if (r.vals->powers)
+        for (size_t o = 0; o < 8 * ns; o += 64) __builtin_prefetch((const uint8_t *)r.vals->powers + o, 0, 0);
+      if (r.mode == TMED_MODE_LIGHT_TRUSTING && cm.addresses)
+        for (size_t o = 0; o < 20 * ns; o += 64) __builtin_prefetch(cm.addresses + o, 0, 0);
+    };
+    prefetch_req(lo);
+    for (size_t q = lo; q < hi && rc == TMED_OK; q++) {
+      prefetch_req(q + 1);
+      rc = plan_request(reqs, q, out[q], plans[q], mine, c, addr);
+    }
     mine.swap(part[t]);
     rcs[t] = rc;
     pc[t] = c;
