@@ -977,11 +977,7 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
   const uint32_t nkeys = keyed ? (uint32_t)st.ks->n : 0u;
   // Signature runs in pinned caller memory go to the device by their own DMA (votes_enqueue)
   // instead of through the staging area: only batches copied on the copy stream.
-  static const bool direct_on = [] {
-    const char *v = getenv("TMED_DIRECT_DMA");
-    return !(v && v[0] == '0');
-  }();
-  bool direct = direct_on && st.total >= tmed::kVoteCopyStreamMin;
+  bool direct = st.total >= tmed::kVoteCopyStreamMin;
   // pinned-memory lookups once per request (a registry lookup per run took a global lock per
   // vote where runs are single votes: Trusting candidates, C3)
   // (only requests with a run long enough for its own DMA: a light-client batch has none)

@@ -819,31 +819,6 @@ hipError_t zip_msm(tmed_ctx *c, const ZipBufs &z, uint32_t N, uint32_t lo, uint3
   hipLaunchKernelGGL(zip_sort_hist_kernel<1>, sg, dim3(kSortWaves * 64), 0, s, a);
   hipLaunchKernelGGL(zip_sort_scan_kernel, dim3(kZipWin), dim3(1024), 0, s, a.hist, a.tiles);
   hipLaunchKernelGGL(zip_sort_scatter_kernel<1>, sc, dim3(64), 0, s, a);
-  if (getenv("TMED_ZIP_DEBUG")) {  // diagnostics: the sorted windows against the digits
-    hipStreamSynchronize(s);
-    std::vector<int16_t> dg((size_t)kZipWin * 2 * N);
-    hipMemcpy(dg.data(), z.dig, dg.size() * 2, hipMemcpyDeviceToHost);
-    for (int w = 0; w < kZipWin; w++) {
-      const uint32_t M = (w < kZipZWin ? 2u : 1u) * cnt;
-      std::vector<uint16_t> kk(M);
-      std::vector<uint32_t> vv(M);
-      hipMemcpy(kk.data(), z.keys[1] + (size_t)w * z.cap, M * 2, hipMemcpyDeviceToHost);
-      hipMemcpy(vv.data(), z.vals[1] + (size_t)w * z.cap, M * 4, hipMemcpyDeviceToHost);
-      size_t unsorted = 0, badkey = 0, dup = 0;
-      std::vector<uint8_t> seen(2 * (size_t)N, 0);
-      for (uint32_t e = 0; e < M; e++) {
-        if (e && kk[e] < kk[e - 1]) unsorted++;
-        const uint32_t j = vv[e] & 0x7fffffffu;
-        if (j >= 2 * N) { badkey++; continue; }
-        if (seen[j]++) dup++;
-        const int d = dg[(size_t)w * 2 * N + j];
-        if ((uint32_t)(d < 0 ? -d : d) != kk[e] || ((vv[e] >> 31) != 0) != (d < 0)) badkey++;
-      }
-      if (unsorted || badkey || dup)
-        fprintf(stderr, "[zip] lo=%u cnt=%u window %d: M=%u unsorted=%zu badkey=%zu dup=%zu\n", lo, cnt, w, M,
-                unsorted, badkey, dup);
-    }
-  }
   uint32_t n_it[4] = {kZipItemsMax, (kZipItemsMax + 63) / 64, ((kZipItemsMax + 63) / 64 + 63) / 64, 1};
   ZipItems it[4];
   for (int L = 0; L < 4; L++) it[L] = ZipItems{z.items[L], n_it[L]};
