@@ -95,10 +95,10 @@ struct Run {
 struct Cands {
   std::vector<Run> runs;
   std::vector<size_t> off;  // runs.size() + 1 candidate offsets
-  // (candidate, the candidate whose bit it takes), ascending: see find_aliases
+  // (candidate, the candidate whose bit it takes), ascending: see pair_request
   std::vector<std::pair<uint32_t, uint32_t>> alias;
   // request -> the request whose device template its candidates use (empty: its own); a
-  // Trusting request shares the template of the Light request of the same commit (find_aliases)
+  // Trusting request shares the template of the Light request of the same commit (pair_request)
   std::vector<uint32_t> tmpl_of;
   size_t size() const { return off.empty() ? 0 : off.back(); }
   uint32_t tmpl_row(uint32_t q) const { return tmpl_of.empty() ? q : tmpl_of[q]; }
@@ -151,14 +151,50 @@ struct RawBuf {
   }
 };
 
-// The plans of one seam call; vof of every Trusting request lives in one flat array.  The
-// per-thread run parts are kept between calls (blocksync plans batch after batch), so their pages
-// are touched once.
+// The run segments of one device group (one key set) and their staging positions: segment j is
+// run rix[j]'s candidates from ub[j] on, staged at pos[j] .. pos[j + 1) (rix empty: every run
+// whole, in order; ub empty: segments start at their run's first candidate).
+struct Group {
+  std::vector<uint32_t> rix, ub;
+  std::vector<size_t> pos;
+  size_t size(const Cands &c) const { return rix.empty() ? c.size() : pos.back(); }
+  uint32_t run(const Cands &c, size_t j) const { (void)c; return rix.empty() ? (uint32_t)j : rix[j]; }
+  uint32_t base(size_t j) const { return ub.empty() ? 0u : ub[j]; }
+  size_t nruns(const Cands &c) const { return rix.empty() ? c.runs.size() : rix.size(); }
+  const size_t *positions(const Cands &c) const { return rix.empty() ? c.off.data() : pos.data(); }
+  void start() {
+    rix.clear();
+    ub.clear();
+    pos.assign(1, 0);
+  }
+  // run r without its aliased candidates (al[ap..] ascending; ap advances past run r's)
+  void add_run(const Cands &c, uint32_t r, const std::vector<std::pair<uint32_t, uint32_t>> &al, size_t &ap) {
+    const size_t c0 = c.off[r], c1 = c.off[r + 1];
+    size_t k = c0;
+    auto seg = [&](size_t a, size_t b) {
+      if (a >= b) return;
+      rix.push_back(r);
+      ub.push_back((uint32_t)(a - c0));
+      pos.push_back(pos.back() + (b - a));
+    };
+    for (; ap < al.size() && al[ap].first < c1; ap++) {
+      seg(k, al[ap].first);
+      k = (size_t)al[ap].first + 1;
+    }
+    seg(k, c1);
+  }
+};
+
+// The plans of one seam call and the planning workers' parts, kept between calls (blocksync
+// plans batch after batch), so their pages are touched once.
 struct Plans {
   std::vector<Plan> v;
-  RawBuf<int32_t> bits;
+  std::vector<RawBuf<int32_t>> tbits;  // per planning worker: its Trusting requests' vof arrays
   std::vector<std::vector<Run>> parts;
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> aparts;  // per worker: its aliases
+  std::vector<Group> gparts;                                       // per worker: its group segments
 };
+
 
 // Per-thread "seen" marks of the Trusting loops (first index of each validator), reset in
 // O(1) per request by an epoch stamp instead of a fresh n-sized vector.
@@ -428,66 +464,54 @@ static size_t total_sigs(const tmed_commit_request *reqs, size_t n) {
   return s;
 }
 
-static void find_aliases(const tmed_commit_request *reqs, size_t n, const Plans &ps, Cands &cands);
+static void pair_request(const tmed_commit_request *reqs, const std::vector<Plan> &plans, Cands &cands, size_t q,
+                         size_t lo, size_t hi, std::vector<std::pair<uint32_t, uint32_t>> &mine);
 
 // Candidates of requests [0, n) in request order (identical to a serial plan).
 static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, Plans &ps, Cands &cands,
-                     const KcCall *kc = nullptr) {
+                     const KcCall *kc = nullptr, Group *grp = nullptr) {
   PhaseClock clk;
   std::vector<Plan> &plans = ps.v;
   plans.assign(n, Plan());
   cands.clear();
-  // every request checked, and the signature count of each Trusting request (its vof), in parallel
-  // (the requests' sets and commits are cold in the cache)
-  // (the calling thread's buffer, taken by reference: a thread_local named inside the worker
-  // lambda would be each worker's own)
-  thread_local std::vector<size_t> tn_buf;
-  std::vector<size_t> &tn = tn_buf;
-  tn.resize(n);
-  std::atomic<bool> bad{false};
-  std::atomic<size_t> sigs_all{0};
-  parallel_ranges(n, n >= 256 ? host_threads(n * 64) : 1, [&](size_t lo, size_t hi, unsigned) {
-    size_t sg = 0;
-    for (size_t q = lo; q < hi; q++) {
-      if (q + 4 < hi) {  // the structs behind the requests are cold: fetched a few requests ahead
-        __builtin_prefetch(reqs[q + 4].commit, 0, 0);
-        __builtin_prefetch(reqs[q + 4].vals, 0, 0);
-      }
-      tn[q] = 0;
-      if (check_request(reqs[q]) != TMED_OK) {
-        bad = true;
-        continue;
-      }
-      sg += reqs[q].commit->n_sigs;
-      if (reqs[q].mode == TMED_MODE_LIGHT_TRUSTING) tn[q] = reqs[q].commit->n_sigs;
-    }
-    sigs_all += sg;
-  });
-  if (bad) return TMED_EINVAL;
-  size_t nbits = 0;
-  for (size_t q = 0; q < n; q++) nbits += tn[q];
-  int32_t *bits = ps.bits.ensure(std::max<size_t>(nbits, 1));
-  nbits = 0;
-  for (size_t q = 0; q < n; q++)
-    if (tn[q]) {
-      plans[q].vof = bits + nbits;
-      nbits += tn[q];
-    }
-  clk.lap("check");
-  const unsigned nt = host_threads(sigs_all.load());
+  // worker count: calls of 1,024+ requests fan out at once; smaller ones by their signature count
+  // (a blocksync batch: 128 requests of 10k signatures).  Each worker checks its requests as it
+  // plans them (plan_request) and keeps the vof arrays of its Trusting requests in a buffer of its
+  // own, so no separate pass over the (cold) requests runs first.
+  size_t sigs_est = 0;
+  if (n < 1024)
+    for (size_t q = 0; q < n; q++) sigs_est += reqs[q].commit ? reqs[q].commit->n_sigs : 0;
+  const unsigned nt = n >= 1024 ? host_threads(~(size_t)0) : host_threads(sigs_est);
   const unsigned np = std::max(1u, nt);
   if (ps.parts.size() < np) ps.parts.resize(np);
+  if (ps.tbits.size() < np) ps.tbits.resize(np);
   std::vector<std::vector<Run>> &part = ps.parts;
   std::vector<size_t> lo_of(np, 0), hi_of(np, 0), pc(np, 0);
   std::vector<int> rcs(np, TMED_OK);
-  // (each worker plans into a vector header on its own stack and a local status: the per-thread
-  // slots of part / rcs share cache lines, and a push_back per Trusting candidate into them
-  // bounced those lines between the workers)
+  std::vector<uint8_t> trusting(np, 0);
   auto plan_range = [&](size_t lo, size_t hi, unsigned t) {
     lo_of[t] = lo; hi_of[t] = hi;
     AddrScratch addr;
     addr.kc = kc;
     size_t c = 0;
+    {  // the vof arrays of this range's Trusting requests
+      size_t nb = 0;
+      for (size_t q = lo; q < hi; q++) {
+        if (q + 4 < hi) {  // the structs behind the requests are cold: fetched a few requests ahead
+          __builtin_prefetch(reqs[q + 4].commit, 0, 0);
+          __builtin_prefetch(reqs[q + 4].vals, 0, 0);
+        }
+        if (reqs[q].mode == TMED_MODE_LIGHT_TRUSTING && reqs[q].commit) nb += reqs[q].commit->n_sigs;
+      }
+      int32_t *bits = ps.tbits[t].ensure(std::max<size_t>(nb, 1));
+      nb = 0;
+      for (size_t q = lo; q < hi; q++)
+        if (reqs[q].mode == TMED_MODE_LIGHT_TRUSTING && reqs[q].commit) {
+          plans[q].vof = bits + nb;
+          nb += reqs[q].commit->n_sigs;
+        }
+      trusting[t] = nb != 0;
+    }
     std::vector<Run> mine;
     mine.swap(part[t]);
     int rc = TMED_OK;
@@ -521,7 +545,10 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
   for (int rc : rcs)
     if (rc != TMED_OK) return rc;
   clk.lap("plan_requests");
-  // merge: the parts' runs in thread order (= request order), candidate offsets made global
+  // merge: the parts' runs in thread order (= request order), candidate offsets made global; in the
+  // same pass each worker pairs its Trusting requests with their Light partners (pair_request)
+  // and, for a device batch (grp), lays out its runs' staging segments without the aliased
+  // candidates; one more pass joins the workers' aliases and segments
   std::vector<size_t> rbase(np + 1, 0), cbase(np + 1, 0);
   for (unsigned t = 0; t < np; t++) {
     rbase[t + 1] = rbase[t] + part[t].size();
@@ -530,6 +557,15 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
   const size_t nr = rbase[np], cb = cbase[np];
   cands.runs.resize(nr);
   cands.off.resize(nr + 1);
+  cands.off[nr] = cb;
+  bool any_trusting = false;
+  for (unsigned t = 0; t < np; t++) any_trusting = any_trusting || trusting[t];
+  const bool pair = any_trusting && cb <= 0xffffffffu;
+  if (pair) {
+    cands.tmpl_of.resize(n);
+    if (ps.aparts.size() < np) ps.aparts.resize(np);
+    if (grp && ps.gparts.size() < np) ps.gparts.resize(np);
+  }
   auto merge_part = [&](size_t t) {
     size_t c = cbase[t];
     Run *dst = cands.runs.data() + rbase[t];
@@ -544,6 +580,25 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
       plans[q].run_lo += rbase[t];
       plans[q].run_hi += rbase[t];
     }
+    if (!pair) return;
+    for (size_t q = lo_of[t]; q < hi_of[t]; q++) cands.tmpl_of[q] = (uint32_t)q;
+    std::vector<std::pair<uint32_t, uint32_t>> mine;  // (a header of its own: see seam_plan)
+    mine.swap(ps.aparts[t]);
+    mine.clear();
+    for (size_t q = lo_of[t]; q < hi_of[t]; q++) pair_request(reqs, plans, cands, q, lo_of[t], hi_of[t], mine);
+    if (grp) {
+      Group g;
+      g.rix.swap(ps.gparts[t].rix);
+      g.ub.swap(ps.gparts[t].ub);
+      g.pos.swap(ps.gparts[t].pos);
+      g.start();
+      size_t ap = 0;
+      for (size_t r = rbase[t]; r < rbase[t + 1]; r++) g.add_run(cands, (uint32_t)r, mine, ap);
+      g.rix.swap(ps.gparts[t].rix);
+      g.ub.swap(ps.gparts[t].ub);
+      g.pos.swap(ps.gparts[t].pos);
+    }
+    mine.swap(ps.aparts[t]);
   };
   if (nt <= 1) {
     for (unsigned t = 0; t < np; t++) merge_part(t);
@@ -552,9 +607,45 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
       for (size_t t = lo; t < hi; t++) merge_part(t);
     });
   }
-  cands.off[nr] = cb;
   clk.lap("merge");
-  if (nbits && cb <= 0xffffffffu) find_aliases(reqs, n, ps, cands);
+  cands.alias.clear();
+  if (grp) *grp = Group();  // no aliases: every run whole, in order
+  if (pair) {
+    std::vector<size_t> abase(np + 1, 0), sbase(np + 1, 0), pbase(np + 1, 0);
+    for (unsigned t = 0; t < np; t++) {
+      abase[t + 1] = abase[t] + ps.aparts[t].size();
+      if (grp) {
+        const Group &g = ps.gparts[t];
+        sbase[t + 1] = sbase[t] + g.rix.size();
+        pbase[t + 1] = pbase[t] + (g.rix.empty() ? 0 : g.pos.back());
+      }
+    }
+    if (abase[np]) {
+      cands.alias.resize(abase[np]);
+      if (grp) {
+        grp->rix.resize(sbase[np]);
+        grp->ub.resize(sbase[np]);
+        grp->pos.resize(sbase[np] + 1);
+        grp->pos[0] = 0;
+      }
+      auto join = [&](size_t t) {
+        std::copy(ps.aparts[t].begin(), ps.aparts[t].end(), cands.alias.begin() + abase[t]);
+        if (!grp) return;
+        const Group &g = ps.gparts[t];
+        const size_t k = g.rix.size(), s0 = sbase[t], p0 = pbase[t];
+        std::copy(g.rix.begin(), g.rix.end(), grp->rix.begin() + s0);
+        std::copy(g.ub.begin(), g.ub.end(), grp->ub.begin() + s0);
+        for (size_t j = 0; j < k; j++) grp->pos[s0 + j + 1] = p0 + g.pos[j + 1];
+      };
+      if (nt <= 1 || abase[np] < 8192) {
+        for (unsigned t = 0; t < np; t++) join(t);
+      } else {
+        parallel_ranges(np, np, [&](size_t lo, size_t hi, unsigned) {
+          for (size_t t = lo; t < hi; t++) join(t);
+        });
+      }
+    }
+  }
   clk.lap("aliases");
   clk.emit("plan", n, cb);
   return TMED_OK;
@@ -587,64 +678,46 @@ static bool same_commit(const tmed_commit &a, const tmed_commit &b) {
          block_id_equal(a.block_id, b.block_id);
 }
 
-static void find_aliases(const tmed_commit_request *reqs, size_t n, const Plans &ps, Cands &cands) {
-  PhaseClock clk;
-  std::vector<std::pair<uint32_t, uint32_t>> &alias = cands.alias;
-  alias.clear();
-  cands.tmpl_of.resize(n);
-  for (size_t q = 0; q < n; q++) cands.tmpl_of[q] = (uint32_t)q;
-  const std::vector<Plan> &plans = ps.v;
-  const unsigned nt = host_threads(cands.size());
-  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> part(std::max(1u, nt));
-  parallel_ranges(n, nt, [&](size_t lo, size_t hi, unsigned t) {
-    std::vector<std::pair<uint32_t, uint32_t>> mine;  // (a header of its own: see seam_plan)
-    for (size_t q = lo; q < hi; q++) {
-      const tmed_commit_request &r = reqs[q];
-      const Plan &pl = plans[q];
-      if (r.mode != TMED_MODE_LIGHT_TRUSTING || pl.decided || pl.ncand == 0) continue;
-      for (size_t pq : {q + 1, q - 1}) {  // the pair is adjacent in the light client's batches
-        if (pq >= n) continue;
-        const tmed_commit_request &o = reqs[pq];
-        const Plan &po = plans[pq];
-        if (o.mode == TMED_MODE_LIGHT_TRUSTING || !same_commit(*o.commit, *r.commit) || po.decided || po.ncand == 0 ||
-            o.chain_id_len != r.chain_id_len || memcmp(o.chain_id, r.chain_id, r.chain_id_len) != 0)
-          continue;
-        cands.tmpl_of[q] = (uint32_t)pq;  // one commit, one chain ID: the same sign-bytes template
-        // the two sets' key identities (pool indexes, or the keys) are cold: fetch them at once
-        // instead of one dependent miss per candidate
-        for (const tmed_valset *vs : {r.vals, o.vals}) {
-          const uint8_t *kp = vs->keyset ? (const uint8_t *)vs->keyset_index : vs->pubkeys;
-          const size_t kb = vs->keyset ? 4 * vs->n : 32 * vs->n;
-          if (kp)
-            for (size_t b = 0; b < kb; b += 64) __builtin_prefetch(kp + b);
-        }
-        // o's candidates are its qualifying signatures in order, as runs sorted by signature
-        size_t ro = po.run_lo;
-        for (size_t ri = pl.run_lo; ri < pl.run_hi; ri++) {
-          const Run &run = cands.runs[ri];
-          for (uint32_t u = 0; u < run.len; u++) {
-            const int32_t i = run.sig + (int32_t)u;
-            while (ro < po.run_hi && cands.runs[ro].sig + (int32_t)cands.runs[ro].len <= i) ro++;
-            if (ro == po.run_hi) break;
-            const Run &orun = cands.runs[ro];
-            if (i < orun.sig || !same_key(*r.vals, run.val + (int32_t)u, *o.vals, orun.val + (i - orun.sig))) continue;
-            mine.push_back({(uint32_t)(cands.off[ri] + u), (uint32_t)(cands.off[ro] + (size_t)(i - orun.sig))});
-          }
-        }
-        break;
+// The aliases of Trusting request q (its partner looked for at q + 1, q - 1 inside [lo, hi): the
+// requests one planning worker merged; a pair split across two workers' ranges is not aliased,
+// which costs a duplicate verification and nothing else) into `mine`, in candidate order;
+// tmpl_of[q] set to the partner.  Runs and offsets of [lo, hi) must be global already.
+static void pair_request(const tmed_commit_request *reqs, const std::vector<Plan> &plans, Cands &cands, size_t q,
+                         size_t lo, size_t hi, std::vector<std::pair<uint32_t, uint32_t>> &mine) {
+  const tmed_commit_request &r = reqs[q];
+  const Plan &pl = plans[q];
+  if (r.mode != TMED_MODE_LIGHT_TRUSTING || pl.decided || pl.ncand == 0) return;
+  for (size_t pq : {q + 1, q - 1}) {  // the pair is adjacent in the light client's batches
+    if (pq < lo || pq >= hi) continue;
+    const tmed_commit_request &o = reqs[pq];
+    const Plan &po = plans[pq];
+    if (o.mode == TMED_MODE_LIGHT_TRUSTING || !same_commit(*o.commit, *r.commit) || po.decided || po.ncand == 0 ||
+        o.chain_id_len != r.chain_id_len || memcmp(o.chain_id, r.chain_id, r.chain_id_len) != 0)
+      continue;
+    cands.tmpl_of[q] = (uint32_t)pq;  // one commit, one chain ID: the same sign-bytes template
+    // the two sets' key identities (pool indexes, or the keys) are cold: fetch them at once
+    // instead of one dependent miss per candidate
+    for (const tmed_valset *vs : {r.vals, o.vals}) {
+      const uint8_t *kp = vs->keyset ? (const uint8_t *)vs->keyset_index : vs->pubkeys;
+      const size_t kb = vs->keyset ? 4 * vs->n : 32 * vs->n;
+      if (kp)
+        for (size_t b = 0; b < kb; b += 64) __builtin_prefetch(kp + b);
+    }
+    // o's candidates are its qualifying signatures in order, as runs sorted by signature
+    size_t ro = po.run_lo;
+    for (size_t ri = pl.run_lo; ri < pl.run_hi; ri++) {
+      const Run &run = cands.runs[ri];
+      for (uint32_t u = 0; u < run.len; u++) {
+        const int32_t i = run.sig + (int32_t)u;
+        while (ro < po.run_hi && cands.runs[ro].sig + (int32_t)cands.runs[ro].len <= i) ro++;
+        if (ro == po.run_hi) break;
+        const Run &orun = cands.runs[ro];
+        if (i < orun.sig || !same_key(*r.vals, run.val + (int32_t)u, *o.vals, orun.val + (i - orun.sig))) continue;
+        mine.push_back({(uint32_t)(cands.off[ri] + u), (uint32_t)(cands.off[ro] + (size_t)(i - orun.sig))});
       }
     }
-    part[t].swap(mine);
-  });
-  clk.lap("pairs");
-  std::vector<size_t> abase(part.size() + 1, 0);
-  for (size_t t = 0; t < part.size(); t++) abase[t + 1] = abase[t] + part[t].size();
-  alias.resize(abase.back());
-  parallel_ranges(part.size(), alias.size() >= 8192 ? (unsigned)part.size() : 1u, [&](size_t lo, size_t hi, unsigned) {
-    for (size_t t = lo; t < hi; t++) std::copy(part[t].begin(), part[t].end(), alias.begin() + abase[t]);
-  });
-  clk.lap("concat");
-  clk.emit("aliases", n, alias.size());
+    return;
+  }
 }
 
 // ---- replay of every reference loop over the validity bits (parallel over requests) ----
@@ -821,40 +894,6 @@ static int ctx_verify_host_msgs(tmed_ctx *ctx, const tmed_commit_request *reqs, 
   return TMED_OK;
 }
 
-// The run segments of one device group (one key set) and their staging positions: segment j is
-// run rix[j]'s candidates from ub[j] on, staged at pos[j] .. pos[j + 1) (rix empty: every run
-// whole, in order; ub empty: segments start at their run's first candidate).
-struct Group {
-  std::vector<uint32_t> rix, ub;
-  std::vector<size_t> pos;
-  size_t size(const Cands &c) const { return rix.empty() ? c.size() : pos.back(); }
-  uint32_t run(const Cands &c, size_t j) const { (void)c; return rix.empty() ? (uint32_t)j : rix[j]; }
-  uint32_t base(size_t j) const { return ub.empty() ? 0u : ub[j]; }
-  size_t nruns(const Cands &c) const { return rix.empty() ? c.runs.size() : rix.size(); }
-  const size_t *positions(const Cands &c) const { return rix.empty() ? c.off.data() : pos.data(); }
-  void start() {
-    rix.clear();
-    ub.clear();
-    pos.assign(1, 0);
-  }
-  // run r without its aliased candidates (alias[ap..] ascending; ap advances past run r's)
-  void add_run(const Cands &c, uint32_t r, size_t &ap) {
-    const size_t c0 = c.off[r], c1 = c.off[r + 1];
-    size_t k = c0;
-    auto seg = [&](size_t a, size_t b) {
-      if (a >= b) return;
-      rix.push_back(r);
-      ub.push_back((uint32_t)(a - c0));
-      pos.push_back(pos.back() + (b - a));
-    };
-    for (; ap < c.alias.size() && c.alias[ap].first < c1; ap++) {
-      seg(k, c.alias[ap].first);
-      k = (size_t)c.alias[ap].first + 1;
-    }
-    seg(k, c1);
-  }
-};
-
 // The group of every run without its aliased candidates: run ranges built in parallel (a
 // light-client batch has ~90k aliases, one per Trusting vote), then joined.
 static void build_group(const Cands &c, Group &g) {
@@ -866,7 +905,7 @@ static void build_group(const Cands &c, Group &g) {
     mine.start();
     const auto a0 = std::lower_bound(c.alias.begin(), c.alias.end(), std::make_pair((uint32_t)c.off[lo], 0u));
     size_t ap = (size_t)(a0 - c.alias.begin());
-    for (size_t r = lo; r < hi; r++) mine.add_run(c, (uint32_t)r, ap);
+    for (size_t r = lo; r < hi; r++) mine.add_run(c, (uint32_t)r, c.alias, ap);
     part[t].rix.swap(mine.rix);
     part[t].ub.swap(mine.ub);
     part[t].pos.swap(mine.pos);
@@ -1118,7 +1157,7 @@ static int ctx_verify(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, 
     size_t g = 0;
     while (g < gkeys.size() && gkeys[g] != ks) g++;
     if (g == gkeys.size()) { gkeys.push_back(ks); groups.emplace_back(); groups.back().start(); }
-    groups[g].add_run(cands, (uint32_t)r, ap);
+    groups[g].add_run(cands, (uint32_t)r, cands.alias, ap);
   }
   if (groups.size() == 1 && cands.alias.empty()) groups[0] = Group();  // every run in order: the call's own offsets
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1605,7 +1644,7 @@ static int bs_pump(tmed_ctx *ctx, BsStream &S, BsWindow &w, double ph[3], std::u
     w.inflight++;
     const tmed_commit_request *rq = w.rq + b.lo;
     const auto tp = BsClock::now();
-    rc = seam_plan(rq, b.n, w.out + b.lo, b.plans, b.cands, w.kc);
+    rc = seam_plan(rq, b.n, w.out + b.lo, b.plans, b.cands, w.kc, &b.grp);  // b.grp: the staging segments
     clk.lap("plan");
     const size_t m = b.cands.size();
     bool fits = true;
@@ -1613,12 +1652,6 @@ static int bs_pump(tmed_ctx *ctx, BsStream &S, BsWindow &w, double ph[3], std::u
     clk.lap("templates");
     if (rc == TMED_OK && m) {
       if (fits && m <= 0xffffffffu) {
-        if (b.cands.alias.empty()) {
-          b.grp = Group();
-        } else {
-          build_group(b.cands, b.grp);
-        }
-        clk.lap("group");
         rc = stage_group(ctx, rq, b.n, b.cands, b.grp, w.keyset, b.tmpl, (int)(idx % ns), b.st);
         // key-cached batches alternate between the two kernel lanes, so one batch's small kernels
         // (assembly, key order, prep, finish) run beside the other's main kernel
