@@ -100,6 +100,10 @@ struct Cands {
   // request -> the request whose device template its candidates use (empty: its own); a
   // Trusting request shares the template of the Light request of the same commit (pair_request)
   std::vector<uint32_t> tmpl_of;
+  // the planning workers' parts when the batch was aliased with a staging group (seam_plan):
+  // part t holds requests [preq[t], preq[t+1]), aliases [pal[t], pal[t+1]) and group segments
+  // [pseg[t], pseg[t+1]), every alias inside its part (bs_finish works part by part); else empty
+  std::vector<size_t> preq, pal, pseg;
   size_t size() const { return off.empty() ? 0 : off.back(); }
   uint32_t tmpl_row(uint32_t q) const { return tmpl_of.empty() ? q : tmpl_of[q]; }
   void clear() {
@@ -107,6 +111,9 @@ struct Cands {
     off.assign(1, 0);
     alias.clear();
     tmpl_of.clear();
+    preq.clear();
+    pal.clear();
+    pseg.clear();
   }
 };
 // Append candidate (q, i, v) to a part's runs, extending the last run when it continues it.
@@ -644,6 +651,13 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
           for (size_t t = lo; t < hi; t++) join(t);
         });
       }
+      if (grp && nt > 1) {
+        cands.preq.resize(np + 1);
+        for (unsigned t = 0; t < np; t++) cands.preq[t] = lo_of[t];
+        cands.preq[np] = n;
+        cands.pal = abase;
+        cands.pseg = sbase;
+      }
     }
   }
   clk.lap("aliases");
@@ -1107,20 +1121,24 @@ static int stage_group(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
 
 // Collected bits of a group -> valid[] by candidate (signatures of length != 64 are false:
 // ed25519.go:150-152).
+static void scatter_range(const tmed_commit_request *reqs, const Cands &cands, const Group &grp, const uint8_t *bits,
+                          uint8_t *valid, size_t lo, size_t hi) {
+  for_segments(cands, grp, lo, hi, [&](size_t j, uint32_t u0, uint32_t u1, size_t p) {
+    const uint32_t ri = grp.run(cands, j);
+    const Run &run = cands.runs[ri];
+    const tmed_commit &c = *reqs[run.req].commit;
+    uint8_t *dst = valid + cands.off[ri];
+    for (uint32_t u = u0; u < u1; u++) {
+      const uint32_t sl = c.sig_lens ? c.sig_lens[run.sig + (int32_t)u] : 64;
+      dst[u] = sl == 64 ? bits[p + (u - u0)] : 0;
+    }
+  });
+}
 static void scatter_bits(const tmed_commit_request *reqs, const Cands &cands, const Group &grp, const uint8_t *bits,
                          uint8_t *valid) {
   const size_t m = grp.size(cands);
   parallel_ranges(m, host_threads(m), [&](size_t lo, size_t hi, unsigned) {
-    for_segments(cands, grp, lo, hi, [&](size_t j, uint32_t u0, uint32_t u1, size_t p) {
-      const uint32_t ri = grp.run(cands, j);
-      const Run &run = cands.runs[ri];
-      const tmed_commit &c = *reqs[run.req].commit;
-      uint8_t *dst = valid + cands.off[ri];
-      for (uint32_t u = u0; u < u1; u++) {
-        const uint32_t sl = c.sig_lens ? c.sig_lens[run.sig + (int32_t)u] : 64;
-        dst[u] = sl == 64 ? bits[p + (u - u0)] : 0;
-      }
-    });
+    scatter_range(reqs, cands, grp, bits, valid, lo, hi);
   });
 }
 
@@ -1565,18 +1583,41 @@ static int bs_finish(tmed_ctx *ctx, BsBatch &b, double ph[3]) {
   }
   const auto t1 = BsClock::now();
   PhaseClock clk;
-  if (r == TMED_OK && aliased) {  // bits by staged segment -> by candidate
-    b.valid.resize(m);  // scatter_bits writes every staged candidate, copy_aliases the rest
-    scatter_bits(w.rq + b.lo, b.cands, b.grp, b.bits.data(), b.valid.data());
-    clk.lap("scatter");
-    copy_aliases(b.cands, b.valid.data());
-    clk.lap("aliases");
+  const Cands &cd = b.cands;
+  const size_t np = cd.preq.size() ? cd.preq.size() - 1 : 0;
+  if (r == TMED_OK && aliased && np && !b.grp.rix.empty()) {
+    // part by part (the planning workers' parts: each alias inside its part): the part's staged
+    // bits -> by candidate, its aliased bits, then the replay of its requests — one fork-join
+    b.valid.resize(m);
+    const tmed_commit_request *rq = w.rq + b.lo;
+    std::vector<int> rcs(np, TMED_OK);
+    const Plans &ps = b.plans;
+    parallel_ranges(np, np, [&](size_t lo, size_t hi, unsigned) {
+      for (size_t t = lo; t < hi; t++) {
+        scatter_range(rq, cd, b.grp, b.bits.data(), b.valid.data(), b.grp.pos[cd.pseg[t]], b.grp.pos[cd.pseg[t + 1]]);
+        for (size_t k = cd.pal[t]; k < cd.pal[t + 1]; k++) b.valid[cd.alias[k].first] = b.valid[cd.alias[k].second];
+        for (size_t q = cd.preq[t]; q < cd.preq[t + 1]; q++)
+          if (!ps.v[q].decided && replay_request(rq[q], w.out[b.lo + q], ps.v[q], b.valid.data()) != TMED_OK)
+            rcs[t] = TMED_EINVAL;
+      }
+    });
+    for (int rc : rcs)
+      if (rc != TMED_OK) r = rc;
+    clk.lap("scatter_aliases_replay");
+  } else {
+    if (r == TMED_OK && aliased) {  // bits by staged segment -> by candidate
+      b.valid.resize(m);  // scatter_bits writes every staged candidate, copy_aliases the rest
+      scatter_bits(w.rq + b.lo, b.cands, b.grp, b.bits.data(), b.valid.data());
+      clk.lap("scatter");
+      copy_aliases(b.cands, b.valid.data());
+      clk.lap("aliases");
+    }
+    // the device bits are in candidate order: replay reads them directly (it applies the
+    // signature-length rule itself)
+    if (r == TMED_OK)
+      r = seam_replay(w.rq + b.lo, b.n, w.out + b.lo, b.plans, b.device && !aliased ? b.bits.data() : b.valid.data());
+    clk.lap("replay");
   }
-  // the device bits are in candidate order: replay reads them directly (it applies the
-  // signature-length rule itself)
-  if (r == TMED_OK)
-    r = seam_replay(w.rq + b.lo, b.n, w.out + b.lo, b.plans, b.device && !aliased ? b.bits.data() : b.valid.data());
-  clk.lap("replay");
   if (b.device) clk.emit("blocksync finish", b.n, m);
   ph[2] += bs_us(t1, BsClock::now());
   b.n = 0;

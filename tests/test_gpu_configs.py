@@ -127,7 +127,7 @@ def test_c3_light_client_changing_sets(engine, monkeypatch, keyed, pipelined):
     heights back (overlap 53 validators: Got 530 <= Needed 583), headers 9 and 17 carry bad
     signatures inside the Trusting prefix, header 23 a bad signature after the Light crossing.
     The Trusting candidates that the Light request of the same commit also holds are verified
-    once (commit.hip find_aliases): the bad signatures at 3 and 40 are such shared candidates.
+    once (commit.hip pair_request): the bad signatures at 3 and 40 are such shared candidates.
     pipelined: batches of 16 requests through the pipelined seam (TMED_PIPE_SIGS)."""
     if pipelined:
         monkeypatch.setenv("TMED_PIPE_SIGS", "2500")
@@ -170,13 +170,17 @@ def test_c3_light_client_changing_sets(engine, monkeypatch, keyed, pipelined):
             engine.keyset_free(ks)
 
 
-def test_c3_many_sets_through_the_cache(engine):
-    """A light-client call of 4,100 requests on 2,052 validator sets (8 validators, one key changing
-    per height) passed WITHOUT key-set handles: the key-set cache resolves them (above 4,096 requests
-    the distinct sets are found by the host workers, commit.hip keycache_resolve).  Twice — the
-    first call generic (cold cache), the second on the cached key sets — both equal to the oracle
-    loops; bad signatures in three commits."""
-    nv, H, gap = 8, 2050, 2
+@pytest.mark.parametrize("nv,pipe", [(8, None), (40, "70000")])
+def test_c3_many_sets_through_the_cache(engine, monkeypatch, nv, pipe):
+    """A light-client call of 4,100 requests on 2,052 validator sets (one key changing per height)
+    passed WITHOUT key-set handles: the key-set cache resolves them.  Twice — the first call
+    generic (cold cache), the second on the cached key sets — both equal to the oracle loops; bad
+    signatures in three commits.  pipe: 40 validators, batches of ~70k signatures through the
+    pipelined seam, so every batch is planned and finished by the host workers part by part
+    (aliases, staging segments, scatter + alias copy + replay per planning part)."""
+    if pipe:
+        monkeypatch.setenv("TMED_PIPE_SIGS", pipe)
+    H, gap = 2050, 2
     seeds = seeds_from_tag(b"tmed-c3-many", 0, H + gap + nv)
     pubs = pubkeys_of(engine, seeds)
     sets, specs = {}, []
@@ -186,7 +190,7 @@ def test_c3_many_sets_through_the_cache(engine):
         addrs = np.array([np.frombuffer(v.address, np.uint8) for v in vals.validators])
         specs.append((seeds[h:h + nv][order], addrs, h + 1, 0, _bid(b"c3m-%d" % (h + 1)), T2023 + h, None))
     commits = dict(zip(range(H + gap), sign_commits(engine, CHAIN, specs)))
-    for h, i in ((7, 1), (1000, 5), (2049, 0)):
+    for h, i in ((7, 1), (1000, 5), (2049, 0), (1500, nv - 1)):
         _corrupt(commits[h], i)
     reqs, exp, osets = [], [], {h: _ovals(v) for h, v in sets.items()}
     for h in range(H):
