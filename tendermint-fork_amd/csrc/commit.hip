@@ -192,6 +192,17 @@ struct Group {
   }
 };
 
+// Device templates, one row per request whose candidates use its own (Cands::tmpl_row), rows
+// packed in request order: row_of[q] is request q's row (kNoRow: none).
+constexpr uint32_t kNoRow = 0xffffffffu;
+struct Templates {
+  std::vector<uint8_t> rows;
+  std::vector<uint32_t> row_of;
+  size_t nrows = 0;
+  bool ready = false, fits = true;  // ready: built by seam_plan's merge pass (fits: all within the device assembler)
+  uint32_t row(const Cands &c, uint32_t q) const { return row_of[c.tmpl_row(q)]; }
+};
+
 // The plans of one seam call and the planning workers' parts, kept between calls (blocksync
 // plans batch after batch), so their pages are touched once.
 struct Plans {
@@ -200,6 +211,7 @@ struct Plans {
   std::vector<std::vector<Run>> parts;
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> aparts;  // per worker: its aliases
   std::vector<Group> gparts;                                       // per worker: its group segments
+  std::vector<std::vector<uint8_t>> trows;                         // per worker: its template rows
 };
 
 
@@ -475,8 +487,10 @@ static void pair_request(const tmed_commit_request *reqs, const std::vector<Plan
                          size_t lo, size_t hi, std::vector<std::pair<uint32_t, uint32_t>> &mine);
 
 // Candidates of requests [0, n) in request order (identical to a serial plan).
+static bool template_row(const tmed_commit_request &rq, uint8_t *row, bool *fit);
+
 static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out, Plans &ps, Cands &cands,
-                     const KcCall *kc = nullptr, Group *grp = nullptr) {
+                     const KcCall *kc = nullptr, Group *grp = nullptr, Templates *tp = nullptr) {
   PhaseClock clk;
   std::vector<Plan> &plans = ps.v;
   plans.assign(n, Plan());
@@ -493,7 +507,8 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
   if (ps.parts.size() < np) ps.parts.resize(np);
   if (ps.tbits.size() < np) ps.tbits.resize(np);
   std::vector<std::vector<Run>> &part = ps.parts;
-  std::vector<size_t> lo_of(np, 0), hi_of(np, 0), pc(np, 0);
+  // (parts that never run — parallel_ranges uses at most n of them — keep the empty range [n, n))
+  std::vector<size_t> lo_of(np, n), hi_of(np, n), pc(np, 0);
   std::vector<int> rcs(np, TMED_OK);
   std::vector<uint8_t> trusting(np, 0);
   auto plan_range = [&](size_t lo, size_t hi, unsigned t) {
@@ -573,6 +588,15 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
     if (ps.aparts.size() < np) ps.aparts.resize(np);
     if (grp && ps.gparts.size() < np) ps.gparts.resize(np);
   }
+  // a device batch planned by several workers also gets its template rows here, each worker
+  // encoding the requests of its part that own a row (row_of holds part-local rows until the join)
+  const bool rows_here = tp && nt > 1;
+  std::vector<uint8_t> tfit(np, 1), tbad(np, 0);
+  if (tp) tp->ready = false;
+  if (rows_here) {
+    tp->row_of.resize(n);
+    if (ps.trows.size() < np) ps.trows.resize(np);
+  }
   auto merge_part = [&](size_t t) {
     size_t c = cbase[t];
     Run *dst = cands.runs.data() + rbase[t];
@@ -587,7 +611,29 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
       plans[q].run_lo += rbase[t];
       plans[q].run_hi += rbase[t];
     }
-    if (!pair) return;
+    auto rows_of_part = [&] {
+      std::vector<uint8_t> rows;  // (a header of its own: see seam_plan)
+      rows.swap(ps.trows[t]);
+      rows.clear();
+      uint32_t k = 0;
+      bool fit = true;
+      for (size_t q = lo_of[t]; q < hi_of[t]; q++) {
+        const Plan &pl = plans[q];
+        if (pl.run_lo == pl.run_hi || cands.tmpl_row((uint32_t)q) != q) {
+          tp->row_of[q] = kNoRow;
+          continue;
+        }
+        rows.resize((size_t)(k + 1) * tmed::kVoteTmplBytes);
+        if (!template_row(reqs[q], rows.data() + (size_t)k * tmed::kVoteTmplBytes, &fit)) tbad[t] = 1;
+        tp->row_of[q] = k++;
+      }
+      tfit[t] = fit;
+      rows.swap(ps.trows[t]);
+    };
+    if (!pair) {
+      if (rows_here) rows_of_part();
+      return;
+    }
     for (size_t q = lo_of[t]; q < hi_of[t]; q++) cands.tmpl_of[q] = (uint32_t)q;
     std::vector<std::pair<uint32_t, uint32_t>> mine;  // (a header of its own: see seam_plan)
     mine.swap(ps.aparts[t]);
@@ -606,6 +652,7 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
       g.pos.swap(ps.gparts[t].pos);
     }
     mine.swap(ps.aparts[t]);
+    if (rows_here) rows_of_part();  // after the pairing: tmpl_of of the part is final
   };
   if (nt <= 1) {
     for (unsigned t = 0; t < np; t++) merge_part(t);
@@ -617,9 +664,10 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
   clk.lap("merge");
   cands.alias.clear();
   if (grp) *grp = Group();  // no aliases: every run whole, in order
-  if (pair) {
-    std::vector<size_t> abase(np + 1, 0), sbase(np + 1, 0), pbase(np + 1, 0);
-    for (unsigned t = 0; t < np; t++) {
+  std::vector<size_t> abase(np + 1, 0), sbase(np + 1, 0), pbase(np + 1, 0), tbase(np + 1, 0);
+  bool rows_bad = false, rows_fit = true;
+  for (unsigned t = 0; t < np; t++) {
+    if (pair) {
       abase[t + 1] = abase[t] + ps.aparts[t].size();
       if (grp) {
         const Group &g = ps.gparts[t];
@@ -627,38 +675,61 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
         pbase[t + 1] = pbase[t] + (g.rix.empty() ? 0 : g.pos.back());
       }
     }
-    if (abase[np]) {
-      cands.alias.resize(abase[np]);
-      if (grp) {
-        grp->rix.resize(sbase[np]);
-        grp->ub.resize(sbase[np]);
-        grp->pos.resize(sbase[np] + 1);
-        grp->pos[0] = 0;
-      }
-      auto join = [&](size_t t) {
-        std::copy(ps.aparts[t].begin(), ps.aparts[t].end(), cands.alias.begin() + abase[t]);
-        if (!grp) return;
-        const Group &g = ps.gparts[t];
-        const size_t k = g.rix.size(), s0 = sbase[t], p0 = pbase[t];
-        std::copy(g.rix.begin(), g.rix.end(), grp->rix.begin() + s0);
-        std::copy(g.ub.begin(), g.ub.end(), grp->ub.begin() + s0);
-        for (size_t j = 0; j < k; j++) grp->pos[s0 + j + 1] = p0 + g.pos[j + 1];
-      };
-      if (nt <= 1 || abase[np] < 8192) {
-        for (unsigned t = 0; t < np; t++) join(t);
-      } else {
-        parallel_ranges(np, np, [&](size_t lo, size_t hi, unsigned) {
-          for (size_t t = lo; t < hi; t++) join(t);
-        });
-      }
-      if (grp && nt > 1) {
-        cands.preq.resize(np + 1);
-        for (unsigned t = 0; t < np; t++) cands.preq[t] = lo_of[t];
-        cands.preq[np] = n;
-        cands.pal = abase;
-        cands.pseg = sbase;
-      }
+    if (rows_here) {
+      tbase[t + 1] = tbase[t] + ps.trows[t].size() / tmed::kVoteTmplBytes;
+      rows_bad = rows_bad || tbad[t];
+      rows_fit = rows_fit && tfit[t];
     }
+  }
+  if (rows_bad) return TMED_EINVAL;  // the encoder rejected a request (as device_templates does)
+  const bool aliases = pair && abase[np] != 0;
+  if (aliases) {
+    cands.alias.resize(abase[np]);
+    if (grp) {
+      grp->rix.resize(sbase[np]);
+      grp->ub.resize(sbase[np]);
+      grp->pos.resize(sbase[np] + 1);
+      grp->pos[0] = 0;
+    }
+  }
+  if (rows_here) {
+    tp->nrows = tbase[np];
+    tp->rows.resize(std::max<size_t>(tp->nrows, 1) * tmed::kVoteTmplBytes);
+  }
+  if (aliases || rows_here) {
+    auto join = [&](size_t t) {
+      if (rows_here) {
+        std::copy(ps.trows[t].begin(), ps.trows[t].end(), tp->rows.begin() + tbase[t] * tmed::kVoteTmplBytes);
+        for (size_t q = lo_of[t]; q < hi_of[t]; q++)
+          if (tp->row_of[q] != kNoRow) tp->row_of[q] += (uint32_t)tbase[t];
+      }
+      if (!aliases) return;
+      std::copy(ps.aparts[t].begin(), ps.aparts[t].end(), cands.alias.begin() + abase[t]);
+      if (!grp) return;
+      const Group &g = ps.gparts[t];
+      const size_t k = g.rix.size(), s0 = sbase[t], p0 = pbase[t];
+      std::copy(g.rix.begin(), g.rix.end(), grp->rix.begin() + s0);
+      std::copy(g.ub.begin(), g.ub.end(), grp->ub.begin() + s0);
+      for (size_t j = 0; j < k; j++) grp->pos[s0 + j + 1] = p0 + g.pos[j + 1];
+    };
+    if (nt <= 1) {
+      for (unsigned t = 0; t < np; t++) join(t);
+    } else {
+      parallel_ranges(np, np, [&](size_t lo, size_t hi, unsigned) {
+        for (size_t t = lo; t < hi; t++) join(t);
+      });
+    }
+    if (aliases && grp && nt > 1) {
+      cands.preq.resize(np + 1);
+      for (unsigned t = 0; t < np; t++) cands.preq[t] = lo_of[t];
+      cands.preq[np] = n;
+      cands.pal = abase;
+      cands.pseg = sbase;
+    }
+  }
+  if (rows_here) {
+    tp->fits = rows_fit;
+    tp->ready = true;
   }
   clk.lap("aliases");
   clk.emit("plan", n, cb);
@@ -970,15 +1041,27 @@ static void for_segments(const Cands &c, const Group &g, size_t lo, size_t hi, F
   }
 }
 
-// Device templates, one row per request whose candidates use its own (Cands::tmpl_row), rows
-// packed in request order: row_of[q] is request q's row (kNoRow: none).
-constexpr uint32_t kNoRow = 0xffffffffu;
-struct Templates {
-  std::vector<uint8_t> rows;
-  std::vector<uint32_t> row_of;
-  size_t nrows = 0;
-  uint32_t row(const Cands &c, uint32_t q) const { return row_of[c.tmpl_row(q)]; }
-};
+// Request q's template row (kVoteTmplBytes at row); false: the encoder rejected the request
+// (bad), or *fit = false when its template does not fit the device assembler.
+static bool template_row(const tmed_commit_request &rq, uint8_t *row, bool *fit) {
+  const tmed_commit &c = *rq.commit;
+  tmed_vote_template t;
+  t.chain_id = rq.chain_id;
+  t.chain_id_len = rq.chain_id_len;
+  t.height = c.height;
+  t.round = c.round;
+  t.block_hash = c.block_id.hash;
+  t.block_hash_len = c.block_id.hash_len;
+  t.psh_total = c.block_id.psh_total;
+  t.psh_hash = c.block_id.psh_hash;
+  t.psh_hash_len = c.block_id.psh_hash_len;
+  tmed::VoteEncoder e;
+  if (e.init(&t) != TMED_OK) return false;
+  memset(row, 0, tmed::kVoteTmplBytes);
+  if (!e.device_template(row, tmed::kVoteTmplBytes, tmed::kVoteSlot)) *fit = false;
+  return true;
+}
+
 static int device_templates(const tmed_commit_request *reqs, size_t n, const Cands &cands, Templates &tp,
                             bool *fits) {
   tp.row_of.assign(n, kNoRow);
@@ -992,25 +1075,9 @@ static int device_templates(const tmed_commit_request *reqs, size_t n, const Can
   parallel_ranges(n, n >= 64 ? host_threads(cands.size()) : 1, [&](size_t lo, size_t hi, unsigned) {
     for (size_t q = lo; q < hi; q++) {
       if (tp.row_of[q] == kNoRow) continue;
-      const tmed_commit &c = *reqs[q].commit;
-      tmed_vote_template t;
-      t.chain_id = reqs[q].chain_id;
-      t.chain_id_len = reqs[q].chain_id_len;
-      t.height = c.height;
-      t.round = c.round;
-      t.block_hash = c.block_id.hash;
-      t.block_hash_len = c.block_id.hash_len;
-      t.psh_total = c.block_id.psh_total;
-      t.psh_hash = c.block_id.psh_hash;
-      t.psh_hash_len = c.block_id.psh_hash_len;
-      tmed::VoteEncoder e;
-      if (e.init(&t) != TMED_OK) {
-        bad = true;
-        continue;
-      }
-      uint8_t *row = &tp.rows[(size_t)tp.row_of[q] * tmed::kVoteTmplBytes];
-      memset(row, 0, tmed::kVoteTmplBytes);
-      if (!e.device_template(row, tmed::kVoteTmplBytes, tmed::kVoteSlot)) ok = false;
+      bool fit = true;
+      if (!template_row(reqs[q], &tp.rows[(size_t)tp.row_of[q] * tmed::kVoteTmplBytes], &fit)) bad = true;
+      if (!fit) ok = false;
     }
   });
   if (bad) return TMED_EINVAL;
@@ -1685,11 +1752,12 @@ static int bs_pump(tmed_ctx *ctx, BsStream &S, BsWindow &w, double ph[3], std::u
     w.inflight++;
     const tmed_commit_request *rq = w.rq + b.lo;
     const auto tp = BsClock::now();
-    rc = seam_plan(rq, b.n, w.out + b.lo, b.plans, b.cands, w.kc, &b.grp);  // b.grp: the staging segments
+    // b.grp: the staging segments; b.tmpl: the template rows (when several workers planned)
+    rc = seam_plan(rq, b.n, w.out + b.lo, b.plans, b.cands, w.kc, &b.grp, &b.tmpl);
     clk.lap("plan");
     const size_t m = b.cands.size();
-    bool fits = true;
-    if (rc == TMED_OK && m) rc = device_templates(rq, b.n, b.cands, b.tmpl, &fits);
+    bool fits = b.tmpl.fits;
+    if (rc == TMED_OK && m && !b.tmpl.ready) rc = device_templates(rq, b.n, b.cands, b.tmpl, &fits);
     clk.lap("templates");
     if (rc == TMED_OK && m) {
       if (fits && m <= 0xffffffffu) {

@@ -170,17 +170,18 @@ def test_c3_light_client_changing_sets(engine, monkeypatch, keyed, pipelined):
             engine.keyset_free(ks)
 
 
-@pytest.mark.parametrize("nv,pipe", [(8, None), (40, "70000")])
-def test_c3_many_sets_through_the_cache(engine, monkeypatch, nv, pipe):
+@pytest.mark.parametrize("nv,H,pipe", [(8, 2050, None), (40, 2050, "70000")])
+def test_c3_many_sets_through_the_cache(engine, monkeypatch, nv, H, pipe):
     """A light-client call of 4,100 requests on 2,052 validator sets (one key changing per height)
     passed WITHOUT key-set handles: the key-set cache resolves them.  Twice — the first call
     generic (cold cache), the second on the cached key sets — both equal to the oracle loops; bad
-    signatures in three commits.  pipe: 40 validators, batches of ~70k signatures through the
-    pipelined seam, so every batch is planned and finished by the host workers part by part
-    (aliases, staging segments, scatter + alias copy + replay per planning part)."""
+    signatures in four commits.  pipe: batches of ~70k signatures through the pipelined seam,
+    so every batch is planned and finished by the host workers part by part (aliases, staging
+    segments, template rows, scatter + alias copy + replay per planning part), ~1,700 requests
+    per batch."""
     if pipe:
         monkeypatch.setenv("TMED_PIPE_SIGS", pipe)
-    H, gap = 2050, 2
+    gap = 2
     seeds = seeds_from_tag(b"tmed-c3-many", 0, H + gap + nv)
     pubs = pubkeys_of(engine, seeds)
     sets, specs = {}, []
@@ -210,17 +211,19 @@ def test_c3_many_sets_through_the_cache(engine, monkeypatch, nv, pipe):
 
 
 def test_c4_10k_validator_light_window(engine):
-    """C4 shape: a blocksync window of 6 blocks x 10,000 validators (equal power 10: needed 66,666,
+    """C4 shape: a blocksync window of 7 blocks x 10,000 validators (equal power 10: needed 66,666,
     crossed by the 6,667th signature, index 6,666), VerifyCommitLight per block through the pipelined
     blocksync seam (key-cached) and through tmed_verify_commits (generic keys).  Blocks carry a bad
     signature at index 100, at 6,666 (the crossing signature itself), at 6,667 (just after the
-    crossing: never reached) and at 9,999; one block is all valid and one has a wrong BlockID."""
-    nv = 10_000
+    crossing: never reached) and at 9,999; two blocks are all valid and one has a wrong BlockID.
+    The window runs in batches of 2 blocks and in one batch of 7 (70k signatures: planned by more
+    host workers than the batch has requests, the unused parts empty)."""
+    nv, nb = 10_000, 7
     seeds = seeds_from_tag(b"tmed-c4-key", 0, nv)
     pubs = pubkeys_of(engine, seeds)
     vals, order = make_valset(pubs, [10] * nv)
     addrs = np.array([np.frombuffer(v.address, np.uint8) for v in vals.validators])
-    specs = [(seeds[order], addrs, b + 1, 0, _bid(b"c4-%d" % (b + 1)), T2023 + b, None) for b in range(6)]
+    specs = [(seeds[order], addrs, b + 1, 0, _bid(b"c4-%d" % (b + 1)), T2023 + b, None) for b in range(nb)]
     commits = sign_commits(engine, CHAIN, specs)
     for b, i in ((0, 100), (1, 6666), (2, 6667), (3, 9999)):
         _corrupt(commits[b], i)
@@ -229,20 +232,23 @@ def test_c4_10k_validator_light_window(engine):
     heights = [c.height for c in commits]
     ovs = _ovals(vals)
     exp = [C.verify_commit_light(ovs, CHAIN, _obid(bids[b]), heights[b], _ocommit(commits[b]), _port_verify)
-           for b in range(6)]
+           for b in range(nb)]
     assert str(exp[0]).startswith("wrong signature (#100)") and str(exp[1]).startswith("wrong signature (#6666)")
-    assert exp[2] is None and exp[3] is None and exp[4] is None and "wrong block ID" in str(exp[5])
+    assert exp[2] is None and exp[3] is None and exp[4] is None and "wrong block ID" in str(exp[5]) and exp[6] is None
     generic = T.verify_commits(engine, [(T.MODE_LIGHT, vals, CHAIN, bids[b], heights[b], commits[b], 0, 0)
-                                        for b in range(6)])
+                                        for b in range(nb)])
     vals.keyset = engine.keyset_load(np.array([np.frombuffer(v.pub_key, np.uint8) for v in vals.validators]))
     try:
         win = T.BlocksyncWindow(vals, CHAIN, bids, heights, commits)
-        win.run(engine, 2)
-        keyed = win.errors()
-        stats = win.verified()
+        runs = []
+        for batch_blocks in (2, 7):
+            win.run(engine, batch_blocks)
+            runs.append((win.errors(), win.verified()))
     finally:
         engine.keyset_free(vals.keyset)
-    for b in range(6):
+    for b in range(nb):
         assert _same(generic[b], exp[b]), (b, generic[b], exp[b])
-        assert _same(keyed[b], exp[b]), (b, keyed[b], exp[b])
-    assert stats.tolist() == [101, 6667, 6667, 6667, 6667, 0]
+        for keyed, _ in runs:
+            assert _same(keyed[b], exp[b]), (b, keyed[b], exp[b])
+    for _, stats in runs:
+        assert stats.tolist() == [101, 6667, 6667, 6667, 6667, 0, 6667]
