@@ -205,9 +205,28 @@ struct Templates {
 
 // The plans of one seam call and the planning workers' parts, kept between calls (blocksync
 // plans batch after batch), so their pages are touched once.
+// A planning worker's vof arrays: taken from chunks kept between calls (pointers stay valid
+// until the next reset).
+struct VofArena {
+  std::vector<std::pair<std::unique_ptr<int32_t[]>, size_t>> chunks;
+  size_t ci = 0, used = 0;
+  void reset() { ci = 0; used = 0; }
+  int32_t *take(size_t k) {
+    while (ci < chunks.size() && chunks[ci].second - used < k) { ci++; used = 0; }
+    if (ci == chunks.size()) {
+      const size_t sz = std::max<size_t>((size_t)1 << 16, k);
+      chunks.emplace_back(std::unique_ptr<int32_t[]>(new int32_t[sz]), sz);
+      used = 0;
+    }
+    int32_t *p = chunks[ci].first.get() + used;
+    used += k;
+    return p;
+  }
+};
+
 struct Plans {
   std::vector<Plan> v;
-  std::vector<RawBuf<int32_t>> tbits;  // per planning worker: its Trusting requests' vof arrays
+  std::vector<VofArena> tbits;  // per planning worker: its Trusting requests' vof arrays
   std::vector<std::vector<Run>> parts;
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> aparts;  // per worker: its aliases
   std::vector<Group> gparts;                                       // per worker: its group segments
@@ -516,24 +535,9 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
     AddrScratch addr;
     addr.kc = kc;
     size_t c = 0;
-    {  // the vof arrays of this range's Trusting requests
-      size_t nb = 0;
-      for (size_t q = lo; q < hi; q++) {
-        if (q + 4 < hi) {  // the structs behind the requests are cold: fetched a few requests ahead
-          __builtin_prefetch(reqs[q + 4].commit, 0, 0);
-          __builtin_prefetch(reqs[q + 4].vals, 0, 0);
-        }
-        if (reqs[q].mode == TMED_MODE_LIGHT_TRUSTING && reqs[q].commit) nb += reqs[q].commit->n_sigs;
-      }
-      int32_t *bits = ps.tbits[t].ensure(std::max<size_t>(nb, 1));
-      nb = 0;
-      for (size_t q = lo; q < hi; q++)
-        if (reqs[q].mode == TMED_MODE_LIGHT_TRUSTING && reqs[q].commit) {
-          plans[q].vof = bits + nb;
-          nb += reqs[q].commit->n_sigs;
-        }
-      trusting[t] = nb != 0;
-    }
+    VofArena &va = ps.tbits[t];
+    va.reset();
+    bool tr = false;
     std::vector<Run> mine;
     mine.swap(part[t]);
     int rc = TMED_OK;
@@ -552,11 +556,24 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
       if (r.mode == TMED_MODE_LIGHT_TRUSTING && cm.addresses)
         for (size_t o = 0; o < 20 * ns; o += 64) __builtin_prefetch(cm.addresses + o, 0, 0);
     };
+    for (size_t q = lo; q < lo + 4 && q < hi; q++) {  // the structs behind the requests are cold
+      __builtin_prefetch(reqs[q].commit, 0, 0);
+      __builtin_prefetch(reqs[q].vals, 0, 0);
+    }
     prefetch_req(lo);
     for (size_t q = lo; q < hi && rc == TMED_OK; q++) {
+      if (q + 4 < hi) {
+        __builtin_prefetch(reqs[q + 4].commit, 0, 0);
+        __builtin_prefetch(reqs[q + 4].vals, 0, 0);
+      }
       prefetch_req(q + 1);
+      if (reqs[q].mode == TMED_MODE_LIGHT_TRUSTING && reqs[q].commit) {
+        plans[q].vof = va.take(std::max<size_t>(reqs[q].commit->n_sigs, 1));
+        tr = true;
+      }
       rc = plan_request(reqs, q, out[q], plans[q], mine, c, addr);
     }
+    trusting[t] = tr;
     mine.swap(part[t]);
     rcs[t] = rc;
     pc[t] = c;
