@@ -178,3 +178,31 @@ def test_dense_failures_cut_off():
                 assert st["equations"] == want_eq and st["single_sigs"] == 70_000, st
     finally:
         eng.close()
+
+
+def test_failure_policy_across_chunks_of_one_call():
+    """One call over several chunks (TMED_SLAB_SLOTS = 65,536: chunks of 65,536 signatures): the
+    first half of the batch carries the C5 mix, the second half is all valid.  Chunk 0 runs the
+    equation and bisects, chunk 1 (its predecessor failed) is decided singly and its failures are
+    counted, chunk 2 — the first clean chunk — is decided singly too (chunk 1 had failures), and
+    chunk 3 returns to the batch equation (chunk 2 counted none).  Decisions equal the port's."""
+    from conftest import engine_with_env
+    from tmed import Engine
+    from tmed.workload import c5_mix
+    eng = engine_with_env(TMED_SLAB_SLOTS=65536)
+    try:
+        n, half = 4 * 65536, 2 * 65536
+        rng, pubs, sigs, msgs, offs = _signed_batch(eng, n, 0xC4C4)
+        p, s = pubs[:half].copy(), sigs[:half].copy()
+        c5_mix(p, s, seed=0xC4)
+        pubs[:half], sigs[:half] = p, s
+        exp = port.verify_batch(pubs, sigs, msgs, offs.astype(np.uint64), 16, zip215=True)
+        assert int((exp[:65536] == 0).sum()) > 0 and int((exp[65536:half] == 0).sum()) > 0 and exp[half:].all()
+        out = eng.verify_zip215_arrays(pubs, sigs, msgs, offs)
+        st = Engine.zip215_stats()
+        assert int((out != exp).sum()) == 0
+        assert st["chunks"] == 4, st
+        # chunk 0: the equation + its halves (dense), then chunks 1 and 2 singly, chunk 3 one equation
+        assert st["single_sigs"] == 3 * 65536 and st["equations"] == 4, st
+    finally:
+        eng.close()
