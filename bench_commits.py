@@ -402,7 +402,7 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
     import torch
     import torch.distributed as dist
     import tmed.types as T
-    from tmed import PinnedBuffer
+    from tmed import PinnedBuffer, TmedError
     from tmed.dist import aggregate_blocksync, block_range
     if stream:
         pregen = True  # every window exists before the timed stream starts (nothing generated inside it)
@@ -429,9 +429,25 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
         dist.barrier()
     arenas = []
 
+    pinned_failed = []
+
+    class _Pageable:  # the fallback when page-locked memory runs out (e.g. 8 ranks x 8.3 GB on one node)
+        def __init__(self, nbytes):
+            self.buf = np.empty(nbytes, np.uint8)
+
+        def array(self, shape, dtype):
+            return self.buf.view(dtype)[:int(np.prod(shape))].reshape(shape)
+
+        def free(self):
+            self.buf = None
+
     def to_arena(commits, k):
         if k == len(arenas):
-            arenas.append(PinnedBuffer(window * nvals * 64))
+            try:
+                arenas.append(PinnedBuffer(window * nvals * 64))
+            except TmedError:  # the seam stages pageable signatures itself: slower, same decisions
+                pinned_failed.append(k)
+                arenas.append(_Pageable(window * nvals * 64))
         a = arenas[k].array((window * nvals, 64), np.uint8)
         o = 0
         for c in commits:
@@ -582,8 +598,10 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
                        "signed_per_commit": upto,
                        "warmup": "the first window verified twice untimed (first-use buffers of the seam; the "
                                  "key-set cache's generic first call and its key build)",
-                       "commit_memory": "pinned arenas (tmed_host_alloc): signatures DMA'd from them" if pinned
-                       else "pageable: signatures through the seam's staging copy",
+                       "commit_memory": ("pageable: signatures through the seam's staging copy" if not pinned
+                                         else "pinned arenas (tmed_host_alloc): signatures DMA'd from them"
+                                         + ("; %d of %d arenas pageable (tmed_host_alloc failed)"
+                                            % (len(pinned_failed), len(arenas)) if pinned_failed else "")),
                        "unsigned_note": "validators past the 2/3 crossing carry random (invalid) signatures "
                                         "the Light loop never reaches",
                        "keyset_build_s": round(t_ks, 3), "generate_s": round(t_gen, 2)}}
