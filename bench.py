@@ -177,10 +177,10 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from tmed import Engine, lib
+    from tmed import Engine
     from tmed.workload import c2_messages, c2_seeds
 
-    from tmed.launch import dist_setup, gpu_count_fields
+    from tmed.launch import BINDING, dist_setup, gpu_count_fields
     world, rank, local_rank, dev, coll = dist_setup()
     eng = Engine(local_rank)
     n = args.sigs
@@ -249,6 +249,13 @@ def main():
     total = n_all * args.steps
     value = total / elapsed
 
+    # ---- the dominant kernel's roofline, read right after the C2 timed region (rank 0): the
+    # lattice step's window statistics of THIS batch (later legs' seam calls reset them) and one
+    # extra untimed pass with live per-kernel HIP-event timing
+    roof = peak = None
+    if rank == 0:
+        roof, peak = roofline_leg(eng, step, dev, n, offs, kernel_ms, args.no_peak)
+
     # ---- C4 on every rank (weak scaling: c4_blocks per GPU, contiguous heights, RCCL tallies)
     c4 = None
     if not args.no_c4:
@@ -256,45 +263,6 @@ def main():
 
     result = None
     if rank == 0:
-        wstats = window_summary(eng) if MAIN_VARIANT != 5 else None
-        roof = None
-        peak = None
-        if not args.no_peak:
-            import ctypes
-            l = lib()
-            l.tmed_valu_peak.restype = ctypes.c_int
-            l.tmed_valu_peak.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
-            g = ctypes.c_double(0)
-            rc = l.tmed_valu_peak(eng._h, 0, ctypes.byref(g))
-            peak = g.value / 1e3 if rc == 0 else None  # Tmad/s
-            # live per-kernel HIP-event timing of the dominant kernel, one extra (untimed) pass
-            eng.set_kernel_timing(True)
-            step()
-            torch.cuda.synchronize(dev)
-            (prep_ms, main_ms, fin_ms), (prep_launches, launches, fin_launches) = eng.kernel_times()
-            eng.set_kernel_timing(False)
-            try:
-                b_bits = eng.b_window_bits()
-            except AttributeError:  # an older library build (A/B runs through TMED_LIB)
-                b_bits = 16
-            mads_main = MADS_MAIN if wstats is None else mads_main_hs(wstats["wave_W_mean"], b_bits)
-            achieved = n * mads_main / (main_ms * 1e-3) / 1e12
-            traffic, traffic_src = pmc_traffic(n / max(1, launches))
-            roof = {"bound": "valu", "kernel": MAIN_KERNEL, "achieved": round(achieved, 3),
-                    "peak": round(peak, 3) if peak else None,
-                    "unit": "Tmad/s (v_mad_i64_i32 lane-ops; peak = measured sustained rate)",
-                    "frac": round(achieved / peak, 4) if peak else None,
-                    "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
-                    "traffic_source": traffic_src,
-                    "mads_per_verify_main": round(mads_main), "mads_per_verify_total": MADS_PER_VERIFY_GENERIC,
-                    "mads_basis": ("wave-mean window count %.3f (tmed_window_stats), radix-2^%d B windows"
-                                   % (wstats["wave_W_mean"], b_bits)) if wstats else "formula",
-                    "kernel_avg_ms": round(main_ms / max(1, launches), 4), "launches_per_step": launches,
-                    "prep_kernels_ms": round(prep_ms / max(1, launches), 4), "prep_launches": prep_launches,
-                    "finish_kernel_ms": round(fin_ms, 4), "finish_launches": fin_launches,
-                    "step_kernel_ms": round(kernel_ms, 3),
-                    "algorithmic_bytes_per_verify": 32 + 64 + int(offs[-1]) // n + 4 + 1,
-                    "window_stats": wstats}
         cpu = cpu_all = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(d_pub, d_sig, msgs, offs, min(args.cpu_sample, n), d_out,
@@ -345,12 +313,61 @@ def main():
             "c4_shard": c4,
             "c3_light_client": c3,
             "setup_s": round(t_gen, 2),
+            "host_binding_rank0": dict(BINDING),
         }
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
     eng.close()
     return 0
+
+
+def roofline_leg(eng, step, dev, n, offs, kernel_ms, no_peak):
+    """`roofline` of the dominant kernel (verify_main_hs_kernel): achieved = signatures per launch x
+    the kernel's mads at the measured wave-mean window count (tmed_window_stats of the C2 batch just
+    timed) / the launch's live HIP-event duration; peak = the v_mad_i64_i32 rate measured now, on
+    this device (tmed_valu_peak).  Returns (roofline dict or None, peak Tmad/s or None)."""
+    import torch
+    wstats = window_summary(eng) if MAIN_VARIANT != 5 else None
+    if no_peak:
+        return None, None
+    import ctypes
+    from tmed import lib
+    l = lib()
+    l.tmed_valu_peak.restype = ctypes.c_int
+    l.tmed_valu_peak.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    g = ctypes.c_double(0)
+    rc = l.tmed_valu_peak(eng._h, 0, ctypes.byref(g))
+    peak = g.value / 1e3 if rc == 0 else None  # Tmad/s
+    # live per-kernel HIP-event timing of the dominant kernel, one extra (untimed) pass
+    eng.set_kernel_timing(True)
+    step()
+    torch.cuda.synchronize(dev)
+    (prep_ms, main_ms, fin_ms), (prep_launches, launches, fin_launches) = eng.kernel_times()
+    eng.set_kernel_timing(False)
+    try:
+        b_bits = eng.b_window_bits()
+    except AttributeError:  # an older library build (A/B runs through TMED_LIB)
+        b_bits = 16
+    mads_main = MADS_MAIN if wstats is None else mads_main_hs(wstats["wave_W_mean"], b_bits)
+    achieved = n * mads_main / (main_ms * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic(n / max(1, launches))
+    roof = {"bound": "valu", "kernel": MAIN_KERNEL, "achieved": round(achieved, 3),
+            "peak": round(peak, 3) if peak else None,
+            "unit": "Tmad/s (v_mad_i64_i32 lane-ops; peak = measured sustained rate)",
+            "frac": round(achieved / peak, 4) if peak else None,
+            "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_source": traffic_src,
+            "mads_per_verify_main": round(mads_main), "mads_per_verify_total": MADS_PER_VERIFY_GENERIC,
+            "mads_basis": ("wave-mean window count %.3f (tmed_window_stats of the timed C2 batch), radix-2^%d B "
+                           "windows" % (wstats["wave_W_mean"], b_bits)) if wstats else "formula (W = %d)" % HS_W,
+            "kernel_avg_ms": round(main_ms / max(1, launches), 4), "launches_per_step": launches,
+            "prep_kernels_ms": round(prep_ms / max(1, launches), 4), "prep_launches": prep_launches,
+            "finish_kernel_ms": round(fin_ms, 4), "finish_launches": fin_launches,
+            "step_kernel_ms": round(kernel_ms, 3),
+            "algorithmic_bytes_per_verify": 32 + 64 + int(offs[-1]) // n + 4 + 1,
+            "window_stats": wstats}
+    return roof, peak
 
 
 def c2_keyset(eng, dev, torch_stream, n, steps, warmup, peak):

@@ -235,7 +235,43 @@ def _timed_runs(eng, pb, runs: int):
              "wait_or_verify_frac": round(float(frac[1]), 3), "replay_frac": round(float(frac[2]), 3)})
 
 
-def c3(eng, headers: int, gap: int, policy: str = "cache", runs: int = 7, bisect_gap: int = 150):
+def _c3_corrupt(sets, commits, headers: int, gap: int, every: int):
+    """Known-answer bad signatures for C3's direct leg (every > 0).  Header h verifies commit
+    u = h + gap with Trusting(1/3) against set h and Light against set u; commit u is replaced by a
+    copy with one flipped signature bit when u % every == 13 (at j = (u * 7919) % 175, anywhere) or
+    u % every == 50 (at j = 170, past both loops' crossings).  The expected outcomes follow the
+    reference loops at equal powers 10 (types/validator_set.go:722-765, 775-826): Light counts
+    every signature in order and stops once 1170 > 1166 (indices 0..116); Trusting counts only
+    signatures whose address set h holds (GetByAddress) and stops once 590 > 583 (the 59th such
+    match).  A bad signature the loop reaches -> "wrong signature (#j)" (code 4, idx j); else ok.
+    Returns (the direct leg's commits, {request index: (code, idx)} for every request)."""
+    import tmed.types as T
+    dcommits = list(commits)
+    exp = {}
+    for h in range(headers):
+        u = h + gap
+        j = None
+        if every and u % every == 13:
+            j = (u * 7919) % 175
+        elif every and u % every == 50:
+            j = 170
+        if j is None:
+            exp[2 * h] = exp[2 * h + 1] = (0, -1)
+            continue
+        pc = commits[u]
+        c = T.PackedCommit(pc.height, pc.round, pc.block_id, pc.flags, pc.addresses, pc.ts_seconds, pc.ts_nanos,
+                           pc.sigs.copy(), pc.sig_lens)
+        c.sigs[j, 5] ^= 0x20
+        dcommits[u] = c
+        held = {v.address for v in sets[h].validators}
+        matches = [i for i in range(pc.addresses.shape[0]) if pc.addresses[i].tobytes() in held]
+        exp[2 * h] = (4, j) if j in matches[:59] else (0, -1)   # Trusting: reached among the first 59 matches
+        exp[2 * h + 1] = (4, j) if j <= 116 else (0, -1)         # Light: reached before the crossing
+    return dcommits, exp
+
+
+def c3(eng, headers: int, gap: int, policy: str = "cache", runs: int = 7, bisect_gap: int = 150,
+       corrupt_every: int = 97):
     """Light client (BASELINE C3), two workloads over the same synthetic chain:
       direct:    each header h verified from trusted h - gap in one step (Trusting 1/3 + Light),
                  all headers in one seam call, timed `runs` times (median, spread, phase shares);
@@ -248,7 +284,9 @@ def c3(eng, headers: int, gap: int, policy: str = "cache", runs: int = 7, bisect
     "generic" (cache off).  With the cache the first direct call is cold (generic kernels, the keys
     queued) and the second builds the radix-2^10 combs: both are reported, untimed in the median.
     The request marshalling (PreparedBatch: flat arrays + C structs for every request, what the Go
-    shim rebuilds per call) is timed beside the seam.  Every failing Trusting is checked for
+    shim rebuilds per call) is timed beside the seam.  corrupt_every > 0: known-answer bad
+    signatures in the direct leg's commits (_c3_corrupt), every request's code and index checked
+    (outcome_mismatches).  Every failing Trusting of the bisection is checked for
     ErrNotEnoughVotingPowerSigned Got/Needed."""
     import tmed.types as T
     reach = max(gap, bisect_gap)
@@ -262,11 +300,12 @@ def c3(eng, headers: int, gap: int, policy: str = "cache", runs: int = 7, bisect
                                    "header.ValidatorsHash; the cache still compares the keys byte for byte)"
                                    if policy == "cache" else None)}}
     # ---- direct (gap) ----
+    dcommits, exp = _c3_corrupt(sets, commits, headers, gap, corrupt_every)
     reqs = []
     for h in range(headers):
         u = h + gap
-        reqs.append((T.MODE_LIGHT_TRUSTING, sets[h], "test_chain_id", None, 0, commits[u], 1, 3))
-        reqs.append((T.MODE_LIGHT, sets[u], "test_chain_id", commits[u].block_id, u + 1, commits[u], 0, 0))
+        reqs.append((T.MODE_LIGHT_TRUSTING, sets[h], "test_chain_id", None, 0, dcommits[u], 1, 3))
+        reqs.append((T.MODE_LIGHT, sets[u], "test_chain_id", dcommits[u].block_id, u + 1, dcommits[u], 0, 0))
     tm = time.perf_counter()
     pb = T.PreparedBatch(reqs)
     t_marshal = time.perf_counter() - tm
@@ -283,12 +322,16 @@ def c3(eng, headers: int, gap: int, policy: str = "cache", runs: int = 7, bisect
     k2 = eng.keycache_stats()
     codes = pb.codes()
     ver = int(pb.verified().sum())
+    mism = sum(1 for q in range(len(reqs))
+               if int(codes[q]) != exp[q][0] or (exp[q][0] == 4 and pb.res[q].idx != exp[q][1]))
     res["value"] = round(headers / med, 1)
     res["direct"] = {"gap": gap, "headers_per_s": round(headers / med, 1), "verifies_per_s": round(ver / med, 1),
                      "seconds_median": round(med, 4), "seconds_min": round(lo, 4), "seconds_max": round(hi, 4),
                      "headers_per_s_incl_marshal": round(headers / (med + t_marshal), 1),
                      "marshal_seconds": round(t_marshal, 4),
-                     "verifies": ver, "all_ok": bool((codes == 0).all()), "phase_share": phases,
+                     "verifies": ver, "outcomes_checked": corrupt_every > 0, "outcome_mismatches": mism,
+                     "requests_failing_expected": sum(1 for e in exp.values() if e[0] != 0),
+                     "all_ok": mism == 0, "phase_share": phases,
                      "cold_call_seconds": round(t_cold, 4), "second_call_seconds": round(t_warm, 4),
                      "keycache_cold_and_second": {k: k1[k] - k0[k] for k in ("keyed_sets", "generic_sets",
                                                                             "keys_appended", "keys_deferred")},
@@ -554,8 +597,15 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
             del win, commits
     nbatch = -(-(hi - lo) // batch) if batch else 0
     sdt, sver, smism = sync_pass
+    from tmed.launch import BINDING
+    mine = [BINDING.get("numa_node", -1), BINDING.get("cpus", 0), int(os.environ.get("TMED_HOST_THREADS", "16")),
+            len(arenas) - len(pinned_failed) if pinned else 0, len(pinned_failed) if pinned else len(arenas)]
     agg = aggregate_blocksync(ok_bits, blocks, rank, world, ver, mism + smism, dt, extra_max=[t_marshal, sdt],
-                              phases=list(phase) + [nbatch], device=dev)
+                              phases=list(phase) + [nbatch], device=dev, per_rank=mine)
+    ranks = [{"rank": r, "numa_node": int(p[0]), "cpus": int(p[1]), "host_threads": int(p[2]),
+              "pinned_arenas": int(p[3]), "pageable_arenas": int(p[4])} for r, p in enumerate(agg["per_rank"])]
+    n_pageable = sum(x["pageable_arenas"] for x in ranks)
+    n_arenas = sum(x["pinned_arenas"] + x["pageable_arenas"] for x in ranks)
     ok, nb, ver, mism, dt = agg["blocks_ok"], agg["blocks"], agg["verified"], agg["mismatches"], agg["seconds"]
     t_marshal_max, sdt_max = agg["extra_max"]
     ph_all = [p[:3] + [p[4], p[3]] for p in agg["phases"]]  # plan, wait, replay, seconds, batches
@@ -599,9 +649,12 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
                        "warmup": "the first window verified twice untimed (first-use buffers of the seam; the "
                                  "key-set cache's generic first call and its key build)",
                        "commit_memory": ("pageable: signatures through the seam's staging copy" if not pinned
-                                         else "pinned arenas (tmed_host_alloc): signatures DMA'd from them"
-                                         + ("; %d of %d arenas pageable (tmed_host_alloc failed)"
-                                            % (len(pinned_failed), len(arenas)) if pinned_failed else "")),
+                                         else "pinned arenas (tmed_host_alloc) on every rank: signatures DMA'd "
+                                              "from them" if n_pageable == 0
+                                         else "MIXED: %d of %d arenas over %d rank(s) pageable (tmed_host_alloc "
+                                              "failed; those windows go through the seam's staging copy, a slower "
+                                              "path): see ranks[]" % (n_pageable, n_arenas, world)),
+                       "ranks": ranks,
                        "unsigned_note": "validators past the 2/3 crossing carry random (invalid) signatures "
                                         "the Light loop never reaches",
                        "keyset_build_s": round(t_ks, 3), "generate_s": round(t_gen, 2)}}

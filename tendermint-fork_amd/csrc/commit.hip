@@ -24,6 +24,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <thread>
 #include <string>
 #include <unordered_map>
@@ -947,14 +948,18 @@ extern "C" int tmed_seam_phase_us(double out_us[3]) {
 extern "C" int tmed_verify_commits_with(const tmed_commit_request *reqs, size_t n, tmed_commit_result *out,
                                         tmed_batch_verify_fn verify, void *user) {
   if (!verify) return TMED_EINVAL;
-  return run_seam(reqs, n, out,
-                  [&](const tmed_commit_request *rq, size_t nr, const Cands &cands, uint8_t *valid) {
-                    CandBatch cb;
-                    int rc = build_cand_batch(rq, nr, cands, cb);
-                    if (rc != TMED_OK) return rc;
-                    return verify(user, cb.pubs.data(), cb.sigs.data(), cb.lens.data(), cb.msgs.data(),
-                                  cb.offs.data(), cb.m, valid);
-                  });
+  try {  // no C++ exception crosses the C ABI (c_guard below does the same for the device seams)
+    return run_seam(reqs, n, out,
+                    [&](const tmed_commit_request *rq, size_t nr, const Cands &cands, uint8_t *valid) {
+                      CandBatch cb;
+                      int rc = build_cand_batch(rq, nr, cands, cb);
+                      if (rc != TMED_OK) return rc;
+                      return verify(user, cb.pubs.data(), cb.sigs.data(), cb.lens.data(), cb.msgs.data(),
+                                    cb.offs.data(), cb.m, valid);
+                    });
+  } catch (const std::bad_alloc &) {
+    return TMED_ENOMEM;
+  }
 }
 
 // Host fallback of the GPU verifier for templates the device assembler cannot hold.
@@ -1525,8 +1530,7 @@ static size_t pipe_batch_sigs() {
   return e ? std::max<size_t>(1, strtoull(e, nullptr, 10)) : (size_t)1 << 19;
 }
 
-extern "C" int tmed_verify_commits(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
-                                   tmed_commit_result *out) {
+static int verify_commits_impl(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n, tmed_commit_result *out) {
   if (!ctx) return TMED_EINVAL;
   KcCall kc;
   reqs = keycache_resolve(ctx, reqs, n, kc);
@@ -1640,6 +1644,7 @@ void bs_destroy(tmed_ctx *c) {  // tmed_destroy: nothing may still read the wind
   if (!c->bs) return;
   (void)hipStreamSynchronize(c->copy_stream);
   (void)hipStreamSynchronize(c->stream);
+  if (c->lane1.s) (void)hipStreamSynchronize(c->lane1.s);  // key-cached batches alternate lanes
   delete c->bs;  // the windows' cache pins go with them (the cache is destroyed after this)
   c->bs = nullptr;
 }
@@ -1729,6 +1734,9 @@ static int bs_collect(tmed_ctx *ctx, BsStream &S, const BsWindow *keep, double p
 static void bs_abort(tmed_ctx *ctx, BsStream &S, int rc) {
   (void)hipStreamSynchronize(ctx->copy_stream);
   (void)hipStreamSynchronize(ctx->stream);
+  // a dropped key-cached batch may run on the second lane: its slot (idx % ns) and its lane
+  // (idx & 1) need not match the next batch's, so the lane must be idle before any slot is reused
+  if (ctx->lane1.s) (void)hipStreamSynchronize(ctx->lane1.s);
   for (BsBatch &b : S.slots)
     if (b.n) {
       b.n = 0;
@@ -1934,8 +1942,38 @@ static int bs_window(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t bat
   return TMED_OK;
 }
 
+// The seam's C entry points: no C++ exception may cross into the caller (a cgo caller would abort).
+// A host allocation that fails inside a call (the per-part plan vectors, a window's copies) returns
+// TMED_ENOMEM; the context's batch stream is then dropped like after any other error (bs_abort), so
+// no queued batch still reads the caller's buffers.
+template <class F>
+static int c_guard(tmed_ctx *ctx, F &&f) {
+  int rc;
+  try {
+    return f();
+  } catch (const std::bad_alloc &) {
+    rc = TMED_ENOMEM;
+  } catch (...) {
+    rc = TMED_EHIP;
+  }
+  if (ctx) {
+    try {
+      std::lock_guard<std::mutex> lk(ctx->mu);
+      if (ctx->bs) bs_abort(ctx, *ctx->bs, rc);
+    } catch (...) {
+    }
+  }
+  return rc;
+}
+
+extern "C" int tmed_verify_commits(tmed_ctx *ctx, const tmed_commit_request *reqs, size_t n,
+                                   tmed_commit_result *out) {
+  return c_guard(ctx, [&] { return verify_commits_impl(ctx, reqs, n, out); });
+}
+
 extern "C" int tmed_blocksync_submit(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t batch_blocks,
                                      tmed_commit_result *out) {
+  return c_guard(ctx, [&] {
   std::unique_ptr<BsWindow> win;
   int rc = bs_window(ctx, w, batch_blocks, out, win);
   if (rc != TMED_OK) return rc;
@@ -1954,10 +1992,12 @@ extern "C" int tmed_blocksync_submit(tmed_ctx *ctx, const tmed_blocksync_window 
     bs_pop_done(S, gone);
   }
   return rc;
+  });
 }
 
 extern "C" int tmed_blocksync_wait(tmed_ctx *ctx) {
   if (!ctx) return TMED_EINVAL;
+  return c_guard(ctx, [&] {
   std::vector<std::unique_ptr<BsWindow>> gone;
   int rc;
   {
@@ -1973,14 +2013,17 @@ extern "C" int tmed_blocksync_wait(tmed_ctx *ctx) {
     bs_pop_done(S, gone);
   }
   return rc;
+  });
 }
 
 extern "C" int tmed_blocksync_verify(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t batch_blocks,
                                      tmed_commit_result *out) {
-  std::unique_ptr<BsWindow> win;
-  int rc = bs_window(ctx, w, batch_blocks, out, win);
-  if (rc != TMED_OK || win->n == 0) return rc;
-  return run_pipelined(ctx, win->rq, win->n, win->bsz, win->keyset, out, nullptr);
+  return c_guard(ctx, [&] {
+    std::unique_ptr<BsWindow> win;
+    int rc = bs_window(ctx, w, batch_blocks, out, win);
+    if (rc != TMED_OK || win->n == 0) return rc;
+    return run_pipelined(ctx, win->rq, win->n, win->bsz, win->keyset, out, nullptr);
+  });
 }
 
 // ---- several GPUs in one process (§8e): contiguous shards balanced by signature count ----

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -38,6 +39,8 @@ struct HostPool {
   std::atomic<uint64_t> word{0};     // gen (24 bits) | parts (16) | next part (24)
   std::atomic<unsigned> done{0};     // parts finished in the current region
   const Job *job = nullptr;          // the current region's job (valid while a part is unfinished)
+  std::exception_ptr err;            // the region's first exception, rethrown by run() after the join
+  std::mutex err_mu;
   std::mutex m;
   std::condition_variable cv;
   static thread_local bool in_worker;
@@ -56,7 +59,12 @@ struct HostPool {
       uint64_t w = word.load(std::memory_order_acquire);
       if (next_of(w) >= parts_of(w)) return;
       if (!word.compare_exchange_weak(w, w + 1, std::memory_order_acq_rel)) continue;
-      (*job)(next_of(w));  // the region cannot complete before this part: job is its own
+      try {
+        (*job)(next_of(w));  // the region cannot complete before this part: job is its own
+      } catch (...) {        // a part that throws still counts as done: run() joins, then rethrows
+        std::lock_guard<std::mutex> g(err_mu);
+        if (!err) err = std::current_exception();
+      }
       done.fetch_add(1, std::memory_order_release);
     }
   }
@@ -96,12 +104,18 @@ struct HostPool {
     }
     cv.notify_all();
     in_region = true;
-    work();
+    work();  // never throws: parts' exceptions are caught and kept in err
     in_region = false;
     int spins = 0;
     while (done.load(std::memory_order_acquire) < parts)
       if (++spins < kPause) __builtin_ia32_pause();
       else std::this_thread::yield();
+    std::exception_ptr e;
+    {
+      std::lock_guard<std::mutex> g(err_mu);
+      std::swap(e, err);
+    }
+    if (e) std::rethrow_exception(e);  // every part has finished: no worker still reads the job
   }
   static HostPool &get() {
     static HostPool *p = new HostPool(std::max(1u, host_threads(~(size_t)0) - 1));

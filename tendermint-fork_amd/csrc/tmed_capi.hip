@@ -216,6 +216,11 @@ void tmed_destroy(tmed_ctx *c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
   bs_destroy(c);  // submitted blocksync windows never waited for (their cache pins go with them)
+  // The key-build worker (woken by any generic call that queued keys, and by bs_destroy's
+  // unpins) uses the staging buffers, events and streams below: join it before anything is freed.
+  keycache_destroy(c);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->lane1.s) hipStreamSynchronize(c->lane1.s);
   lane_release(c->lane1);
   for (DevBuf *b : {&c->d_a, &c->d_b, &c->d_msg, &c->d_off, &c->d_out, &c->d_c}) b->release();
   for (HostBuf *b : {&c->h_a, &c->h_b, &c->h_msg, &c->h_off, &c->h_out, &c->h_c}) b->release();
@@ -236,7 +241,6 @@ void tmed_destroy(tmed_ctx *c) {
     if (v.cp0) hipEventDestroy(v.cp0);
     if (v.cp1) hipEventDestroy(v.cp1);
   }
-  keycache_destroy(c);
   for (auto &kv : c->keysets) free_keyset(kv.second);
   c->keysets.clear();
   if (c->scratch_ev) hipEventDestroy(c->scratch_ev);

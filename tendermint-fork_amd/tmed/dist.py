@@ -112,13 +112,15 @@ def block_range(blocks: int, rank: int, world: int) -> tuple:
 
 
 def aggregate_blocksync(ok_bits: np.ndarray, blocks: int, rank: int, world: int, verified: int, mismatches: int,
-                        seconds: float, extra_max=(), phases=(), device=None) -> dict:
+                        seconds: float, extra_max=(), phases=(), device=None, per_rank=()) -> dict:
     """The only collectives of a sharded blocksync replay: ONE int64 all-reduce of
     the tallies (blocks ok, blocks, signatures verified, outcome mismatches), a MAX of the ranks' seam
     times (and of `extra_max`, e.g. marshalling times), ONE all-gather of the per-block decision
     bitmaps (packed bits, every rank padded to the largest shard) and of the per-rank `phases`
-    (diagnostics).  ok_bits: this rank's blocks [lo, hi) of block_range.  Returns the same dict on
-    every rank; "ok_bits" is the whole chain's bitmap in height order."""
+    (diagnostics) and of `per_rank` (this rank's placement and memory mode: NUMA node, CPUs, host
+    threads, pinned / pageable arenas — so an N-rank line cannot hide one rank on another path).
+    ok_bits: this rank's blocks [lo, hi) of block_range.  Returns the same dict on every rank;
+    "ok_bits" is the whole chain's bitmap in height order, "per_rank" one list per rank."""
     import torch
     import torch.distributed as dist
     dev = device if device is not None else torch.device("cpu")
@@ -129,6 +131,7 @@ def aggregate_blocksync(ok_bits: np.ndarray, blocks: int, rank: int, world: int,
     per = -(-blocks // world)  # the largest shard
     bits = torch.from_numpy(np.packbits(np.pad(ok_bits.astype(np.uint8), (0, per - (hi - lo))))).to(dev)
     ph = torch.tensor([float(x) for x in phases] + [float(seconds)], dtype=torch.float64, device=dev)
+    pr = torch.tensor([float(x) for x in per_rank] + [float(rank)], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tally)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -136,8 +139,10 @@ def aggregate_blocksync(ok_bits: np.ndarray, blocks: int, rank: int, world: int,
         dist.all_gather(gb, bits)
         gp = [torch.empty_like(ph) for _ in range(world)]
         dist.all_gather(gp, ph)
+        gr = [torch.empty_like(pr) for _ in range(world)]
+        dist.all_gather(gr, pr)
     else:
-        gb, gp = [bits], [ph]
+        gb, gp, gr = [bits], [ph], [pr]
     full = []
     for r in range(world):
         a, b = block_range(blocks, r, world)
@@ -146,4 +151,4 @@ def aggregate_blocksync(ok_bits: np.ndarray, blocks: int, rank: int, world: int,
     tm = tmax.tolist()
     return {"blocks_ok": ok, "blocks": nb, "verified": ver, "mismatches": mism, "seconds": tm[0],
             "extra_max": tm[1:], "ok_bits": np.concatenate(full) if full else np.zeros(0, np.uint8),
-            "phases": [g.tolist() for g in gp]}
+            "phases": [g.tolist() for g in gp], "per_rank": [g.tolist()[:-1] for g in gr]}

@@ -7,16 +7,25 @@ from __future__ import annotations
 import os
 
 
+BINDING: dict = {}  # this rank's host placement (tmed.affinity.bind_rank), reported by the benches
+
+
 def dist_setup():
-    """Returns (world, rank, local_rank, device, collective_device)."""
+    """Returns (world, rank, local_rank, device, collective_device).  Before anything touches the
+    GPU, the process is bound to the CPUs of its GPU's NUMA node (tmed.affinity.bind_rank; the
+    result is kept in BINDING)."""
     import torch
     import torch.distributed as dist
+    from .affinity import bind_rank
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     backend = os.environ.get("TMED_DIST_BACKEND", "nccl")
-    ndev = max(1, torch.cuda.device_count())
+    ndev = max(1, torch.cuda.device_count())  # counts devices without initialising HIP (this image)
     local = local % ndev if backend == "gloo" else local
+    BINDING.clear()
+    BINDING.update(bind_rank(local, local_world, ndev))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     coll = dev

@@ -132,9 +132,10 @@ def _blocksync_worker(rank, world, port, q):
     errs = verify_commits(None, reqs[lo:hi], verifier=_verifier, stats=stats) if hi > lo else []
     ok_bits = np.array([e is None for e in errs], np.uint8)
     agg = aggregate_blocksync(ok_bits, len(reqs), rank, world, sum(stats), mismatches=rank,
-                              seconds=1.0 + rank, extra_max=[0.25 * (rank + 1)], phases=[10.0 * rank, 1.0, 2.0])
+                              seconds=1.0 + rank, extra_max=[0.25 * (rank + 1)], phases=[10.0 * rank, 1.0, 2.0],
+                              per_rank=[rank % 2, 64, 8, 13 - rank, rank])
     q.put((rank, agg["blocks_ok"], agg["blocks"], agg["verified"], agg["mismatches"], agg["seconds"],
-           agg["extra_max"], agg["ok_bits"].tolist(), agg["phases"]))
+           agg["extra_max"], agg["ok_bits"].tolist(), agg["phases"], agg["per_rank"]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -169,11 +170,13 @@ def test_blocksync_aggregation_matches_single_process(world):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, ok, nb, ver, mism, sec, extra, bits, phases in res:
+    for rank, ok, nb, ver, mism, sec, extra, bits, phases, per_rank in res:
         assert (ok, nb, ver) == (int(single.sum()), len(reqs), sum(stats))
         assert mism == sum(range(world)) and sec == 1.0 + (world - 1) and extra == [0.25 * world]
         assert bits == single.tolist()
         assert [p[0] for p in phases] == [10.0 * r for r in range(world)] and all(p[-1] == 1.0 + r for r, p in enumerate(phases))
+        # every rank's placement and memory mode reaches every rank (C4's per-rank report)
+        assert per_rank == [[r % 2, 64, 8, 13 - r, r] for r in range(world)]
 
 
 def test_rehearsal_lines_name_simulated_gpus(monkeypatch):

@@ -170,15 +170,26 @@ def test_c3_light_client_changing_sets(engine, monkeypatch, keyed, pipelined):
             engine.keyset_free(ks)
 
 
+@pytest.fixture
+def cache_on():
+    """A fresh context with the key-set cache ON (tmed_init's default: what the drop-in gets)."""
+    from conftest import engine_with_env
+    e = engine_with_env(TMED_KEYCACHE=1)
+    e.keycache_config(True, 16 << 30)
+    yield e
+    e.close()
+
+
 @pytest.mark.parametrize("nv,H,pipe", [(8, 2050, None), (40, 2050, "70000")])
-def test_c3_many_sets_through_the_cache(engine, monkeypatch, nv, H, pipe):
+def test_c3_many_sets_through_the_cache(engine, cache_on, monkeypatch, nv, H, pipe):
     """A light-client call of 4,100 requests on 2,052 validator sets (one key changing per height)
-    passed WITHOUT key-set handles: the key-set cache resolves them.  Twice — the first call
-    generic (cold cache), the second on the cached key sets — both equal to the oracle loops; bad
-    signatures in four commits.  pipe: batches of ~70k signatures through the pipelined seam,
-    so every batch is planned and finished by the host workers part by part (aliases, staging
-    segments, template rows, scatter + alias copy + replay per planning part), ~1,700 requests
-    per batch."""
+    passed WITHOUT key-set handles to a cache-on context: the key-set cache resolves them.  Three
+    calls: the first generic (cold cache: every set's keys deferred to the context's worker), the
+    second and third keyed on the cached key sets (every lookup keyed, the third all hits), all
+    equal to the oracle loops; bad signatures in four commits, two of them inside the Trusting
+    prefix.  pipe: batches of ~70k signatures through the pipelined seam, so every batch is planned
+    and finished by the host workers part by part (aliases, staging segments, template rows,
+    scatter + alias copy + replay per planning part), ~1,700 requests per batch."""
     if pipe:
         monkeypatch.setenv("TMED_PIPE_SIGS", pipe)
     gap = 2
@@ -203,10 +214,20 @@ def test_c3_many_sets_through_the_cache(engine, monkeypatch, nv, H, pipe):
             reqs.append(req)
             exp.append(_oracle(req, ovs, oc))
     assert len(reqs) > 4096
-    for _ in range(2):
-        got = T.verify_commits(engine, reqs)
+    keys = ("lookups", "hits", "keyed_sets", "generic_sets", "keys_deferred", "keys_appended")
+    for call in range(3):
+        s0 = cache_on.keycache_stats()
+        got = T.verify_commits(cache_on, reqs)
+        cache_on.keycache_wait()
+        d = {k: cache_on.keycache_stats()[k] - s0[k] for k in keys}
         bad = [(q, str(got[q]), str(exp[q])) for q in range(len(reqs)) if not _same(got[q], exp[q])]
-        assert not bad, bad[:4]
+        assert not bad, (call, bad[:4])
+        if call == 0:
+            assert d["keyed_sets"] == 0 and d["generic_sets"] == H + gap and d["keys_deferred"] == H + gap + nv - 1, d
+        else:
+            assert d["generic_sets"] == 0 and d["keyed_sets"] == d["lookups"] == H + gap and d["keys_appended"] == 0, d
+        if call == 2:
+            assert d["hits"] == d["lookups"], d
     assert sum(e is not None for e in exp) >= 2
 
 
