@@ -29,8 +29,36 @@ namespace tmed {
 // read 2.25 lines per lookup, and its traffic cost ~10 % of the clock (profiles/r02/s4).
 // Entry 0 (the identity, cached form (1, 1, 1, 0)) is not stored per lane: every lane reads this
 // one row (an L2 hit), so the slab holds entries 1..8.
-__device__ const int4 kIdentityRow[8] = {{1, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}, {0, 0, 0, 0},
+// (a plain __device__ variable: global address space like the slab, so the row select below stays a
+// global pointer and the table loads are global_load — a select against a constant-address-space
+// row made them flat_load, which also count in lgkmcnt: every s_waitcnt lgkmcnt(0) of the B-row
+// prefetch then waited for the table rows in flight as well)
+__device__ int4 kIdentityRow[8] = {{1, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}, {0, 0, 0, 0},
                                           {1, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+
+// Cache policy of the main kernel's memory streams (A/B knob, bit mask; 0 = default policy):
+// 1 the per-lane table stores, 2 the per-lane table loads, 4 the radix-2^26 / 2^16 B rows
+// (global_load_lds), issued non-temporal (gfx950 nt: streamed, not kept in L2 / MALL).
+#ifndef TMED_SLAB_NT
+#define TMED_SLAB_NT 0
+#endif
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void slab_st(int4 *p, int4 v) {
+#if TMED_SLAB_NT & 1
+  const v4i32 x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<v4i32 *>(p));
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ int4 slab_ld(const int4 *p) {
+#if TMED_SLAB_NT & 2
+  const v4i32 x = __builtin_nontemporal_load(reinterpret_cast<const v4i32 *>(p));
+  return make_int4(x.x, x.y, x.z, x.w);
+#else
+  return *p;
+#endif
+}
 
 struct SlabTab {
   int4 *base;
@@ -48,8 +76,8 @@ struct SlabTab {
     for (int f = 0; f < 4; f++) {
       uint32_t w[8];
       fe_pack256(w, *fs[f]);
-      r[2 * f] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
-      r[2 * f + 1] = make_int4((int)w[4], (int)w[5], (int)w[6], (int)w[7]);
+      slab_st(r + 2 * f, make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]));
+      slab_st(r + 2 * f + 1, make_int4((int)w[4], (int)w[5], (int)w[6], (int)w[7]));
     }
   }
   __device__ __forceinline__ void load(int j, ge_cached &c) const {
@@ -74,7 +102,7 @@ struct SlabTab {
     const int4 *r = row(j);
     const int sx = swap ? 2 : 0;
 #pragma unroll
-    for (int q = 0; q < 8; q++) pv[q] = r[q < 4 ? (q ^ sx) : q];
+    for (int q = 0; q < 8; q++) pv[q] = slab_ld(r + (q < 4 ? (q ^ sx) : q));
   }
   __device__ __forceinline__ void take(ge_cached &c) const {
     fe *fs[4] = {&c.YpX, &c.YmX, &c.Z, &c.T2d};
@@ -118,7 +146,8 @@ struct BPf {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the previous take's LDS reads are done
 #pragma unroll
     for (int q = 0; q < 8; q++)
-      __builtin_amdgcn_global_load_lds((global_void *)(tab + (size_t)j * 8 + q), (lds_void *)(buf + q * 64), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((global_void *)(tab + (size_t)j * 8 + q), (lds_void *)(buf + q * 64), 16, 0,
+                                       (TMED_SLAB_NT & 4) ? 2 : 0);  // aux 2: nt
   }
   __device__ __forceinline__ void take(ge_niels &e) const {
     fe *fs[3] = {&e.YpX, &e.YmX, &e.XY2d};

@@ -35,7 +35,10 @@ type Engine struct {
 	pinMu  sync.Mutex
 	pin    unsafe.Pointer
 	pinCap int
+	arenas chan *arena // reusable C arenas (getArena / putArena)
 }
+
+func newEngine(ctx *C.tmed_ctx) *Engine { return &Engine{ctx: ctx, arenas: make(chan *arena, 8)} }
 
 // pinnedSigs returns the engine's pinned arena grown to at least n bytes (nil if
 // tmed_host_alloc fails: the caller then marshals into ordinary C memory).  Holds pinMu.
@@ -68,7 +71,7 @@ func Default() (*Engine, error) {
 			initErr = errors.New(C.GoString(C.tmed_strerror(rc)))
 			return
 		}
-		defEng = &Engine{ctx: ctx}
+		defEng = newEngine(ctx)
 	})
 	return defEng, initErr
 }
@@ -111,6 +114,7 @@ type ValSet struct {
 	// (a header's ValidatorsHash after its check): the key-set cache's key for this set.  Without it
 	// the library keys the set by a digest of PubKeys; a hit is compared key by key either way.
 	SetHash []byte
+	cmem    bool // PubKeys / Powers / Addresses already live in C memory (Batch.NewValSet)
 }
 
 // valset builds the C struct of v (its slices copied into the arena).
@@ -119,9 +123,17 @@ func (a *arena) valset(v *ValSet) C.tmed_valset {
 	if len(v.SetHash) == 32 {
 		sh = a.bytes(v.SetHash)
 	}
-	return C.tmed_valset{n: C.size_t(len(v.Powers)), pubkeys: a.bytes(v.PubKeys), powers: a.i64(v.Powers),
-		addresses: a.bytes(v.Addresses), total_power: C.int64_t(v.TotalPower), keyset: C.uint64_t(v.Keyset),
+	t := C.tmed_valset{n: C.size_t(len(v.Powers)), total_power: C.int64_t(v.TotalPower), keyset: C.uint64_t(v.Keyset),
 		keyset_index: a.u32(v.KeysetIndex), set_hash: sh}
+	if v.cmem {
+		t.pubkeys, t.addresses = ptr8(v.PubKeys), ptr8(v.Addresses)
+		if len(v.Powers) > 0 {
+			t.powers = (*C.int64_t)(unsafe.Pointer(&v.Powers[0]))
+		}
+	} else {
+		t.pubkeys, t.powers, t.addresses = a.bytes(v.PubKeys), a.i64(v.Powers), a.bytes(v.Addresses)
+	}
+	return t
 }
 
 type BlockID struct {
@@ -141,6 +153,64 @@ type CommitData struct {
 	TsNanos   []int32
 	Sigs      []byte // n x 64 (zero padded)
 	SigLens   []uint32
+	cmem      bool // every array already lives in C memory (Batch.NewCommit / WindowBuilder.NewCommit)
+}
+
+// newCommitIn: a CommitData of n signatures whose arrays are allocated in C memory (the arena;
+// Sigs at sigs when given: a pinned buffer) for the caller to fill in place — the shim then hands
+// the library those pointers with no second copy.
+func newCommitIn(a *arena, n int, sigs unsafe.Pointer) *CommitData {
+	c := &CommitData{cmem: true}
+	c.Flags = unsafe.Slice((*byte)(a.alloc(uintptr(n))), n)
+	c.Addresses = unsafe.Slice((*byte)(a.alloc(uintptr(20*n))), 20*n)
+	c.AddrLens = unsafe.Slice((*uint32)(a.alloc(uintptr(4*n))), n)
+	c.TsSeconds = unsafe.Slice((*int64)(a.alloc(uintptr(8*n))), n)
+	c.TsNanos = unsafe.Slice((*int32)(a.alloc(uintptr(4*n))), n)
+	if sigs == nil {
+		sigs = a.alloc(uintptr(64 * n))
+	}
+	c.Sigs = unsafe.Slice((*byte)(sigs), 64*n)
+	c.SigLens = unsafe.Slice((*uint32)(a.alloc(uintptr(4*n))), n)
+	return c
+}
+
+func newValSetIn(a *arena, n int) *ValSet {
+	v := &ValSet{cmem: true}
+	v.PubKeys = unsafe.Slice((*byte)(a.alloc(uintptr(32*n))), 32*n)
+	v.Powers = unsafe.Slice((*int64)(a.alloc(uintptr(8*n))), n)
+	v.Addresses = unsafe.Slice((*byte)(a.alloc(uintptr(20*n))), 20*n)
+	return v
+}
+
+func ptr8(b []byte) *C.uint8_t {
+	if len(b) == 0 {
+		return nil
+	}
+	return (*C.uint8_t)(unsafe.Pointer(&b[0]))
+}
+
+// commitC: the C struct of c (its arrays passed as they are when they live in C memory, else
+// copied into the arena once).  sigs: where the signatures go instead (nil: as above).
+func (a *arena) commitC(c *CommitData, sigs *C.uint8_t) C.tmed_commit {
+	t := C.tmed_commit{height: C.int64_t(c.Height), round: C.int32_t(c.Round), block_id: a.blockID(&c.BlockID),
+		n_sigs: C.size_t(len(c.Flags))}
+	if c.cmem {
+		t.flags, t.addresses, t.sigs = ptr8(c.Flags), ptr8(c.Addresses), ptr8(c.Sigs)
+		if len(c.Flags) > 0 {
+			t.ts_seconds = (*C.int64_t)(unsafe.Pointer(&c.TsSeconds[0]))
+			t.ts_nanos = (*C.int32_t)(unsafe.Pointer(&c.TsNanos[0]))
+			t.sig_lens = (*C.uint32_t)(unsafe.Pointer(&c.SigLens[0]))
+			t.address_lens = (*C.uint32_t)(unsafe.Pointer(&c.AddrLens[0]))
+		}
+	} else {
+		t.flags, t.addresses, t.sigs = a.bytes(c.Flags), a.bytes(c.Addresses), a.bytes(c.Sigs)
+		t.ts_seconds, t.ts_nanos = a.i64(c.TsSeconds), a.i32(c.TsNanos)
+		t.sig_lens, t.address_lens = a.u32(c.SigLens), a.u32(c.AddrLens)
+	}
+	if sigs != nil {
+		t.sigs = sigs
+	}
+	return t
 }
 
 type Request struct {
@@ -161,33 +231,75 @@ type Result struct {
 	Idx, IdxFirst, ValIdx  int32
 }
 
-// cgo pointer rules (Go 1.18: no runtime.Pinner): C memory must not hold Go
-// pointers, so every input is copied into one C arena for the duration of the
-// call (~200 B per signature, negligible next to the verification).  The
-// library itself copies into pinned buffers before launching.
-type arena struct{ ptrs []unsafe.Pointer }
+// cgo pointer rules (Go 1.18: no runtime.Pinner): C memory must not hold Go pointers, so every
+// input the library reads lives in C memory for the duration of the call.  An arena is a bump
+// allocator over C blocks that are KEPT across calls (Engine.getArena / putArena): a call costs no
+// malloc per array and no fresh pages.  The flat arrays of a Batch's commits and validator sets
+// are allocated in the arena first and filled by the caller in place (NewCommit / NewValSet: Go
+// slices over C memory), so nothing is copied twice; slices the caller built in Go memory (the
+// Request form) are copied in once.
+type arena struct {
+	blocks []unsafe.Pointer // C blocks, reused after reset
+	sizes  []uintptr
+	cur    int     // block being filled
+	off    uintptr // offset in it
+}
+
+const arenaBlock = 8 << 20
+
+func (a *arena) alloc(sz uintptr) unsafe.Pointer {
+	sz = (sz + 15) &^ 15
+	for a.cur < len(a.blocks) {
+		if a.off+sz <= a.sizes[a.cur] {
+			p := unsafe.Add(a.blocks[a.cur], a.off)
+			a.off += sz
+			return p
+		}
+		a.cur++
+		a.off = 0
+	}
+	n := uintptr(arenaBlock)
+	if sz > n {
+		n = sz
+	}
+	p := C.malloc(C.size_t(n))
+	a.blocks = append(a.blocks, p)
+	a.sizes = append(a.sizes, n)
+	a.cur, a.off = len(a.blocks)-1, sz
+	return p
+}
+
+// inArena: b already lives in this arena's C memory (filled in place): pass it as is.
+func (a *arena) inArena(b unsafe.Pointer) bool {
+	for i, blk := range a.blocks {
+		if uintptr(b) >= uintptr(blk) && uintptr(b) < uintptr(blk)+a.sizes[i] {
+			return true
+		}
+	}
+	return false
+}
 
 func (a *arena) bytes(b []byte) *C.uint8_t {
 	if len(b) == 0 {
 		return nil
 	}
-	p := C.CBytes(b)
-	a.ptrs = append(a.ptrs, p)
+	if a.inArena(unsafe.Pointer(&b[0])) {
+		return (*C.uint8_t)(unsafe.Pointer(&b[0]))
+	}
+	p := a.alloc(uintptr(len(b)))
+	copy(unsafe.Slice((*byte)(p), len(b)), b)
 	return (*C.uint8_t)(p)
-}
-
-func (a *arena) alloc(sz uintptr) unsafe.Pointer {
-	p := C.malloc(C.size_t(sz))
-	a.ptrs = append(a.ptrs, p)
-	return p
 }
 
 func (a *arena) i64(v []int64) *C.int64_t {
 	if len(v) == 0 {
 		return nil
 	}
+	if a.inArena(unsafe.Pointer(&v[0])) {
+		return (*C.int64_t)(unsafe.Pointer(&v[0]))
+	}
 	p := a.alloc(uintptr(len(v)) * 8)
-	copy((*[1 << 30]int64)(p)[:len(v):len(v)], v)
+	copy(unsafe.Slice((*int64)(p), len(v)), v)
 	return (*C.int64_t)(p)
 }
 
@@ -195,8 +307,11 @@ func (a *arena) i32(v []int32) *C.int32_t {
 	if len(v) == 0 {
 		return nil
 	}
+	if a.inArena(unsafe.Pointer(&v[0])) {
+		return (*C.int32_t)(unsafe.Pointer(&v[0]))
+	}
 	p := a.alloc(uintptr(len(v)) * 4)
-	copy((*[1 << 30]int32)(p)[:len(v):len(v)], v)
+	copy(unsafe.Slice((*int32)(p), len(v)), v)
 	return (*C.int32_t)(p)
 }
 
@@ -204,16 +319,50 @@ func (a *arena) u32(v []uint32) *C.uint32_t {
 	if len(v) == 0 {
 		return nil
 	}
+	if a.inArena(unsafe.Pointer(&v[0])) {
+		return (*C.uint32_t)(unsafe.Pointer(&v[0]))
+	}
 	p := a.alloc(uintptr(len(v)) * 4)
-	copy((*[1 << 30]uint32)(p)[:len(v):len(v)], v)
+	copy(unsafe.Slice((*uint32)(p), len(v)), v)
 	return (*C.uint32_t)(p)
 }
 
+func (a *arena) cstring(s string) *C.char {
+	p := a.alloc(uintptr(len(s)) + 1)
+	b := unsafe.Slice((*byte)(p), len(s)+1)
+	copy(b, s)
+	b[len(s)] = 0
+	return (*C.char)(p)
+}
+
+// reset keeps the blocks for the next call; free returns them to C.
+func (a *arena) reset() { a.cur, a.off = 0, 0 }
+
 func (a *arena) free() {
-	for _, p := range a.ptrs {
+	for _, p := range a.blocks {
 		C.free(p)
 	}
-	a.ptrs = nil
+	a.blocks, a.sizes = nil, nil
+	a.reset()
+}
+
+// getArena / putArena: a small free list of arenas per engine (calls may run concurrently).
+func (e *Engine) getArena() *arena {
+	select {
+	case a := <-e.arenas:
+		a.reset()
+		return a
+	default:
+		return &arena{}
+	}
+}
+
+func (e *Engine) putArena(a *arena) {
+	select {
+	case e.arenas <- a:
+	default:
+		a.free()
+	}
 }
 
 func (a *arena) blockID(b *BlockID) C.tmed_block_id {
@@ -223,8 +372,8 @@ func (a *arena) blockID(b *BlockID) C.tmed_block_id {
 
 // LoadKeyset decodes a validator set's keys once and builds their comb tables in HBM.
 func (e *Engine) LoadKeyset(pubKeys []byte) (uint64, error) {
-	var a arena
-	defer a.free()
+	a := e.getArena()
+	defer e.putArena(a)
 	var h C.uint64_t
 	if rc := C.tmed_keyset_load(e.ctx, a.bytes(pubKeys), C.size_t(len(pubKeys)/32), &h); rc != 0 {
 		return 0, errors.New(C.GoString(C.tmed_strerror(rc)))
@@ -238,8 +387,8 @@ func (e *Engine) FreeKeyset(h uint64) { C.tmed_keyset_free(e.ctx, C.uint64_t(h))
 // ExtendKeyset appends keys to a key set; existing keys keep their indexes, the new ones start at
 // the returned index (tmed_keyset_extend).
 func (e *Engine) ExtendKeyset(h uint64, pubKeys []byte) (uint32, error) {
-	var a arena
-	defer a.free()
+	a := e.getArena()
+	defer e.putArena(a)
 	var first C.uint32_t
 	if rc := C.tmed_keyset_extend(e.ctx, C.uint64_t(h), a.bytes(pubKeys), C.size_t(len(pubKeys)/32), &first); rc != 0 {
 		return 0, errors.New(C.GoString(C.tmed_strerror(rc)))
@@ -269,8 +418,8 @@ func (e *Engine) KeyCacheStats() (C.tmed_keycache_counters, error) {
 // WarmKeyCache builds a set's missing keys now — e.g. when EndBlock changes the validator set —
 // so that even its first commit is keyed (tmed_keycache_warm).
 func (e *Engine) WarmKeyCache(v *ValSet) error {
-	var a arena
-	defer a.free()
+	a := e.getArena()
+	defer e.putArena(a)
 	cv := a.valset(v)
 	if rc := C.tmed_keycache_warm(e.ctx, &cv); rc != 0 {
 		return errors.New(C.GoString(C.tmed_strerror(rc)))
@@ -288,12 +437,17 @@ func (e *Engine) VerifyCommits(reqs []Request) ([]Result, error) {
 
 func (e *Engine) verifyCommitsWith(reqs []Request, call func(*arena, *C.tmed_commit_request, C.size_t,
 	*C.tmed_commit_result) C.int) ([]Result, error) {
+	a := e.getArena()
+	defer e.putArena(a)
+	return e.verifyIn(a, reqs, call)
+}
+
+func (e *Engine) verifyIn(a *arena, reqs []Request, call func(*arena, *C.tmed_commit_request, C.size_t,
+	*C.tmed_commit_result) C.int) ([]Result, error) {
 	n := len(reqs)
 	if n == 0 {
 		return nil, nil
 	}
-	var a arena
-	defer a.free()
 	creqs := (*[1 << 26]C.tmed_commit_request)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_commit_request{})))[:n:n]
 	vs := (*[1 << 26]C.tmed_valset)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_valset{})))[:n:n]
 	cs := (*[1 << 26]C.tmed_commit)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_commit{})))[:n:n]
@@ -315,10 +469,7 @@ func (e *Engine) verifyCommitsWith(reqs []Request, call func(*arena, *C.tmed_com
 		c := r.Commit
 		cc, ok := seenC[c]
 		if !ok {
-			cs[i] = C.tmed_commit{height: C.int64_t(c.Height), round: C.int32_t(c.Round), block_id: a.blockID(&c.BlockID),
-				n_sigs: C.size_t(len(c.Flags)), flags: a.bytes(c.Flags), addresses: a.bytes(c.Addresses),
-				ts_seconds: a.i64(c.TsSeconds), ts_nanos: a.i32(c.TsNanos), sigs: a.bytes(c.Sigs), sig_lens: a.u32(c.SigLens),
-				address_lens: a.u32(c.AddrLens)}
+			cs[i] = a.commitC(c, nil)
 			cc = &cs[i]
 			seenC[c] = cc
 		}
@@ -326,17 +477,50 @@ func (e *Engine) verifyCommitsWith(reqs []Request, call func(*arena, *C.tmed_com
 		if r.BlockID != nil {
 			bids[i] = a.blockID(r.BlockID)
 		}
-		cid := C.CString(r.ChainID)
-		a.ptrs = append(a.ptrs, unsafe.Pointer(cid))
+		cid := a.cstring(r.ChainID)
 		creqs[i] = C.tmed_commit_request{mode: C.int(r.Mode), chain_id: cid, chain_id_len: C.uint32_t(len(r.ChainID)),
 			vals: cv, block_id: &bids[i], height: C.int64_t(r.Height), commit: cc,
 			trust_num: C.int64_t(r.TrustNum), trust_den: C.int64_t(r.TrustDen)}
 	}
 	res := make([]C.tmed_commit_result, n)
-	if rc := call(&a, &creqs[0], C.size_t(n), &res[0]); rc != 0 {
+	if rc := call(a, &creqs[0], C.size_t(n), &res[0]); rc != 0 {
 		return nil, errors.New(C.GoString(C.tmed_strerror(rc)))
 	}
 	return toResults(res), nil
+}
+
+// Batch is one VerifyCommits call whose commits and validator sets are flattened by the caller
+// straight into C memory (NewCommit / NewValSet), so the shim copies nothing: package types fills
+// them from its Commit / ValidatorSet (INTEGRATION.md §2).  Verify, then Release.
+type Batch struct {
+	e    *Engine
+	a    *arena
+	reqs []Request
+}
+
+func (e *Engine) NewBatch() *Batch { return &Batch{e: e, a: e.getArena()} }
+
+// NewCommit: a commit of n signatures to fill in place.
+func (b *Batch) NewCommit(n int) *CommitData { return newCommitIn(b.a, n, nil) }
+
+// NewValSet: a validator set of n validators to fill in place (TotalPower / SetHash set by the caller).
+func (b *Batch) NewValSet(n int) *ValSet { return newValSetIn(b.a, n) }
+
+func (b *Batch) Add(r Request) { b.reqs = append(b.reqs, r) }
+
+func (b *Batch) Verify() ([]Result, error) {
+	return b.e.verifyIn(b.a, b.reqs, func(a *arena, creqs *C.tmed_commit_request, n C.size_t,
+		res *C.tmed_commit_result) C.int {
+		return C.tmed_verify_commits(b.e.ctx, creqs, n, res)
+	})
+}
+
+// Release returns the batch's C memory to the engine (the CommitData / ValSet it made are invalid after).
+func (b *Batch) Release() {
+	if b.a != nil {
+		b.e.putArena(b.a)
+		b.a, b.reqs = nil, nil
+	}
 }
 
 func toResults(res []C.tmed_commit_result) []Result {
@@ -358,6 +542,7 @@ type BlocksyncWindow struct {
 	BlockIDs []BlockID
 	Heights  []int64
 	Commits  []*CommitData
+	builder  *WindowBuilder // set by WindowBuilder.Window: the commits already live in its C memory
 }
 
 // BlocksyncVerify returns the VerifyCommitLight outcome of every block of the window,
@@ -368,8 +553,8 @@ func (e *Engine) BlocksyncVerify(w *BlocksyncWindow, batchBlocks int) ([]Result,
 	if n == 0 {
 		return nil, nil
 	}
-	var a arena
-	defer a.free()
+	a := e.getArena()
+	defer e.putArena(a)
 	vs := (*C.tmed_valset)(a.alloc(unsafe.Sizeof(C.tmed_valset{})))
 	*vs = a.valset(w.Vals)
 	cs := (*[1 << 26]C.tmed_commit)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_commit{})))[:n:n]
@@ -385,21 +570,15 @@ func (e *Engine) BlocksyncVerify(w *BlocksyncWindow, batchBlocks int) ([]Result,
 	off := 0
 	for i, c := range w.Commits {
 		sigs := (*C.uint8_t)(nil)
-		if arenaBase != nil && len(c.Sigs) > 0 {
+		if !c.cmem && arenaBase != nil && len(c.Sigs) > 0 {
 			p := unsafe.Add(arenaBase, off)
 			copy(unsafe.Slice((*byte)(p), len(c.Sigs)), c.Sigs)
 			sigs, off = (*C.uint8_t)(p), off+len(c.Sigs)
-		} else {
-			sigs = a.bytes(c.Sigs)
 		}
-		cs[i] = C.tmed_commit{height: C.int64_t(c.Height), round: C.int32_t(c.Round), block_id: a.blockID(&c.BlockID),
-			n_sigs: C.size_t(len(c.Flags)), flags: a.bytes(c.Flags), addresses: a.bytes(c.Addresses),
-			ts_seconds: a.i64(c.TsSeconds), ts_nanos: a.i32(c.TsNanos), sigs: sigs, sig_lens: a.u32(c.SigLens),
-			address_lens: a.u32(c.AddrLens)}
+		cs[i] = a.commitC(c, sigs)
 		bids[i] = a.blockID(&w.BlockIDs[i])
 	}
-	cid := C.CString(w.ChainID)
-	a.ptrs = append(a.ptrs, unsafe.Pointer(cid))
+	cid := a.cstring(w.ChainID)
 	win := (*C.tmed_blocksync_window)(a.alloc(unsafe.Sizeof(C.tmed_blocksync_window{})))
 	*win = C.tmed_blocksync_window{chain_id: cid, chain_id_len: C.uint32_t(len(w.ChainID)), vals: vs,
 		n_blocks: C.size_t(n), block_ids: &bids[0], heights: a.i64(w.Heights), commits: &cs[0]}
@@ -416,7 +595,7 @@ func (e *Engine) BlocksyncVerify(w *BlocksyncWindow, batchBlocks int) ([]Result,
 // into C memory: cgo forbids C retaining Go pointers after a call returns).
 type PendingWindow struct {
 	e   *Engine
-	a   arena
+	a   *arena
 	pin unsafe.Pointer
 	res *C.tmed_commit_result
 	n   int
@@ -427,11 +606,19 @@ type PendingWindow struct {
 // drained between windows.  When it returns, every earlier submitted window's Results are final.
 func (e *Engine) BlocksyncSubmit(w *BlocksyncWindow, batchBlocks int) (*PendingWindow, error) {
 	n := len(w.Commits)
-	p := &PendingWindow{e: e, n: n}
+	if w.builder != nil { // built in place (NewWindow): its arena and pinned buffer travel with it
+		return w.builder.submit(w, batchBlocks)
+	}
+	p := &PendingWindow{e: e, n: n, a: e.getArena()}
 	if n == 0 {
 		return p, nil
 	}
-	a := &p.a
+	return p.submit(w, batchBlocks, true)
+}
+
+// submit marshals w into p's arena (signatures into p.pin when copyPin) and queues it.
+func (p *PendingWindow) submit(w *BlocksyncWindow, batchBlocks int, copyPin bool) (*PendingWindow, error) {
+	e, a, n := p.e, p.a, len(w.Commits)
 	vs := (*C.tmed_valset)(a.alloc(unsafe.Sizeof(C.tmed_valset{})))
 	*vs = a.valset(w.Vals)
 	cs := (*[1 << 26]C.tmed_commit)(a.alloc(uintptr(n) * unsafe.Sizeof(C.tmed_commit{})))[:n:n]
@@ -441,27 +628,21 @@ func (e *Engine) BlocksyncSubmit(w *BlocksyncWindow, batchBlocks int) (*PendingW
 		total += len(c.Sigs)
 	}
 	// a pinned buffer per window in flight (the engine's shared arena serves synchronous calls)
-	if total > 0 && C.tmed_host_alloc(C.size_t(total), &p.pin) != 0 {
+	if copyPin && total > 0 && C.tmed_host_alloc(C.size_t(total), &p.pin) != 0 {
 		p.pin = nil
 	}
 	off := 0
 	for i, c := range w.Commits {
 		sigs := (*C.uint8_t)(nil)
-		if p.pin != nil && len(c.Sigs) > 0 {
+		if copyPin && !c.cmem && p.pin != nil && len(c.Sigs) > 0 {
 			q := unsafe.Add(p.pin, off)
 			copy(unsafe.Slice((*byte)(q), len(c.Sigs)), c.Sigs)
 			sigs, off = (*C.uint8_t)(q), off+len(c.Sigs)
-		} else {
-			sigs = a.bytes(c.Sigs)
 		}
-		cs[i] = C.tmed_commit{height: C.int64_t(c.Height), round: C.int32_t(c.Round), block_id: a.blockID(&c.BlockID),
-			n_sigs: C.size_t(len(c.Flags)), flags: a.bytes(c.Flags), addresses: a.bytes(c.Addresses),
-			ts_seconds: a.i64(c.TsSeconds), ts_nanos: a.i32(c.TsNanos), sigs: sigs, sig_lens: a.u32(c.SigLens),
-			address_lens: a.u32(c.AddrLens)}
+		cs[i] = a.commitC(c, sigs)
 		bids[i] = a.blockID(&w.BlockIDs[i])
 	}
-	cid := C.CString(w.ChainID)
-	a.ptrs = append(a.ptrs, unsafe.Pointer(cid))
+	cid := a.cstring(w.ChainID)
 	win := (*C.tmed_blocksync_window)(a.alloc(unsafe.Sizeof(C.tmed_blocksync_window{})))
 	*win = C.tmed_blocksync_window{chain_id: cid, chain_id_len: C.uint32_t(len(w.ChainID)), vals: vs,
 		n_blocks: C.size_t(n), block_ids: &bids[0], heights: a.i64(w.Heights), commits: &cs[0]}
@@ -497,8 +678,59 @@ func (p *PendingWindow) free() {
 		C.tmed_host_free(p.pin)
 		p.pin = nil
 	}
-	p.a.free()
+	if p.a != nil {
+		p.e.putArena(p.a)
+		p.a = nil
+	}
 	p.n = 0
+}
+
+// WindowBuilder lays a blocksync window out in C memory as the reactor flattens its blocks: each
+// commit's arrays in the window's arena, its signatures in the window's pinned buffer (the library
+// DMAs them from there), filled in place by package types (INTEGRATION.md §3: up to the
+// VerifyCommitLight crossing).  Submit with BlocksyncSubmit(w.Window(...)).
+type WindowBuilder struct {
+	p   *PendingWindow
+	off uintptr
+	cap uintptr
+}
+
+// NewWindow: room for maxSigs signatures over the window's commits.
+func (e *Engine) NewWindow(maxSigs int) *WindowBuilder {
+	b := &WindowBuilder{p: &PendingWindow{e: e, a: e.getArena()}}
+	if maxSigs > 0 && C.tmed_host_alloc(C.size_t(64*maxSigs), &b.p.pin) != 0 {
+		b.p.pin = nil // no page-locked memory: the signatures go to the arena (the library stages them)
+	}
+	if b.p.pin != nil {
+		b.cap = uintptr(64 * maxSigs)
+	}
+	return b
+}
+
+// NewCommit: a commit of n signatures, its Sigs in the pinned buffer when room is left.
+func (b *WindowBuilder) NewCommit(n int) *CommitData {
+	var sigs unsafe.Pointer
+	if b.p.pin != nil && b.off+uintptr(64*n) <= b.cap {
+		sigs = unsafe.Add(b.p.pin, b.off)
+		b.off += uintptr(64 * n)
+	}
+	return newCommitIn(b.p.a, n, sigs)
+}
+
+// Window wraps the built commits for BlocksyncSubmit.
+func (b *WindowBuilder) Window(chainID string, vals *ValSet, blockIDs []BlockID, heights []int64,
+	commits []*CommitData) *BlocksyncWindow {
+	return &BlocksyncWindow{ChainID: chainID, Vals: vals, BlockIDs: blockIDs, Heights: heights, Commits: commits,
+		builder: b}
+}
+
+func (b *WindowBuilder) submit(w *BlocksyncWindow, batchBlocks int) (*PendingWindow, error) {
+	p := b.p
+	p.n = len(w.Commits)
+	if p.n == 0 {
+		return p, nil
+	}
+	return p.submit(w, batchBlocks, false)
 }
 
 // ValsetHashes returns ValidatorSet.Hash() of every set: set s is validators
@@ -508,8 +740,8 @@ func (e *Engine) ValsetHashes(pubKeys []byte, powers []int64, setOff []uint32) (
 	if ns <= 0 {
 		return nil, nil
 	}
-	var a arena
-	defer a.free()
+	a := e.getArena()
+	defer e.putArena(a)
 	out := (*[1 << 26][32]byte)(a.alloc(uintptr(ns) * 32))[:ns:ns]
 	if rc := C.tmed_valset_hashes(e.ctx, a.bytes(pubKeys), a.i64(powers), a.u32(setOff), C.size_t(ns),
 		(*C.uint8_t)(unsafe.Pointer(&out[0]))); rc != 0 {
@@ -535,8 +767,8 @@ func (e *Engine) MerkleRoots(trees [][][]byte) ([][32]byte, error) {
 		treeOff = append(treeOff, uint32(len(leafOff)-1))
 	}
 	flat = append(flat, make([]byte, 8)...) // the device reader may touch the last dword
-	var a arena
-	defer a.free()
+	a := e.getArena()
+	defer e.putArena(a)
 	lo := (*[1 << 26]C.uint64_t)(a.alloc(uintptr(len(leafOff)) * 8))[:len(leafOff):len(leafOff)]
 	for i, v := range leafOff {
 		lo[i] = C.uint64_t(v)
@@ -589,8 +821,8 @@ func (e *Engine) batch(pubKeys []byte, msgs, sigs [][]byte, zip215 bool) ([]bool
 	if n == 0 {
 		return nil, nil
 	}
-	var a arena
-	defer a.free()
+	a := e.getArena()
+	defer e.putArena(a)
 	pk, sg, sl, mg, mo := batchArgs(&a, pubKeys, msgs, sigs)
 	out := (*[1 << 28]C.uint8_t)(a.alloc(uintptr(n)))[:n:n]
 	var rc C.int
@@ -625,7 +857,7 @@ func NewPool(n int) (*Pool, error) {
 			}
 			return nil, errors.New(C.GoString(C.tmed_strerror(rc)))
 		}
-		p.engines = append(p.engines, &Engine{ctx: ctx})
+		p.engines = append(p.engines, newEngine(ctx))
 	}
 	return p, nil
 }

@@ -438,6 +438,37 @@ def seam_phase_us():
     return tuple(out)
 
 
+def run_requests(engine, reqs, n: int, verifier=None):
+    """tmed_verify_commits (engine), tmed_verify_commits_multi (a list of engines) or
+    tmed_verify_commits_with (verifier: a Python batch verifier, the CPU tests) over n C requests
+    already marshalled (a POINTER(_RequestC) or an array of them); returns the _ResultC array."""
+    l = _bind()
+    res = (_ResultC * max(n, 1))()
+    if verifier is None and isinstance(engine, (list, tuple)):  # several GPUs, one process
+        rc = l.tmed_verify_commits_multi(_ctx_array(engine), len(engine), reqs, n, res)
+    elif verifier is None:
+        rc = l.tmed_verify_commits(engine._h, reqs, n, res)
+    else:
+        def cb(user, pubs, sigs, lens, msgs, offs, m, out):
+            try:
+                P = ctypes.POINTER(ctypes.c_uint8)
+                pa = np.ctypeslib.as_array(ctypes.cast(pubs, P), (m * 32,)).reshape(m, 32)
+                sa = np.ctypeslib.as_array(ctypes.cast(sigs, P), (m * 64,)).reshape(m, 64)
+                la = np.ctypeslib.as_array(ctypes.cast(lens, ctypes.POINTER(ctypes.c_uint32)), (m,))
+                oa = np.ctypeslib.as_array(ctypes.cast(offs, ctypes.POINTER(ctypes.c_uint32)), (m + 1,))
+                ma = np.ctypeslib.as_array(ctypes.cast(msgs, P), (int(oa[-1]) + 1,))
+                dec = verifier(pa.copy(), sa.copy(), la.copy(), ma.copy(), oa.copy())
+                np.ctypeslib.as_array(ctypes.cast(out, P), (m,))[:] = dec
+                return 0
+            except Exception:  # never raise across the ABI
+                return -3
+        fn = VERIFY_FN(cb)
+        rc = l.tmed_verify_commits_with(reqs, n, res, fn, None)
+    if rc != TMED_OK:
+        raise TmedError(rc, "tmed_verify_commits")
+    return res
+
+
 def verify_commits(engine, requests: Sequence[tuple], verifier=None, stats: Optional[list] = None):
     """Verify many commits with one device batch.
 
@@ -467,29 +498,7 @@ def verify_commits(engine, requests: Sequence[tuple], verifier=None, stats: Opti
         keep.extend([vs, cc, cid, bid])
         reqs[q] = _RequestC(mode, cid, len(cid), ctypes.pointer(vs),
                             ctypes.pointer(bid) if bid is not None else None, height, ctypes.pointer(cc), num, den)
-    res = (_ResultC * max(n, 1))()
-    if verifier is None and isinstance(engine, (list, tuple)):  # several GPUs, one process
-        rc = l.tmed_verify_commits_multi(_ctx_array(engine), len(engine), reqs, n, res)
-    elif verifier is None:
-        rc = l.tmed_verify_commits(engine._h, reqs, n, res)
-    else:
-        def cb(user, pubs, sigs, lens, msgs, offs, m, out):
-            try:
-                P = ctypes.POINTER(ctypes.c_uint8)
-                pa = np.ctypeslib.as_array(ctypes.cast(pubs, P), (m * 32,)).reshape(m, 32)
-                sa = np.ctypeslib.as_array(ctypes.cast(sigs, P), (m * 64,)).reshape(m, 64)
-                la = np.ctypeslib.as_array(ctypes.cast(lens, ctypes.POINTER(ctypes.c_uint32)), (m,))
-                oa = np.ctypeslib.as_array(ctypes.cast(offs, ctypes.POINTER(ctypes.c_uint32)), (m + 1,))
-                ma = np.ctypeslib.as_array(ctypes.cast(msgs, P), (int(oa[-1]) + 1,))
-                dec = verifier(pa.copy(), sa.copy(), la.copy(), ma.copy(), oa.copy())
-                np.ctypeslib.as_array(ctypes.cast(out, P), (m,))[:] = dec
-                return 0
-            except Exception:  # never raise across the ABI
-                return -3
-        fn = VERIFY_FN(cb)
-        rc = l.tmed_verify_commits_with(reqs, n, res, fn, None)
-    if rc != TMED_OK:
-        raise TmedError(rc, "tmed_verify_commits")
+    res = run_requests(engine, reqs, n, verifier)
     out = []
     for q, (mode, vals, chain_id, block_id, height, commit, num, den) in enumerate(requests):
         out.append(_to_error(res[q].code, res[q], vals, block_id, commit))

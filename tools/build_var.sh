@@ -8,7 +8,7 @@ name=$1; shift
 cd "$(dirname "$0")/../tendermint-fork_amd"
 make -s >/dev/null
 mkdir -p lib_var/$name /tmp/tmed_var_$name
-all="kernels latency tmed_capi signbytes microbench commit keyset merkle zip215"
+all="kernels latency tmed_capi signbytes microbench commit keyset merkle zip215 keycache"
 objs=""
 for s in $all; do
   if [[ " ${VAR_SRCS:-kernels} " == *" $s "* ]]; then
