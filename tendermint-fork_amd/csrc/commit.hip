@@ -1419,17 +1419,15 @@ static const tmed_commit_request *keycache_resolve(tmed_ctx *ctx, const tmed_com
         sr.key = tmed::kc_key(v.pubkeys, v.n, v.set_hash);
         sr.e = tmed::keycache_find(ctx, sr.key);
       }
-      // the byte compares (~5.6 KB per set from the caller and as many from the entry, both cold):
-      // the next set's two arrays are prefetched while this one is compared
+      // the byte compares (~5.6 KB per set from the caller, cold, against the pool's key table through
+      // the entry's indexes): the next set's keys and indexes are prefetched while this one is compared
       auto prefetch_set = [&](size_t s) {
         if (s >= hi || sets[s].skip || !sets[s].e) return;
         const tmed_valset &v = *sets[s].v;
-        const uint8_t *a = v.pubkeys, *b = sets[s].e->pubs.data();
-        const size_t nb = std::min(32 * v.n, sets[s].e->pubs.size());
-        for (size_t o = 0; o < nb; o += 64) {
-          __builtin_prefetch(a + o, 0, 0);
-          __builtin_prefetch(b + o, 0, 0);
-        }
+        const uint8_t *a = v.pubkeys, *b = (const uint8_t *)sets[s].e->idx.data();
+        const size_t nb = std::min(v.n, sets[s].e->idx.size());
+        for (size_t o = 0; o < 32 * v.n; o += 64) __builtin_prefetch(a + o, 0, 0);
+        for (size_t o = 0; o < 4 * nb; o += 64) __builtin_prefetch(b + o, 0, 0);
       };
       prefetch_set(lo);
       for (size_t s = lo; s < hi; s++) {
@@ -1437,7 +1435,7 @@ static const tmed_commit_request *keycache_resolve(tmed_ctx *ctx, const tmed_com
         prefetch_set(s + 1);
         if (sr.skip) continue;
         const tmed_valset &v = *sr.v;
-        sr.hit = sr.e && tmed::kc_same_keys(*sr.e, v.pubkeys, v.n);
+        sr.hit = sr.e && tmed::keycache_same_keys(ctx, *sr.e, v.pubkeys, v.n);
         if (sr.hit) {
           const_cast<tmed::KcSet *>(sr.e)->touch(tick);
           h++;

@@ -101,6 +101,8 @@ uint64_t keycache_pool_handle(const tmed_ctx *c);  // 0 before the first key is 
 // KeyCache::find: read-only, callable from several threads while the caller holds ctx->mu (after
 // keycache_touch has created the cache)
 const KcSet *keycache_find(tmed_ctx *c, const KcKey &key);
+// a cached set's keys equal pubs[0, n) byte for byte (read-only: safe from a call's threads under ctx->mu)
+bool keycache_same_keys(const tmed_ctx *c, const KcSet &e, const uint8_t *pubs, size_t n);
 uint64_t keycache_call_tick(tmed_ctx *c);                        // KeyCache::call_tick
 void keycache_hits(tmed_ctx *c, size_t sets, size_t sigs);       // KeyCache::hits
 void keycache_touch(tmed_ctx *c);

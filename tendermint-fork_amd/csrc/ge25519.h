@@ -50,6 +50,22 @@ TMED_HD void ge_p1p1_to_p3(ge_p3 &r, const ge_p1p1 &p) {
   fe_mul(r.T, p.X, p.Y);
 }
 TMED_HD void ge_p3_to_p2(ge_p2 &r, const ge_p3 &p) { fe_copy(r.X, p.X); fe_copy(r.Y, p.Y); fe_copy(r.Z, p.Z); }
+// Cached (Y+X, Y-X, Z, 2dT) -> extended, every coordinate scaled by 2 (the same point):
+// (Y+X) - (Y-X) = 2X, (Y+X) + (Y-X) = 2Y, 2Z, and 2T = 2dT * d^-1 — one product.  Outputs
+// carried (the inputs may be unpacked table entries, limbs up to twice a carried limb).
+TMED_HD void ge_cached_to_p3(ge_p3 &r, const ge_cached &c) {
+  fe inv_d;  // d^-1 mod p, carried form
+  const int32_t k[10] = {30013526, 3972531, -24787780, 12719051, 2979674, -4599962, -15693209, -3644061, 18959709, -16629253};
+#pragma unroll
+  for (int i = 0; i < 10; i++) inv_d.v[i] = k[i];
+  fe_sub(r.X, c.YpX, c.YmX);
+  fe_carry(r.X, r.X);
+  fe_add(r.Y, c.YpX, c.YmX);
+  fe_carry(r.Y, r.Y);
+  fe_add(r.Z, c.Z, c.Z);
+  fe_carry(r.Z, r.Z);
+  fe_mul(r.T, c.T2d, inv_d);
+}
 TMED_HD void ge_p3_to_cached(ge_cached &r, const ge_p3 &p) {
   fe d2; fe_const_d2(d2);
   fe_add(r.YpX, p.Y, p.X);

@@ -386,8 +386,8 @@ __global__ __launch_bounds__(kThreadsPerBlock, TMED_PREP_R_WAVES) void verify_pr
 #pragma unroll
   for (int j = 0; j < 8; j++) { k[j] = (uint32_t)w[j]; s[j] = (uint32_t)w[8 + j]; }
   bool dneg;
-  int W;
-  hs_scalars(k, s, cr, dr, er, dneg, W, /*raw_e=*/true);  // (hs_prep_r's two phases, in this order)
+  int W, Wl;  // W: the tight window count (top digits 0..16, hs_straus), Wl the latency kernels' count
+  hs_scalars(k, s, cr, dr, er, dneg, Wl, /*raw_e=*/true, &W);  // (hs_prep_r's two phases, in this order)
   const bool ok = prep[(size_t)9 * stride + slot].x != 0;  // word 36
 #pragma unroll
   for (int j = 0; j < 8; j++) { w[j] = (int32_t)cr[j]; w[13 + j] = (int32_t)er[j]; }

@@ -160,16 +160,16 @@ struct AddrIndex {
   }
 };
 
-// One cached validator set: its keys (for the byte compare) and validator i -> pool index; and,
-// built at the first LightTrusting request against it, its address index over a private copy of
-// the addresses that request passed (a later request uses it only if its addresses are the same
-// bytes: tmed_valset.addresses is not part of the cache key).
+// One cached validator set: validator i -> pool index (the byte compare of a hit reads the keys
+// through it from the pool's own key table: KeyCache::same_keys); and, built at the first
+// LightTrusting request against it, its address index over a private copy of the addresses that
+// request passed (a later request uses it only if its addresses are the same bytes:
+// tmed_valset.addresses is not part of the cache key).
 struct KcSet {
-  std::vector<uint8_t> pubs;
   std::vector<uint32_t> idx;
   std::atomic<uint64_t> tick{0};  // LRU: the call that last used it (set from a call's threads)
   void touch(uint64_t t) { tick.store(t, std::memory_order_relaxed); }
-  size_t bytes() const { return pubs.size() + 4 * idx.size() + 64; }
+  size_t bytes() const { return 4 * idx.size() + 64; }
   // nullptr when `addrs` (n x 20) differ from the addresses the cached index was built from
   const AddrIndex *addr_index(const uint8_t *addrs, size_t n) const {
     std::call_once(addr_once_, [&] {
@@ -185,9 +185,6 @@ struct KcSet {
   mutable AddrIndex addr_ix_;
 };
 
-inline bool kc_same_keys(const KcSet &s, const uint8_t *pubs, size_t n) {
-  return s.pubs.size() == 32 * n && memcmp(s.pubs.data(), pubs, 32 * n) == 0;
-}
 
 // Counters (tmed_keycache_stats).
 struct KcCounters {
@@ -220,6 +217,22 @@ class KeyCache {
   KcCounters st;
 
   size_t pool_keys() const { return slot_.size(); }
+
+  // A cached set's keys are the caller's, byte for byte: key i against pool key idx[i] (the pool's
+  // key table: a few hundred KB, cache-resident, against a private copy of every set's keys —
+  // ~5.6 KB per 175-validator set, 56 MB for a light client's 10k sets, read back on every call).
+  // A stale set_hash or a digest collision therefore costs a miss, never a wrong index.
+  bool same_keys(const KcSet &e, const uint8_t *pubs, size_t n) const {
+    if (e.idx.size() != n) return false;
+    const uint8_t *pk = keys_.data();
+    for (size_t i = 0; i < n; i++) {
+      uint64_t a[4], b[4];
+      memcpy(a, pk + 32 * (size_t)e.idx[i], 32);
+      memcpy(b, pubs + 32 * i, 32);
+      if (((a[0] ^ b[0]) | (a[1] ^ b[1]) | (a[2] ^ b[2]) | (a[3] ^ b[3])) != 0) return false;
+    }
+    return true;
+  }
   size_t sets_cached() const { return sets_.size(); }
   size_t pending_keys() const { return pending_.size() / 32; }
   bool has_work() const { return !pending_.empty() || !deferred_.empty(); }
@@ -266,7 +279,7 @@ class KeyCache {
     auto it = sets_.find(key);
     if (it != sets_.end()) {
       KcSet &s = *it->second;
-      if (kc_same_keys(s, pubs, n)) {
+      if (same_keys(s, pubs, n)) {
         s.touch(++tick_);
         st.hits++;
         return keyed(it->second.get(), sigs, hold);
@@ -274,10 +287,9 @@ class KeyCache {
       drop_(it);  // same key, other keys (a stale or wrong set_hash, a digest collision)
     }
     auto e = std::make_unique<KcSet>();
-    e->pubs.assign(pubs, pubs + 32 * n);
     e->idx.resize(n);
     std::vector<size_t> fresh;  // first position of each key the pool lacks
-    if (!resolve_(*e, fresh)) return generic(sigs);  // more distinct new keys than the pool can hold
+    if (!resolve_(*e, pubs, fresh)) return generic(sigs);  // more distinct new keys than the pool can hold
     if (fresh.empty()) return insert_keyed(std::move(e), key, sigs, hold);
     const size_t nf = fresh.size();
     if (slot_.size() + nf > be.capacity_keys()) {
@@ -285,7 +297,7 @@ class KeyCache {
       reset();
       st.pool_resets++;
       fresh.clear();
-      if (!resolve_(*e, fresh)) return generic(sigs);
+      if (!resolve_(*e, pubs, fresh)) return generic(sigs);
     }
     if (!force_build && sigs < kAmortizeSigsPerKey * fresh.size()) {  // generic now, keys built after the call
       for (size_t f : fresh) {
@@ -297,7 +309,7 @@ class KeyCache {
     std::vector<uint8_t> add(32 * fresh.size());
     for (size_t j = 0; j < fresh.size(); j++) memcpy(&add[32 * j], pubs + 32 * fresh[j], 32);
     if (!append_(add.data(), fresh.size())) return generic(sigs);
-    resolve_(*e, fresh);  // every key present now
+    resolve_(*e, pubs, fresh);  // every key present now
     return insert_keyed(std::move(e), key, sigs, hold);
   }
 
@@ -365,6 +377,7 @@ class KeyCache {
   void reset() {
     be.reset();
     slot_.clear();
+    keys_.clear();
     if (users_ > 0)
       for (auto &kv : sets_) retired_.push_back(std::move(kv.second));
     sets_.clear();
@@ -388,11 +401,11 @@ class KeyCache {
   }
   // idx of every key already in the pool; `fresh` gets the first position of each key it lacks.
   // False when there are more such keys than the pool could ever hold.
-  bool resolve_(KcSet &e, std::vector<size_t> &fresh) {
+  bool resolve_(KcSet &e, const uint8_t *pubs, std::vector<size_t> &fresh) {
     const size_t n = e.idx.size();
     std::unordered_map<Pub32, uint32_t, Pub32Hash> local;  // new keys repeated inside the set
     for (size_t i = 0; i < n; i++) {
-      const Pub32 k = pub32(&e.pubs[32 * i]);
+      const Pub32 k = pub32(pubs + 32 * i);
       auto s = slot_.find(k);
       if (s != slot_.end()) {
         e.idx[i] = s->second;
@@ -414,6 +427,7 @@ class KeyCache {
   bool append_(const uint8_t *keys, size_t m) {
     if (be.append(keys, m) != 0) return false;
     for (size_t j = 0; j < m; j++) slot_.emplace(pub32(keys + 32 * j), (uint32_t)slot_.size());
+    keys_.insert(keys_.end(), keys, keys + 32 * m);
     st.keys_appended += m;
     return true;
   }
@@ -449,6 +463,7 @@ class KeyCache {
   }
 
   std::unordered_map<Pub32, uint32_t, Pub32Hash> slot_;  // pool index of every key in the pool
+  std::vector<uint8_t> keys_;  // the pool's keys in index order (32 B each): same_keys reads them
   std::unordered_map<KcKey, std::unique_ptr<KcSet>, KcKeyHash> sets_;
   std::vector<std::unique_ptr<KcSet>> retired_;  // dropped while a call was pinned
   std::vector<uint8_t> pending_;  // keys queued by generic calls

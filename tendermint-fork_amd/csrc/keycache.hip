@@ -112,6 +112,9 @@ void keycache_destroy(tmed_ctx *c) {  // ctx->mu not held: the worker may be wai
 // ---- the seam's side (commit.hip keycache_resolve); the caller holds ctx->mu -----------------
 uint64_t keycache_pool_handle(const tmed_ctx *c) { return c->kc ? c->kc->kc.be.handle : 0; }
 const KcSet *keycache_find(tmed_ctx *c, const KcKey &key) { return cache_of(c).find(key); }
+bool keycache_same_keys(const tmed_ctx *c, const KcSet &e, const uint8_t *pubs, size_t n) {
+  return c->kc && c->kc->kc.same_keys(e, pubs, n);
+}
 uint64_t keycache_call_tick(tmed_ctx *c) { return cache_of(c).call_tick(); }
 void keycache_hits(tmed_ctx *c, size_t sets, size_t sigs) { cache_of(c).hits(sets, sigs); }
 void keycache_touch(tmed_ctx *c) { (void)cache_of(c); }

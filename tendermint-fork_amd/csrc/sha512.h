@@ -154,31 +154,70 @@ __device__ __forceinline__ uint64_t sha_Maj(uint64_t a, uint64_t b, uint64_t c) 
 #define TMED_SHA_MAJ(a, b, c) (((a) & (b)) ^ ((c) & ((a) ^ (b))))
 #endif
 
-// 80 rounds as 5 x 16 (the message-schedule window w[i & 15] stays register-indexed);
-// the round constants come from a uniform table (scalar loads on the device), so the
-// rolled outer loop keeps the live set at state + window (~50 VGPRs).
+// One round on the working variables (the caller rotates their roles by renaming, below).
+TMED_HD void sha512_round(const uint64_t a, const uint64_t b, const uint64_t c, uint64_t &d, const uint64_t e,
+                          const uint64_t f, const uint64_t g, uint64_t &h, uint64_t kw) {
+  const uint64_t S1 = TMED_SHA_S1(e);
+  const uint64_t ch = (e & f) ^ (~e & g);
+  const uint64_t t1 = h + S1 + ch + kw;
+  const uint64_t S0 = TMED_SHA_S0(a);
+  const uint64_t mj = TMED_SHA_MAJ(a, b, c);
+  d += t1;           // the next round's e
+  h = t1 + S0 + mj;  // the next round's a
+}
+TMED_HD void sha512_sched(uint64_t w[16], int j) {
+  const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+  w[j] += TMED_SHA_s0(w15) + w[(j + 9) & 15] + TMED_SHA_s1(w2);
+}
+// Eight rounds with the roles of the working variables rotated by renaming (no register moves).
+#define TMED_SHA_8ROUNDS(R, J, SCHED)                                                  \
+  do {                                                                                 \
+    if (SCHED) sha512_sched(w, (J) + 0);                                               \
+    sha512_round(v0, v1, v2, v3, v4, v5, v6, v7, sha512_k((R) + (J) + 0) + w[(J) + 0]); \
+    if (SCHED) sha512_sched(w, (J) + 1);                                               \
+    sha512_round(v7, v0, v1, v2, v3, v4, v5, v6, sha512_k((R) + (J) + 1) + w[(J) + 1]); \
+    if (SCHED) sha512_sched(w, (J) + 2);                                               \
+    sha512_round(v6, v7, v0, v1, v2, v3, v4, v5, sha512_k((R) + (J) + 2) + w[(J) + 2]); \
+    if (SCHED) sha512_sched(w, (J) + 3);                                               \
+    sha512_round(v5, v6, v7, v0, v1, v2, v3, v4, sha512_k((R) + (J) + 3) + w[(J) + 3]); \
+    if (SCHED) sha512_sched(w, (J) + 4);                                               \
+    sha512_round(v4, v5, v6, v7, v0, v1, v2, v3, sha512_k((R) + (J) + 4) + w[(J) + 4]); \
+    if (SCHED) sha512_sched(w, (J) + 5);                                               \
+    sha512_round(v3, v4, v5, v6, v7, v0, v1, v2, sha512_k((R) + (J) + 5) + w[(J) + 5]); \
+    if (SCHED) sha512_sched(w, (J) + 6);                                               \
+    sha512_round(v2, v3, v4, v5, v6, v7, v0, v1, sha512_k((R) + (J) + 6) + w[(J) + 6]); \
+    if (SCHED) sha512_sched(w, (J) + 7);                                               \
+    sha512_round(v1, v2, v3, v4, v5, v6, v7, v0, sha512_k((R) + (J) + 7) + w[(J) + 7]); \
+  } while (0)
+
+// 80 rounds.  TMED_SHA_PEEL 1: the first 16 (no message schedule) peeled, then 4 x 16 with the
+// schedule, so the rolled loop carries no per-round branch on the pass index; 0: 5 x 16 with the
+// schedule under `r > 0` (each round then compiles to a basic block of its own).  The
+// message-schedule window w[i & 15] stays register-indexed; the round constants come from a
+// uniform table (scalar loads on the device).
+#ifndef TMED_SHA_PEEL
+#define TMED_SHA_PEEL 1
+#endif
 TMED_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
-  uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+  uint64_t v0 = st[0], v1 = st[1], v2 = st[2], v3 = st[3], v4 = st[4], v5 = st[5], v6 = st[6], v7 = st[7];
+#if TMED_SHA_PEEL
+  TMED_SHA_8ROUNDS(0, 0, false);
+  TMED_SHA_8ROUNDS(0, 8, false);
+#pragma unroll 1
+  for (int r = 16; r < 80; r += 16) {
+    TMED_SHA_8ROUNDS(r, 0, true);
+    TMED_SHA_8ROUNDS(r, 8, true);
+  }
+#else
 #pragma unroll 1
   for (int r = 0; r < 80; r += 16) {
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-      if (r > 0) {
-        const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
-        const uint64_t s0 = TMED_SHA_s0(w15);
-        const uint64_t s1 = TMED_SHA_s1(w2);
-        w[j] += s0 + w[(j + 9) & 15] + s1;
-      }
-      const uint64_t S1 = TMED_SHA_S1(e);
-      const uint64_t ch = (e & f) ^ (~e & g);
-      const uint64_t t1 = h + S1 + ch + sha512_k(r + j) + w[j];
-      const uint64_t S0 = TMED_SHA_S0(a);
-      const uint64_t mj = TMED_SHA_MAJ(a, b, c);
-      h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
-    }
+    TMED_SHA_8ROUNDS(r, 0, r > 0);
+    TMED_SHA_8ROUNDS(r, 8, r > 0);
   }
-  st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+#endif
+  st[0] += v0; st[1] += v1; st[2] += v2; st[3] += v3; st[4] += v4; st[5] += v5; st[6] += v6; st[7] += v7;
 }
+#undef TMED_SHA_8ROUNDS
 
 TMED_HD uint32_t bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);

@@ -168,8 +168,11 @@ TMED_HD void hs_euclid_step(uint32_t x[8], const uint32_t y[8], uint32_t tx[kHsT
 // roles instead of being moved: the round-1 loop spent ~300 instructions a step, ~0.5 ms per
 // 2^20 signatures, mostly register moves and control flow).  FAST = false: that round-1 loop,
 // kept as the reference of tests/test_kernel_host.py.
+// tight (optional): the window count when the top digit may take values up to 16 (x < 2^(4W):
+// the throughput path, whose first window adds two table entries per scalar — hs_straus); the
+// return value is the count for top digits up to 8 (x < 2^(4W-1): the latency kernels).
 template <bool FAST = true>
-TMED_HD int sc_halfsize(uint32_t c[8], uint32_t dm[8], bool &dneg, const uint32_t k[8]) {
+TMED_HD int sc_halfsize(uint32_t c[8], uint32_t dm[8], bool &dneg, const uint32_t k[8], int *tight = nullptr) {
   uint32_t a[8], b[8], ta[kHsTW], tb[kHsTW], nb[8], nt[kHsTW];
   sc_const_8L(a);
 #pragma unroll
@@ -246,6 +249,7 @@ TMED_HD int sc_halfsize(uint32_t c[8], uint32_t dm[8], bool &dneg, const uint32_
 #pragma unroll
     for (int i = 0; i < 8; i++) { c[i] = k[i]; dm[i] = i == 0 ? 1u : 0u; }
     dneg = false;
+    if (tight) *tight = 64;
     return 64;
   }
 #pragma unroll
@@ -256,20 +260,26 @@ TMED_HD int sc_halfsize(uint32_t c[8], uint32_t dm[8], bool &dneg, const uint32_
 #pragma unroll
     for (int i = 0; i < 8; i++) { c[i] = k[i]; dm[i] = i == 0 ? 1u : 0u; }
     dneg = false;
+    if (tight) *tight = 64;
     return 64;
   }
   const int bits = bc > bd ? bc : bd;
   // |x| < 2^(4W-1): the recoding's carry out of nibble W-1 is folded into the top digit
-  // (hs_top_digit, digits -8..8), so 4W-1 bits suffice — one window less on a quarter of the lanes
+  // (hs_top_digit, digits 0..8), so 4W-1 bits suffice — one window less on a quarter of the lanes
   const int W = bits / 4 + 1;
+  // |x| < 2^(4W): top digits 0..16 — one window less again for the half of the lanes whose
+  // longer scalar has exactly 4W bits (128: c < 2^128 by the Euclid stop, |d| <= 2^127)
+  const int Wt = (bits + 3) / 4;
+  if (tight) *tight = Wt < 29 ? 29 : Wt;
   return W < 29 ? 29 : W;
 }
 
-// Top digit (window W-1) of a W-window signed radix-16 recoding (sc_recode16) of x < 2^(4W-1):
-// nibble W-1 minus 8, plus 16 times the carry the recoding moved into nibble W (that nibble is
-// 8 or 9; every nibble above it is 8).  In [0, 8]: the tables hold j*P for j = 1..8.  w_top is
-// the recoded word holding nibble W-1, w_next the one holding nibble W (W < 64; at W = 64 the
-// (k, 1) fallback has x < 2^253 and no carry).
+// Top digit (window W-1) of a W-window signed radix-16 recoding (sc_recode16) of x: nibble W-1
+// minus 8, plus 16 times the carry the recoding moved into nibble W (that nibble is 8 or 9; every
+// nibble above it is 8).  In [0, 8] for x < 2^(4W-1) (the latency kernels' window count), in
+// [0, 16] for x < 2^(4W) (the throughput path's tight count: hs_straus adds two table entries).
+// w_top is the recoded word holding nibble W-1, w_next the one holding nibble W (W < 64; at
+// W = 64 the (k, 1) fallback has x < 2^253 and no carry).
 TMED_HD int hs_top_digit(uint32_t w_top, uint32_t w_next, int W) {
   const int n = W - 1;
   const int d = (int)((w_top >> (4 * (n & 7))) & 15u) - 8;
@@ -280,9 +290,9 @@ TMED_HD int hs_top_digit(uint32_t w_top, uint32_t w_next, int W) {
 // scalars — cr, dr: signed radix-16 (sc_recode16; dr words 5..7 are 0x88888888, i.e. zero
 // digits, since |d| < 2^150), er: signed radix-2^16 — and the window count W.
 TMED_HD void hs_scalars(const uint32_t k[8], const uint32_t s[8], uint32_t cr[8], uint32_t dr[8], uint32_t er[8],
-                        bool &dneg, int &W, bool raw_e = false) {
+                        bool &dneg, int &W, bool raw_e = false, int *W_tight = nullptr) {
   uint32_t c[8], dm[8], e[8];
-  W = sc_halfsize(c, dm, dneg, k);
+  W = sc_halfsize(c, dm, dneg, k, W_tight);
   uint32_t zero[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) zero[i] = 0;
@@ -314,7 +324,7 @@ TMED_HD void hs_scalars(const uint32_t k[8], const uint32_t s[8], uint32_t cr[8]
 // the sign bit accepted) instead of strictly.
 TMED_HD bool hs_prep_r(const uint32_t k[8], const uint32_t s[8], const uint32_t Rw[8], uint32_t cr[8],
                        uint32_t dr[8], uint32_t er[8], bool &dneg, fe &Rx, fe &Ry, int &W,
-                       bool permissive = false, bool raw_e = false) {
+                       bool permissive = false, bool raw_e = false, int *W_tight = nullptr) {
   bool rok;
   if (permissive) {
     ge_p3 P;
@@ -325,7 +335,7 @@ TMED_HD bool hs_prep_r(const uint32_t k[8], const uint32_t s[8], const uint32_t 
     rok = r_decode_strict(Rx, Ry, Rw);
   }
   if (!rok) { fe_0(Rx); fe_1(Ry); }
-  hs_scalars(k, s, cr, dr, er, dneg, W, raw_e);
+  hs_scalars(k, s, cr, dr, er, dneg, W, raw_e, W_tight);
   return rok;
 }
 
@@ -336,13 +346,15 @@ struct HsDigits {
   TMED_HDM uint32_t dword(int w) const { return dr[w]; }
 };
 
-// Both phases of the half-size prep (the host simulation's single pass).
+// Both phases of the half-size prep (the host simulation's single pass of the throughput path):
+// W is the tight window count (top digits up to 16), as verify_prep_r_kernel hands over.
 TMED_HD bool verify_prep_hs(const uint32_t pubw[8], const uint32_t sigw[16], const uint8_t *msg, uint32_t mlen,
                             HsDigits &dg, uint32_t er[8], bool &dneg, ge_p3 &A, fe &Rx, fe &Ry, int &W,
                             bool raw_e = false) {
   uint32_t k[8], s[8];
   const bool ok = verify_prep(pubw, sigw, msg, mlen, k, s, A);
-  const bool rok = hs_prep_r(k, s, sigw, dg.cr, dg.dr, er, dneg, Rx, Ry, W, false, raw_e);
+  int Wl;
+  const bool rok = hs_prep_r(k, s, sigw, dg.cr, dg.dr, er, dneg, Rx, Ry, Wl, false, raw_e, &W);
   return ok && rok;
 }
 
@@ -426,15 +438,31 @@ TMED_HD void hs_straus(ge_p2 &out, const DS &ds, const uint32_t er[8], int W, TA
       cw = ds.cword(n >> 3);
       dw = ds.dword(n >> 3);
     }
-    const int sh = 4 * (n & 7);
-    int dc = (int)((cw >> sh) & 15u) - 8, dd = (int)((dw >> sh) & 15u) - 8;
     if (n == W - 1) {
-      // word W >> 3 holds nibble W; at W = 64 (the (k, 1) fallback) there is none and no carry
-      dc = hs_top_digit(cw, W < 64 ? ((W & 7) ? cw : ds.cword(W >> 3)) : 0u, W);
-      dd = hs_top_digit(dw, W < 64 ? ((W & 7) ? dw : ds.dword(W >> 3)) : 0u, W);
-      ge_p3_0(r);
-      if (TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc, dc < 0);
+      // The top window.  Its digits lie in [0, 16] (word W >> 3 holds nibble W; at W = 64, the
+      // (k, 1) fallback, there is none and no carry): each is added as two table entries,
+      // j1 = min(digit, 8) and digit - j1.  r starts as -A's first entry itself (cached ->
+      // extended: one product) instead of an addition to the identity.
+      const int dc = hs_top_digit(cw, W < 64 ? ((W & 7) ? cw : ds.cword(W >> 3)) : 0u, W);
+      const int dd = hs_top_digit(dw, W < 64 ? ((W & 7) ? dw : ds.dword(W >> 3)) : 0u, W);
+      const int c1 = dc < 8 ? dc : 8, d1 = dd < 8 ? dd : 8;
+      ta.prefetch(c1, false);
+      ta.take(ca);
+      ta.prefetch(dc - c1, false);
+      ge_cached_to_p3(r, ca);
+      ta.take(ca);
+      tr.prefetch(d1, false);
+      ge_add_cached_pre(t, r, ca, false);
+      ge_p1p1_to_p3(r, t);
+      tr.take(ca);
+      tr.prefetch(dd - d1, false);
+      ge_add_cached_pre(t, r, ca, false);
+      ge_p1p1_to_p3(r, t);
+      tr.take(ca);
+      ge_add_cached_pre(t, r, ca, false);
     } else {
+      const int sh = 4 * (n & 7);
+      const int dc = (int)((cw >> sh) & 15u) - 8, dd = (int)((dw >> sh) & 15u) - 8;
 #pragma unroll 1
       for (int k = 0; k < 3; k++) {
         ge_p2_dbl(t, q);
@@ -444,15 +472,15 @@ TMED_HD void hs_straus(ge_p2 &out, const DS &ds, const uint32_t er[8], int W, TA
       if (TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc, dc < 0);  // the row load overlaps the last doubling
       ge_p2_dbl(t, q);
       ge_p1p1_to_p3(r, t);
+      if (!TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc, dc < 0);
+      ta.take(ca);
+      if (TMED_SLAB_PF) tr.prefetch(dd < 0 ? -dd : dd, dd < 0);  // the row load overlaps the A addition
+      ge_add_cached_pre(t, r, ca, dc < 0);
+      ge_p1p1_to_p3(r, t);
+      if (!TMED_SLAB_PF) tr.prefetch(dd < 0 ? -dd : dd, dd < 0);
+      tr.take(ca);
+      ge_add_cached_pre(t, r, ca, dd < 0);
     }
-    if (!TMED_SLAB_PF) ta.prefetch(dc < 0 ? -dc : dc, dc < 0);
-    ta.take(ca);
-    if (TMED_SLAB_PF) tr.prefetch(dd < 0 ? -dd : dd, dd < 0);  // the row load overlaps the A addition
-    ge_add_cached_pre(t, r, ca, dc < 0);
-    ge_p1p1_to_p3(r, t);
-    if (!TMED_SLAB_PF) tr.prefetch(dd < 0 ? -dd : dd, dd < 0);
-    tr.take(ca);
-    ge_add_cached_pre(t, r, ca, dd < 0);
     if (b26) {
       if (n == 0 || n == 13 || n == 26) hs_b26_add(t, r, n / 13 * 2, d26l, d26h, bl, bh);
     } else if ((n & 3) == 0 && n <= 28) {

@@ -50,7 +50,7 @@ int kct_lookup(void *h, const uint8_t *pubs, size_t n, const uint8_t *set_hash, 
   bool keyed = false;
   if (fast) {
     hold = kc.find(key);
-    if (hold && kc_same_keys(*hold, pubs, n)) {
+    if (hold && kc.same_keys(*hold, pubs, n)) {
       kc.hit(*hold, sigs);
       keyed = true;
     } else {

@@ -277,9 +277,11 @@ def test_halfsize_fast_euclid_equals_reference_loop(hostsim):
 
 def test_halfsize_top_digit_and_wave_max(hostsim):
     """Random signatures through the half-size path (host build of verify_hs.h): with each lane's
-    own W (the top digit carries the recoding's overflow, digits up to 8) and with W raised above
-    it, as in a wave whose largest W exceeds the lane's; one flipped bit of S or of the message
-    makes each invalid.  Decisions equal the oracle's C port."""
+    own tight W (x < 2^(4W): the top digit carries the recoding's overflow, digits up to 16, added
+    as two table entries) and with W raised above it, as in a wave whose largest W exceeds the
+    lane's; one flipped bit of S or of the message makes each invalid.  Decisions equal the
+    oracle's C port; the tight count puts ~88 % of the lanes at 32 windows (the latency kernels'
+    count, x < 2^(4W-1), ~40 %)."""
     rng = np.random.default_rng(17)
     n = 1536
     seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
@@ -299,7 +301,7 @@ def test_halfsize_top_digit_and_wave_max(hostsim):
         hostsim.hostsim_verify_batch_hs_w(_p(pub), _p(sig), _p(msgs), _p(offs), ctypes.c_size_t(n), _p(out),
                                           _p(wins) if extra is None else None, wmin)
         assert (out == exp).all(), (extra, np.nonzero(out != exp)[0][:8])
-    assert wins.min() >= 29 and (wins == 32).sum() > n // 4, np.bincount(wins)
+    assert wins.min() >= 29 and (wins == 32).sum() > n * 3 // 4 and wins.max() <= 34, np.bincount(wins)
 
 
 def test_fused_carry_at_the_limb_extremes(hostsim):
