@@ -72,8 +72,8 @@ MADS_PER_VERIFY_GENERIC = MADS_STRAUS + MADS_TABLE + MADS_DECODE + MADS_ENCODE +
 MADS_MAIN = MADS_STRAUS + MADS_TABLE + MUL
 MAIN_KERNEL = "verify_main_kernel"
 if MAIN_VARIANT == 6:
-    # half-size scalars (verify_hs.h, the default): W = 33 radix-16 windows (the usual wave
-    # maximum; some waves run 34) of 4 dbl (16 S + 13 M) and two cached adds with their
+    # half-size scalars (verify_hs.h, the default): W = 32 radix-16 windows (the usual wave
+    # maximum; some waves run 33) of 4 dbl (16 S + 13 M) and two cached adds with their
     # conversions (15 M), 5 B steps of two niels adds (+14 M each; radix-2^26 tables, 8 steps at
     # radix 2^16 — mads_main_hs), two tables (-A, -sign(d) R)
     # and T = XY of A and R; no finish.  Outside the main kernel: decode of A and strict decode
@@ -81,8 +81,8 @@ if MAIN_VARIANT == 6:
     # ~130 Euclid steps) is not counted in mads.
     # tables by build_table_affine: 2d*xy (1 M) + 7 x (mixed add 3 M + p1p1->p3 4 M + 2dT 1 M)
     MADS_TABLE_HS = 57 * MUL
-    HS_W = 33
-    MADS_MAIN = (HS_W - 1) * (16 * SQ + 13 * MUL) + HS_W * 15 * MUL + 5 * 14 * MUL + 2 * MADS_TABLE_HS + 2 * MUL
+    HS_W = 32  # the tight window count's usual wave maximum (33 on ~9 % of the waves)
+    MADS_MAIN = (HS_W - 1) * (16 * SQ + 13 * MUL) + HS_W * 15 * MUL + 9 * MUL + 5 * 14 * MUL + 2 * MADS_TABLE_HS + 2 * MUL
     MADS_PER_VERIFY_GENERIC = MADS_MAIN + 2 * MADS_DECODE + MADS_SCALAR + 64 + 188
     MAIN_KERNEL = "verify_main_hs_kernel"
 # key-cached main kernel (C2 variant, kernels.hip keyset_straus_b24 / keyset_straus_pf): 32 rows of the
@@ -144,9 +144,11 @@ def spawn_ranks(n: int) -> int:
 
 def mads_main_hs(w: float, b_bits: int = 26) -> float:
     """v_mad_i64_i32 of verify_main_hs_kernel per signature at a wave loop length of w windows:
-    B steps of two niels adds (+14 M each) — five with the radix-2^26 tables, eight with radix 2^16."""
+    B steps of two niels adds (+14 M each) — five with the radix-2^26 tables, eight with radix 2^16;
+    the top window (digits 0..16 since round 5) adds two table entries per scalar: -A's first entry
+    converted to extended (1 M) and three cached additions instead of two (+9 M)."""
     b_steps = 5 if b_bits == 26 else 8
-    return (w - 1) * (16 * SQ + 13 * MUL) + w * 15 * MUL + b_steps * 14 * MUL + 2 * 57 * MUL + 2 * MUL
+    return (w - 1) * (16 * SQ + 13 * MUL) + w * 15 * MUL + 9 * MUL + b_steps * 14 * MUL + 2 * 57 * MUL + 2 * MUL
 
 
 def window_summary(eng):
@@ -352,6 +354,7 @@ def roofline_leg(eng, step, dev, n, offs, kernel_ms, no_peak):
     mads_main = MADS_MAIN if wstats is None else mads_main_hs(wstats["wave_W_mean"], b_bits)
     achieved = n * mads_main / (main_ms * 1e-3) / 1e12
     traffic, traffic_src = pmc_traffic(n / max(1, launches))
+    clk_main, clk_probe = pmc_clock(MAIN_KERNEL), pmc_clock("valu_probe")
     roof = {"bound": "valu", "kernel": MAIN_KERNEL, "achieved": round(achieved, 3),
             "peak": round(peak, 3) if peak else None,
             "unit": "Tmad/s (v_mad_i64_i32 lane-ops; peak = measured sustained rate)",
@@ -366,7 +369,12 @@ def roofline_leg(eng, step, dev, n, offs, kernel_ms, no_peak):
             "finish_kernel_ms": round(fin_ms, 4), "finish_launches": fin_launches,
             "step_kernel_ms": round(kernel_ms, 3),
             "algorithmic_bytes_per_verify": 32 + 64 + int(offs[-1]) // n + 4 + 1,
-            "window_stats": wstats}
+            "window_stats": wstats,
+            # effective clocks from the committed PMC pass (GRBM_GUI_ACTIVE / 8 XCDs / dispatch time):
+            # the main kernel's table traffic costs clock, not bandwidth
+            "clock_ghz": {"main_kernel": clk_main, "valu_peak_probe": clk_probe,
+                          "source": "profiles/pmc_summary.json (rocprofv3 --pmc GRBM_GUI_ACTIVE, same run for both)"}
+            if clk_main else None}
     return roof, peak
 
 
@@ -575,6 +583,19 @@ def pmc_traffic(sigs_per_launch, kernel=None):
         if k.split("<")[0] == kernel and "hbm_bytes_per_sig" in d:
             return round(d["hbm_bytes_per_sig"] * sigs_per_launch), "profiles/pmc_summary.json[%s]" % k
     return None, None
+
+
+def pmc_clock(kernel):
+    """Effective clock (GHz) of `kernel` from the committed PMC summary, or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_summary.json")) as fh:
+            pmc = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    for k, d in pmc.items():
+        if k.split("<")[0] == kernel and "effective_clock_ghz" in d:
+            return round(d["effective_clock_ghz"], 3)
+    return None
 
 
 def _cpu_model():
