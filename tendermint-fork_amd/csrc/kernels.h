@@ -107,15 +107,22 @@ hipError_t launch_comb_bases(const uint8_t *pubs, uint32_t n, int negate, uint8_
                              hipStream_t stream);
 // comb[key] from bases[key] (n * 32 workgroups of 128 lanes).
 hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStream_t stream);
-// Signed radix-2^10 comb of -A for the key-cached throughput kernel: entry [w][j] = j * 2^(10w) * (-A),
-// w = 0..25, j = 0..512; digit m of k is bits [10m, 10m + 10) + bit (10m - 1) - 2^10 * bit (10m + 9)
-// in [-512, 512] (no carry chain; k < 2^253 leaves digit 25 without a carry out): 26 rows per
-// signature instead of 32, 1.7 MB per key, built at a key set's first throughput batch.
-constexpr int kComb10Windows = 26;
-constexpr uint32_t kComb10Entries = 513;
-constexpr size_t kComb10BytesPerKey = (size_t)kComb10Windows * kComb10Entries * kCombEntryInt4 * 16;
-// comb10[key] of -A_key (bases: scratch of n * 26 * 40 int32).
-hipError_t launch_build_comb10(const uint8_t *pubs, uint32_t n, int32_t *bases, int4 *comb10, hipStream_t stream);
+// Signed radix-2^11 comb of -A for the key-cached throughput kernel: entry [w][j] = j * 2^(11w) * (-A).
+// Digit m of k (m < 22) is bits [11m, 11m + 11) + bit (11m - 1) - 2^11 * bit (11m + 10), in
+// [-1024, 1024] (no carry chain); the top digit (m = 22, bits 242..252) keeps its top bit: it is
+// bits [242, 253) + bit 241, in [0, 2048], so window 22 holds j = 0..2048 (k < L < 2^253: 23
+// windows cover it).  23 rows per signature (radix 2^10: 26; radix 256: 32), 3.1 MB per key, built
+// at a key set's first throughput batch.
+constexpr int kCombABits = 11;
+constexpr int kCombAWindows = 23;
+constexpr uint32_t kCombAEntries = 1025;     // windows 0..21: j = 0..1024
+constexpr uint32_t kCombATopEntries = 2049;  // window 22: j = 0..2048
+constexpr size_t kCombARowsPerKey = (size_t)(kCombAWindows - 1) * kCombAEntries + kCombATopEntries;
+constexpr size_t kCombABytesPerKey = kCombARowsPerKey * kCombEntryInt4 * 16;
+// row of entry j of window w within a key's comb
+constexpr size_t comba_row(int w, uint32_t j) { return (size_t)w * kCombAEntries + j; }
+// comba[key] of -A_key (bases: scratch of n * kCombAWindows * 40 int32).
+hipError_t launch_build_comba(const uint8_t *pubs, uint32_t n, int32_t *bases, int4 *comba, hipStream_t stream);
 // Key-cached verification: key index per signature into a keyset of nkeys keys (an index
 // >= nkeys rejects that signature).  perm (nullable, n entries of scratch) + order_scratch
 // (key_order_scratch_words): the main and finish kernels visit each chunk's signatures in
@@ -126,7 +133,7 @@ hipError_t launch_verify_keyset(const uint32_t *val_idx, uint32_t nkeys, const u
                                 int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots = false,
                                 KernelTimer *timer = nullptr, uint32_t *perm = nullptr,
                                 uint32_t *order_scratch = nullptr, const int4 *bcomb24 = nullptr,
-                                const int4 *acomb10 = nullptr);
+                                const int4 *acomba = nullptr);
 // Key-grouped visiting order of a key-cached batch (counting sort of val_idx by groups of
 // consecutive keys, indices >= nkeys last): perm[0..n) = signature indices grouped by key.
 // scratch: key_order_scratch_words(n, nkeys) u32.  The comb rows of the lanes in flight then

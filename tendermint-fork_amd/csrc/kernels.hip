@@ -1201,37 +1201,39 @@ __device__ __forceinline__ void keyset_straus_b24(ge_p2 &out, const uint32_t k[8
   }
 }
 
-// The same sum with -A from its radix-2^10 comb (kernels.h kComb10*): 26 A rows, then the eleven
-// B rows.  Digit m of k is read off k shifted right by 10m bits (bits [10m, 10m + 10) plus the
-// bit below, minus 2^10 times the top bit of the field).
-__device__ __forceinline__ const int4 *ks_a10row(const int4 *ak, int w, int d, bool &neg) {
+// The same sum with -A from its radix-2^11 comb (kernels.h kCombA*): 23 A rows, then the eleven
+// B rows.  Digit m of k is read off k shifted right by 11m bits (bits [11m, 11m + 11) plus the
+// bit below, minus 2^11 times the top bit of the field; the top digit keeps its top bit).
+__device__ __forceinline__ const int4 *ks_arow(const int4 *ak, int w, int d, bool &neg) {
   neg = d < 0;
-  return ak + ((size_t)w * kComb10Entries + (uint32_t)(neg ? -d : d)) * kCombEntryInt4;
+  return ak + comba_row(w, (uint32_t)(neg ? -d : d)) * kCombEntryInt4;
 }
-__device__ __forceinline__ void keyset_straus_a10b24(ge_p2 &out, const uint32_t k[8], const uint32_t s[8],
-                                                     const int4 *ak, const int4 *bc) {
+__device__ __forceinline__ void keyset_straus_ab24(ge_p2 &out, const uint32_t k[8], const uint32_t s[8],
+                                                   const int4 *ak, const int4 *bc) {
   uint32_t kw[8], sw[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) { kw[i] = k[i]; sw[i] = s[i]; }
   CombRowPf pf;
   bool ng;
   {
-    const uint32_t u = kw[0] & 0x3ffu;
-    pf.fetch(ks_a10row(ak, 0, (int)u - (int)((u >> 9) << 10), ng), ng);
+    const uint32_t u = kw[0] & 0x7ffu;
+    pf.fetch(ks_arow(ak, 0, (int)u - (int)((u >> 10) << 11), ng), ng);
   }
   ge_p3 acc;
   ge_p1p1 t;
   ge_niels e;
 #pragma unroll 1
-  for (int m = 0; m < kComb10Windows; m++) {
+  for (int m = 0; m < kCombAWindows; m++) {
     pf.take(e);
-    if (m + 1 < kComb10Windows) {
-      const uint32_t below = (kw[0] >> 9) & 1u;  // bit 10(m + 1) - 1
+    if (m + 1 < kCombAWindows) {
+      const uint32_t below = (kw[0] >> 10) & 1u;  // bit 11(m + 1) - 1
 #pragma unroll
-      for (int i = 0; i < 7; i++) kw[i] = __builtin_amdgcn_alignbit(kw[i + 1], kw[i], 10);
-      kw[7] >>= 10;
-      const uint32_t u = kw[0] & 0x3ffu;
-      pf.fetch(ks_a10row(ak, m + 1, (int)(u + below) - (int)((u >> 9) << 10), ng), ng);
+      for (int i = 0; i < 7; i++) kw[i] = __builtin_amdgcn_alignbit(kw[i + 1], kw[i], 11);
+      kw[7] >>= 11;
+      const uint32_t u = kw[0] & 0x7ffu;
+      // the top window's digit keeps its top bit (bits 242..252 + bit 241, in [0, 2048])
+      const int top = m + 2 == kCombAWindows ? 0 : (int)((u >> 10) << 11);
+      pf.fetch(ks_arow(ak, m + 1, (int)(u + below) - top, ng), ng);
     } else {  // the first B row: digit 0
       const uint32_t u = sw[0] & 0xffffffu;
       pf.fetch(ks_b24row(bc, 0, (int)u - (int)((u >> 23) << 24), ng), ng);
@@ -1260,7 +1262,7 @@ __device__ __forceinline__ void keyset_straus_a10b24(ge_p2 &out, const uint32_t 
   }
 }
 
-template <int WAVES, bool B24 = false, bool A10 = false>
+template <int WAVES, bool B24 = false, bool ACOMB = false>
 __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_keyset_main_kernel(
     const uint32_t *__restrict__ val_idx, uint32_t nkeys, const int4 *__restrict__ acomb,
     const int4 *__restrict__ bcomb, uint32_t base, uint32_t count, const int4 *__restrict__ prep, uint32_t stride,
@@ -1286,7 +1288,7 @@ __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_keyset_main_ke
   for (int j = 0; j < 8; j++) { k[j] = (uint32_t)w[j]; s[j] = (uint32_t)w[8 + j]; }
 #if TMED_KS_PF
   ge_p2 R;
-  if (A10) keyset_straus_a10b24(R, k, s, acomb + (size_t)v * kComb10Windows * kComb10Entries * kCombEntryInt4, bcomb);
+  if (ACOMB) keyset_straus_ab24(R, k, s, acomb + (size_t)v * kCombARowsPerKey * kCombEntryInt4, bcomb);
   else if (B24) keyset_straus_b24(R, k, s, acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4, bcomb);
   else keyset_straus_pf(R, k, s, acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4, bcomb);
 #else
@@ -1415,9 +1417,9 @@ hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStr
 }
 
 
-// ---- radix-2^10 comb of -A (kernels.h kComb10*) ------------------------------------------
-__global__ __launch_bounds__(64) void comb10_bases_kernel(const uint8_t *__restrict__ pubs, uint32_t n,
-                                                         int32_t *__restrict__ bases) {
+// ---- radix-2^11 comb of -A (kernels.h kCombA*) ------------------------------------------
+__global__ __launch_bounds__(64) void comba_bases_kernel(const uint8_t *__restrict__ pubs, uint32_t n,
+                                                        int32_t *__restrict__ bases) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t pw[8];
@@ -1427,28 +1429,36 @@ __global__ __launch_bounds__(64) void comb10_bases_kernel(const uint8_t *__restr
   fe_neg(P.X, P.X);
   fe_neg(P.T, P.T);
 #pragma unroll 1
-  for (int w = 0; w < kComb10Windows; w++) {
-    p3_store(bases + ((size_t)i * kComb10Windows + w) * 40, P);
-    ge_mul256(P);  // x 1024: two more doublings
+  for (int w = 0; w < kCombAWindows; w++) {
+    p3_store(bases + ((size_t)i * kCombAWindows + w) * 40, P);
+    ge_mul256(P);  // x 2048: three more doublings
     ge_p1p1 t;
     ge_p2 q;
     ge_p3_to_p2(q, P);
-    ge_p2_dbl(t, q);
-    ge_p1p1_to_p2(q, t);
-    ge_p2_dbl(t, q);
+#pragma unroll 1
+    for (int d = 0; d < kCombABits - 8; d++) {
+      ge_p2_dbl(t, q);
+      if (d + 1 < kCombABits - 8) ge_p1p1_to_p2(q, t);
+    }
     ge_p1p1_to_p3(P, t);
   }
 }
 
-// Four 128-lane workgroups per (key, window): lane j of the window computes j * base.
-__global__ __launch_bounds__(128) void comb10_fill_kernel(const int32_t *__restrict__ bases, int4 *__restrict__ comb) {
-  const uint32_t kw = blockIdx.x >> 2;  // key * 26 + window
-  const uint32_t j = (blockIdx.x & 3u) * 128u + threadIdx.x + 1u;  // 1..512
+// 128-lane workgroups per (key, window), eight of them (sixteen for the top window): lane j of
+// the window computes j * base.
+constexpr uint32_t kCombAGroups = (kCombAEntries - 1) / 128;         // 8: j = 1..1024
+constexpr uint32_t kCombATopGroups = (kCombATopEntries - 1) / 128;   // 16: j = 1..2048
+constexpr uint32_t kCombAGroupsPerKey = (kCombAWindows - 1) * kCombAGroups + kCombATopGroups;
+__global__ __launch_bounds__(128) void comba_fill_kernel(const int32_t *__restrict__ bases, int4 *__restrict__ comb) {
+  const uint32_t key = blockIdx.x / kCombAGroupsPerKey, g = blockIdx.x % kCombAGroupsPerKey;
+  const uint32_t w = g < (kCombAWindows - 1) * kCombAGroups ? g / kCombAGroups : kCombAWindows - 1;
+  const uint32_t gw = g - w * kCombAGroups;  // group within the window
+  const uint32_t j = gw * 128u + threadIdx.x + 1u;
   ge_p3 P;
-  p3_load(P, bases + (size_t)kw * 40);
+  p3_load(P, bases + ((size_t)key * kCombAWindows + w) * 40);
   ge_niels e;
-  comb_entry(e, P, j, 10);
-  int4 *row = comb + (size_t)kw * kComb10Entries * kCombEntryInt4;
+  comb_entry(e, P, j, w + 1 == kCombAWindows ? kCombABits + 1 : kCombABits);
+  int4 *row = comb + ((size_t)key * kCombARowsPerKey + comba_row((int)w, 0)) * kCombEntryInt4;
   niels_store(row + (size_t)j * kCombEntryInt4, e);
   if (j == 1) {
     ge_niels id;
@@ -1457,10 +1467,10 @@ __global__ __launch_bounds__(128) void comb10_fill_kernel(const int32_t *__restr
   }
 }
 
-hipError_t launch_build_comb10(const uint8_t *pubs, uint32_t n, int32_t *bases, int4 *comb10, hipStream_t stream) {
+hipError_t launch_build_comba(const uint8_t *pubs, uint32_t n, int32_t *bases, int4 *comba, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(comb10_bases_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, pubs, n, bases);
-  hipLaunchKernelGGL(comb10_fill_kernel, dim3(n * kComb10Windows * 4), dim3(128), 0, stream, bases, comb10);
+  hipLaunchKernelGGL(comba_bases_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, pubs, n, bases);
+  hipLaunchKernelGGL(comba_fill_kernel, dim3(n * kCombAGroupsPerKey), dim3(128), 0, stream, bases, comba);
   return hipGetLastError();
 }
 
@@ -1615,7 +1625,7 @@ hipError_t launch_verify_keyset(const uint32_t *val_idx, uint32_t nkeys, const u
                                 const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
                                 int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots, KernelTimer *timer,
                                 uint32_t *perm, uint32_t *order_scratch, const int4 *bcomb24,
-                                const int4 *acomb10) {
+                                const int4 *acomba) {
   const MsgSrc ms{msgs, off, msg_slots};
   if (stride > kFinCap) stride = kFinCap;
   if (timer) timer->mark(stream, -1);
@@ -1631,9 +1641,9 @@ hipError_t launch_verify_keyset(const uint32_t *val_idx, uint32_t nkeys, const u
       hipLaunchKernelGGL(verify_keyset_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, val_idx,
                          nkeys, key_pub, key_ok, sig, ms, base, count, prep, stride);
       if (timer) timer->mark(stream, 0);
-      if (bcomb24 && acomb10)
+      if (bcomb24 && acomba)
         hipLaunchKernelGGL((verify_keyset_main_kernel<2, true, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream,
-                           val_idx, nkeys, acomb10, bcomb24, base, count, prep, stride, fin, fbase, out, perm);
+                           val_idx, nkeys, acomba, bcomb24, base, count, prep, stride, fin, fbase, out, perm);
       else if (bcomb24)
         hipLaunchKernelGGL((verify_keyset_main_kernel<2, true>), dim3(blocks), dim3(kThreadsPerBlock), 0, stream,
                            val_idx, nkeys, acomb, bcomb24, base, count, prep, stride, fin, fbase, out, perm);

@@ -185,8 +185,8 @@ int tmed_keycache_stats(tmed_ctx *c, tmed_keycache_counters *o) {
   auto it = c->keysets.find(kc.be.handle);
   if (kc.be.handle && it != c->keysets.end()) {
     const Keyset &k = it->second;
-    o->pool_bytes = k.cap * (33 + kCombBytesPerKey) + (k.d_comb10 ? k.cap * kComb10BytesPerKey : 0);
-    o->pool_a_window_bits = k.d_comb10 && k.comb10_n == k.n ? 10 : 8;
+    o->pool_bytes = k.cap * (33 + kCombBytesPerKey) + (k.d_comba ? k.cap * kCombABytesPerKey : 0);
+    o->pool_a_window_bits = k.d_comba && k.comba_n == k.n ? kCombABits : 8;
   }
   return TMED_OK;
 }

@@ -33,7 +33,7 @@ void free_keyset(Keyset &k) {
   if (k.d_pub) (void)hipFree(k.d_pub);
   if (k.d_ok) (void)hipFree(k.d_ok);
   if (k.d_comb) (void)hipFree(k.d_comb);
-  if (k.d_comb10) (void)hipFree(k.d_comb10);
+  if (k.d_comba) (void)hipFree(k.d_comba);
   k = Keyset();
 }
 
@@ -47,39 +47,39 @@ static bool key_order_on(const Keyset &k, uint32_t n) {
   return n >= 4096 && k.n > 1 && k.n <= kKeyOrderMaxKeys;
 }
 
-// The key set's radix-2^10 comb (kernels.h kComb10*) for keys [comb10_n, n), on stream s (queued
+// The key set's radix-2^11 comb (kernels.h kCombA*) for keys [comba_n, n), on stream s (queued
 // in front of the batch that needs it; the bases scratch is freed after a sync of s): at the set's
-// first throughput batch, then for keys appended after it.  TMED_KS_A10=0 (read at tmed_init) keeps
-// the radix-256 comb; so does a failed allocation (comb10_failed).
-static void comb10_extend(tmed_ctx *c, Keyset &k, hipStream_t s) {
-  if (!c->a10_on || k.comb10_failed || k.comb10_n >= k.n) return;
-  if (!k.d_comb10 && hipMalloc((void **)&k.d_comb10, k.cap * kComb10BytesPerKey) != hipSuccess) {
+// first throughput batch, then for keys appended after it.  TMED_KS_ACOMB=0 (read at tmed_init) keeps
+// the radix-256 comb; so does a failed allocation (comba_failed).
+static void comba_extend(tmed_ctx *c, Keyset &k, hipStream_t s) {
+  if (!c->acomb_on || k.comba_failed || k.comba_n >= k.n) return;
+  if (!k.d_comba && hipMalloc((void **)&k.d_comba, k.cap * kCombABytesPerKey) != hipSuccess) {
     (void)hipGetLastError();
-    k.d_comb10 = nullptr;
-    k.comb10_failed = true;
+    k.d_comba = nullptr;
+    k.comba_failed = true;
     return;
   }
-  const size_t m = k.n - k.comb10_n;
+  const size_t m = k.n - k.comba_n;
   int32_t *bases = nullptr;
-  hipError_t e = hipMalloc((void **)&bases, m * kComb10Windows * 40 * sizeof(int32_t));
+  hipError_t e = hipMalloc((void **)&bases, m * kCombAWindows * 40 * sizeof(int32_t));
   if (e == hipSuccess)
-    e = launch_build_comb10(k.d_pub + 32 * k.comb10_n, (uint32_t)m, bases,
-                            k.d_comb10 + k.comb10_n * (kComb10BytesPerKey / sizeof(int4)), s);
+    e = launch_build_comba(k.d_pub + 32 * k.comba_n, (uint32_t)m, bases,
+                            k.d_comba + k.comba_n * (kCombABytesPerKey / sizeof(int4)), s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (bases) (void)hipFree(bases);
   if (e == hipSuccess) {
-    k.comb10_n = k.n;
+    k.comba_n = k.n;
   } else {  // an allocation failure leaves the radix-256 comb in use
     (void)hipGetLastError();
-    (void)hipFree(k.d_comb10);
-    k.d_comb10 = nullptr;
-    k.comb10_n = 0;
-    k.comb10_failed = true;
+    (void)hipFree(k.d_comba);
+    k.d_comba = nullptr;
+    k.comba_n = 0;
+    k.comba_failed = true;
   }
 }
 
 size_t keyset_bytes_per_key(const tmed_ctx *c) {
-  return 33 + kCombBytesPerKey + (c->a10_on ? kComb10BytesPerKey : 0);
+  return 33 + kCombBytesPerKey + (c->acomb_on ? kCombABytesPerKey : 0);
 }
 
 Keyset *find_keyset(tmed_ctx *c, uint64_t handle) {
@@ -87,41 +87,41 @@ Keyset *find_keyset(tmed_ctx *c, uint64_t handle) {
   return it == c->keysets.end() || it->second.pooled ? nullptr : &it->second;
 }
 
-// Room for `cap` keys: new buffers, the built keys (and their radix-2^10 combs) copied over on s,
-// a synchronisation of s, the old buffers freed.  A radix-2^10 comb that no longer fits is dropped
+// Room for `cap` keys: new buffers, the built keys (and their radix-2^11 combs) copied over on s,
+// a synchronisation of s, the old buffers freed.  A radix-2^11 comb that no longer fits is dropped
 // (rebuilt at the next throughput batch, or the radix-256 comb is used).
 static int keyset_reserve(tmed_ctx *c, Keyset &k, size_t cap, hipStream_t s) {
   if (cap <= k.cap) return TMED_OK;
   uint8_t *pub = nullptr, *ok = nullptr;
-  int4 *comb = nullptr, *comb10 = nullptr;
+  int4 *comb = nullptr, *comba = nullptr;
   hipError_t e = hipMalloc((void **)&pub, cap * 32);
   if (e == hipSuccess) e = hipMalloc((void **)&ok, cap);
   if (e == hipSuccess) e = hipMalloc((void **)&comb, cap * kCombBytesPerKey);
-  if (e == hipSuccess && k.d_comb10 && hipMalloc((void **)&comb10, cap * kComb10BytesPerKey) != hipSuccess) {
+  if (e == hipSuccess && k.d_comba && hipMalloc((void **)&comba, cap * kCombABytesPerKey) != hipSuccess) {
     (void)hipGetLastError();
-    comb10 = nullptr;
+    comba = nullptr;
   }
   if (e == hipSuccess && k.n) {
     e = hipMemcpyAsync(pub, k.d_pub, k.n * 32, hipMemcpyDeviceToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(ok, k.d_ok, k.n, hipMemcpyDeviceToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(comb, k.d_comb, k.n * kCombBytesPerKey, hipMemcpyDeviceToDevice, s);
-    if (e == hipSuccess && comb10 && k.comb10_n)
-      e = hipMemcpyAsync(comb10, k.d_comb10, k.comb10_n * kComb10BytesPerKey, hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess && comba && k.comba_n)
+      e = hipMemcpyAsync(comba, k.d_comba, k.comba_n * kCombABytesPerKey, hipMemcpyDeviceToDevice, s);
   }
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e == hipSuccess && c->lane1.s) e = hipStreamSynchronize(c->lane1.s);  // its batches read the old buffers
   if (e != hipSuccess) {
-    for (void *p : {(void *)pub, (void *)ok, (void *)comb, (void *)comb10})
+    for (void *p : {(void *)pub, (void *)ok, (void *)comb, (void *)comba})
       if (p) (void)hipFree(p);
     return map_err(e);
   }
-  for (void *p : {(void *)k.d_pub, (void *)k.d_ok, (void *)k.d_comb, (void *)k.d_comb10})
+  for (void *p : {(void *)k.d_pub, (void *)k.d_ok, (void *)k.d_comb, (void *)k.d_comba})
     if (p) (void)hipFree(p);
   k.d_pub = pub;
   k.d_ok = ok;
   k.d_comb = comb;
-  k.d_comb10 = comb10;
-  if (!comb10) k.comb10_n = 0;
+  k.d_comba = comba;
+  if (!comba) k.comba_n = 0;
   k.cap = cap;
   return TMED_OK;
 }
@@ -162,8 +162,8 @@ static hipError_t keyset_verify(tmed_ctx *c, Keyset &k, const uint32_t *d_idx, c
     return launch_verify_keyset_lat(d_idx, (uint32_t)k.n, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb, d_sig, d_msgs, d_off, n, d_out,
                                     c->d_fin, c->d_fin_pre, s, msg_slots, va);
   if (va) return hipErrorInvalidValue;
-  if (c->d_b24) comb10_extend(c, k, s);
-  const int4 *comb10 = c->d_b24 && k.d_comb10 && k.comb10_n == k.n ? k.d_comb10 : nullptr;
+  if (c->d_b24) comba_extend(c, k, s);
+  const int4 *comba = c->d_b24 && k.d_comba && k.comba_n == k.n ? k.d_comba : nullptr;
   KernelTimer *timer = (c->timing && !msg_slots) ? &c->timer : nullptr;
   uint32_t *perm = nullptr, *scratch = nullptr;
   DevBuf &korder = lane ? lane->d_korder : c->d_korder;
@@ -178,7 +178,7 @@ static hipError_t keyset_verify(tmed_ctx *c, Keyset &k, const uint32_t *d_idx, c
   return launch_verify_keyset(d_idx, (uint32_t)k.n, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb16, d_sig, d_msgs, d_off, n,
                               d_out, lane ? lane->d_prep : c->d_prep, c->slab_slots, lane ? lane->d_fin : c->d_fin,
                               lane ? lane->d_fin_pre : c->d_fin_pre, s, msg_slots, timer, perm, scratch, c->d_b24,
-                              comb10);
+                              comba);
 }
 
 int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st, int slot) {

@@ -191,7 +191,7 @@ int tmed_init(int device, tmed_ctx **out) {
   // TMED_B26 / TMED_B24 are read here, per context (a process may hold contexts of both kinds)
   if (e == hipSuccess && !env_off("TMED_B26")) c->d_b26 = bshare_acquire(0, device, c->d_bcomb16, c->stream);
   c->b24_on = !env_off("TMED_B24");
-  c->a10_on = !env_off("TMED_KS_A10");
+  c->acomb_on = !env_off("TMED_KS_ACOMB");
   c->kc_on = !env_off("TMED_KEYCACHE");
   if (const char *v = getenv("TMED_KEYCACHE_GB")) c->kc_budget = (size_t)strtoull(v, nullptr, 10) << 30;
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_bcomb, kCombBytesPerKey);
@@ -351,7 +351,7 @@ int tmed_keyset_a_window_bits(tmed_ctx *c, uint64_t handle) {
   std::lock_guard<std::mutex> lk(c->mu);
   const Keyset *k = find_keyset(c, handle);
   if (!k) return -1;
-  return k->d_comb10 && k->comb10_n == k->n && c->d_b24 ? 10 : 8;
+  return k->d_comba && k->comba_n == k->n && c->d_b24 ? kCombABits : 8;
 }
 
 int tmed_window_stats(tmed_ctx *c, uint32_t lane_hist[65], uint32_t wave_hist[65]) {

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 def radix_engines():
     es = {"default": engine_with_env(TMED_GLAT_MAX=0, TMED_LAT_MAX=0),
           "radix16": engine_with_env(TMED_GLAT_MAX=0, TMED_LAT_MAX=0, TMED_B26=0, TMED_B24=0),
-          "a8": engine_with_env(TMED_GLAT_MAX=0, TMED_LAT_MAX=0, TMED_KS_A10=0)}
+          "a8": engine_with_env(TMED_GLAT_MAX=0, TMED_LAT_MAX=0, TMED_KS_ACOMB=0)}
     yield es
     for e in es.values():
         e.close()
@@ -36,11 +36,11 @@ def _golden_arrays(golden):
     return vs, karr, idx, sigs, msgs, offs, exp
 
 
-@pytest.mark.parametrize("cfg,b_bits,ks_bits,a_bits", [("default", 26, 24, 10), ("radix16", 16, 16, 8),
+@pytest.mark.parametrize("cfg,b_bits,ks_bits,a_bits", [("default", 26, 24, 11), ("radix16", 16, 16, 8),
                                                        ("a8", 26, 24, 8)])
 def test_b_window_radix_and_decisions(radix_engines, golden, cfg, b_bits, ks_bits, a_bits):
-    """...and the key-cached throughput kernel's -A comb: radix 2^10 (built at the key set's first
-    throughput batch) by default, the radix-256 comb with TMED_KS_A10=0 or without the radix-2^24 B
+    """...and the key-cached throughput kernel's -A comb: radix 2^11 (built at the key set's first
+    throughput batch) by default, the radix-256 comb with TMED_KS_ACOMB=0 or without the radix-2^24 B
     comb."""
     eng = radix_engines[cfg]
     assert eng.b_window_bits() == b_bits

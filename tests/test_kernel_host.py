@@ -350,3 +350,30 @@ def test_fused_carry_at_the_limb_extremes(hostsim):
         a = carried()
         hostsim.hostsim_fe_raw(2, A(a), A(a), out, enc)
         assert int.from_bytes(enc.raw, "little") == 2 * val(a) ** 2 % P
+
+
+def test_radix_2_11_key_comb_digits():
+    """The key-cached throughput kernel's signed radix-2^11 digits of k (kernels.hip
+    keyset_straus_ab24, kernels.h kCombA*), restated: digit m < 22 is bits [11m, 11m + 11) + bit
+    (11m - 1) - 2^11 * bit (11m + 10), in [-1024, 1024]; the top digit (m = 22) keeps its top bit
+    and lies in [0, 2048] (the comb's top window holds j = 0..2048).  Sum of digit_m * 2^(11m) = k
+    for every k < L — including k in [2^252, L), where bit 252 is set (a 23 x 11 = 253-bit span with
+    a plain signed top digit would drop 2^253 there)."""
+    L = 2**252 + 27742317777372353535851937790883648493
+    rng = random.Random(11)
+    ks = [rng.randrange(L) for _ in range(3000)] + [L - 1, L - 2, 2**252, 2**252 + 12345, 0, 1, 2**241,
+                                                     2**252 - 1, (2**253 - 1) % L]
+    for k in ks:
+        w = [(k >> (32 * i)) & 0xffffffff for i in range(8)]
+        digits = []
+        u = w[0] & 0x7ff
+        digits.append(u - ((u >> 10) << 11))
+        for m in range(22):
+            below = (w[0] >> 10) & 1
+            w = [((w[i] >> 11) | (w[i + 1] << 21)) & 0xffffffff for i in range(7)] + [w[7] >> 11]
+            u = w[0] & 0x7ff
+            top = 0 if m + 2 == 23 else (u >> 10) << 11
+            digits.append(u + below - top)
+        assert len(digits) == 23
+        assert all(-1024 <= d <= 1024 for d in digits[:22]) and 0 <= digits[22] <= 2048, (k, digits)
+        assert sum(d << (11 * m) for m, d in enumerate(digits)) == k, k

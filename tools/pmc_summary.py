@@ -16,7 +16,7 @@ import sys
 
 KERNELS = ("verify_main_hs_kernel", "verify_prep_r_kernel", "verify_main_kernel", "verify_prep_kernel", "verify_finish_kernel",
            "verify_keyset_main_kernel", "verify_keyset_prep_kernel", "verify_keyset_lat_kernel", "verify_lat_finish_kernel",
-           "verify_glat_prep_kernel", "verify_glat_main_kernel", "sign_kernel", "merkle", "sha256")
+           "verify_glat_prep_kernel", "verify_glat_main_kernel", "sign_kernel", "merkle", "sha256", "valu_probe")
 
 
 def files(args):
