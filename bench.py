@@ -93,10 +93,10 @@ if MAIN_VARIANT == 6:
 
 def mads_keyset_main(b_bits: int = 24, a_bits: int = 8) -> int:
     """Field products of the key-cached main kernel per signature, in mads: one comb row per
-    window (23 with the radix-2^11 -A comb, 26 with radix 2^10, 32 with radix 256; 11 B rows with the
+    window (21 with the radix-2^12 -A comb, 23 with radix 2^11, 32 with radix 256; 11 B rows with the
     radix-2^24 B comb, 16 with the radix-2^16 one); the first row is a conversion (1 M), the
     last stops at projective (6 M), the rest are mixed additions (7 M)."""
-    rows = {8: 32, 10: 26, 11: 23}[a_bits] + (11 if b_bits == 24 else 16)
+    rows = {8: 32, 10: 25, 11: 23, 12: 21}[a_bits] + (11 if b_bits == 24 else 16)
     return (1 + (rows - 2) * 7 + 6) * MUL
 
 

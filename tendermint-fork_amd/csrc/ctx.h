@@ -69,7 +69,7 @@ struct Keyset {
   uint8_t *d_pub = nullptr;   // cap x 32 raw encodings (hashed into k)
   uint8_t *d_ok = nullptr;    // cap: Point.SetBytes accepted the key
   int4 *d_comb = nullptr;     // cap x kCombBytesPerKey: signed radix-256 comb of -A
-  // cap x kCombABytesPerKey: radix-2^11 comb of -A for the throughput kernel, keys [0, comba_n)
+  // cap x kCombABytesPerKey: radix-2^12 comb of -A for the throughput kernel (kernels.h kCombA*), keys [0, comba_n)
   // built (at the set's first throughput batch and for keys appended after it: keyset.hip
   // comba_extend; null / comba_failed: TMED_KS_ACOMB=0 or no memory -> the radix-256 comb)
   int4 *d_comba = nullptr;
@@ -84,7 +84,7 @@ int build_comb(tmed_ctx *c, const uint8_t *d_pubs, size_t n, int negate, uint8_t
 // queues their radix-256 combs; nothing waits for the build (later work on s is ordered behind it).
 // TMED_EINVAL past max_cap keys.
 int keyset_append(tmed_ctx *c, Keyset &k, const uint8_t *pubkeys, size_t m, hipStream_t s, size_t max_cap);
-// Device bytes one key of a key set can take (radix-256 comb + radix-2^11 comb + encoding + flag).
+// Device bytes one key of a key set can take (radix-256 comb + radix-2^12 comb + encoding + flag).
 size_t keyset_bytes_per_key(const tmed_ctx *c);
 // The public key set of `handle` (nullptr for unknown and pooled handles).
 Keyset *find_keyset(tmed_ctx *c, uint64_t handle);
@@ -220,7 +220,7 @@ struct tmed_ctx {
   int4 *d_b24 = nullptr;      // radix-2^24 B comb of the key-cached main kernel (11.8 GB, shared per device)
   bool b24_tried = false;     // d_b24 acquired (or given up) at the first key-set load
   bool b24_on = true;         // TMED_B24 at tmed_init
-  bool acomb_on = true;         // TMED_KS_ACOMB at tmed_init (radix-2^11 -A combs, keyset.hip comba_extend)
+  bool acomb_on = true;         // TMED_KS_ACOMB at tmed_init (radix-2^12 -A combs, keyset.hip comba_extend)
   int4 *d_slab = nullptr;
   int4 *d_prep = nullptr;
   int4 *d_fin = nullptr;      // batched-finish hand-off (kFinBytes)
@@ -252,7 +252,7 @@ struct tmed_ctx {
   uint64_t next_keyset = 1;
   tmed::KeyCacheDev *kc = nullptr;  // key-set cache of the commit seam (keycache.hip), created at first use
   bool kc_on = true;                // TMED_KEYCACHE at tmed_init / tmed_keycache_config
-  size_t kc_budget = (size_t)96 << 30;  // its pool's HBM budget (~26k keys at 3.7 MB: a light client's and a replay's sets together)
+  size_t kc_budget = (size_t)160 << 30;  // its pool's HBM budget (~25k keys at 6.3 MB: a light client's and a replay's sets together)
   tmed::DevBuf d_kbases;            // comb-base scratch of keyset_append (ordered on the context stream)
   tmed::HostBuf h_kup;              // pinned staging of keys keyset_append uploads
   hipEvent_t kup_ev = nullptr;      // the last upload from h_kup (reused after it completes)

@@ -107,16 +107,25 @@ hipError_t launch_comb_bases(const uint8_t *pubs, uint32_t n, int negate, uint8_
                              hipStream_t stream);
 // comb[key] from bases[key] (n * 32 workgroups of 128 lanes).
 hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStream_t stream);
-// Signed radix-2^11 comb of -A for the key-cached throughput kernel: entry [w][j] = j * 2^(11w) * (-A).
-// Digit m of k (m < 22) is bits [11m, 11m + 11) + bit (11m - 1) - 2^11 * bit (11m + 10), in
-// [-1024, 1024] (no carry chain); the top digit (m = 22, bits 242..252) keeps its top bit: it is
-// bits [242, 253) + bit 241, in [0, 2048], so window 22 holds j = 0..2048 (k < L < 2^253: 23
-// windows cover it).  23 rows per signature (radix 2^10: 26; radix 256: 32), 3.1 MB per key, built
-// at a key set's first throughput batch.
-constexpr int kCombABits = 11;
-constexpr int kCombAWindows = 23;
-constexpr uint32_t kCombAEntries = 1025;     // windows 0..21: j = 0..1024
-constexpr uint32_t kCombATopEntries = 2049;  // window 22: j = 0..2048
+// Signed radix-2^B comb of -A for the key-cached throughput kernel (B = kCombABits, 12 by default):
+// entry [w][j] = j * 2^(Bw) * (-A).  W = floor(253 / B) windows; digit m < W - 1 is bits
+// [Bm, Bm + B) + bit (Bm - 1) - 2^B * bit (Bm + B - 1), in [-2^(B-1), 2^(B-1)] (no carry chain);
+// the top digit (m = W - 1) is every bit from B(W - 1) up + bit (B(W - 1) - 1), unsigned: k < L
+// puts it in [0, 2^(252 - B(W - 1)) + 1] (B = 12: bits 240..252, [0, 4097]), so window W - 1 holds
+// j = 0 .. kCombATopEntries - 1 (whole 128-entry fill groups).  B = 12: 21 rows per signature
+// (radix 2^11: 23, radix 2^10: 26, radix 256: 32), 5.8 MB per key (58 GB for 10k keys), built at a
+// key set's first throughput batch.  TMED_COMBA_BITS picks B in 10..12.
+#ifndef TMED_COMBA_BITS
+#define TMED_COMBA_BITS 12
+#endif
+constexpr int kCombABits = TMED_COMBA_BITS;
+constexpr int kCombAWindows = 253 / kCombABits;                             // 21 (B = 12), 23 (11), 25 (10)
+constexpr int kCombATopField = 253 - kCombABits * (kCombAWindows - 1);      // 13 (B = 12)
+constexpr uint32_t kCombAEntries = (1u << (kCombABits - 1)) + 1;            // 2049: j = 0..2048
+constexpr uint32_t kCombATopMax = (1u << (kCombATopField - 1)) + 1;         // 4097 (k < L)
+constexpr uint32_t kCombATopGroups = (kCombATopMax + 127) / 128;            // 33
+constexpr uint32_t kCombATopEntries = kCombATopGroups * 128 + 1;            // 4225
+static_assert(kCombABits >= 10 && kCombABits <= 12 && kCombATopField >= kCombABits, "comb radix");
 constexpr size_t kCombARowsPerKey = (size_t)(kCombAWindows - 1) * kCombAEntries + kCombATopEntries;
 constexpr size_t kCombABytesPerKey = kCombARowsPerKey * kCombEntryInt4 * 16;
 // row of entry j of window w within a key's comb

@@ -1201,9 +1201,9 @@ __device__ __forceinline__ void keyset_straus_b24(ge_p2 &out, const uint32_t k[8
   }
 }
 
-// The same sum with -A from its radix-2^11 comb (kernels.h kCombA*): 23 A rows, then the eleven
-// B rows.  Digit m of k is read off k shifted right by 11m bits (bits [11m, 11m + 11) plus the
-// bit below, minus 2^11 times the top bit of the field; the top digit keeps its top bit).
+// The same sum with -A from its radix-2^B comb (kernels.h kCombA*, B = 12: 21 A rows), then the
+// eleven B rows.  Digit m of k is read off k shifted right by Bm bits (bits [Bm, Bm + B) plus the
+// bit below, minus 2^B times the top bit of the field; the top digit is every bit left, unsigned).
 __device__ __forceinline__ const int4 *ks_arow(const int4 *ak, int w, int d, bool &neg) {
   neg = d < 0;
   return ak + comba_row(w, (uint32_t)(neg ? -d : d)) * kCombEntryInt4;
@@ -1215,9 +1215,10 @@ __device__ __forceinline__ void keyset_straus_ab24(ge_p2 &out, const uint32_t k[
   for (int i = 0; i < 8; i++) { kw[i] = k[i]; sw[i] = s[i]; }
   CombRowPf pf;
   bool ng;
+  constexpr uint32_t kMask = (1u << kCombABits) - 1u;
   {
-    const uint32_t u = kw[0] & 0x7ffu;
-    pf.fetch(ks_arow(ak, 0, (int)u - (int)((u >> 10) << 11), ng), ng);
+    const uint32_t u = kw[0] & kMask;
+    pf.fetch(ks_arow(ak, 0, (int)u - (int)((u >> (kCombABits - 1)) << kCombABits), ng), ng);
   }
   ge_p3 acc;
   ge_p1p1 t;
@@ -1226,13 +1227,14 @@ __device__ __forceinline__ void keyset_straus_ab24(ge_p2 &out, const uint32_t k[
   for (int m = 0; m < kCombAWindows; m++) {
     pf.take(e);
     if (m + 1 < kCombAWindows) {
-      const uint32_t below = (kw[0] >> 10) & 1u;  // bit 11(m + 1) - 1
+      const uint32_t below = (kw[0] >> (kCombABits - 1)) & 1u;  // bit B(m + 1) - 1
 #pragma unroll
-      for (int i = 0; i < 7; i++) kw[i] = __builtin_amdgcn_alignbit(kw[i + 1], kw[i], 11);
-      kw[7] >>= 11;
-      const uint32_t u = kw[0] & 0x7ffu;
-      // the top window's digit keeps its top bit (bits 242..252 + bit 241, in [0, 2048])
-      const int top = m + 2 == kCombAWindows ? 0 : (int)((u >> 10) << 11);
+      for (int i = 0; i < 7; i++) kw[i] = __builtin_amdgcn_alignbit(kw[i + 1], kw[i], kCombABits);
+      kw[7] >>= kCombABits;
+      // the top window's digit: every bit left (k < L: bits B(W-1)..252) + the bit below, unsigned
+      const bool last = m + 2 == kCombAWindows;
+      const uint32_t u = last ? kw[0] : kw[0] & kMask;
+      const int top = last ? 0 : (int)((u >> (kCombABits - 1)) << kCombABits);
       pf.fetch(ks_arow(ak, m + 1, (int)(u + below) - top, ng), ng);
     } else {  // the first B row: digit 0
       const uint32_t u = sw[0] & 0xffffffu;
@@ -1417,7 +1419,7 @@ hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStr
 }
 
 
-// ---- radix-2^11 comb of -A (kernels.h kCombA*) ------------------------------------------
+// ---- radix-2^B comb of -A (kernels.h kCombA*) -------------------------------------------
 __global__ __launch_bounds__(64) void comba_bases_kernel(const uint8_t *__restrict__ pubs, uint32_t n,
                                                         int32_t *__restrict__ bases) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1431,7 +1433,7 @@ __global__ __launch_bounds__(64) void comba_bases_kernel(const uint8_t *__restri
 #pragma unroll 1
   for (int w = 0; w < kCombAWindows; w++) {
     p3_store(bases + ((size_t)i * kCombAWindows + w) * 40, P);
-    ge_mul256(P);  // x 2048: three more doublings
+    ge_mul256(P);  // x 2^B: B - 8 more doublings
     ge_p1p1 t;
     ge_p2 q;
     ge_p3_to_p2(q, P);
@@ -1444,10 +1446,9 @@ __global__ __launch_bounds__(64) void comba_bases_kernel(const uint8_t *__restri
   }
 }
 
-// 128-lane workgroups per (key, window), eight of them (sixteen for the top window): lane j of
-// the window computes j * base.
-constexpr uint32_t kCombAGroups = (kCombAEntries - 1) / 128;         // 8: j = 1..1024
-constexpr uint32_t kCombATopGroups = (kCombATopEntries - 1) / 128;   // 16: j = 1..2048
+// 128-lane workgroups per (key, window), 2^(B-1) / 128 of them (kCombATopGroups for the top
+// window): lane j of the window computes j * base.
+constexpr uint32_t kCombAGroups = (kCombAEntries - 1) / 128;         // 16: j = 1..2048 (B = 12)
 constexpr uint32_t kCombAGroupsPerKey = (kCombAWindows - 1) * kCombAGroups + kCombATopGroups;
 __global__ __launch_bounds__(128) void comba_fill_kernel(const int32_t *__restrict__ bases, int4 *__restrict__ comb) {
   const uint32_t key = blockIdx.x / kCombAGroupsPerKey, g = blockIdx.x % kCombAGroupsPerKey;
@@ -1457,7 +1458,7 @@ __global__ __launch_bounds__(128) void comba_fill_kernel(const int32_t *__restri
   ge_p3 P;
   p3_load(P, bases + ((size_t)key * kCombAWindows + w) * 40);
   ge_niels e;
-  comb_entry(e, P, j, w + 1 == kCombAWindows ? kCombABits + 1 : kCombABits);
+  comb_entry(e, P, j, w + 1 == kCombAWindows ? kCombATopField : kCombABits);  // j < 2^nbits
   int4 *row = comb + ((size_t)key * kCombARowsPerKey + comba_row((int)w, 0)) * kCombEntryInt4;
   niels_store(row + (size_t)j * kCombEntryInt4, e);
   if (j == 1) {

@@ -47,7 +47,7 @@ static bool key_order_on(const Keyset &k, uint32_t n) {
   return n >= 4096 && k.n > 1 && k.n <= kKeyOrderMaxKeys;
 }
 
-// The key set's radix-2^11 comb (kernels.h kCombA*) for keys [comba_n, n), on stream s (queued
+// The key set's radix-2^12 comb (kernels.h kCombA*) for keys [comba_n, n), on stream s (queued
 // in front of the batch that needs it; the bases scratch is freed after a sync of s): at the set's
 // first throughput batch, then for keys appended after it.  TMED_KS_ACOMB=0 (read at tmed_init) keeps
 // the radix-256 comb; so does a failed allocation (comba_failed).
@@ -87,8 +87,8 @@ Keyset *find_keyset(tmed_ctx *c, uint64_t handle) {
   return it == c->keysets.end() || it->second.pooled ? nullptr : &it->second;
 }
 
-// Room for `cap` keys: new buffers, the built keys (and their radix-2^11 combs) copied over on s,
-// a synchronisation of s, the old buffers freed.  A radix-2^11 comb that no longer fits is dropped
+// Room for `cap` keys: new buffers, the built keys (and their radix-2^12 combs) copied over on s,
+// a synchronisation of s, the old buffers freed.  A radix-2^12 comb that no longer fits is dropped
 // (rebuilt at the next throughput batch, or the radix-256 comb is used).
 static int keyset_reserve(tmed_ctx *c, Keyset &k, size_t cap, hipStream_t s) {
   if (cap <= k.cap) return TMED_OK;

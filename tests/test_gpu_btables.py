@@ -36,10 +36,10 @@ def _golden_arrays(golden):
     return vs, karr, idx, sigs, msgs, offs, exp
 
 
-@pytest.mark.parametrize("cfg,b_bits,ks_bits,a_bits", [("default", 26, 24, 11), ("radix16", 16, 16, 8),
+@pytest.mark.parametrize("cfg,b_bits,ks_bits,a_bits", [("default", 26, 24, 12), ("radix16", 16, 16, 8),
                                                        ("a8", 26, 24, 8)])
 def test_b_window_radix_and_decisions(radix_engines, golden, cfg, b_bits, ks_bits, a_bits):
-    """...and the key-cached throughput kernel's -A comb: radix 2^11 (built at the key set's first
+    """...and the key-cached throughput kernel's -A comb: radix 2^12 (built at the key set's first
     throughput batch) by default, the radix-256 comb with TMED_KS_ACOMB=0 or without the radix-2^24 B
     comb."""
     eng = radix_engines[cfg]

@@ -203,7 +203,7 @@ def test_budget_resets_and_wrong_set_hash(cached):
     Every call equals the oracle."""
     a = _c1(cached, b"kc-A")
     b = _c1(cached, b"kc-B")
-    per_key = 33 + 32 * 129 * 128 + (22 * 1025 + 2049) * 128  # keyset_bytes_per_key with the radix-2^11 comb
+    per_key = 33 + 32 * 129 * 128 + (20 * 2049 + 4225) * 128  # keyset_bytes_per_key with the radix-2^12 comb
     cached.keycache_config(True, 300 * per_key)
     ra, ea = _c1_requests(*a)
     rb, eb = _c1_requests(*b)

@@ -352,28 +352,36 @@ def test_fused_carry_at_the_limb_extremes(hostsim):
         assert int.from_bytes(enc.raw, "little") == 2 * val(a) ** 2 % P
 
 
-def test_radix_2_11_key_comb_digits():
-    """The key-cached throughput kernel's signed radix-2^11 digits of k (kernels.hip
-    keyset_straus_ab24, kernels.h kCombA*), restated: digit m < 22 is bits [11m, 11m + 11) + bit
-    (11m - 1) - 2^11 * bit (11m + 10), in [-1024, 1024]; the top digit (m = 22) keeps its top bit
-    and lies in [0, 2048] (the comb's top window holds j = 0..2048).  Sum of digit_m * 2^(11m) = k
-    for every k < L — including k in [2^252, L), where bit 252 is set (a 23 x 11 = 253-bit span with
-    a plain signed top digit would drop 2^253 there)."""
+@pytest.mark.parametrize("B", [10, 11, 12])
+def test_radix_2_b_key_comb_digits(B):
+    """The key-cached throughput kernel's signed radix-2^B digits of k (kernels.hip
+    keyset_straus_ab24, kernels.h kCombA*; B = 12 by default), restated: W = floor(253 / B) windows;
+    digit m < W - 1 is bits [Bm, Bm + B) + bit (Bm - 1) - 2^B * bit (Bm + B - 1), in
+    [-2^(B-1), 2^(B-1)]; the top digit (m = W - 1) is every bit left + the bit below, unsigned, in
+    [0, kCombATopMax] (B = 12: bits 240..252, [0, 4097]) — inside the comb's top window.  Sum of
+    digit_m * 2^(Bm) = k for every k < L, including k in [2^252, L) where bit 252 is set."""
     L = 2**252 + 27742317777372353535851937790883648493
-    rng = random.Random(11)
+    W = 253 // B
+    top_field = 253 - B * (W - 1)
+    top_max = (1 << (top_field - 1)) + 1           # kernels.h kCombATopMax
+    top_rows = ((top_max + 127) // 128) * 128 + 1  # kCombATopEntries
+    mask = (1 << B) - 1
+    rng = random.Random(11 + B)
     ks = [rng.randrange(L) for _ in range(3000)] + [L - 1, L - 2, 2**252, 2**252 + 12345, 0, 1, 2**241,
-                                                     2**252 - 1, (2**253 - 1) % L]
+                                                     2**252 - 1, (2**253 - 1) % L, 2**240 - 1, 2**252 - 2**239]
     for k in ks:
         w = [(k >> (32 * i)) & 0xffffffff for i in range(8)]
         digits = []
-        u = w[0] & 0x7ff
-        digits.append(u - ((u >> 10) << 11))
-        for m in range(22):
-            below = (w[0] >> 10) & 1
-            w = [((w[i] >> 11) | (w[i + 1] << 21)) & 0xffffffff for i in range(7)] + [w[7] >> 11]
-            u = w[0] & 0x7ff
-            top = 0 if m + 2 == 23 else (u >> 10) << 11
+        u = w[0] & mask
+        digits.append(u - ((u >> (B - 1)) << B))
+        for m in range(W - 1):
+            below = (w[0] >> (B - 1)) & 1
+            w = [((w[i] >> B) | (w[i + 1] << (32 - B))) & 0xffffffff for i in range(7)] + [w[7] >> B]
+            last = m + 2 == W
+            u = w[0] if last else w[0] & mask
+            top = 0 if last else (u >> (B - 1)) << B
             digits.append(u + below - top)
-        assert len(digits) == 23
-        assert all(-1024 <= d <= 1024 for d in digits[:22]) and 0 <= digits[22] <= 2048, (k, digits)
-        assert sum(d << (11 * m) for m, d in enumerate(digits)) == k, k
+        assert len(digits) == W
+        h = 1 << (B - 1)
+        assert all(-h <= d <= h for d in digits[:-1]) and 0 <= digits[-1] <= top_max < top_rows, (k, digits)
+        assert sum(d << (B * m) for m, d in enumerate(digits)) == k, k
