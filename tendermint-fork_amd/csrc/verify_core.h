@@ -259,6 +259,9 @@ TMED_HD bool verify_main(const uint32_t k[8], const uint32_t s[8], const ge_p3 &
 // Z = 0 cannot come out of the complete formulas for points on the curve; it is still
 // guarded (replaced by 1 and the signature rejected) so one bad value cannot poison the
 // inversion of its whole group.
+#ifndef TMED_FIN_BGCD
+#define TMED_FIN_BGCD 1  // the group's inversion by binary GCD (fe_invert_bgcd); 0: z^(p-2)
+#endif
 template <class Acc>
 TMED_HD void finish_group(Acc &a) {
   const int cnt = a.count();
@@ -278,7 +281,11 @@ TMED_HD void finish_group(Acc &a) {
     a.store_pre(j, acc);
   }
   fe inv;
-  fe_invert(inv, acc);  // 1 / (Z_0 ... Z_{cnt-1})
+#if TMED_FIN_BGCD
+  fe_invert_bgcd(inv, acc);  // 1 / (Z_0 ... Z_{cnt-1})
+#else
+  fe_invert(inv, acc);
+#endif
   fe pre, X, Y, pren, Xn, Yn;
   uint32_t Rw[8], Rn[8];
   auto load_row = [&](int j, fe &p, fe &zr, fe &x, fe &y, uint32_t r[8]) {

@@ -414,6 +414,7 @@ void hostsim_fe_op(int op, const uint8_t *a, const uint8_t *b, uint8_t *out) {
     case 6: fe_sq2(fo, fa); break;
     case 7: { fe t; fe_add(t, fa, fb); fe_add(t, t, fa); fe_mul(fo, t, t); break; }  // 3-sum input
     case 8: { fe t; fe_add(t, fa, fb); fe_add(t, t, fa); fe_sq(fo, t); break; }
+    case 9: fe_invert_bgcd(fo, fa); break;
     default: fe_copy(fo, fa);
   }
   fe_to_words(wo, fo);

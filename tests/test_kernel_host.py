@@ -33,9 +33,22 @@ def test_field_ops_vs_bigint(hostsim):
         for b in edge[:6] + [rng.randrange(2**255)]:
             A, B = a % P, b % P
             exp = {0: A * B % P, 1: A * A % P, 2: pow(A, P - 2, P), 3: pow(A, (P - 5) // 8, P), 4: (A + B) % P,
-                   5: (A - B) % P, 6: 2 * A * A % P, 7: (2 * A + B) ** 2 % P, 8: (2 * A + B) ** 2 % P}
+                   5: (A - B) % P, 6: 2 * A * A % P, 7: (2 * A + B) ** 2 % P, 8: (2 * A + B) ** 2 % P,
+                   9: pow(A, P - 2, P)}
             for op, e in exp.items():
                 assert _fe(hostsim, op, a, b) == e, (op, hex(a), hex(b))
+
+
+def test_binary_gcd_inversion(hostsim):
+    """fe25519.h fe_invert_bgcd (the batched finish's inversion): equal to z^(p-2) on random values,
+    powers of two and their neighbours, values near p and 0 (0 -> 0, as z^(p-2))."""
+    P = E.P
+    rng = random.Random(23)
+    vals = [0, 1, 2, 3, P - 1, P - 2, P, P + 1, 2**255 - 1, 2**254, 2**64, 2**64 - 1, 2**30, 2**30 - 1, 2**60 + 1]
+    vals += [2**rng.randrange(255) for _ in range(60)] + [(2**rng.randrange(255)) - 1 for _ in range(60)]
+    vals += [rng.randrange(2**rng.randrange(1, 256)) for _ in range(400)] + [P - rng.randrange(2**40) for _ in range(40)]
+    for a in vals:
+        assert _fe(hostsim, 9, a, 0) == pow(a % P, P - 2, P), hex(a)
 
 
 def test_pack256_roundtrip_at_the_limb_extremes(hostsim):
