@@ -375,6 +375,16 @@ def roofline_leg(eng, step, dev, n, offs, kernel_ms, no_peak):
             "clock_ghz": {"main_kernel": clk_main, "valu_peak_probe": clk_probe,
                           "source": "profiles/pmc_summary.json (rocprofv3 --pmc GRBM_GUI_ACTIVE, same run for both)"}
             if clk_main else None}
+    if peak and clk_main and clk_probe:
+        # the same fraction with the peak scaled to the main kernel's own clock: what is left when
+        # the clock the table traffic costs is taken out
+        roof["frac_at_kernel_clock"] = round(achieved / (peak * clk_main / clk_probe), 4)
+    va = pmc_field(MAIN_KERNEL, "valu_active_frac", 4)
+    if va is not None:
+        # SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES per wave x the kernel's 2 waves per SIMD: ~1 means
+        # the SIMD issues a VALU instruction every slot (issue-bound at its instruction mix)
+        roof["valu_issue_busy_est"] = {"valu_active_per_wave": va, "waves_per_simd": 2,
+                                       "busy": round(2 * va, 3), "source": "profiles/pmc_summary.json"}
     return roof, peak
 
 
@@ -585,17 +595,22 @@ def pmc_traffic(sigs_per_launch, kernel=None):
     return None, None
 
 
-def pmc_clock(kernel):
-    """Effective clock (GHz) of `kernel` from the committed PMC summary, or None."""
+def pmc_field(kernel, key, nd=3):
+    """`key` of `kernel` in the committed PMC summary (profiles/pmc_summary.json), or None."""
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_summary.json")) as fh:
             pmc = json.load(fh)
     except (OSError, ValueError):
         return None
     for k, d in pmc.items():
-        if k.split("<")[0] == kernel and "effective_clock_ghz" in d:
-            return round(d["effective_clock_ghz"], 3)
+        if k.split("<")[0] == kernel and key in d:
+            return round(d[key], nd)
     return None
+
+
+def pmc_clock(kernel):
+    """Effective clock (GHz) of `kernel` from the committed PMC summary, or None."""
+    return pmc_field(kernel, "effective_clock_ghz")
 
 
 def _cpu_model():

@@ -572,6 +572,9 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
             return np.array([self.res[h].verified for h in range(self.n)], np.int64)
 
     marshals = []  # one shim context per window held at once (a window in flight keeps its arrays)
+    # the overlapped pass keeps each window's Go objects until both of its flattens ran (~1.6 GB per
+    # 1000-block window, 13 per shard): one rank per node only, so an 8-rank node does not hold 8x that
+    overlap = marshal == "compiled" and stream and pregen and world == 1
 
     def to_arena(commits, k):
         if k == len(arenas):
@@ -608,7 +611,7 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
                     arenas.append(_Pageable(window * nvals * 64))
             cw = _CompiledWindow(marshals[k], None, len(commits),
                                  (heap, si, ci, [c.height for c in commits], arenas[k].ptr if pinned else None))
-            if not (stream and pregen):  # marshalled here; the stream marshals inside its overlapped pass
+            if not overlap:  # marshalled here; otherwise inside the stream's overlapped pass
                 tm = time.perf_counter()
                 cw.marshal()
                 t_marshal += time.perf_counter() - tm
@@ -659,13 +662,13 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
             t_gen += time.perf_counter() - tg
             if world > 1:
                 dist.barrier()
-            if marshal == "compiled" and stream and first:
+            if overlap and first:
                 wins[0][2].marshal()  # the warmup's own (untimed) flatten of window 0
             for _ in range(2 if first else 0):  # untimed warmup (see below)
                 wins[0][2].run(eng, batch)
                 eng.keycache_wait()
             first = False
-            if marshal == "compiled" and stream:
+            if overlap:
                 # the drop-in's pipeline: each window flattened by the shim right before its submit,
                 # so the flatten of window k+1 runs while the device verifies window k (submit is
                 # asynchronous); timed from the first flatten to the wait.  The flattens alone are
