@@ -328,7 +328,7 @@ def c3(eng, headers: int, gap: int, policy: str = "cache", runs: int = 7, bisect
     policy: "cache" (the sets carry no handle: the seam's key-set cache pools their keys — the
     drop-in as patched), "pool" (one explicit key set of every key, keyset_index per set) or
     "generic" (cache off).  With the cache the first direct call is cold (generic kernels, the keys
-    queued) and the second builds the radix-2^10 combs: both are reported, untimed in the median.
+    queued) and the second builds the radix-2^12 combs: both are reported, untimed in the median.
     The request marshalling (PreparedBatch: flat arrays + C structs for every request, what the Go
     shim rebuilds per call) is timed beside the seam.  corrupt_every > 0: known-answer bad
     signatures in the direct leg's commits (_c3_corrupt), every request's code and index checked
@@ -361,7 +361,7 @@ def c3(eng, headers: int, gap: int, policy: str = "cache", runs: int = 7, bisect
     t_cold = time.perf_counter() - t0
     eng.keycache_wait()
     t0 = time.perf_counter()
-    pb.run(eng)  # warm-up (cache: first keyed call, radix-2^10 combs built)
+    pb.run(eng)  # warm-up (cache: first keyed call, radix-2^12 combs built)
     t_warm = time.perf_counter() - t0
     k1 = eng.keycache_stats()
     med, lo, hi, phases = _timed_runs(eng, pb, runs)
@@ -681,12 +681,19 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
                 ready = [threading.Event() for _ in wins]
                 tmar = [0.0] * len(wins)
 
+                perr = []
+
                 def producer():
-                    for i, (_, _, pw, _, _) in enumerate(wins):
-                        tq = time.perf_counter()
-                        pw.marshal()
-                        tmar[i] = time.perf_counter() - tq
-                        ready[i].set()
+                    try:
+                        for i, (_, _, pw, _, _) in enumerate(wins):
+                            tq = time.perf_counter()
+                            pw.marshal()
+                            tmar[i] = time.perf_counter() - tq
+                            ready[i].set()
+                    except BaseException as e:  # wake the submitting thread; it re-raises
+                        perr.append(e)
+                        for ev in ready:
+                            ev.set()
 
                 if world > 1:
                     dist.barrier()
@@ -695,9 +702,13 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
                 th.start()
                 for i, (w0, w1, win, exp, _) in enumerate(wins):
                     ready[i].wait()
+                    if perr:
+                        break
                     win.submit(eng, batch)
                 T.blocksync_wait(eng)
                 th.join()
+                if perr:
+                    raise perr[0]
                 ov_pass[0] += time.perf_counter() - t0
                 ov_pass[3] += sum(tmar)
                 for w0, w1, win, exp, _ in wins:
@@ -751,7 +762,7 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
             t_gen += time.perf_counter() - tg
             if w0 == lo:
                 # untimed warmup: first-use buffers and events of the seam; with the key-set cache the
-                # first call runs generic and queues the keys, the second builds the radix-2^10 combs
+                # first call runs generic and queues the keys, the second builds the radix-2^12 combs
                 for _ in range(2):
                     win.run(eng, batch)
                     eng.keycache_wait()

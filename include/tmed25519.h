@@ -112,11 +112,12 @@ int tmed_b_window_bits(const tmed_ctx *ctx);
  */
 int tmed_keyset_b_window_bits(const tmed_ctx *ctx);
 /*
- * Radix (in bits) of the -A comb the key-cached throughput kernel reads for key set `handle`: 10
- * (26 windows of 513 multiples, 1.7 MB per key, built at the set's first throughput batch with the
- * radix-2^24 B comb in use: 37 comb rows per signature) or 8 (the radix-256 comb every key set
- * holds, also used by the latency kernels: TMED_KS_A10=0, before the first throughput batch, or
- * no memory).  -1 for an unknown handle.  Diagnostic; decisions are identical.
+ * Radix (in bits) of the -A comb the key-cached throughput kernel reads for key set `handle`: 12
+ * (21 windows of 2049 multiples, the top one 4225, 5.8 MB per key, built at the set's first
+ * throughput batch with the radix-2^24 B comb in use: 32 comb rows per signature) or 8 (the
+ * radix-256 comb every key set holds, also used by the latency kernels: TMED_KS_ACOMB=0, before
+ * the first throughput batch, or no memory).  -1 for an unknown handle.  Diagnostic; decisions
+ * are identical.
  */
 int tmed_keyset_a_window_bits(tmed_ctx *ctx, uint64_t handle);
 
@@ -313,8 +314,8 @@ typedef struct {
  * are cache hits).  Decisions are identical either way.
  *   enabled: 1 on, 0 off (sets without a handle stay generic), -1 unchanged (default on; env
  *            TMED_KEYCACHE=0 turns it off at tmed_init);
- *   budget_bytes: 0 unchanged, else the pool's HBM budget (default 64 GiB, env TMED_KEYCACHE_GB;
- *            ~2.2 MB per key with the radix-2^10 comb): a set that does not fit empties the pool
+ *   budget_bytes: 0 unchanged, else the pool's HBM budget (default 160 GiB, env TMED_KEYCACHE_GB;
+ *            ~6.3 MB per key with the radix-2^12 comb): a set that does not fit empties the pool
  *            when no call is using it, else stays generic.
  */
 int tmed_keycache_config(tmed_ctx *ctx, int enabled, size_t budget_bytes);

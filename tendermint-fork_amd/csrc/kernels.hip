@@ -36,29 +36,11 @@ namespace tmed {
 __device__ int4 kIdentityRow[8] = {{1, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}, {0, 0, 0, 0},
                                           {1, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
 
-// Cache policy of the main kernel's memory streams (A/B knob, bit mask; 0 = default policy):
-// 1 the per-lane table stores, 2 the per-lane table loads, 4 the radix-2^26 / 2^16 B rows
-// (global_load_lds), issued non-temporal (gfx950 nt: streamed, not kept in L2 / MALL).
-#ifndef TMED_SLAB_NT
-#define TMED_SLAB_NT 0
-#endif
-typedef int v4i32 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void slab_st(int4 *p, int4 v) {
-#if TMED_SLAB_NT & 1
-  const v4i32 x = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(x, reinterpret_cast<v4i32 *>(p));
-#else
-  *p = v;
-#endif
-}
-__device__ __forceinline__ int4 slab_ld(const int4 *p) {
-#if TMED_SLAB_NT & 2
-  const v4i32 x = __builtin_nontemporal_load(reinterpret_cast<const v4i32 *>(p));
-  return make_int4(x.x, x.y, x.z, x.w);
-#else
-  return *p;
-#endif
-}
+// Per-lane table rows go through the default cache policy: a non-temporal policy for the slab
+// stores, the slab loads or the B rows was measured at -12 / -6 / -0.5 % on C2 (all three -26 %,
+// profiles/r05/s2/): a lane re-reads its rows ~4 times and nt sends every re-read to HBM.
+__device__ __forceinline__ void slab_st(int4 *p, int4 v) { *p = v; }
+__device__ __forceinline__ int4 slab_ld(const int4 *p) { return *p; }
 
 struct SlabTab {
   int4 *base;
@@ -146,8 +128,7 @@ struct BPf {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the previous take's LDS reads are done
 #pragma unroll
     for (int q = 0; q < 8; q++)
-      __builtin_amdgcn_global_load_lds((global_void *)(tab + (size_t)j * 8 + q), (lds_void *)(buf + q * 64), 16, 0,
-                                       (TMED_SLAB_NT & 4) ? 2 : 0);  // aux 2: nt
+      __builtin_amdgcn_global_load_lds((global_void *)(tab + (size_t)j * 8 + q), (lds_void *)(buf + q * 64), 16, 0, 0);
   }
   __device__ __forceinline__ void take(ge_niels &e) const {
     fe *fs[3] = {&e.YpX, &e.YmX, &e.XY2d};
@@ -816,22 +797,127 @@ __device__ __forceinline__ void niels_load(ge_niels &e, const int4 *src) {
   }
 }
 
-// One workgroup per (key, window); lane j computes (j+1) * base (verify_core.h comb_entry).
-__global__ __launch_bounds__(128) void comb_fill_kernel(const int32_t *__restrict__ bases, uint32_t n,
+// Comb entries in runs of kCombARun consecutive j per lane: the run's first entry j0 * base by
+// double-and-add over nbits bits of j0, the next ones by one cached addition each (8 M), the run's
+// projective points parked in their own comb rows (X, Y, Z: 30 of the row's 32 words) and their
+// prefix products of Z in LDS, ONE inversion per run (Montgomery's trick: 3 M per entry), then
+// each row rewritten in affine niels form.  ~6k mads per entry against ~34k for a double-and-add
+// and an inversion per entry (the round-5 radix-2^12 comb of 10k keys: 1.6 s of device time that
+// way, 98 ms like this — profiles/r05/final/ and s14/ kernel_stats.csv).
+constexpr uint32_t kCombARun = 8;
+__device__ __forceinline__ void row_store_xyz(int4 *row, const ge_p3 &P) {
+  const fe *fs[3] = {&P.X, &P.Y, &P.Z};
+#pragma unroll
+  for (int q = 0; q < kCombEntryInt4; q++) {
+    int32_t w[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int f = 4 * q + c;
+      w[c] = f < 30 ? fs[f / 10]->v[f % 10] : 0;
+    }
+    row[q] = make_int4(w[0], w[1], w[2], w[3]);
+  }
+}
+__device__ __forceinline__ void row_load_xyz(const int4 *row, fe &X, fe &Y, fe &Z) {
+  fe *fs[3] = {&X, &Y, &Z};
+#pragma unroll
+  for (int q = 0; q < kCombEntryInt4; q++) {
+    const int4 v = row[q];
+    const int32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int f = 4 * q + c;
+      if (f < 30) fs[f / 10]->v[f % 10] = w[c];
+    }
+  }
+}
+// rows[j] = j * base for j = j0 .. j0 + kCombARun - 1 (rows: the window's entry 0; base: p3 words;
+// pre: this block's LDS, 64 lanes)
+__device__ __forceinline__ void comb_fill_run(int4 *rows, const int32_t *base, uint32_t j0, int nbits,
+                              fe (*pre)[64], uint32_t lane) {
+  ge_p3 B, P;
+  p3_load(B, base);
+  ge_cached cB;
+  ge_p3_to_cached(cB, B);
+  {  // P = j0 * B, double-and-add over j0's bits
+    ge_p3 sum;
+    ge_p1p1 t;
+    ge_p2 q;
+    ge_p3_0(P);
+#pragma unroll 1
+    for (int b = nbits - 1; b >= 0; b--) {
+      ge_p3_to_p2(q, P);
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p3(P, t);
+      ge_add_cached(t, P, cB, false);
+      ge_p1p1_to_p3(sum, t);
+      const bool bit = (j0 >> b) & 1u;
+      fe_select(P.X, P.X, sum.X, bit);
+      fe_select(P.Y, P.Y, sum.Y, bit);
+      fe_select(P.Z, P.Z, sum.Z, bit);
+      fe_select(P.T, P.T, sum.T, bit);
+    }
+  }
+  fe acc;
+#pragma unroll 1
+  for (uint32_t t = 0; t < kCombARun; t++) {
+    if (t) {
+      ge_p1p1 s;
+      ge_add_cached(s, P, cB, false);
+      ge_p1p1_to_p3(P, s);
+      fe_mul(acc, acc, P.Z);
+    } else {
+      fe_copy(acc, P.Z);
+    }
+    row_store_xyz(rows + (size_t)(j0 + t) * kCombEntryInt4, P);
+    pre[t][lane] = acc;
+  }
+  fe inv, d2;
+  fe_invert_bgcd(inv, acc);
+  fe_const_d2(d2);
+#pragma unroll 1
+  for (int t = (int)kCombARun - 1; t >= 0; t--) {
+    int4 *r = rows + (size_t)(j0 + t) * kCombEntryInt4;
+    fe X, Y, Z, zi, x, y, xy;
+    row_load_xyz(r, X, Y, Z);
+    if (t) {
+      fe_mul(zi, inv, pre[t - 1][lane]);
+      fe_mul(inv, inv, Z);
+    } else {
+      fe_copy(zi, inv);
+    }
+    fe_mul_x2(x, X, zi, y, Y, zi);
+    ge_niels e;
+    fe_add(e.YpX, y, x); fe_carry(e.YpX, e.YpX);
+    fe_sub(e.YmX, y, x); fe_carry(e.YmX, e.YmX);
+    fe_mul(xy, x, y);
+    fe_mul(e.XY2d, xy, d2);
+    niels_store(r, e);
+  }
+}
+// the bit length of a run's largest start 1 + kCombARun (runs - 1)
+constexpr int comb_start_bits(uint32_t runs) {
+  int b = 0;
+  for (uint32_t v = 1 + kCombARun * (runs - 1); v; v >>= 1) b++;
+  return b;
+}
+
+// The radix-256 comb: 16 runs of 8 per (key, window) (j = 1..128), four windows per 64-lane block.
+constexpr uint32_t kCombRuns = (kCombEntries - 1) / kCombARun;  // 16
+static_assert((kCombEntries - 1) % kCombARun == 0 && 64 % kCombRuns == 0, "radix-256 comb runs");
+__global__ __launch_bounds__(64) void comb_fill_kernel(const int32_t *__restrict__ bases, uint32_t n,
                                                        int4 *__restrict__ comb) {
-  const uint32_t kw = blockIdx.x;  // key * 32 + window
-  const uint32_t j = threadIdx.x + 1;  // 1..128
-  ge_p3 P;
-  p3_load(P, bases + (size_t)kw * 40);
-  ge_niels e;
-  comb_entry(e, P, j);
-  int4 *row = comb + (size_t)kw * kCombEntries * kCombEntryInt4;
-  niels_store(row + (size_t)j * kCombEntryInt4, e);
-  if (threadIdx.x == 0) {
+  __shared__ fe pre[kCombARun][64];
+  const uint32_t kw = blockIdx.x * (64 / kCombRuns) + threadIdx.x / kCombRuns;  // key * 32 + window
+  const uint32_t run = threadIdx.x % kCombRuns;
+  if (kw >= n * kCombWindows) return;
+  int4 *rows = comb + (size_t)kw * kCombEntries * kCombEntryInt4;
+  if (run == 0) {
     ge_niels id;
     ge_niels_0(id);
-    niels_store(row, id);
+    niels_store(rows, id);
   }
+  comb_fill_run(rows, bases + (size_t)kw * 40, 1u + kCombARun * run, comb_start_bits(kCombRuns), pre, threadIdx.x);
 }
 
 struct GlobalComb {
@@ -1414,7 +1500,8 @@ hipError_t launch_comb_bases(const uint8_t *pubs, uint32_t n, int negate, uint8_
 
 hipError_t launch_comb_fill(const int32_t *bases, uint32_t n, int4 *comb, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(comb_fill_kernel, dim3(n * kCombWindows), dim3(128), 0, stream, bases, n, comb);
+  hipLaunchKernelGGL(comb_fill_kernel, dim3((n * kCombWindows + 64 / kCombRuns - 1) / (64 / kCombRuns)), dim3(64), 0,
+                     stream, bases, n, comb);
   return hipGetLastError();
 }
 
@@ -1446,32 +1533,34 @@ __global__ __launch_bounds__(64) void comba_bases_kernel(const uint8_t *__restri
   }
 }
 
-// 128-lane workgroups per (key, window), 2^(B-1) / 128 of them (kCombATopGroups for the top
-// window): lane j of the window computes j * base.
-constexpr uint32_t kCombAGroups = (kCombAEntries - 1) / 128;         // 16: j = 1..2048 (B = 12)
-constexpr uint32_t kCombAGroupsPerKey = (kCombAWindows - 1) * kCombAGroups + kCombATopGroups;
-__global__ __launch_bounds__(128) void comba_fill_kernel(const int32_t *__restrict__ bases, int4 *__restrict__ comb) {
-  const uint32_t key = blockIdx.x / kCombAGroupsPerKey, g = blockIdx.x % kCombAGroupsPerKey;
-  const uint32_t w = g < (kCombAWindows - 1) * kCombAGroups ? g / kCombAGroups : kCombAWindows - 1;
-  const uint32_t gw = g - w * kCombAGroups;  // group within the window
-  const uint32_t j = gw * 128u + threadIdx.x + 1u;
-  ge_p3 P;
-  p3_load(P, bases + ((size_t)key * kCombAWindows + w) * 40);
-  ge_niels e;
-  comb_entry(e, P, j, w + 1 == kCombAWindows ? kCombATopField : kCombABits);  // j < 2^nbits
-  int4 *row = comb + ((size_t)key * kCombARowsPerKey + comba_row((int)w, 0)) * kCombEntryInt4;
-  niels_store(row + (size_t)j * kCombEntryInt4, e);
-  if (j == 1) {
+// The radix-2^B comb of -A: runs of 8 (comb_fill_run), 64 runs per block, each block within one
+// (key, window).
+constexpr uint32_t kCombARunsReg = (kCombAEntries - 1) / kCombARun;     // 256: j = 1..2048
+constexpr uint32_t kCombARunsTop = (kCombATopEntries - 1) / kCombARun;  // 528: j = 1..4224
+static_assert((kCombAEntries - 1) % kCombARun == 0 && (kCombATopEntries - 1) % kCombARun == 0, "runs");
+constexpr uint32_t kCombABlocksReg = (kCombARunsReg + 63) / 64, kCombABlocksTop = (kCombARunsTop + 63) / 64;
+constexpr uint32_t kCombABlocksPerKey = (kCombAWindows - 1) * kCombABlocksReg + kCombABlocksTop;
+__global__ __launch_bounds__(64) void comba_fill_kernel(const int32_t *__restrict__ bases, int4 *__restrict__ comb) {
+  __shared__ fe pre[kCombARun][64];
+  const uint32_t key = blockIdx.x / kCombABlocksPerKey, g = blockIdx.x % kCombABlocksPerKey;
+  const bool top = g >= (kCombAWindows - 1) * kCombABlocksReg;
+  const uint32_t w = top ? kCombAWindows - 1 : g / kCombABlocksReg;
+  const uint32_t run = (g - w * kCombABlocksReg) * 64u + threadIdx.x;
+  int4 *rows = comb + ((size_t)key * kCombARowsPerKey + comba_row((int)w, 0)) * kCombEntryInt4;
+  if (run == 0) {
     ge_niels id;
     ge_niels_0(id);
-    niels_store(row, id);
+    niels_store(rows, id);
   }
+  if (run >= (top ? kCombARunsTop : kCombARunsReg)) return;
+  comb_fill_run(rows, bases + ((size_t)key * kCombAWindows + w) * 40, 1u + kCombARun * run,
+                top ? comb_start_bits(kCombARunsTop) : comb_start_bits(kCombARunsReg), pre, threadIdx.x);
 }
 
 hipError_t launch_build_comba(const uint8_t *pubs, uint32_t n, int32_t *bases, int4 *comba, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(comba_bases_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, pubs, n, bases);
-  hipLaunchKernelGGL(comba_fill_kernel, dim3(n * kCombAGroupsPerKey), dim3(128), 0, stream, bases, comba);
+  hipLaunchKernelGGL(comba_fill_kernel, dim3(n * kCombABlocksPerKey), dim3(64), 0, stream, bases, comba);
   return hipGetLastError();
 }
 

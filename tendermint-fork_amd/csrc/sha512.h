@@ -190,17 +190,13 @@ TMED_HD void sha512_sched(uint64_t w[16], int j) {
     sha512_round(v1, v2, v3, v4, v5, v6, v7, v0, sha512_k((R) + (J) + 7) + w[(J) + 7]); \
   } while (0)
 
-// 80 rounds.  TMED_SHA_PEEL 1: the first 16 (no message schedule) peeled, then 4 x 16 with the
-// schedule, so the rolled loop carries no per-round branch on the pass index; 0: 5 x 16 with the
-// schedule under `r > 0` (each round then compiles to a basic block of its own).  The
-// message-schedule window w[i & 15] stays register-indexed; the round constants come from a
-// uniform table (scalar loads on the device).
-#ifndef TMED_SHA_PEEL
-#define TMED_SHA_PEEL 1
-#endif
+// 80 rounds: the first 16 (no message schedule) peeled, then 4 x 16 with the schedule, so the
+// rolled loop carries no per-round branch on the pass index (5 x 16 under `r > 0` compiled every
+// round to a basic block of its own and spilled 4 VGPRs in the keyed prep: keyed C2 490 against
+// 521 M/s, profiles/r05/s6/).  The message-schedule window w[i & 15] stays register-indexed; the
+// round constants come from a uniform table (scalar loads on the device).
 TMED_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
   uint64_t v0 = st[0], v1 = st[1], v2 = st[2], v3 = st[3], v4 = st[4], v5 = st[5], v6 = st[6], v7 = st[7];
-#if TMED_SHA_PEEL
   TMED_SHA_8ROUNDS(0, 0, false);
   TMED_SHA_8ROUNDS(0, 8, false);
 #pragma unroll 1
@@ -208,13 +204,6 @@ TMED_HD void sha512_compress(uint64_t st[8], uint64_t w[16]) {
     TMED_SHA_8ROUNDS(r, 0, true);
     TMED_SHA_8ROUNDS(r, 8, true);
   }
-#else
-#pragma unroll 1
-  for (int r = 0; r < 80; r += 16) {
-    TMED_SHA_8ROUNDS(r, 0, r > 0);
-    TMED_SHA_8ROUNDS(r, 8, r > 0);
-  }
-#endif
   st[0] += v0; st[1] += v1; st[2] += v2; st[3] += v3; st[4] += v4; st[5] += v5; st[6] += v6; st[7] += v7;
 }
 #undef TMED_SHA_8ROUNDS

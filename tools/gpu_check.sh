@@ -52,7 +52,7 @@ for s in $STEPS; do
       IFS='|' read -ra SETS <<< "$PMC_SETS"
       for ctr in "${SETS[@]}"; do
         tag=$(echo $ctr | tr ' ' '_')
-        timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$OUT/pmc_$tag -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-peak --c1-reps 50 --no-c4 --no-c5 --no-zip215 > $GRAFT_REPO_ROOT/$OUT/pmc_$tag.log 2>&1; rc=$?
+        timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$OUT/pmc_$tag -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline ${PMC_ARGS---no-peak} --c1-reps 50 --no-c4 --no-c5 --no-zip215 > $GRAFT_REPO_ROOT/$OUT/pmc_$tag.log 2>&1; rc=$?
         echo "pmc $ctr rc=$rc" | tee -a $GRAFT_REPO_ROOT/$OUT/pmc.log
         if fatal $rc; then break; fi
       done
