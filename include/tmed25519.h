@@ -120,6 +120,16 @@ int tmed_keyset_b_window_bits(const tmed_ctx *ctx);
  * are identical.
  */
 int tmed_keyset_a_window_bits(tmed_ctx *ctx, uint64_t handle);
+/*
+ * Diagnostic (tests): entry j of window `window` of key `key`'s comb in key set `handle`, as the 30
+ * int32 limbs (radix 2^25.5) the kernels read: y + x, y - x, 2d x y of the affine point
+ * j * R^window * (-A_key), with R = 256 for radix_bits 8 (the comb every key set holds) or
+ * R = 2^radix_bits for the throughput comb (radix_bits = tmed_keyset_a_window_bits(handle)).
+ * Drains the device first.  TMED_EINVAL for an unknown handle, an index out of range or a comb
+ * not built.
+ */
+int tmed_keyset_comb_entry(tmed_ctx *ctx, uint64_t handle, uint32_t key, int radix_bits, uint32_t window, uint32_t j,
+                           int32_t out[30]);
 
 /* Device time (ms) of the last verify/sign launch on this context (HIP events).  A commit batch
  * small enough for the zero-copy latency mode (a single commit), or a tmed_verify_batch of at most

@@ -354,6 +354,32 @@ int tmed_keyset_a_window_bits(tmed_ctx *c, uint64_t handle) {
   return k->d_comba && k->comba_n == k->n && c->d_b24 ? kCombABits : 8;
 }
 
+int tmed_keyset_comb_entry(tmed_ctx *c, uint64_t handle, uint32_t key, int radix_bits, uint32_t window, uint32_t j,
+                           int32_t out[30]) {
+  if (!c || !out) return TMED_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  const Keyset *k = find_keyset(c, handle);
+  if (!k || key >= k->n) return TMED_EINVAL;
+  const int4 *src;
+  if (radix_bits == 8) {
+    if (window >= (uint32_t)kCombWindows || j >= kCombEntries || !k->d_comb) return TMED_EINVAL;
+    src = k->d_comb + ((size_t)key * kCombWindows * kCombEntries + (size_t)window * kCombEntries + j) * kCombEntryInt4;
+  } else if (radix_bits == kCombABits) {
+    if (!k->d_comba || key >= k->comba_n || window >= (uint32_t)kCombAWindows) return TMED_EINVAL;
+    if (j >= (window + 1 == (uint32_t)kCombAWindows ? kCombATopEntries : kCombAEntries)) return TMED_EINVAL;
+    src = k->d_comba + ((size_t)key * kCombARowsPerKey + comba_row((int)window, j)) * kCombEntryInt4;
+  } else {
+    return TMED_EINVAL;
+  }
+  int4 row[kCombEntryInt4];
+  // the builds are queued on the context stream / the key worker's stream: drain both first
+  if (hipStreamSynchronize(c->stream) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return TMED_EHIP;
+  if (hipMemcpy(row, src, sizeof(row), hipMemcpyDeviceToHost) != hipSuccess) return TMED_EHIP;
+  const int32_t *w = reinterpret_cast<const int32_t *>(row);
+  for (int i = 0; i < 30; i++) out[i] = w[i];
+  return TMED_OK;
+}
+
 int tmed_window_stats(tmed_ctx *c, uint32_t lane_hist[65], uint32_t wave_hist[65]) {
   if (!c || !lane_hist || !wave_hist) return TMED_EINVAL;
   std::lock_guard<std::mutex> lk(c->mu);

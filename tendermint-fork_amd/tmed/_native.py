@@ -96,6 +96,9 @@ def lib() -> ctypes.CDLL:
     l.tmed_keyset_b_window_bits.argtypes = [P]
     l.tmed_keyset_a_window_bits.restype = I
     l.tmed_keyset_a_window_bits.argtypes = [P, ctypes.c_uint64]
+    l.tmed_keyset_comb_entry.restype = I
+    l.tmed_keyset_comb_entry.argtypes = [P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32,
+                                         ctypes.c_uint32, P]
     l.tmed_host_alloc.restype = I
     l.tmed_host_alloc.argtypes = [SZ, ctypes.POINTER(ctypes.c_void_p)]
     l.tmed_host_free.restype = I
@@ -122,7 +125,7 @@ EXPORTED_SYMBOLS = [
     "tmed_keycache_config", "tmed_keycache_stats", "tmed_keycache_flush", "tmed_keycache_warm", "tmed_keycache_wait", "tmed_verify_batch_keyset_device",
     "tmed_set_kernel_timing", "tmed_kernel_times", "tmed_blocksync_verify", "tmed_blocksync_submit", "tmed_blocksync_wait",
     "tmed_merkle_roots", "tmed_valset_hashes", "tmed_header_hashes", "tmed_partset_roots",
-    "tmed_verify_commits_multi", "tmed_blocksync_verify_multi", "tmed_window_stats", "tmed_b_window_bits", "tmed_keyset_b_window_bits", "tmed_keyset_a_window_bits", "tmed_seam_phase_us",
+    "tmed_verify_commits_multi", "tmed_blocksync_verify_multi", "tmed_window_stats", "tmed_b_window_bits", "tmed_keyset_b_window_bits", "tmed_keyset_a_window_bits", "tmed_keyset_comb_entry", "tmed_seam_phase_us",
     "tmed_verify_batch_zip215", "tmed_verify_batch_zip215_device", "tmed_zip215_set_seed", "tmed_zip215_stats",
     "tmed_host_alloc", "tmed_host_free", "tmed_host_register", "tmed_host_unregister",
 ]

@@ -301,9 +301,18 @@ class Engine:
         return int(lib().tmed_keyset_b_window_bits(self._h))
 
     def keyset_a_window_bits(self, handle: int) -> int:
-        """Radix (bits) of the -A comb the throughput kernel reads for a key set: 10 or 8
-        (tmed_keyset_a_window_bits; 10 once the set's first throughput batch built it)."""
+        """Radix (bits) of the -A comb the throughput kernel reads for a key set: 12 or 8
+        (tmed_keyset_a_window_bits; 12 once the set's first throughput batch built it)."""
         return int(lib().tmed_keyset_a_window_bits(self._h, handle))
+
+    def keyset_comb_entry(self, handle: int, key: int, radix_bits: int, window: int, j: int) -> np.ndarray:
+        """Diagnostic: one comb row of a key set as its 30 int32 limbs (y + x, y - x, 2d x y of
+        j * R^window * (-A); tmed_keyset_comb_entry)."""
+        out = np.zeros(30, np.int32)
+        rc = lib().tmed_keyset_comb_entry(self._h, handle, key, radix_bits, window, j, out.ctypes.data)
+        if rc != 0:
+            raise TmedError(rc, "tmed_keyset_comb_entry")
+        return out
 
     def last_kernel_ms(self) -> float:
         return float(lib().tmed_last_kernel_ms(self._h))

@@ -59,3 +59,55 @@ def test_b_window_radix_and_decisions(radix_engines, golden, cfg, b_bits, ks_bit
         assert (out == exp).all(), [vs[i]["class"] for i in np.nonzero(out != exp)[0]][:10]
     finally:
         eng.keyset_free(h)
+
+
+def _limbs_to_int(v):
+    """30 int32 limbs of radix 2^25.5 (limb i weighs 2^ceil(25.5 i)) -> an integer (mod p)."""
+    off = [0, 26, 51, 77, 102, 128, 153, 179, 204, 230]
+    return sum(int(x) << o for x, o in zip(v, off))
+
+
+def _niels(pt):
+    from oracle import ed25519_go as E
+    x, y, z, _ = pt
+    zi = pow(z, E.P - 2, E.P)
+    x, y = x * zi % E.P, y * zi % E.P
+    return ((y + x) % E.P, (y - x) % E.P, 2 * E.D * x * y % E.P)
+
+
+def test_key_comb_rows_equal_the_oracle(radix_engines, golden):
+    """Both key combs, read back row by row (tmed_keyset_comb_entry) and compared with
+    j * R^w * (-A) from the oracle: the radix-256 comb every key set holds (R = 256) and the
+    throughput comb (R = 2^12, built at the set's first throughput batch), at the edges of the
+    kernels' runs of 8 entries (comb_fill_run: one double-and-add, then additions, one batched
+    inversion per run), the windows' last entries and the top window's range, for keys that decode
+    and keys that do not (their base is the identity, every row (1, 1, 0))."""
+    from oracle import ed25519_go as E
+    eng = radix_engines["default"]
+    vs, karr, idx, sigs, msgs, offs, exp = _golden_arrays(golden)
+    pts = [E.decode(bytes(k)) for k in karr]
+    good = [i for i, p in enumerate(pts) if p is not None][:3]
+    bad = [i for i, p in enumerate(pts) if p is None][:1]
+    h = eng.keyset_load(karr)
+    try:
+        eng.verify_keyset_arrays(h, idx, sigs, msgs, offs)  # the first throughput batch builds the 2^12 comb
+        B = eng.keyset_a_window_bits(h)
+        assert B == 12
+        W = 253 // B
+        cases = [(8, w, j) for w in (0, 1, 17, 31) for j in (0, 1, 2, 8, 9, 16, 17, 64, 127, 128)]
+        cases += [(B, w, j) for w in (0, 1, 11, W - 2) for j in (0, 1, 7, 8, 9, 10, 1023, 1024, 2041, 2047, 2048)]
+        cases += [(B, W - 1, j) for j in (0, 1, 8, 9, 2048, 2049, 4096, 4097, 4217, 4224)]
+        for key in good + bad:
+            for bits, w, j in cases:
+                row = eng.keyset_comb_entry(h, key, bits, w, j)
+                got = tuple(_limbs_to_int(row[10 * c:10 * c + 10]) % E.P for c in range(3))
+                if pts[key] is None or j == 0:
+                    assert got == (1, 1, 0), (key, bits, w, j)
+                    continue
+                base = E.pt_neg(pts[key])
+                want = _niels(E.pt_mul(j * (1 << ((8 if bits == 8 else bits) * w)), base))
+                assert got == want, (key, bits, w, j)
+        with pytest.raises(Exception):
+            eng.keyset_comb_entry(h, 0, B, W - 1, 4225)  # past the top window
+    finally:
+        eng.keyset_free(h)
