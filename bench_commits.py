@@ -700,13 +700,15 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
                 t0 = time.perf_counter()
                 th = threading.Thread(target=producer)
                 th.start()
-                for i, (w0, w1, win, exp, _) in enumerate(wins):
-                    ready[i].wait()
-                    if perr:
-                        break
-                    win.submit(eng, batch)
-                T.blocksync_wait(eng)
-                th.join()
+                try:
+                    for i, (w0, w1, win, exp, _) in enumerate(wins):
+                        ready[i].wait()
+                        if perr:
+                            break
+                        win.submit(eng, batch)
+                    T.blocksync_wait(eng)
+                finally:
+                    th.join()  # the producer writes into the shim contexts: never leave it running
                 if perr:
                     raise perr[0]
                 ov_pass[0] += time.perf_counter() - t0
