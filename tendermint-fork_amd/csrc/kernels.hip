@@ -596,13 +596,15 @@ __global__ __launch_bounds__(kThreadsPerBlock) void verify_finish_kernel(
   finish_group(a);
 }
 
-// Finish launch for the m signatures at fin_base: group size G = m / 65536 clamped to
-// [1, 16] (65,536 lanes keep every SIMD busy; each lane pays one inversion per group).
+// Finish launch for the m signatures at fin_base: group size G = ceil(m / 65536) clamped to
+// [1, 16], so at most 65,536 lanes = one wave per SIMD: each lane pays one inversion per group,
+// a latency-bound chain, and a SIMD holding two such waves runs them ~twice as long (a C4 batch of
+// ~853k votes took 13 per group = 1,025 waves with the floor: C4 585 -> 591 M/s, profiles/r05/s17/).
 hipError_t launch_finish(const int4 *fin, int4 *pre, const uint8_t *sig, uint8_t *out, uint32_t fin_base, uint32_t m,
                          hipStream_t stream, const uint32_t *perm = nullptr) {
   if (m == 0) return hipSuccess;
   constexpr uint32_t kLanes = 65536;  // one inversion per lane and group; 65,536 lanes fill every SIMD
-  uint32_t G = m / kLanes;
+  uint32_t G = (m + kLanes - 1) / kLanes;
   if (G < 1) G = 1;
   if (G > kFinGroupMax) G = kFinGroupMax;
   const uint32_t L = (m + G - 1) / G;
