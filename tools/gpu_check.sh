@@ -17,7 +17,7 @@ for s in $STEPS; do
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?
       echo "smoke rc=$rc" | tee -a $OUT/smoke.log ;;
     bench)
-      timeout -k 10 600 python bench.py > $OUT/bench.log 2>&1; rc=$?
+      t0=$(date +%s); timeout -k 10 600 python bench.py > $OUT/bench.log 2>&1; rc=$?; echo "bench wall $(( $(date +%s) - t0 )) s" >> $OUT/bench.log
       echo "bench rc=$rc" | tee -a $OUT/bench.log; tail -1 $OUT/bench.log ;;
     prof)
       cd /tmp && export TMPDIR=/tmp
