@@ -68,21 +68,40 @@ struct Keyset {
   size_t n = 0, cap = 0;
   uint8_t *d_pub = nullptr;   // cap x 32 raw encodings (hashed into k)
   uint8_t *d_ok = nullptr;    // cap: Point.SetBytes accepted the key
-  int4 *d_comb = nullptr;     // cap x kCombBytesPerKey: signed radix-256 comb of -A
-  // cap x kCombABytesPerKey: radix-2^12 comb of -A for the throughput kernel (kernels.h kCombA*), keys [0, comba_n)
-  // built (at the set's first throughput batch and for keys appended after it: keyset.hip
-  // comba_extend; null / comba_failed: TMED_KS_ACOMB=0 or no memory -> the radix-256 comb)
-  int4 *d_comba = nullptr;
+  // The combs in chunks of kKeyChunkKeys keys (kernels.h kKeyChunk*): chunk c holds keys
+  // [c * 512, c * 512 + keys[c]); every chunk but the last allocated one is full.  comb: signed
+  // radix-256 comb of -A (kCombBytesPerKey a key).  comba: radix-2^12 comb of -A for the throughput
+  // kernel (kernels.h kCombA*), keys [0, comba_n) built (at the set's first throughput batch and for
+  // keys appended after it: keyset.hip comba_extend; none / comba_failed: TMED_KS_ACOMB=0 or no
+  // memory -> the radix-256 comb).
+  std::vector<int4 *> comb, comba;
+  std::vector<uint32_t> comb_keys, comba_keys;
+  // device: the chunk bases, kKeyChunksMax of the radix-256 comb then kKeyChunksMax of the
+  // radix-2^12 comb (the kernels' tables); entries are set on the set's stream as chunks appear
+  int4 **d_tab = nullptr;
+  int4 **h_tab = nullptr;  // pinned mirror (the source of the entries' copies)
   size_t comba_n = 0;
   bool comba_failed = false;
   bool pooled = false;  // the context's key-set cache pool: not reachable through the public handles
+  const int4 *const *comb_tab() const { return d_tab; }
+  const int4 *const *comba_tab() const { return d_tab + kKeyChunksMax; }
+  size_t comb_room() const { return comb.empty() ? 0 : (comb.size() - 1) * (size_t)kKeyChunkKeys + comb_keys.back(); }
+  size_t comba_room() const { return comba.empty() ? 0 : (comba.size() - 1) * (size_t)kKeyChunkKeys + comba_keys.back(); }
+  // the row of entry (window w, j) of key v: radix-256 / radix-2^12
+  int4 *comb_row(size_t v, size_t row) const {
+    return comb[v >> kKeyChunkBits] + ((v & (kKeyChunkKeys - 1)) * kCombWindows * kCombEntries + row) * kCombEntryInt4;
+  }
+  int4 *comba_row_of(size_t v, size_t row) const {
+    return comba[v >> kKeyChunkBits] + ((v & (kKeyChunkKeys - 1)) * kCombARowsPerKey + row) * kCombEntryInt4;
+  }
 };
 
 int build_comb(tmed_ctx *c, const uint8_t *d_pubs, size_t n, int negate, uint8_t *d_ok, int4 *d_comb);
-// Append m keys (host pointer) to k on stream s: grows the buffers when needed (a copy of the built
-// keys and a synchronisation of s), uploads the keys through the context's pinned key staging and
-// queues their radix-256 combs; nothing waits for the build (later work on s is ordered behind it).
-// TMED_EINVAL past max_cap keys.
+// Append m keys (host pointer) to k on stream s: adds comb chunks when needed (the pool's hold
+// kKeyChunkKeys keys, up to max_cap; an explicit set's last chunk holds exactly its keys and is
+// replaced by a larger one when the set grows), uploads the keys through the context's pinned key
+// staging and queues their radix-256 combs; nothing waits for the build (later work on s is ordered
+// behind it).  TMED_EINVAL past max_cap keys.
 int keyset_append(tmed_ctx *c, Keyset &k, const uint8_t *pubkeys, size_t m, hipStream_t s, size_t max_cap);
 // Device bytes one key of a key set can take (radix-256 comb + radix-2^12 comb + encoding + flag).
 size_t keyset_bytes_per_key(const tmed_ctx *c);

@@ -101,6 +101,14 @@ constexpr int kCombWindows = 32;
 constexpr int kCombEntries = 129;
 constexpr int kCombEntryInt4 = 8;  // 128 B
 constexpr size_t kCombBytesPerKey = (size_t)kCombWindows * kCombEntries * kCombEntryInt4 * 16;
+// A key set's combs live in chunks of kKeyChunkKeys keys, each chunk its own allocation, so a set
+// grows by adding chunks: the keys already built never move, nothing is copied or freed (a pool
+// of 20k keys is ~130 GB, and freeing a large allocation costs ~1.5 s per 68 GB on the box).  Key
+// v's rows are in chunk v >> kKeyChunkBits at key offset v & (kKeyChunkKeys - 1); the kernels take
+// a device table of chunk bases (keyset.hip: the radix-256 comb's table, then the radix-2^12's).
+constexpr int kKeyChunkBits = 9;                                  // 512 keys: 270 MB radix-256, 2.96 GB radix-2^12
+constexpr uint32_t kKeyChunkKeys = 1u << kKeyChunkBits;
+constexpr uint32_t kKeyChunksMax = (1u << 24) >> kKeyChunkBits;  // key indexes are < 2^24
 
 // bases[key][w] = 256^w * (negate ? -A : A) as p3 (40 limbs); ok[key] = decode accepted.
 hipError_t launch_comb_bases(const uint8_t *pubs, uint32_t n, int negate, uint8_t *ok, int32_t *bases,
@@ -133,16 +141,16 @@ constexpr size_t comba_row(int w, uint32_t j) { return (size_t)w * kCombAEntries
 // comba[key] of -A_key (bases: scratch of n * kCombAWindows * 40 int32).
 hipError_t launch_build_comba(const uint8_t *pubs, uint32_t n, int32_t *bases, int4 *comba, hipStream_t stream);
 // Key-cached verification: key index per signature into a keyset of nkeys keys (an index
-// >= nkeys rejects that signature).  perm (nullable, n entries of scratch) + order_scratch
+// >= nkeys rejects that signature); acomb / acomba: the key set's chunk tables (kKeyChunk*).  perm (nullable, n entries of scratch) + order_scratch
 // (key_order_scratch_words): the main and finish kernels visit each chunk's signatures in
 // key-grouped order (launch_key_order per chunk); decisions still land at out[i].
 hipError_t launch_verify_keyset(const uint32_t *val_idx, uint32_t nkeys, const uint8_t *key_pub, const uint8_t *key_ok,
-                                const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
+                                const int4 *const *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                 const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
                                 int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots = false,
                                 KernelTimer *timer = nullptr, uint32_t *perm = nullptr,
                                 uint32_t *order_scratch = nullptr, const int4 *bcomb24 = nullptr,
-                                const int4 *acomba = nullptr);
+                                const int4 *const *acomba = nullptr);
 // Key-grouped visiting order of a key-cached batch (counting sort of val_idx by groups of
 // consecutive keys, indices >= nkeys last): perm[0..n) = signature indices grouped by key.
 // scratch: key_order_scratch_words(n, nkeys) u32.  The comb rows of the lanes in flight then
@@ -166,7 +174,7 @@ struct VoteAsm;
 // va (vote slots only): every lane of a signature's group assembles the vote's sign-bytes into
 // its slot first (identical bytes; no separate assemble_votes launch in front).
 hipError_t launch_verify_keyset_lat(const uint32_t *val_idx, uint32_t nkeys, const uint8_t *key_pub, const uint8_t *key_ok,
-                                    const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
+                                    const int4 *const *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                     const uint32_t *off, uint32_t n, uint8_t *out, int4 *fin, int4 *dec,
                                     hipStream_t stream, bool msg_slots = false, const VoteAsm *va = nullptr);
 

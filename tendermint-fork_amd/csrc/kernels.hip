@@ -1352,9 +1352,15 @@ __device__ __forceinline__ void keyset_straus_ab24(ge_p2 &out, const uint32_t k[
   }
 }
 
+// First row of key v's comb in a chunked key set (kernels.h kKeyChunk*): one 8-B table load per
+// signature in front of its first comb row.
+__device__ __forceinline__ const int4 *key_rows(const int4 *const *__restrict__ tab, uint32_t v, size_t int4_per_key) {
+  return tab[v >> kKeyChunkBits] + (size_t)(v & (kKeyChunkKeys - 1)) * int4_per_key;
+}
+
 template <int WAVES, bool B24 = false, bool ACOMB = false>
 __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_keyset_main_kernel(
-    const uint32_t *__restrict__ val_idx, uint32_t nkeys, const int4 *__restrict__ acomb,
+    const uint32_t *__restrict__ val_idx, uint32_t nkeys, const int4 *const *__restrict__ acomb,
     const int4 *__restrict__ bcomb, uint32_t base, uint32_t count, const int4 *__restrict__ prep, uint32_t stride,
     int4 *__restrict__ fin, uint32_t fin_base, uint8_t *__restrict__ out, const uint32_t *__restrict__ perm) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1378,11 +1384,11 @@ __global__ __launch_bounds__(kThreadsPerBlock, WAVES) void verify_keyset_main_ke
   for (int j = 0; j < 8; j++) { k[j] = (uint32_t)w[j]; s[j] = (uint32_t)w[8 + j]; }
 #if TMED_KS_PF
   ge_p2 R;
-  if (ACOMB) keyset_straus_ab24(R, k, s, acomb + (size_t)v * kCombARowsPerKey * kCombEntryInt4, bcomb);
-  else if (B24) keyset_straus_b24(R, k, s, acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4, bcomb);
-  else keyset_straus_pf(R, k, s, acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4, bcomb);
+  if (ACOMB) keyset_straus_ab24(R, k, s, key_rows(acomb, v, kCombARowsPerKey * kCombEntryInt4), bcomb);
+  else if (B24) keyset_straus_b24(R, k, s, key_rows(acomb, v, (size_t)kCombWindows * kCombEntries * kCombEntryInt4), bcomb);
+  else keyset_straus_pf(R, k, s, key_rows(acomb, v, (size_t)kCombWindows * kCombEntries * kCombEntryInt4), bcomb);
 #else
-  const GlobalComb ac{acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4};
+  const GlobalComb ac{key_rows(acomb, v, (size_t)kCombWindows * kCombEntries * kCombEntryInt4)};
   const GlobalComb16 bc{bcomb};
   ge_p3 R;
   verify_main_comb_point(R, k, s, ac, bc);
@@ -1619,7 +1625,7 @@ __device__ __forceinline__ void comb_partial_pf(ge_p3 &acc, const uint32_t kr[8]
 __global__ __launch_bounds__(64) void verify_keyset_lat_kernel(
     const uint32_t *__restrict__ val_idx, uint32_t nkeys, const uint8_t *__restrict__ key_pub,
     const uint8_t *__restrict__ key_ok,
-    const int4 *__restrict__ acomb, const int4 *__restrict__ bcomb, const uint8_t *__restrict__ sig, MsgSrc ms,
+    const int4 *const *__restrict__ acomb, const int4 *__restrict__ bcomb, const uint8_t *__restrict__ sig, MsgSrc ms,
     uint32_t m, uint32_t nR, int4 *__restrict__ fin, int4 *__restrict__ dec, uint8_t *__restrict__ out, VoteAsm va,
     int assemble) {
   __shared__ int4 tl[64][kVoteTmplBytes / 16];  // the comb lanes' vote templates (assemble_vote)
@@ -1656,7 +1662,7 @@ __global__ __launch_bounds__(64) void verify_keyset_lat_kernel(
   sc_recode256(kr, k);
   sc_recode256(sr, s);
   ge_p3 acc, o;
-  comb_partial_pf(acc, kr, sr, r, acomb + (size_t)v * kCombWindows * kCombEntries * kCombEntryInt4, bcomb);
+  comb_partial_pf(acc, kr, sr, r, key_rows(acomb, v, (size_t)kCombWindows * kCombEntries * kCombEntryInt4), bcomb);
 #pragma unroll 1
   for (int L = 1; L < kLatLanes; L <<= 1) {
     shfl_down_fe(o.X, acc.X, L);
@@ -1697,7 +1703,7 @@ __global__ __launch_bounds__(kThreadsPerBlock) void verify_lat_finish_kernel(con
 }
 
 hipError_t launch_verify_keyset_lat(const uint32_t *val_idx, uint32_t nkeys, const uint8_t *key_pub, const uint8_t *key_ok,
-                                    const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
+                                    const int4 *const *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                     const uint32_t *off, uint32_t n, uint8_t *out, int4 *fin, int4 *dec,
                                     hipStream_t stream, bool msg_slots, const VoteAsm *va) {
   if (n == 0) return hipSuccess;
@@ -1713,11 +1719,11 @@ hipError_t launch_verify_keyset_lat(const uint32_t *val_idx, uint32_t nkeys, con
 }
 
 hipError_t launch_verify_keyset(const uint32_t *val_idx, uint32_t nkeys, const uint8_t *key_pub, const uint8_t *key_ok,
-                                const int4 *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
+                                const int4 *const *acomb, const int4 *bcomb, const uint8_t *sig, const uint8_t *msgs,
                                 const uint32_t *off, uint32_t n, uint8_t *out, int4 *prep, uint32_t stride,
                                 int4 *fin, int4 *fin_pre, hipStream_t stream, bool msg_slots, KernelTimer *timer,
                                 uint32_t *perm, uint32_t *order_scratch, const int4 *bcomb24,
-                                const int4 *acomba) {
+                                const int4 *const *acomba) {
   const MsgSrc ms{msgs, off, msg_slots};
   if (stride > kFinCap) stride = kFinCap;
   if (timer) timer->mark(stream, -1);

@@ -185,8 +185,8 @@ int tmed_keycache_stats(tmed_ctx *c, tmed_keycache_counters *o) {
   auto it = c->keysets.find(kc.be.handle);
   if (kc.be.handle && it != c->keysets.end()) {
     const Keyset &k = it->second;
-    o->pool_bytes = k.cap * (33 + kCombBytesPerKey) + (k.d_comba ? k.cap * kCombABytesPerKey : 0);
-    o->pool_a_window_bits = k.d_comba && k.comba_n == k.n ? kCombABits : 8;
+    o->pool_bytes = k.cap * 33 + k.comb_room() * kCombBytesPerKey + k.comba_room() * kCombABytesPerKey;
+    o->pool_a_window_bits = !k.comba.empty() && k.comba_n == k.n ? kCombABits : 8;
   }
   return TMED_OK;
 }

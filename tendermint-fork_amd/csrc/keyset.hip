@@ -29,11 +29,19 @@ int build_comb(tmed_ctx *c, const uint8_t *d_pubs, size_t n, int negate, uint8_t
   return map_err(e);
 }
 
+static void free_chunks(std::vector<int4 *> &ch, std::vector<uint32_t> &keys) {
+  for (int4 *p : ch) (void)hipFree(p);
+  ch.clear();
+  keys.clear();
+}
+
 void free_keyset(Keyset &k) {
   if (k.d_pub) (void)hipFree(k.d_pub);
   if (k.d_ok) (void)hipFree(k.d_ok);
-  if (k.d_comb) (void)hipFree(k.d_comb);
-  if (k.d_comba) (void)hipFree(k.d_comba);
+  free_chunks(k.comb, k.comb_keys);
+  free_chunks(k.comba, k.comba_keys);
+  if (k.d_tab) (void)hipFree(k.d_tab);
+  if (k.h_tab) (void)hipHostFree(k.h_tab);
   k = Keyset();
 }
 
@@ -47,33 +55,88 @@ static bool key_order_on(const Keyset &k, uint32_t n) {
   return n >= 4096 && k.n > 1 && k.n <= kKeyOrderMaxKeys;
 }
 
+// Chunks of one comb (kernels.h kKeyChunk*, bytes_per_key a key) with room for keys [0, want): a
+// missing chunk c is allocated for min(kKeyChunkKeys, limit - c * 512) keys (limit >= want); a
+// partial chunk too small for `want` is replaced by a larger one, its built keys (those below
+// `built`) copied over on s and the old chunk left in `retired` (freed by the caller once the
+// streams reading it are drained).  Each new base goes into the set's table, ordered on s.
+static hipError_t chunks_grow(std::vector<int4 *> &ch, std::vector<uint32_t> &keys, int4 **h_tab, int4 **d_tab,
+                              size_t want, size_t limit, size_t bytes_per_key, size_t built, hipStream_t s,
+                              std::vector<void *> &retired) {
+  for (size_t c = 0; c * kKeyChunkKeys < want; c++) {
+    const size_t first = c * kKeyChunkKeys;
+    const size_t need = std::min<size_t>(kKeyChunkKeys, want - first);
+    if (c < ch.size() && keys[c] >= need) continue;
+    const size_t alloc = std::min<size_t>(kKeyChunkKeys, std::max(need, limit - first));
+    int4 *p = nullptr;
+    hipError_t e = hipMalloc((void **)&p, alloc * bytes_per_key);
+    if (e != hipSuccess) return e;
+    if (c < ch.size()) {
+      const size_t nb = built > first ? std::min<size_t>(built - first, keys[c]) : 0;
+      if (nb) e = hipMemcpyAsync(p, ch[c], nb * bytes_per_key, hipMemcpyDeviceToDevice, s);
+      if (e != hipSuccess) {
+        (void)hipFree(p);
+        return e;
+      }
+      retired.push_back(ch[c]);
+      ch[c] = p;
+      keys[c] = (uint32_t)alloc;
+    } else {
+      ch.push_back(p);
+      keys.push_back((uint32_t)alloc);
+    }
+    h_tab[c] = p;
+    e = hipMemcpyAsync(d_tab + c, h_tab + c, sizeof(int4 *), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// Free what chunks_grow / keyset_reserve replaced, after the streams that may read it (s and the
+// second kernel lane) are drained.
+static hipError_t free_retired(tmed_ctx *c, std::vector<void *> &retired, hipStream_t s) {
+  if (retired.empty()) return hipSuccess;
+  hipError_t e = hipStreamSynchronize(s);
+  if (e == hipSuccess && c->lane1.s) e = hipStreamSynchronize(c->lane1.s);
+  for (void *p : retired) (void)hipFree(p);
+  retired.clear();
+  return e;
+}
+
+// The radix-2^12 comb gone (no memory for it): the radix-256 comb serves the set.
+static void comba_drop(Keyset &k) {
+  (void)hipGetLastError();
+  free_chunks(k.comba, k.comba_keys);  // hipFree waits for the kernels still reading them
+  k.comba_n = 0;
+}
+
 // The key set's radix-2^12 comb (kernels.h kCombA*) for keys [comba_n, n), on stream s (queued
 // in front of the batch that needs it; the bases scratch is freed after a sync of s): at the set's
-// first throughput batch, then for keys appended after it.  TMED_KS_ACOMB=0 (read at tmed_init) keeps
-// the radix-256 comb; so does a failed allocation (comba_failed).
+// first throughput batch, then for keys appended after it.  Its chunks mirror the radix-256 comb's.
+// TMED_KS_ACOMB=0 (read at tmed_init) keeps the radix-256 comb; so does a failed allocation
+// (comba_failed).
 static void comba_extend(tmed_ctx *c, Keyset &k, hipStream_t s) {
   if (!c->acomb_on || k.comba_failed || k.comba_n >= k.n) return;
-  if (!k.d_comba && hipMalloc((void **)&k.d_comba, k.cap * kCombABytesPerKey) != hipSuccess) {
-    (void)hipGetLastError();
-    k.d_comba = nullptr;
-    k.comba_failed = true;
-    return;
-  }
-  const size_t m = k.n - k.comba_n;
+  std::vector<void *> retired;
+  hipError_t e = chunks_grow(k.comba, k.comba_keys, k.h_tab + kKeyChunksMax, k.d_tab + kKeyChunksMax, k.n,
+                             k.comb_room(), kCombABytesPerKey, k.comba_n, s, retired);
   int32_t *bases = nullptr;
-  hipError_t e = hipMalloc((void **)&bases, m * kCombAWindows * 40 * sizeof(int32_t));
-  if (e == hipSuccess)
-    e = launch_build_comba(k.d_pub + 32 * k.comba_n, (uint32_t)m, bases,
-                            k.d_comba + k.comba_n * (kCombABytesPerKey / sizeof(int4)), s);
+  const size_t m = k.n - k.comba_n;
+  if (e == hipSuccess) e = hipMalloc((void **)&bases, std::min<size_t>(m, kKeyChunkKeys) * kCombAWindows * 40 * sizeof(int32_t));
+  for (size_t a = k.comba_n; e == hipSuccess && a < k.n;) {  // one launch pair per chunk the keys fall in
+    const size_t end = std::min<size_t>(k.n, ((a >> kKeyChunkBits) + 1) * kKeyChunkKeys);
+    e = launch_build_comba(k.d_pub + 32 * a, (uint32_t)(end - a), bases, k.comba_row_of(a, 0), s);
+    a = end;
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (bases) (void)hipFree(bases);
+  if (e == hipSuccess) e = free_retired(c, retired, s);
   if (e == hipSuccess) {
     k.comba_n = k.n;
   } else {  // an allocation failure leaves the radix-256 comb in use
     (void)hipGetLastError();
-    (void)hipFree(k.d_comba);
-    k.d_comba = nullptr;
-    k.comba_n = 0;
+    (void)free_retired(c, retired, s);
+    comba_drop(k);
     k.comba_failed = true;
   }
 }
@@ -87,51 +150,55 @@ Keyset *find_keyset(tmed_ctx *c, uint64_t handle) {
   return it == c->keysets.end() || it->second.pooled ? nullptr : &it->second;
 }
 
-// Room for `cap` keys: new buffers, the built keys (and their radix-2^12 combs) copied over on s,
-// a synchronisation of s, the old buffers freed.  A radix-2^12 comb that no longer fits is dropped
-// (rebuilt at the next throughput batch, or the radix-256 comb is used).
-static int keyset_reserve(tmed_ctx *c, Keyset &k, size_t cap, hipStream_t s) {
-  if (cap <= k.cap) return TMED_OK;
-  uint8_t *pub = nullptr, *ok = nullptr;
-  int4 *comb = nullptr, *comba = nullptr;
-  hipError_t e = hipMalloc((void **)&pub, cap * 32);
-  if (e == hipSuccess) e = hipMalloc((void **)&ok, cap);
-  if (e == hipSuccess) e = hipMalloc((void **)&comb, cap * kCombBytesPerKey);
-  if (e == hipSuccess && k.d_comba && hipMalloc((void **)&comba, cap * kCombABytesPerKey) != hipSuccess) {
-    (void)hipGetLastError();
-    comba = nullptr;
+// Room for keys [0, want): the encodings and flags (33 B a key) in new buffers when they are full
+// (doubling up to `limit`, the built ones copied over), the radix-256 comb's chunks added
+// (chunks_grow: nothing built moves, except the keys of a partial last chunk); a synchronisation of
+// s and the second lane only when a replaced buffer is freed.  The radix-2^12 comb follows at the
+// next throughput batch (comba_extend).
+static int keyset_reserve(tmed_ctx *c, Keyset &k, size_t want, size_t limit, hipStream_t s) {
+  hipError_t e = hipSuccess;
+  const size_t tab_bytes = 2 * (size_t)kKeyChunksMax * sizeof(int4 *);
+  if (!k.d_tab) {
+    e = hipMalloc((void **)&k.d_tab, tab_bytes);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&k.h_tab, tab_bytes, hipHostMallocDefault);
+    if (e == hipSuccess) {
+      memset(k.h_tab, 0, tab_bytes);
+      e = hipMemsetAsync(k.d_tab, 0, tab_bytes, s);
+    }
+    if (e != hipSuccess) return map_err(e);
   }
-  if (e == hipSuccess && k.n) {
-    e = hipMemcpyAsync(pub, k.d_pub, k.n * 32, hipMemcpyDeviceToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(ok, k.d_ok, k.n, hipMemcpyDeviceToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(comb, k.d_comb, k.n * kCombBytesPerKey, hipMemcpyDeviceToDevice, s);
-    if (e == hipSuccess && comba && k.comba_n)
-      e = hipMemcpyAsync(comba, k.d_comba, k.comba_n * kCombABytesPerKey, hipMemcpyDeviceToDevice, s);
+  std::vector<void *> retired;
+  if (want > k.cap) {
+    const size_t cap = std::max(want, std::min(2 * k.cap, limit));
+    uint8_t *pub = nullptr, *ok = nullptr;
+    e = hipMalloc((void **)&pub, cap * 32);
+    if (e == hipSuccess) e = hipMalloc((void **)&ok, cap);
+    if (e == hipSuccess && k.n) {
+      e = hipMemcpyAsync(pub, k.d_pub, k.n * 32, hipMemcpyDeviceToDevice, s);
+      if (e == hipSuccess) e = hipMemcpyAsync(ok, k.d_ok, k.n, hipMemcpyDeviceToDevice, s);
+    }
+    if (e != hipSuccess) {
+      if (pub) (void)hipFree(pub);
+      if (ok) (void)hipFree(ok);
+      return map_err(e);
+    }
+    if (k.d_pub) retired.push_back(k.d_pub);
+    if (k.d_ok) retired.push_back(k.d_ok);
+    k.d_pub = pub;
+    k.d_ok = ok;
+    k.cap = cap;
   }
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e == hipSuccess && c->lane1.s) e = hipStreamSynchronize(c->lane1.s);  // its batches read the old buffers
-  if (e != hipSuccess) {
-    for (void *p : {(void *)pub, (void *)ok, (void *)comb, (void *)comba})
-      if (p) (void)hipFree(p);
-    return map_err(e);
-  }
-  for (void *p : {(void *)k.d_pub, (void *)k.d_ok, (void *)k.d_comb, (void *)k.d_comba})
-    if (p) (void)hipFree(p);
-  k.d_pub = pub;
-  k.d_ok = ok;
-  k.d_comb = comb;
-  k.d_comba = comba;
-  if (!comba) k.comba_n = 0;
-  k.cap = cap;
-  return TMED_OK;
+  e = chunks_grow(k.comb, k.comb_keys, k.h_tab, k.d_tab, want, limit, kCombBytesPerKey, k.n, s, retired);
+  const hipError_t ef = free_retired(c, retired, s);
+  return map_err(e != hipSuccess ? e : ef);
 }
 
 int keyset_append(tmed_ctx *c, Keyset &k, const uint8_t *pubkeys, size_t m, hipStream_t s, size_t max_cap) {
   if (m == 0) return TMED_OK;
   max_cap = std::min<size_t>(max_cap, 0xffffffu);
   if (k.n + m > max_cap) return TMED_EINVAL;
-  int rc = TMED_OK;
-  if (k.n + m > k.cap) rc = keyset_reserve(c, k, std::max(k.n + m, std::min(2 * k.cap, max_cap)), s);
+  // the pool's chunks are whole up to its budget; an explicit set holds exactly its keys
+  int rc = keyset_reserve(c, k, k.n + m, k.pooled ? max_cap : k.n + m, s);
   if (rc != TMED_OK) return rc;
   // the pinned key staging and the comb-base scratch are reused once the previous build is done
   hipError_t e = hipSuccess;
@@ -145,7 +212,11 @@ int keyset_append(tmed_ctx *c, Keyset &k, const uint8_t *pubkeys, size_t m, hipS
   e = hipMemcpyAsync(k.d_pub + 32 * k.n, c->h_kup.p, m * 32, hipMemcpyHostToDevice, s);
   int32_t *bases = (int32_t *)c->d_kbases.p;
   if (e == hipSuccess) e = launch_comb_bases(k.d_pub + 32 * k.n, (uint32_t)m, /*negate=*/1, k.d_ok + k.n, bases, s);
-  if (e == hipSuccess) e = launch_comb_fill(bases, (uint32_t)m, k.d_comb + k.n * (kCombBytesPerKey / sizeof(int4)), s);
+  for (size_t a = k.n; e == hipSuccess && a < k.n + m;) {  // one fill launch per chunk the keys fall in
+    const size_t end = std::min<size_t>(k.n + m, ((a >> kKeyChunkBits) + 1) * kKeyChunkKeys);
+    e = launch_comb_fill(bases + (a - k.n) * kCombWindows * 40, (uint32_t)(end - a), k.comb_row(a, 0), s);
+    a = end;
+  }
   if (e == hipSuccess) e = hipEventRecord(c->kup_ev, s);
   if (e != hipSuccess) return map_err(e);
   k.n += m;
@@ -159,11 +230,11 @@ static hipError_t keyset_verify(tmed_ctx *c, Keyset &k, const uint32_t *d_idx, c
                                 hipStream_t s, bool msg_slots, const VoteAsm *va = nullptr, Lane *lane = nullptr) {
   c->last_hs_count = 0;  // d_prep now holds another path's hand-off (tmed_window_stats)
   if (n <= c->lat_max)
-    return launch_verify_keyset_lat(d_idx, (uint32_t)k.n, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb, d_sig, d_msgs, d_off, n, d_out,
+    return launch_verify_keyset_lat(d_idx, (uint32_t)k.n, k.d_pub, k.d_ok, k.comb_tab(), c->d_bcomb, d_sig, d_msgs, d_off, n, d_out,
                                     c->d_fin, c->d_fin_pre, s, msg_slots, va);
   if (va) return hipErrorInvalidValue;
   if (c->d_b24) comba_extend(c, k, s);
-  const int4 *comba = c->d_b24 && k.d_comba && k.comba_n == k.n ? k.d_comba : nullptr;
+  const int4 *const *comba = c->d_b24 && !k.comba.empty() && k.comba_n == k.n ? k.comba_tab() : nullptr;
   KernelTimer *timer = (c->timing && !msg_slots) ? &c->timer : nullptr;
   uint32_t *perm = nullptr, *scratch = nullptr;
   DevBuf &korder = lane ? lane->d_korder : c->d_korder;
@@ -175,7 +246,7 @@ static hipError_t keyset_verify(tmed_ctx *c, Keyset &k, const uint32_t *d_idx, c
     perm = scratch + sw;
   }
   // (the key order runs in front of each chunk's prep and is charged to prep by the timer)
-  return launch_verify_keyset(d_idx, (uint32_t)k.n, k.d_pub, k.d_ok, k.d_comb, c->d_bcomb16, d_sig, d_msgs, d_off, n,
+  return launch_verify_keyset(d_idx, (uint32_t)k.n, k.d_pub, k.d_ok, k.comb_tab(), c->d_bcomb16, d_sig, d_msgs, d_off, n,
                               d_out, lane ? lane->d_prep : c->d_prep, c->slab_slots, lane ? lane->d_fin : c->d_fin,
                               lane ? lane->d_fin_pre : c->d_fin_pre, s, msg_slots, timer, perm, scratch, c->d_b24,
                               comba);
@@ -454,7 +525,8 @@ int tmed_keyset_load(tmed_ctx *c, const uint8_t *pubkeys, size_t n, uint64_t *ha
   std::lock_guard<std::mutex> lk(c->mu);
   (void)hipSetDevice(c->device);
   Keyset k;
-  int rc = keyset_reserve(c, k, n ? n : 1, c->stream);
+  // room for one key at least: an index past an empty set still reads key 0's rows (and rejects)
+  int rc = keyset_reserve(c, k, n ? n : 1, n ? n : 1, c->stream);
   if (rc == TMED_OK) rc = keyset_append(c, k, pubkeys, n, c->stream, n);
   if (rc == TMED_OK) rc = map_err(hipStreamSynchronize(c->stream));
   if (rc == TMED_OK) (void)ctx_bcomb24(c);  // the shared radix-2^24 B comb (null: radix 2^16)

@@ -351,7 +351,7 @@ int tmed_keyset_a_window_bits(tmed_ctx *c, uint64_t handle) {
   std::lock_guard<std::mutex> lk(c->mu);
   const Keyset *k = find_keyset(c, handle);
   if (!k) return -1;
-  return k->d_comba && k->comba_n == k->n && c->d_b24 ? kCombABits : 8;
+  return !k->comba.empty() && k->comba_n == k->n && c->d_b24 ? kCombABits : 8;
 }
 
 int tmed_keyset_comb_entry(tmed_ctx *c, uint64_t handle, uint32_t key, int radix_bits, uint32_t window, uint32_t j,
@@ -362,12 +362,12 @@ int tmed_keyset_comb_entry(tmed_ctx *c, uint64_t handle, uint32_t key, int radix
   if (!k || key >= k->n) return TMED_EINVAL;
   const int4 *src;
   if (radix_bits == 8) {
-    if (window >= (uint32_t)kCombWindows || j >= kCombEntries || !k->d_comb) return TMED_EINVAL;
-    src = k->d_comb + ((size_t)key * kCombWindows * kCombEntries + (size_t)window * kCombEntries + j) * kCombEntryInt4;
+    if (window >= (uint32_t)kCombWindows || j >= kCombEntries) return TMED_EINVAL;
+    src = k->comb_row(key, (size_t)window * kCombEntries + j);
   } else if (radix_bits == kCombABits) {
-    if (!k->d_comba || key >= k->comba_n || window >= (uint32_t)kCombAWindows) return TMED_EINVAL;
+    if (k->comba.empty() || key >= k->comba_n || window >= (uint32_t)kCombAWindows) return TMED_EINVAL;
     if (j >= (window + 1 == (uint32_t)kCombAWindows ? kCombATopEntries : kCombAEntries)) return TMED_EINVAL;
-    src = k->d_comba + ((size_t)key * kCombARowsPerKey + comba_row((int)window, j)) * kCombEntryInt4;
+    src = k->comba_row_of(key, comba_row((int)window, j));
   } else {
     return TMED_EINVAL;
   }

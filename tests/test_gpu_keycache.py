@@ -27,6 +27,9 @@ def cached():
     e.close()
 
 
+_PER_KEY = 33 + 32 * 129 * 128 + (20 * 2049 + 4225) * 128  # keyset_bytes_per_key with the radix-2^12 comb
+
+
 def _delta(a, b):
     return {k: b[k] - a[k] for k in ("lookups", "hits", "keyed_sets", "generic_sets", "keys_appended",
                                      "keys_deferred", "pool_resets", "keyed_sigs", "generic_sigs")}
@@ -203,8 +206,7 @@ def test_budget_resets_and_wrong_set_hash(cached):
     Every call equals the oracle."""
     a = _c1(cached, b"kc-A")
     b = _c1(cached, b"kc-B")
-    per_key = 33 + 32 * 129 * 128 + (20 * 2049 + 4225) * 128  # keyset_bytes_per_key with the radix-2^12 comb
-    cached.keycache_config(True, 300 * per_key)
+    cached.keycache_config(True, 300 * _PER_KEY)
     ra, ea = _c1_requests(*a)
     rb, eb = _c1_requests(*b)
     for rnd in range(2):
@@ -213,7 +215,8 @@ def test_budget_resets_and_wrong_set_hash(cached):
             s0 = cached.keycache_stats()
             got = T.verify_commits(cached, reqs)
             assert _delta(s0, cached.keycache_stats())["keyed_sets"] == 1
-            assert all(_same(got[q], exp[q]) for q in range(len(reqs)))
+            bad = [(q, str(got[q]), str(exp[q])) for q in range(len(reqs)) if not _same(got[q], exp[q])]
+            assert not bad, (rnd, bad[:3], cached.keycache_stats())
     assert cached.keycache_stats()["pool_resets"] >= 3
     cached.keycache_config(True, 8 << 30)
     h = bytes(range(32))
@@ -224,7 +227,8 @@ def test_budget_resets_and_wrong_set_hash(cached):
             for (reqs, exp) in ((ra, ea), (rb, eb)):
                 got = T.verify_commits(cached, reqs)
                 cached.keycache_wait()
-                assert all(_same(got[q], exp[q]) for q in range(len(reqs)))
+                bad = [(q, str(got[q]), str(exp[q])) for q in range(len(reqs)) if not _same(got[q], exp[q])]
+                assert not bad, (bad[:3], cached.keycache_stats())
     finally:
         a[0].set_hash = b[0].set_hash = None
 
@@ -248,3 +252,53 @@ def test_keyset_extend_keeps_indexes(cached):
         assert s["lookups"] == 0  # a set with a handle never reaches the cache
     finally:
         cached.keyset_free(ks)
+
+
+def _bs_window(eng, tag, nv=64, nb=4096):
+    """A blocksync window (64 validators x 4,096 blocks, VerifyCommitLight per block) whose
+    signatures pay for its keys: keyed, through the throughput kernels, on its first call."""
+    seeds = seeds_from_tag(tag, 0, nv)
+    vals, order = make_valset(pubkeys_of(eng, seeds), [10] * nv)
+    addrs = np.array([np.frombuffer(v.address, np.uint8) for v in vals.validators])
+    upto = nv * 2 // 3 + 1
+    specs = [(seeds[order], addrs, b + 1, 0, _bid(tag + b"-%d" % b), T2023 + b, None) for b in range(nb)]
+    commits = sign_commits(eng, CHAIN, specs, sign_upto=upto)
+    for b in range(5, nb, 89):
+        _corrupt(commits[b], (b * 7) % upto)
+    return vals, CHAIN, [c.block_id for c in commits], [c.height for c in commits], commits
+
+
+def test_pool_grows_under_throughput_batches(engine):
+    """The pool grows while its radix-2^12 combs are in use: window A's 64 keys are built (combs of
+    both radixes, throughput kernels), then window B's 64 keys are appended (the pool's chunk gains
+    keys, the radix-2^12 comb is extended for them), then A runs again over the keys built before.
+    Every outcome equals the cache-off generic path's."""
+    eng = engine_with_env(TMED_KEYCACHE=1)
+    try:
+        eng.keycache_config(True, 8 << 30)
+        wins = [_bs_window(eng, t) for t in (b"kc-grow-A", b"kc-grow-B")]
+        refs = []
+        for w in wins:
+            r = T.BlocksyncWindow(*w)
+            r.run(engine, 128)
+            refs.append(r)
+        for i in (0, 1, 0, 1):
+            s0 = eng.keycache_stats()
+            got = T.BlocksyncWindow(*wins[i])
+            got.run(eng, 128)
+            d = _delta(s0, eng.keycache_stats())
+            assert d["keyed_sets"] == 1 and d["generic_sets"] == 0
+            assert (got.codes() == refs[i].codes()).all() and (got.verified() == refs[i].verified()).all(), i
+            assert not got.codes().all() and got.codes().any()  # both outcomes present
+        assert eng.keycache_stats()["pool_keys"] == 128
+        # the budget shrinks below the pool: the pool is dropped at once (its memory freed, not
+        # kept for reuse) and A's next call builds its keys again, in plain allocations
+        eng.keycache_config(True, 64 * _PER_KEY)
+        assert eng.keycache_stats()["pool_keys"] == 0
+        s0 = eng.keycache_stats()
+        got = T.BlocksyncWindow(*wins[0])
+        got.run(eng, 128)
+        assert (got.codes() == refs[0].codes()).all() and (got.verified() == refs[0].verified()).all()
+        assert _delta(s0, eng.keycache_stats())["keys_appended"] == 64 and eng.keycache_stats()["pool_keys"] == 64
+    finally:
+        eng.close()

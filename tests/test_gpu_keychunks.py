@@ -1,0 +1,71 @@
+"""Key sets across comb chunks (kernels.h kKeyChunk*: 512 keys a chunk, each its own allocation,
+the kernels reading a table of chunk bases).  An explicit key set of 1,100 keys (chunks of 512,
+512 and 76 keys) is extended by 600 (the partial chunk replaced by a larger one, its built keys
+copied over; one new chunk).  Batches through the throughput kernels (both combs) and the latency
+kernels, with indexes over every key, equal the port oracle before and after; comb rows read back
+at the chunk edges equal j * R^w * (-A)."""
+import numpy as np
+import pytest
+
+from oracle import port
+from test_gpu_btables import _limbs_to_int, _niels
+
+pytestmark = pytest.mark.gpu
+
+
+def _keys(n, seed):
+    seeds = np.random.default_rng(seed).integers(0, 256, (n, 32), dtype=np.uint8)
+    offs = np.arange(n + 1, dtype=np.uint64) * 8
+    msgs = np.zeros(8 * n + 16, np.uint8)
+    _, pubs = port.sign_batch(seeds, msgs, offs, 8)
+    return seeds, pubs
+
+
+def _batch(seeds, pubs, nkeys, n, seed):
+    rng = np.random.default_rng(seed)
+    vi = rng.integers(0, nkeys, n).astype(np.uint32)
+    vi[:4] = [0, nkeys - 1, min(511, nkeys - 1), min(512, nkeys - 1)]
+    lens = rng.integers(100, 140, n)
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    msgs = rng.integers(0, 256, int(offs[-1]) + 16, dtype=np.uint8)
+    sigs, _ = port.sign_batch(seeds[vi], msgs, offs, 8)
+    sigs[::37, 5] ^= 2
+    exp = port.verify_batch(pubs[vi], sigs, msgs, offs, 8)
+    return vi, sigs, msgs, offs.astype(np.uint32), exp
+
+
+def _rows_match(eng, h, pubs, keys, bits_list):
+    from oracle import ed25519_go as E
+    for key in keys:
+        pt = E.decode(bytes(pubs[key]))
+        assert pt is not None
+        base = E.pt_neg(pt)
+        for bits in bits_list:
+            W = 32 if bits == 8 else 253 // bits
+            top = 128 if bits == 8 else 4224
+            for w, j in ((0, 1), (1, 9), (W - 1, top)):
+                row = eng.keyset_comb_entry(h, key, bits, w, j)
+                got = tuple(_limbs_to_int(row[10 * c:10 * c + 10]) % E.P for c in range(3))
+                assert got == _niels(E.pt_mul(j * (1 << (bits * w)), base)), (key, bits, w, j)
+
+
+def test_key_set_across_chunks(engine):
+    seeds, pubs = _keys(1700, 77)
+    h = engine.keyset_load(pubs[:1100])
+    try:
+        big = _batch(seeds, pubs, 1100, 40000, 1)
+        assert (engine.verify_keyset_arrays(h, *big[:4]) == big[4]).all()  # throughput: builds the 2^12 comb
+        assert engine.keyset_a_window_bits(h) == 12
+        small = _batch(seeds, pubs, 1100, 700, 2)
+        assert (engine.verify_keyset_arrays(h, *small[:4]) == small[4]).all()  # latency kernels
+        _rows_match(engine, h, pubs, (511, 512, 1023, 1024, 1099), (8, 12))
+        assert engine.keyset_extend(h, pubs[1100:]) == 1100
+        big2 = _batch(seeds, pubs, 1700, 40000, 3)
+        assert (engine.verify_keyset_arrays(h, *big2[:4]) == big2[4]).all()  # the 2^12 comb extended
+        assert engine.keyset_a_window_bits(h) == 12
+        small2 = _batch(seeds, pubs, 1700, 700, 4)
+        assert (engine.verify_keyset_arrays(h, *small2[:4]) == small2[4]).all()
+        _rows_match(engine, h, pubs, (1024, 1099, 1100, 1535, 1536, 1699), (8, 12))
+    finally:
+        engine.keyset_free(h)
