@@ -45,6 +45,8 @@ def c1(eng, reps: int, cpu: bool, first_sets: int = 30):
       first_call_after_set_change  the same harness on `first_sets` sets never seen before, one call
                        each (generic kernels; the call queues the set's keys for the next one), the
                        device idle between calls as between blocks;
+      first_call_after_warmed_set_change  sets the node warmed when it learnt them
+                       (tmed_keycache_warm at the validator update, two heights ahead), then one call;
       generic_cache_off  the cache off: every call generic;
       explicit_keyset  a tmed_keyset_load handle passed by the caller (round-3 headline path).
     p50 / p90 / min over `reps` calls of one prepared request, and the p50 with the request marshalled
@@ -120,6 +122,25 @@ def c1(eng, reps: int, cpu: bool, first_sets: int = 30):
         eng.keycache_wait()  # the queued key build finishes before the next block's commit
     out["first_call_after_set_change"] = summary(np.array(firsts) * 1e3)
     out["first_call_after_set_change"]["generic_calls"] = eng.keycache_stats()["generic_sets"] - gen_before
+    # the same on sets the node warmed when it learnt them (tmed_keycache_warm: EndBlock's validator
+    # updates take effect two heights later, state/execution.go updateState, so the keys are built
+    # before the set's first commit arrives) — untimed warm, then the first call
+    firsts_w, specs = [], []
+    for k in range(first_sets):
+        sd, v2, o2, a2 = c1_set(b"tmed-c1-warm-%d" % k)
+        specs.append((sd[o2], a2, 3, 0, bid, T2023, None, v2))
+    fc = sign_commits(eng, "test_chain_id", [s[:7] for s in specs])
+    hits_before = eng.keycache_stats()["hits"]
+    for (spec, c2) in zip(specs, fc):
+        eng.keycache_warm(spec[7])
+        p2 = T.PreparedBatch([(T.MODE_COMMIT, spec[7], "test_chain_id", bid, 3, c2, 0, 0)])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        p2.run(eng)
+        firsts_w.append(time.perf_counter() - t0)
+        assert p2.codes()[0] == 0
+    out["first_call_after_warmed_set_change"] = summary(np.array(firsts_w) * 1e3)
+    out["first_call_after_warmed_set_change"]["cache_hits"] = eng.keycache_stats()["hits"] - hits_before
     eng.keycache_config(False)
     # the same first calls with the cache off (fresh sets, a fresh batch each, the device idle
     # before each): what a first call costs without the cache's resolution and queued build
