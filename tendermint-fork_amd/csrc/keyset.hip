@@ -92,12 +92,13 @@ static hipError_t chunks_grow(std::vector<int4 *> &ch, std::vector<uint32_t> &ke
   return hipSuccess;
 }
 
-// Free what chunks_grow / keyset_reserve replaced, after the streams that may read it (s and the
-// second kernel lane) are drained.
+// Free what chunks_grow / keyset_reserve replaced, after the streams that may read it (s, the
+// context stream and the second kernel lane) are drained.
 static hipError_t free_retired(tmed_ctx *c, std::vector<void *> &retired, hipStream_t s) {
   if (retired.empty()) return hipSuccess;
   hipError_t e = hipStreamSynchronize(s);
-  if (e == hipSuccess && c->lane1.s) e = hipStreamSynchronize(c->lane1.s);
+  if (e == hipSuccess && s != c->stream) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess && c->lane1.s && s != c->lane1.s) e = hipStreamSynchronize(c->lane1.s);
   for (void *p : retired) (void)hipFree(p);
   retired.clear();
   return e;
@@ -106,7 +107,8 @@ static hipError_t free_retired(tmed_ctx *c, std::vector<void *> &retired, hipStr
 // The radix-2^12 comb gone (no memory for it): the radix-256 comb serves the set.
 static void comba_drop(Keyset &k) {
   (void)hipGetLastError();
-  free_chunks(k.comba, k.comba_keys);  // hipFree waits for the kernels still reading them
+  (void)hipDeviceSynchronize();  // no kernel of either lane still reads them (a failure path only)
+  free_chunks(k.comba, k.comba_keys);
   k.comba_n = 0;
 }
 
