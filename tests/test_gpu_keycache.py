@@ -255,7 +255,7 @@ def test_keyset_extend_keeps_indexes(cached):
 
 
 def _bs_window(eng, tag, nv=64, nb=4096):
-    """A blocksync window (64 validators x 4,096 blocks, VerifyCommitLight per block) whose
+    """A blocksync window (default 64 validators x 4,096 blocks, VerifyCommitLight per block) whose
     signatures pay for its keys: keyed, through the throughput kernels, on its first call."""
     seeds = seeds_from_tag(tag, 0, nv)
     vals, order = make_valset(pubkeys_of(eng, seeds), [10] * nv)
@@ -300,5 +300,42 @@ def test_pool_grows_under_throughput_batches(engine):
         got.run(eng, 128)
         assert (got.codes() == refs[0].codes()).all() and (got.verified() == refs[0].verified()).all()
         assert _delta(s0, eng.keycache_stats())["keys_appended"] == 64 and eng.keycache_stats()["pool_keys"] == 64
+    finally:
+        eng.close()
+
+
+def test_pool_partial_chunk_replaced_after_budget_grows(engine):
+    """The pool's comb chunks (512 keys each) are whole up to its budget, so a budget of 700 keys
+    leaves chunk 1 holding 188.  A set of 600 validators is warmed and verified through the
+    throughput kernels (both combs built, chunk 1 partial); the budget then grows to 2,000 keys and
+    a set of 300 new validators is warmed: chunk 1 is replaced by a whole one with its 88 built keys
+    copied over (radix-256 comb at the append, radix-2^12 comb at the next throughput batch).  Both
+    sets' windows, before and after, equal the cache-off generic path's."""
+    eng = engine_with_env(TMED_KEYCACHE=1)
+    try:
+        eng.keycache_config(True, 700 * _PER_KEY)
+        wa = _bs_window(eng, b"kc-part-A", nv=600, nb=64)
+        wb = _bs_window(eng, b"kc-part-B", nv=300, nb=96)
+        refs = []
+        for w in (wa, wb):
+            r = T.BlocksyncWindow(*w)
+            r.run(engine, 64)
+            refs.append(r)
+
+        def run(i, w):
+            s0 = eng.keycache_stats()
+            got = T.BlocksyncWindow(*w)
+            got.run(eng, 64)
+            assert _delta(s0, eng.keycache_stats())["keyed_sets"] == 1
+            assert (got.codes() == refs[i].codes()).all() and (got.verified() == refs[i].verified()).all(), i
+
+        eng.keycache_warm(wa[0])
+        assert eng.keycache_stats()["pool_keys"] == 600
+        run(0, wa)
+        eng.keycache_config(True, 2000 * _PER_KEY)
+        eng.keycache_warm(wb[0])
+        assert eng.keycache_stats()["pool_keys"] == 900
+        run(1, wb)
+        run(0, wa)
     finally:
         eng.close()
