@@ -69,3 +69,51 @@ def test_key_set_across_chunks(engine):
         _rows_match(engine, h, pubs, (1024, 1099, 1100, 1535, 1536, 1699), (8, 12))
     finally:
         engine.keyset_free(h)
+
+
+def test_full_size_keyed_property(engine):
+    """BASELINE's key-cached C2 variant at full size: 2^20 GPU-signed signatures by 10,000 keys (20
+    comb chunks, 64 GB of combs) through the throughput kernels on the radix-2^12 comb: every
+    decision valid; a bit flipped in every signature flips every decision (size-independent); a
+    4,096-signature sample equals the port; an index past the set rejects."""
+    import torch
+    from tmed.workload import c2_messages, seeds_from_tag
+    n, nk = 1 << 20, 10_000
+    kseeds = seeds_from_tag(b"tmed-c2k-key", 0, nk)
+    val_idx = np.random.default_rng(7).integers(0, nk, n).astype(np.uint32)
+    msgs, offs = c2_messages(0, n)
+    dev = torch.device("cuda", 0)
+    d_seed = torch.from_numpy(kseeds[val_idx]).to(dev)
+    d_msg = torch.from_numpy(np.concatenate([msgs, np.zeros(16, np.uint8)])).to(dev)
+    d_off = torch.from_numpy(offs.view(np.int32)).to(dev)
+    d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    d_pub = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    d_out = torch.zeros(n, dtype=torch.uint8, device=dev)
+    engine.sign_device(d_seed, d_msg, d_off, d_sig, d_pub, n)
+    torch.cuda.synchronize()
+    pubs = np.zeros((nk, 32), np.uint8)
+    pubs[val_idx] = d_pub.cpu().numpy()
+    del d_seed, d_pub
+    h = engine.keyset_load(pubs)
+    try:
+        d_vi = torch.from_numpy(val_idx.view(np.int32)).to(dev)
+        engine.verify_keyset_device(h, d_vi, d_sig, d_msg, d_off, d_out, n)
+        torch.cuda.synchronize()
+        assert engine.keyset_a_window_bits(h) == 12
+        assert int(d_out.sum().item()) == n
+        d_sig[:, 40] ^= 1
+        engine.verify_keyset_device(h, d_vi, d_sig, d_msg, d_off, d_out, n)
+        torch.cuda.synchronize()
+        assert int(d_out.sum().item()) == 0
+        d_sig[:, 40] ^= 1
+        d_vi[12345] = nk  # past the set: rejected, the rest unchanged
+        engine.verify_keyset_device(h, d_vi, d_sig, d_msg, d_off, d_out, n)
+        torch.cuda.synchronize()
+        out = d_out.cpu().numpy()
+        assert out[12345] == 0 and int(out.sum()) == n - 1
+        m = 4096
+        sl = slice(n - m, n)
+        exp = port.verify_batch(pubs[val_idx[sl]], d_sig[sl].cpu().numpy(), msgs, offs[n - m:].astype(np.uint64), 16)
+        assert exp.all() and out[sl].all()
+    finally:
+        engine.keyset_free(h)
