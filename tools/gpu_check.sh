@@ -23,6 +23,10 @@ for s in $STEPS; do
       cd /tmp && export TMPDIR=/tmp
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline ${PROF_ARGS:-} > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1; rc=$?
       cd $GRAFT_REPO_ROOT; echo "prof rc=$rc" | tee -a $OUT/prof.log ;;
+    profc2)  # the C2 leg alone: every main-kernel launch is the full batch (its rocprof average = the roofline's)
+      cd /tmp && export TMPDIR=/tmp
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/profc2 -o c2 --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-keyset --no-c1 --no-c4 --no-c3 --no-c5 --no-zip215 --steps 100 > $GRAFT_REPO_ROOT/$OUT/profc2.log 2>&1; rc=$?
+      cd $GRAFT_REPO_ROOT; echo "profc2 rc=$rc" | tee -a $OUT/profc2.log ;;
     variants)
       rc=0
       IFS='|' read -ra VLIST <<< "${VARIANTS:-TMED_MAIN_WAVES=2|TMED_MAIN_WAVES=-2|TMED_MAIN_WAVES=3}"
