@@ -240,6 +240,9 @@ struct tmed_ctx {
   bool b24_tried = false;     // d_b24 acquired (or given up) at the first key-set load
   bool b24_on = true;         // TMED_B24 at tmed_init
   bool acomb_on = true;         // TMED_KS_ACOMB at tmed_init (radix-2^12 -A combs, keyset.hip comba_extend)
+  // TMED_TEST_FAIL_KS_ALLOC=n at tmed_init (tests only): the context's n-th key-set device allocation
+  // (keyset.hip ks_malloc: table, encodings, comb chunks, build scratch) reports out of memory
+  int test_fail_ks_alloc = 0;
   int4 *d_slab = nullptr;
   int4 *d_prep = nullptr;
   int4 *d_fin = nullptr;      // batched-finish hand-off (kFinBytes)

@@ -29,6 +29,16 @@ int build_comb(tmed_ctx *c, const uint8_t *d_pubs, size_t n, int negate, uint8_t
   return map_err(e);
 }
 
+// Every key-set device allocation goes through here (TMED_TEST_FAIL_KS_ALLOC: the failure paths
+// below are exercised by tests/test_gpu_keychunks.py).
+static hipError_t ks_malloc(tmed_ctx *c, void **p, size_t bytes) {
+  if (c->test_fail_ks_alloc > 0 && --c->test_fail_ks_alloc == 0) {
+    *p = nullptr;
+    return hipErrorOutOfMemory;
+  }
+  return hipMalloc(p, bytes);
+}
+
 static void free_chunks(std::vector<int4 *> &ch, std::vector<uint32_t> &keys) {
   for (int4 *p : ch) (void)hipFree(p);
   ch.clear();
@@ -60,7 +70,7 @@ static bool key_order_on(const Keyset &k, uint32_t n) {
 // partial chunk too small for `want` is replaced by a larger one, its built keys (those below
 // `built`) copied over on s and the old chunk left in `retired` (freed by the caller once the
 // streams reading it are drained).  Each new base goes into the set's table, ordered on s.
-static hipError_t chunks_grow(std::vector<int4 *> &ch, std::vector<uint32_t> &keys, int4 **h_tab, int4 **d_tab,
+static hipError_t chunks_grow(tmed_ctx *ctx, std::vector<int4 *> &ch, std::vector<uint32_t> &keys, int4 **h_tab, int4 **d_tab,
                               size_t want, size_t limit, size_t bytes_per_key, size_t built, hipStream_t s,
                               std::vector<void *> &retired) {
   for (size_t c = 0; c * kKeyChunkKeys < want; c++) {
@@ -69,7 +79,7 @@ static hipError_t chunks_grow(std::vector<int4 *> &ch, std::vector<uint32_t> &ke
     if (c < ch.size() && keys[c] >= need) continue;
     const size_t alloc = std::min<size_t>(kKeyChunkKeys, std::max(need, limit - first));
     int4 *p = nullptr;
-    hipError_t e = hipMalloc((void **)&p, alloc * bytes_per_key);
+    hipError_t e = ks_malloc(ctx, (void **)&p, alloc * bytes_per_key);
     if (e != hipSuccess) return e;
     if (c < ch.size()) {
       const size_t nb = built > first ? std::min<size_t>(built - first, keys[c]) : 0;
@@ -120,11 +130,11 @@ static void comba_drop(Keyset &k) {
 static void comba_extend(tmed_ctx *c, Keyset &k, hipStream_t s) {
   if (!c->acomb_on || k.comba_failed || k.comba_n >= k.n) return;
   std::vector<void *> retired;
-  hipError_t e = chunks_grow(k.comba, k.comba_keys, k.h_tab + kKeyChunksMax, k.d_tab + kKeyChunksMax, k.n,
+  hipError_t e = chunks_grow(c, k.comba, k.comba_keys, k.h_tab + kKeyChunksMax, k.d_tab + kKeyChunksMax, k.n,
                              k.comb_room(), kCombABytesPerKey, k.comba_n, s, retired);
   int32_t *bases = nullptr;
   const size_t m = k.n - k.comba_n;
-  if (e == hipSuccess) e = hipMalloc((void **)&bases, std::min<size_t>(m, kKeyChunkKeys) * kCombAWindows * 40 * sizeof(int32_t));
+  if (e == hipSuccess) e = ks_malloc(c, (void **)&bases, std::min<size_t>(m, kKeyChunkKeys) * kCombAWindows * 40 * sizeof(int32_t));
   for (size_t a = k.comba_n; e == hipSuccess && a < k.n;) {  // one launch pair per chunk the keys fall in
     const size_t end = std::min<size_t>(k.n, ((a >> kKeyChunkBits) + 1) * kKeyChunkKeys);
     e = launch_build_comba(k.d_pub + 32 * a, (uint32_t)(end - a), bases, k.comba_row_of(a, 0), s);
@@ -161,20 +171,28 @@ static int keyset_reserve(tmed_ctx *c, Keyset &k, size_t want, size_t limit, hip
   hipError_t e = hipSuccess;
   const size_t tab_bytes = 2 * (size_t)kKeyChunksMax * sizeof(int4 *);
   if (!k.d_tab) {
-    e = hipMalloc((void **)&k.d_tab, tab_bytes);
-    if (e == hipSuccess) e = hipHostMalloc((void **)&k.h_tab, tab_bytes, hipHostMallocDefault);
-    if (e == hipSuccess) {
-      memset(k.h_tab, 0, tab_bytes);
-      e = hipMemsetAsync(k.d_tab, 0, tab_bytes, s);
+    e = ks_malloc(c, (void **)&k.d_tab, tab_bytes);
+    if (e == hipSuccess) e = hipMemsetAsync(k.d_tab, 0, tab_bytes, s);
+    if (e != hipSuccess) {
+      if (k.d_tab) (void)hipFree(k.d_tab);
+      k.d_tab = nullptr;
+      return map_err(e);
     }
-    if (e != hipSuccess) return map_err(e);
+  }
+  if (!k.h_tab) {
+    e = hipHostMalloc((void **)&k.h_tab, tab_bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      k.h_tab = nullptr;
+      return map_err(e);
+    }
+    memset(k.h_tab, 0, tab_bytes);
   }
   std::vector<void *> retired;
   if (want > k.cap) {
     const size_t cap = std::max(want, std::min(2 * k.cap, limit));
     uint8_t *pub = nullptr, *ok = nullptr;
-    e = hipMalloc((void **)&pub, cap * 32);
-    if (e == hipSuccess) e = hipMalloc((void **)&ok, cap);
+    e = ks_malloc(c, (void **)&pub, cap * 32);
+    if (e == hipSuccess) e = ks_malloc(c, (void **)&ok, cap);
     if (e == hipSuccess && k.n) {
       e = hipMemcpyAsync(pub, k.d_pub, k.n * 32, hipMemcpyDeviceToDevice, s);
       if (e == hipSuccess) e = hipMemcpyAsync(ok, k.d_ok, k.n, hipMemcpyDeviceToDevice, s);
@@ -190,7 +208,7 @@ static int keyset_reserve(tmed_ctx *c, Keyset &k, size_t want, size_t limit, hip
     k.d_ok = ok;
     k.cap = cap;
   }
-  e = chunks_grow(k.comb, k.comb_keys, k.h_tab, k.d_tab, want, limit, kCombBytesPerKey, k.n, s, retired);
+  e = chunks_grow(c, k.comb, k.comb_keys, k.h_tab, k.d_tab, want, limit, kCombBytesPerKey, k.n, s, retired);
   const hipError_t ef = free_retired(c, retired, s);
   return map_err(e != hipSuccess ? e : ef);
 }

@@ -192,6 +192,7 @@ int tmed_init(int device, tmed_ctx **out) {
   if (e == hipSuccess && !env_off("TMED_B26")) c->d_b26 = bshare_acquire(0, device, c->d_bcomb16, c->stream);
   c->b24_on = !env_off("TMED_B24");
   c->acomb_on = !env_off("TMED_KS_ACOMB");
+  if (const char *v = getenv("TMED_TEST_FAIL_KS_ALLOC")) c->test_fail_ks_alloc = atoi(v);
   c->kc_on = !env_off("TMED_KEYCACHE");
   if (const char *v = getenv("TMED_KEYCACHE_GB")) c->kc_budget = (size_t)strtoull(v, nullptr, 10) << 30;
   if (e == hipSuccess) e = hipMalloc((void **)&c->d_bcomb, kCombBytesPerKey);

@@ -94,6 +94,7 @@ def test_concurrent_callers_share_one_context(engine):
     def device_stream():
         st = torch.cuda.Stream(dev)
         d_out = torch.zeros(pubs.shape[0], dtype=torch.uint8, device=dev)
+        st.wait_stream(torch.cuda.current_stream(dev))  # the zero fill (torch's stream) before the engine's work on st
         engine.verify_device(d_pub, d_sig, d_msg, d_off, d_out, pubs.shape[0], st.cuda_stream)
         st.synchronize()
         assert (d_out.cpu().numpy() == exp_generic).all()

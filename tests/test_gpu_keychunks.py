@@ -89,6 +89,7 @@ def test_full_size_keyed_property(engine):
     d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
     d_pub = torch.empty((n, 32), dtype=torch.uint8, device=dev)
     d_out = torch.zeros(n, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()  # torch's fills before the engine's own stream (NULL = the context stream)
     engine.sign_device(d_seed, d_msg, d_off, d_sig, d_pub, n)
     torch.cuda.synchronize()
     pubs = np.zeros((nk, 32), np.uint8)
@@ -102,11 +103,13 @@ def test_full_size_keyed_property(engine):
         assert engine.keyset_a_window_bits(h) == 12
         assert int(d_out.sum().item()) == n
         d_sig[:, 40] ^= 1
+        torch.cuda.synchronize()  # torch's flip before the engine's own (NULL = context) stream reads it
         engine.verify_keyset_device(h, d_vi, d_sig, d_msg, d_off, d_out, n)
         torch.cuda.synchronize()
         assert int(d_out.sum().item()) == 0
         d_sig[:, 40] ^= 1
         d_vi[12345] = nk  # past the set: rejected, the rest unchanged
+        torch.cuda.synchronize()
         engine.verify_keyset_device(h, d_vi, d_sig, d_msg, d_off, d_out, n)
         torch.cuda.synchronize()
         out = d_out.cpu().numpy()
@@ -117,3 +120,57 @@ def test_full_size_keyed_property(engine):
         assert exp.all() and out[sl].all()
     finally:
         engine.keyset_free(h)
+
+
+@pytest.mark.parametrize("fail_at,what", [(5, "load"), (7, "comba chunk"), (8, "comba scratch")])
+def test_key_set_allocation_failures(fail_at, what, engine):
+    """Out of memory at each step of a key set's life (TMED_TEST_FAIL_KS_ALLOC=n: the context's n-th
+    key-set allocation fails; a 700-key set allocates its table, encodings, flags and comb chunks
+    1-5 at load, then the radix-2^12 comb's chunks 6-7 and build scratch 8 at its first throughput
+    batch).  A failed load reports ENOMEM and leaves nothing behind (the next load works); a failed
+    radix-2^12 comb leaves the set on its radix-256 comb.  Decisions equal the port either way."""
+    from conftest import engine_with_env
+    from tmed._native import TmedError
+    eng = engine_with_env(TMED_TEST_FAIL_KS_ALLOC=fail_at)
+    try:
+        seeds, pubs = _keys(700, 31)
+        if what == "load":
+            with pytest.raises(TmedError):
+                eng.keyset_load(pubs)
+        h = eng.keyset_load(pubs)
+        try:
+            big = _batch(seeds, pubs, 700, 30000, 5)
+            assert (eng.verify_keyset_arrays(h, *big[:4]) == big[4]).all()
+            assert eng.keyset_a_window_bits(h) == (12 if what == "load" else 8)
+            small = _batch(seeds, pubs, 700, 500, 6)
+            assert (eng.verify_keyset_arrays(h, *small[:4]) == small[4]).all()
+            assert (eng.verify_keyset_arrays(h, *big[:4]) == big[4]).all()
+        finally:
+            eng.keyset_free(h)
+    finally:
+        eng.close()
+
+
+def test_pool_append_failure_stays_generic(engine):
+    """The key-set cache's pool runs out of memory at its first append (TMED_TEST_FAIL_KS_ALLOC=4:
+    its first comb chunk): that window runs on the generic kernels with the same outcomes, nothing
+    is pooled, and the next window of the set builds its keys and is keyed."""
+    from conftest import engine_with_env
+    from test_gpu_keycache import _bs_window, _delta
+    import tmed.types as T
+    eng = engine_with_env(TMED_KEYCACHE=1, TMED_TEST_FAIL_KS_ALLOC=4)
+    try:
+        eng.keycache_config(True, 8 << 30)
+        w = _bs_window(eng, b"kc-oom", nv=64, nb=4096)
+        ref = T.BlocksyncWindow(*w)
+        ref.run(engine, 128)
+        for keyed in (0, 1):
+            s0 = eng.keycache_stats()
+            got = T.BlocksyncWindow(*w)
+            got.run(eng, 128)
+            d = _delta(s0, eng.keycache_stats())
+            assert (got.codes() == ref.codes()).all() and (got.verified() == ref.verified()).all()
+            assert d["keyed_sets"] == keyed and d["keys_appended"] == 64 * keyed, d
+        assert eng.keycache_stats()["pool_keys"] == 64
+    finally:
+        eng.close()

@@ -117,6 +117,7 @@ def test_full_size_property(engine):
     d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
     d_pub = torch.empty((n, 32), dtype=torch.uint8, device=dev)
     d_out = torch.zeros(n, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()  # torch's fills before the engine's own stream (NULL = the context stream)
     engine.sign_device(d_seed, d_msg, d_off, d_sig, d_pub, n)
     engine.verify_device(d_pub, d_sig, d_msg, d_off, d_out, n)
     torch.cuda.synchronize()
@@ -130,10 +131,14 @@ def test_full_size_property(engine):
     assert 32.0 < lane_mean < 33.0 and wave_mean - lane_mean < 0.3, (lane_mean, wave_mean)
     assert int(wh[32]) > n // 64 // 4
     d_sig[:, 40] ^= 1
+    # (torch's flip runs on torch's stream; the engine's NULL stream is the context's own stream,
+    # which is not ordered after it: the flip must be complete before the call)
+    torch.cuda.synchronize()
     engine.verify_device(d_pub, d_sig, d_msg, d_off, d_out, n)
     torch.cuda.synchronize()
     assert int(d_out.sum().item()) == 0
     d_sig[:, 40] ^= 1
+    torch.cuda.synchronize()
     m = 4096
     sl = slice(n - m, n)
     exp = port.verify_batch(d_pub[sl].cpu().numpy(), d_sig[sl].cpu().numpy(), msgs,
