@@ -175,9 +175,12 @@ struct Group {
     ub.clear();
     pos.assign(1, 0);
   }
-  // run r without its aliased candidates (al[ap..] ascending; ap advances past run r's)
+  // run r without its aliased candidates (al[ap..] ascending; ap advances past run r's).  The end
+  // is off[r] + len, not off[r + 1]: seam_plan's merge calls this for a part's runs while the next
+  // part's worker is still writing its offsets, and off[r + 1] of a part's last run is the next
+  // part's first (read before it was written, it held the slot's previous batch's offset).
   void add_run(const Cands &c, uint32_t r, const std::vector<std::pair<uint32_t, uint32_t>> &al, size_t &ap) {
-    const size_t c0 = c.off[r], c1 = c.off[r + 1];
+    const size_t c0 = c.off[r], c1 = c0 + c.runs[r].len;
     size_t k = c0;
     auto seg = [&](size_t a, size_t b) {
       if (a >= b) return;
@@ -615,7 +618,12 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
     tp->row_of.resize(n);
     if (ps.trows.size() < np) ps.trows.resize(np);
   }
+  // TMED_TEST_MERGE_SKEW=1 (tests): odd parts start their merge 2 ms late, so a part that read what
+  // the next part's worker writes (add_run's end of a part's last run, before the fix) reads it
+  // unwritten every time instead of rarely
+  const bool skew = nt > 1 && getenv("TMED_TEST_MERGE_SKEW") != nullptr;
   auto merge_part = [&](size_t t) {
+    if (skew && (t & 1)) std::this_thread::sleep_for(std::chrono::milliseconds(2));
     size_t c = cbase[t];
     Run *dst = cands.runs.data() + rbase[t];
     size_t *off = cands.off.data() + rbase[t];
@@ -1653,6 +1661,66 @@ static double bs_us(BsClock::time_point a, BsClock::time_point b) {
   return std::chrono::duration<double, std::micro>(b - a).count();
 }
 
+// TMED_DEBUG_ZERO=1 (diagnostics only): every staged candidate of a pipelined generic batch whose
+// device bit is 0 is recorded with what the host staged (key, signature), what the device held
+// (its copy of both, the assembled sign-bytes) and which request / signature it was, for
+// tmed_debug_zero_bits.  It tells a false reject from the verification kernels apart from one
+// in the staging, the copy or the assembly.
+namespace {
+struct ZeroRec {
+  uint64_t req;  // request index in the call's window
+  int32_t sig;   // signature index in its commit
+  uint32_t pos, msg_len, batch_m;
+  uint8_t key_host[32], sig_host[64], key_dev[32], sig_dev[64], msg[256];
+};
+std::mutex g_zero_mu;
+std::vector<ZeroRec> g_zero;
+bool debug_zero_on() {
+  static const bool on = getenv("TMED_DEBUG_ZERO") != nullptr;
+  return on;
+}
+}  // namespace
+
+static void debug_record_zeros(tmed_ctx *ctx, const BsBatch &b) {
+  if (b.st.ks || b.st.zc || b.st.sig_direct) return;  // generic staged batches only
+  const tmed::VoteSlot &vs = ctx->vslot[b.st.slot];
+  const size_t m = b.bits.size();
+  std::vector<ZeroRec> recs;
+  for_segments(b.cands, b.grp, 0, m, [&](size_t j, uint32_t u0, uint32_t u1, size_t p0) {
+    const Run &run = b.cands.runs[b.grp.run(b.cands, j)];
+    for (uint32_t u = u0; u < u1; u++) {
+      const size_t p = p0 + (u - u0);
+      if (b.bits[p]) continue;
+      ZeroRec z{};
+      z.req = b.lo + run.req;
+      z.sig = run.sig + (int32_t)u;
+      z.pos = (uint32_t)p;
+      z.batch_m = (uint32_t)m;
+      memcpy(z.key_host, b.st.key + 32 * p, 32);
+      memcpy(z.sig_host, b.st.sig + 64 * p, 64);
+      const uint8_t *d = (const uint8_t *)vs.d_votes.p;
+      (void)hipMemcpy(z.key_dev, d + b.st.o_key + 32 * p, 32, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(z.sig_dev, d + b.st.o_sig + 64 * p, 64, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(z.msg, (const uint8_t *)vs.d_vmsg.p + (size_t)tmed::kVoteSlot * p, 256, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(&z.msg_len, (const uint32_t *)vs.d_off.p + p, 4, hipMemcpyDeviceToHost);
+      recs.push_back(z);
+    }
+  });
+  std::lock_guard<std::mutex> g(g_zero_mu);
+  g_zero.insert(g_zero.end(), recs.begin(), recs.end());
+}
+
+// The recorded zero bits (TMED_DEBUG_ZERO), oldest first: copies up to cap records of
+// sizeof(ZeroRec) bytes into out and removes them; *n = records copied.
+extern "C" int tmed_debug_zero_bits(void *out, size_t cap, size_t *n) {
+  std::lock_guard<std::mutex> g(g_zero_mu);
+  const size_t k = std::min(cap, g_zero.size());
+  if (k && out) memcpy(out, g_zero.data(), k * sizeof(ZeroRec));
+  g_zero.erase(g_zero.begin(), g_zero.begin() + (ptrdiff_t)k);
+  if (n) *n = k;
+  return (int)sizeof(ZeroRec);
+}
+
 // Collect batch b (ctx->mu held): its bits, the alias copies, the replay into its window's results.
 // ph: tmed_seam_phase_us — host plan + templates + staging, host time blocked on the device
 // (enqueueing the copies and kernels, votes_collect), host replay.
@@ -1667,6 +1735,7 @@ static int bs_finish(tmed_ctx *ctx, BsBatch &b, double ph[3]) {
     const auto t0 = BsClock::now();
     r = tmed::votes_collect(ctx, b.st, b.bits.data());
     ph[1] += bs_us(t0, BsClock::now());
+    if (r == TMED_OK && debug_zero_on()) debug_record_zeros(ctx, b);
   }
   const auto t1 = BsClock::now();
   PhaseClock clk;
