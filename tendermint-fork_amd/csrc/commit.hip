@@ -1721,6 +1721,9 @@ extern "C" int tmed_debug_zero_bits(void *out, size_t cap, size_t *n) {
   return (int)sizeof(ZeroRec);
 }
 
+// Tests: every host-pool part starts up to max_us microseconds late (0: off), see host_pool.h.
+extern "C" void tmed_test_pool_jitter(int max_us) { g_pool_jitter_us.store(max_us < 0 ? 0 : max_us); }
+
 // Collect batch b (ctx->mu held): its bits, the alias copies, the replay into its window's results.
 // ph: tmed_seam_phase_us — host plan + templates + staging, host time blocked on the device
 // (enqueueing the copies and kernels, votes_collect), host replay.

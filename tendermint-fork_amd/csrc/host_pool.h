@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <exception>
 #include <functional>
@@ -126,6 +127,21 @@ thread_local bool HostPool::in_worker = false;
 thread_local bool HostPool::in_region = false;
 }  // namespace
 
+// Tests (tmed_test_pool_jitter): each part of a region starts after a pseudo-random delay of up to
+// this many microseconds, so a part that reads what another part of the same region writes sees
+// it unwritten in some runs instead of almost never (0: off, the product default).
+inline std::atomic<int> g_pool_jitter_us{0};
+inline void pool_jitter(unsigned t) {
+  const int us = g_pool_jitter_us.load(std::memory_order_relaxed);
+  if (us <= 0) return;
+  static std::atomic<uint64_t> ctr{0};
+  uint64_t x = (ctr.fetch_add(1, std::memory_order_relaxed) + 1) * 0x9e3779b97f4a7c15ull ^ ((uint64_t)t << 32);
+  x ^= x >> 31;
+  x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 29;
+  std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(x % (uint64_t)us)));
+}
+
 // f(lo, hi, t) over nt contiguous parts of [0, n) (part t; each part runs exactly once, on some
 // thread: per-part buffers are indexed by t).
 template <class F>
@@ -133,6 +149,9 @@ static void parallel_ranges(size_t n, unsigned nt, F &&f) {
   if (nt <= 1 || n < 2 || HostPool::in_worker || HostPool::in_region) { f(0, n, 0u); return; }
   if (nt > n) nt = (unsigned)n;
   if (nt > 0xffffu) nt = 0xffffu;
-  const HostPool::Job job = [&](unsigned t) { f(n * t / nt, n * (t + 1) / nt, t); };
+  const HostPool::Job job = [&](unsigned t) {
+    pool_jitter(t);
+    f(n * t / nt, n * (t + 1) / nt, t);
+  };
   HostPool::get().run(nt, job);
 }
