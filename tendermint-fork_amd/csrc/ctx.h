@@ -191,6 +191,8 @@ constexpr size_t kLatencyUntimedMax = 1024;
 int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st, int slot = 0);
 // The shared radix-2^24 B comb (tmed_capi.hip), acquired on the first call; null: radix 2^16.
 const int4 *ctx_bcomb24(tmed_ctx *c);
+// Tests: microseconds of delay queued in front of the seam's producer-side copies (tmed_test_stream_delay).
+uint32_t test_stream_delay_us();
 int votes_enqueue(tmed_ctx *c, VoteStage &st);
 int votes_collect(tmed_ctx *c, const VoteStage &st, uint8_t *out);
 int votes_launch(tmed_ctx *c, VoteStage &st, uint8_t *out);

@@ -163,6 +163,10 @@ hipError_t launch_key_order(const uint32_t *val_idx, uint32_t n, uint32_t nkeys,
 
 // Window-count statistics of the last half-size chunk in the prep hand-off (count lanes):
 // d_hist[0..64] per-lane W, d_hist[65..129] per-wave maximum W.
+// Tests (tmed_test_stream_delay): one wave that sleeps about `us` microseconds on `stream` before
+// the work queued after it, so a consumer on another stream that does not wait for that work
+// reads it unfinished.  us = 0: nothing is launched.
+hipError_t launch_test_delay(hipStream_t stream, uint32_t us);
 hipError_t launch_window_stats(const int4 *prep, uint32_t stride, uint32_t count, uint32_t *d_hist,
                                hipStream_t stream);
 

@@ -518,6 +518,17 @@ __global__ __launch_bounds__(kThreadsPerBlock) void window_stats_kernel(const in
   }
 }
 
+// (s_sleep 127 is ~8k clocks, ~3.4 us at 2.4 GHz; a bounded loop, no memory access)
+__global__ __launch_bounds__(64) void test_delay_kernel(uint32_t iters) {
+  for (uint32_t i = 0; i < iters; i++) __builtin_amdgcn_s_sleep(127);
+}
+
+hipError_t launch_test_delay(hipStream_t stream, uint32_t us) {
+  if (us == 0) return hipSuccess;
+  hipLaunchKernelGGL(test_delay_kernel, dim3(1), dim3(64), 0, stream, (us < 100000u ? us : 100000u) / 3u + 1u);
+  return hipGetLastError();
+}
+
 hipError_t launch_window_stats(const int4 *prep, uint32_t stride, uint32_t count, uint32_t *d_hist,
                                hipStream_t stream) {
   if (count == 0) return hipSuccess;

@@ -229,7 +229,8 @@ int keyset_append(tmed_ctx *c, Keyset &k, const uint8_t *pubkeys, size_t m, hipS
   if (e == hipSuccess) e = c->h_kup.ensure(m * 32);
   if (e != hipSuccess) return map_err(e);
   memcpy(c->h_kup.p, pubkeys, m * 32);
-  e = hipMemcpyAsync(k.d_pub + 32 * k.n, c->h_kup.p, m * 32, hipMemcpyHostToDevice, s);
+  e = launch_test_delay(s, test_stream_delay_us());  // tests only (0): the appended keys land late
+  if (e == hipSuccess) e = hipMemcpyAsync(k.d_pub + 32 * k.n, c->h_kup.p, m * 32, hipMemcpyHostToDevice, s);
   int32_t *bases = (int32_t *)c->d_kbases.p;
   if (e == hipSuccess) e = launch_comb_bases(k.d_pub + 32 * k.n, (uint32_t)m, /*negate=*/1, k.d_ok + k.n, bases, s);
   for (size_t a = k.n; e == hipSuccess && a < k.n + m;) {  // one fill launch per chunk the keys fall in
@@ -271,6 +272,9 @@ static hipError_t keyset_verify(tmed_ctx *c, Keyset &k, const uint32_t *d_idx, c
                               lane ? lane->d_fin_pre : c->d_fin_pre, s, msg_slots, timer, perm, scratch, c->d_b24,
                               comba);
 }
+
+static std::atomic<uint32_t> g_test_stream_delay{0};
+uint32_t test_stream_delay_us() { return g_test_stream_delay.load(std::memory_order_relaxed); }
 
 int votes_stage(tmed_ctx *c, uint64_t keyset, uint32_t m, size_t n_tmpl, VoteStage &st, int slot) {
   st.slot = slot;
@@ -414,6 +418,7 @@ int votes_enqueue(tmed_ctx *c, VoteStage &st) {
     if (trace && !vs.cp0 && e == hipSuccess) e = hipEventCreate(&vs.cp0);
     if (trace && !vs.cp1 && e == hipSuccess) e = hipEventCreate(&vs.cp1);
     if (trace && e == hipSuccess) e = hipEventRecord(vs.cp0, c->copy_stream);
+    if (e == hipSuccess) e = launch_test_delay(c->copy_stream, test_stream_delay_us());  // tests only (0)
     const uint8_t *h = (const uint8_t *)vs.h_votes.p;
     if (st.sig_direct) {  // the staged area without its (unused) signature region
       if (e == hipSuccess) e = hipMemcpyAsync(d, h, st.o_sig, hipMemcpyHostToDevice, c->copy_stream);
@@ -663,3 +668,5 @@ int tmed_verify_batch_keyset(tmed_ctx *c, uint64_t handle, const uint32_t *val_i
 }
 
 }  // extern "C"
+
+extern "C" void tmed_test_stream_delay(int us) { tmed::g_test_stream_delay.store(us < 0 ? 0u : (uint32_t)us); }
