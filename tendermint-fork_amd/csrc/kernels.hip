@@ -193,10 +193,19 @@ __device__ __forceinline__ bool prep_load(const int4 *prep, uint32_t stride, uin
 
 // Phase 1: SHA-512(R||A||M) mod L, S < L, A = Point.SetBytes(pub)  (one lane per signature
 // of the chunk [base, base + count)).
+// Threads per block of the generic throughput kernels (prep, prep_r, the half-size main).  A block's
+// wave slots (and the main kernel's LDS) are handed back only when its LAST wave ends, so a 4-wave
+// block holds up to three idle slots behind its slowest wave, and at the end of a launch.
+#ifndef TMED_HS_BLOCK
+#define TMED_HS_BLOCK 256
+#endif
+constexpr uint32_t kHsBlock = TMED_HS_BLOCK;
+static_assert(kHsBlock % 64 == 0 && kThreadsPerBlock % kHsBlock == 0, "whole waves, dividing the chunk granule");
+
 #ifndef TMED_PREP_WAVES
 #define TMED_PREP_WAVES 3  // 152 VGPRs, no spills (4 waves with a leaner decode: no faster, profiles/r03/prep_joint)
 #endif
-__global__ __launch_bounds__(kThreadsPerBlock, TMED_PREP_WAVES) void verify_prep_kernel(
+__global__ __launch_bounds__(kHsBlock, TMED_PREP_WAVES) void verify_prep_kernel(
     const uint8_t *__restrict__ pub, const uint8_t *__restrict__ sig, MsgSrc ms, uint32_t base, uint32_t count,
     int4 *__restrict__ prep, uint32_t stride, uint32_t *__restrict__ place) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
@@ -337,7 +346,7 @@ static_assert((kPrepInt4 + kPrepHsInt4) * 16 <= kPrepSlotBytes, "prep slot too s
 #ifndef TMED_PREP_R_WAVES
 #define TMED_PREP_R_WAVES 3  // 168 VGPRs, 6 spilled: -0.06 ms per 2^20 against 2 waves (the Euclid loop hides its memory waits)
 #endif
-__global__ __launch_bounds__(kThreadsPerBlock, TMED_PREP_R_WAVES) void verify_prep_r_kernel(
+__global__ __launch_bounds__(kHsBlock, TMED_PREP_R_WAVES) void verify_prep_r_kernel(
     const uint8_t *__restrict__ sig, uint32_t base, uint32_t count, const int4 *__restrict__ prep,
     int4 *__restrict__ prep2, uint32_t stride, uint32_t *__restrict__ place, int zip215) {
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
@@ -432,14 +441,14 @@ struct HsDigitsDev {
 // 16 (windows 0 and 8 of the 2^16 comb, sixteen; when the 8.6-GB tables are unavailable).  The
 // hand-off carries e unrecoded (hs_prep_r raw_e); radix 16 recodes it here.
 template <int BB>
-__global__ __launch_bounds__(kThreadsPerBlock, TMED_HS_WAVES) void verify_main_hs_kernel(
+__global__ __launch_bounds__(kHsBlock, TMED_HS_WAVES) void verify_main_hs_kernel(
     uint32_t base, uint32_t count, const int4 *__restrict__ prep, const int4 *__restrict__ prep2, uint32_t stride,
     int4 *__restrict__ slab, const int4 *__restrict__ btab, uint8_t *__restrict__ out, int zip215) {
-  __shared__ int4 sbl[kThreadsPerBlock / 64][8 * 64];
+  __shared__ int4 sbl[kHsBlock / 64][8 * 64];
 #if TMED_B16_ONEBUF
   auto &sbh = sbl;
 #else
-  __shared__ int4 sbh[kThreadsPerBlock / 64][8 * 64];
+  __shared__ int4 sbh[kHsBlock / 64][8 * 64];
 #endif
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // position in the placed hand-off
   const bool active = slot < count;
@@ -674,20 +683,21 @@ hipError_t launch_verify(const uint8_t *pub, const uint8_t *sig, const uint8_t *
     for (uint32_t base = fbase; base < fbase + m; base += chunk) {
       const uint32_t count = (fbase + m - base) < chunk ? (fbase + m - base) : chunk;
       const uint32_t blocks = (count + kThreadsPerBlock - 1) / kThreadsPerBlock;
+      const uint32_t hblocks = (count + kHsBlock - 1) / kHsBlock;
 
-      hipLaunchKernelGGL(verify_prep_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, pub, sig, ms, base,
+      hipLaunchKernelGGL(verify_prep_kernel, dim3(hblocks), dim3(kHsBlock), 0, stream, pub, sig, ms, base,
                          count, prep, slab_stride, hs ? place : nullptr);
       if (timer) timer->mark(stream, 0);
       if (hs) {  // default: half-size scalars (verify_hs.h): R decode + lattice, main; no finish
         int4 *prep2 = prep + (size_t)kPrepInt4 * slab_stride;
-        hipLaunchKernelGGL(verify_prep_r_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, sig, base, count,
+        hipLaunchKernelGGL(verify_prep_r_kernel, dim3(hblocks), dim3(kHsBlock), 0, stream, sig, base, count,
                            prep, prep2, slab_stride, place, zip215 ? 1 : 0);
         if (timer) timer->mark(stream, 0);
         if (btab.b26)
-          hipLaunchKernelGGL(verify_main_hs_kernel<26>, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base, count,
+          hipLaunchKernelGGL(verify_main_hs_kernel<26>, dim3(hblocks), dim3(kHsBlock), 0, stream, base, count,
                              prep, prep2, slab_stride, slab, btab.b26, out, zip215 ? 1 : 0);
         else
-          hipLaunchKernelGGL(verify_main_hs_kernel<16>, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base, count,
+          hipLaunchKernelGGL(verify_main_hs_kernel<16>, dim3(hblocks), dim3(kHsBlock), 0, stream, base, count,
                              prep, prep2, slab_stride, slab, btab.comb16, out, zip215 ? 1 : 0);
       } else {  // fallback 5: full-length Straus + batched finish
         hipLaunchKernelGGL(verify_main_kernel, dim3(blocks), dim3(kThreadsPerBlock), 0, stream, base, count, prep,
@@ -710,8 +720,8 @@ hipError_t launch_verify_prep(const uint8_t *pub, const uint8_t *sig, const uint
   if (count == 0) return hipSuccess;
   if (count > stride) return hipErrorInvalidValue;
   const MsgSrc ms{msgs, off, msg_slots};
-  hipLaunchKernelGGL(verify_prep_kernel, dim3((count + kThreadsPerBlock - 1) / kThreadsPerBlock),
-                     dim3(kThreadsPerBlock), 0, stream, pub, sig, ms, base, count, prep, stride, nullptr);
+  hipLaunchKernelGGL(verify_prep_kernel, dim3((count + kHsBlock - 1) / kHsBlock),
+                     dim3(kHsBlock), 0, stream, pub, sig, ms, base, count, prep, stride, nullptr);
   return hipGetLastError();
 }
 
