@@ -335,10 +335,12 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_kernel(
 //
 // Placement by window count: the main kernel runs every lane of a wave over the wave's largest
 // W, and W is 32 or 33 for almost every signature (a few lanes 34+).  The R kernel therefore
-// writes signatures with W <= 32 from the front of the region and the others from the back (one
-// atomic per wave and group on place[0] / place[1], the lanes of a group at consecutive
-// positions, so the stores stay coalesced): the waves of the front part run 32 windows instead
+// writes signatures with W > 32 from the front of the region and the others (W <= 32) from the back
+// (one atomic per wave and group on place[0] / place[1], the lanes of a group at consecutive
+// positions, so the stores stay coalesced): the waves of the W <= 32 part run 32 windows instead
 // of the unsorted wave maximum (~33.3 on average, tmed_window_stats), ~2 % of the main kernel.
+// The longer waves go first, so the launch's last round holds short ones (-0.3 % per C2 step, 9
+// of 11 alternating rounds, profiles/r05/s33/).
 constexpr int kPrepHsInt4 = 16;
 constexpr int kHsWSmall = 32;
 static_assert((kPrepInt4 + kPrepHsInt4) * 16 <= kPrepSlotBytes, "prep slot too small for the half-size hand-off");
@@ -393,9 +395,13 @@ __global__ __launch_bounds__(kHsBlock, TMED_PREP_R_WAVES) void verify_prep_r_ker
     const int4 v = prep[(size_t)q * stride + slot];
     w[28 + 4 * q] = v.x; w[29 + 4 * q] = v.y; w[30 + 4 * q] = v.z; w[31 + 4 * q] = v.w;
   }
-  // position: W <= kHsWSmall from the front, the rest from the back (count - 1 downwards)
-  const bool small = W <= kHsWSmall;
-  const uint64_t act = __ballot(1), sm = __ballot(small);
+  // position: W > kHsWSmall from the front, the rest from the back (count - 1 downwards), so the
+  // main kernel's longest waves are dispatched first (TMED_HS_LONG_FIRST=0: the other way round)
+#ifndef TMED_HS_LONG_FIRST
+#define TMED_HS_LONG_FIRST 1
+#endif
+  const bool front = TMED_HS_LONG_FIRST ? W > kHsWSmall : W <= kHsWSmall;
+  const uint64_t act = __ballot(1), sm = __ballot(front);
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
   uint32_t fs = 0, fl = 0;
@@ -407,7 +413,7 @@ __global__ __launch_bounds__(kHsBlock, TMED_PREP_R_WAVES) void verify_prep_r_ker
   const int leader = __builtin_ctzll(act);
   fs = (uint32_t)__shfl((int)fs, leader);
   fl = (uint32_t)__shfl((int)fl, leader);
-  const uint32_t pos = small ? fs + (uint32_t)__builtin_popcountll(sm & below)
+  const uint32_t pos = front ? fs + (uint32_t)__builtin_popcountll(sm & below)
                              : count - 1u - (fl + (uint32_t)__builtin_popcountll(act & ~sm & below));
 #pragma unroll
   for (int q = 0; q < kPrepHsInt4; q++)
