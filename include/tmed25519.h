@@ -244,6 +244,26 @@ int tmed_vote_sign_bytes(const tmed_vote_template *t, size_t n, const uint8_t *f
  */
 int tmed_valu_peak(tmed_ctx *ctx, int kind, double *giga_ops_per_s);
 
+/*
+ * Test hooks of the commit seam (process-wide, 0 = off, the product default; tests only):
+ * tmed_test_pool_jitter — every part of the seam's host-parallel regions starts up to max_us
+ * microseconds late (a part reading what another part of the same region writes then sees it
+ * unwritten); tmed_test_stream_delay — a wave sleeping ~us microseconds is queued in front of every
+ * batch copy on the copy stream and every key append on the context stream (a kernel lane that does
+ * not wait for its producer then reads unfinished data).  tests/test_gpu_jitter.py,
+ * tests/test_gpu_stream_delay.py.
+ */
+void tmed_test_pool_jitter(int max_us);
+void tmed_test_stream_delay(int us);
+
+/*
+ * With TMED_DEBUG_ZERO set at the first pipelined generic batch: every staged candidate whose
+ * device bit is 0 is recorded (request, signature, staging position, the staged and the device
+ * copies of its key and signature, the assembled sign-bytes).  Copies up to cap records into out
+ * and removes them; *n = records copied; returns the record size in bytes (tools/r05/c3_stress.py).
+ */
+int tmed_debug_zero_bits(void *out, size_t cap, size_t *n);
+
 /* ------------------------------------------------------- commit seam (C++) */
 
 /* BlockID as compared by BlockID.Equals (types/block.go:1170-1173). */

@@ -111,6 +111,12 @@ def lib() -> ctypes.CDLL:
     l.tmed_verify_batch_zip215_device.argtypes = [P, P, P, P, P, SZ, P, P]
     l.tmed_zip215_set_seed.argtypes = [P]
     l.tmed_zip215_stats.argtypes = [P]
+    l.tmed_test_pool_jitter.restype = None
+    l.tmed_test_pool_jitter.argtypes = [I]
+    l.tmed_test_stream_delay.restype = None
+    l.tmed_test_stream_delay.argtypes = [I]
+    l.tmed_debug_zero_bits.restype = I
+    l.tmed_debug_zero_bits.argtypes = [P, SZ, ctypes.POINTER(SZ)]
     _lib = l
     return l
 
@@ -121,6 +127,7 @@ EXPORTED_SYMBOLS = [
     "tmed_verify_batch", "tmed_verify_batch_device",
     "tmed_sign_batch", "tmed_sign_batch_device", "tmed_last_kernel_ms",
     "tmed_vote_sign_bytes", "tmed_valu_peak", "tmed_verify_commits", "tmed_verify_commits_with",
+    "tmed_test_pool_jitter", "tmed_test_stream_delay", "tmed_debug_zero_bits",
     "tmed_keyset_load", "tmed_keyset_free", "tmed_keyset_extend", "tmed_verify_batch_keyset",
     "tmed_keycache_config", "tmed_keycache_stats", "tmed_keycache_flush", "tmed_keycache_warm", "tmed_keycache_wait", "tmed_verify_batch_keyset_device",
     "tmed_set_kernel_timing", "tmed_kernel_times", "tmed_blocksync_verify", "tmed_blocksync_submit", "tmed_blocksync_wait",
