@@ -3,7 +3,7 @@ test_c3_many_sets_through_the_cache[40-2050-70000]) through the GENERIC pipeline
 one cache-off context, for each batch size in TMED_PIPE_SIGS-like steps, counting outcome
 mismatches against the oracle loops.  For every mismatch it prints the request, whether its
 Trusting/Light pair was split across two planning parts (16 parts per batch) and what a repeat of
-that request alone returns.  Usage: python tools/r05/c3_stress.py [calls_per_size] [sizes...]"""
+that request alone returns.  Usage: python tools/r05/c3_stress.py [calls_per_size] [sizes...] [cache]"""
 import ctypes
 import os
 import sys
@@ -78,7 +78,8 @@ def split_points(n, bsz, parts=16):
 
 def main():
     calls = int(sys.argv[1]) if len(sys.argv) > 1 else 200
-    sizes = [int(x) for x in sys.argv[2:]] or [70000, 40000]
+    cache = "cache" in sys.argv[2:]  # the key-set cache on: the first call generic, then keyed (lane 0 / 1)
+    sizes = [int(x) for x in sys.argv[2:] if x != "cache"] or [70000, 40000]
     base = engine_with_env()
     reqs, exp = workload(base)
     base.close()
@@ -91,11 +92,15 @@ def main():
         os.environ["TMED_PIPE_SIGS"] = str(size)
         bsz = max(16, size // max(1, sigs // n))
         pts = split_points(n, bsz)
-        e = engine_with_env(TMED_KEYCACHE=0)
+        e = engine_with_env(TMED_KEYCACHE=1 if cache else 0)
+        if cache:
+            e.keycache_config(True, 16 << 30)
         t0 = time.perf_counter()
         bad_calls = 0
         for call in range(calls):
             got = T.verify_commits(e, reqs)
+            if cache:
+                e.keycache_wait()
             bad = [q for q in range(n) if not _same(got[q], exp[q])]
             zs = check_zeros(reqs, zero_records(), ocache)
             if zs:
