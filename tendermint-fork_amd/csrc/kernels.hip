@@ -193,14 +193,10 @@ __device__ __forceinline__ bool prep_load(const int4 *prep, uint32_t stride, uin
 
 // Phase 1: SHA-512(R||A||M) mod L, S < L, A = Point.SetBytes(pub)  (one lane per signature
 // of the chunk [base, base + count)).
-// Threads per block of the generic throughput kernels (prep, prep_r, the half-size main).  A block's
-// wave slots (and the main kernel's LDS) are handed back only when its LAST wave ends, so a 4-wave
-// block holds up to three idle slots behind its slowest wave, and at the end of a launch.
-#ifndef TMED_HS_BLOCK
-#define TMED_HS_BLOCK 256
-#endif
-constexpr uint32_t kHsBlock = TMED_HS_BLOCK;
-static_assert(kHsBlock % 64 == 0 && kThreadsPerBlock % kHsBlock == 0, "whole waves, dividing the chunk granule");
+// Threads per block of the generic throughput kernels (prep, prep_r, the half-size main): 256.
+// (Blocks of 64 / 128 threads, whose wave slots come back sooner at a launch's end, were level /
+// 4 % slower per C2 step: profiles/r05/s32/.)
+constexpr uint32_t kHsBlock = kThreadsPerBlock;
 
 #ifndef TMED_PREP_WAVES
 #define TMED_PREP_WAVES 3  // 152 VGPRs, no spills (4 waves with a leaner decode: no faster, profiles/r03/prep_joint)
@@ -339,8 +335,8 @@ __global__ __launch_bounds__(kThreadsPerBlock, 2) void verify_main_kernel(
 // (one atomic per wave and group on place[0] / place[1], the lanes of a group at consecutive
 // positions, so the stores stay coalesced): the waves of the W <= 32 part run 32 windows instead
 // of the unsorted wave maximum (~33.3 on average, tmed_window_stats), ~2 % of the main kernel.
-// The longer waves go first, so the launch's last round holds short ones (-0.3 % per C2 step, 9
-// of 11 alternating rounds, profiles/r05/s33/).
+// The longer waves go first, so the launch's last round holds short ones (-0.3 % per C2 step
+// against short first, 9 of 11 alternating rounds, profiles/r05/s33/).
 constexpr int kPrepHsInt4 = 16;
 constexpr int kHsWSmall = 32;
 static_assert((kPrepInt4 + kPrepHsInt4) * 16 <= kPrepSlotBytes, "prep slot too small for the half-size hand-off");
@@ -396,11 +392,8 @@ __global__ __launch_bounds__(kHsBlock, TMED_PREP_R_WAVES) void verify_prep_r_ker
     w[28 + 4 * q] = v.x; w[29 + 4 * q] = v.y; w[30 + 4 * q] = v.z; w[31 + 4 * q] = v.w;
   }
   // position: W > kHsWSmall from the front, the rest from the back (count - 1 downwards), so the
-  // main kernel's longest waves are dispatched first (TMED_HS_LONG_FIRST=0: the other way round)
-#ifndef TMED_HS_LONG_FIRST
-#define TMED_HS_LONG_FIRST 1
-#endif
-  const bool front = TMED_HS_LONG_FIRST ? W > kHsWSmall : W <= kHsWSmall;
+  // main kernel's longest waves are dispatched first
+  const bool front = W > kHsWSmall;
   const uint64_t act = __ballot(1), sm = __ballot(front);
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
