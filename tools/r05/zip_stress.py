@@ -1,0 +1,57 @@
+"""Diagnostic (round 5): the opt-in ZIP-215 batch mode (randomized batch equations with a fresh
+CSPRNG draw per call, bisection, single checks) on a 200k-signature batch with 0-6 fresh bit flips
+per call, repeated, every decision compared with the C port's ZIP-215 rule (the base batch checked
+once in full, the flipped signatures each call).  Usage: python tools/r05/zip_stress.py [calls]"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "tendermint-fork_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+from conftest import engine_with_env  # noqa: E402
+from oracle import port  # noqa: E402
+
+
+def main():
+    calls = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+    e = engine_with_env()
+    n = 200_000
+    rng = np.random.default_rng(215)
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    offs = (np.arange(n + 1) * 114).astype(np.uint32)
+    msgs = rng.integers(0, 256, int(offs[-1]) + 16, dtype=np.uint8)
+    sigs, pubs = e.sign_arrays(seeds, msgs, offs)
+    base = port.verify_batch(pubs, sigs, msgs, offs.astype(np.uint64), 16, zip215=True)
+    bad, t0 = 0, time.perf_counter()
+    for c in range(calls):
+        k = int(rng.integers(0, 7))
+        idx = np.unique(rng.integers(0, n, k))
+        saved = sigs[idx].copy()
+        for i in idx:
+            sigs[i, int(rng.integers(0, 64))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+        exp = base.copy()
+        if idx.size:
+            sub_off = np.zeros(idx.size + 1, np.uint64)
+            sub_off[1:] = 114 * np.arange(1, idx.size + 1)
+            sub_msgs = np.concatenate([msgs[offs[i]:offs[i] + 114] for i in idx] + [np.zeros(16, np.uint8)])
+            exp[idx] = port.verify_batch(pubs[idx], sigs[idx], sub_msgs, sub_off, 1, zip215=True)
+        out = e.verify_zip215_arrays(pubs, sigs, msgs, offs)
+        diff = np.nonzero(out != exp)[0]
+        if diff.size:
+            bad += 1
+            print("call %d: %d mismatches at %s (flipped %s)" % (c, diff.size, diff[:8], idx), flush=True)
+        sigs[idx] = saved
+        if c % 25 == 24:
+            print("%d calls, %d with mismatches, %.1f s" % (c + 1, bad, time.perf_counter() - t0), flush=True)
+    e.close()
+    print("calls with mismatches", bad, flush=True)
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
