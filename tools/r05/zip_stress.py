@@ -1,7 +1,8 @@
 """Diagnostic (round 5): the opt-in ZIP-215 batch mode (randomized batch equations with a fresh
 CSPRNG draw per call, bisection, single checks) on a 200k-signature batch with 0-6 fresh bit flips
 per call, repeated, every decision compared with the C port's ZIP-215 rule (the base batch checked
-once in full, the flipped signatures each call).  Usage: python tools/r05/zip_stress.py [calls]"""
+once in full, the flipped signatures each call); "go" runs the default rule through the generic
+kernels the same way.  Usage: python tools/r05/zip_stress.py [calls] [go]"""
 import os
 import sys
 import time
@@ -19,6 +20,7 @@ from oracle import port  # noqa: E402
 
 def main():
     calls = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+    z = "go" not in sys.argv[2:]  # "go": the default (Go 1.18) rule through the generic kernels instead
     e = engine_with_env()
     n = 200_000
     rng = np.random.default_rng(215)
@@ -26,7 +28,7 @@ def main():
     offs = (np.arange(n + 1) * 114).astype(np.uint32)
     msgs = rng.integers(0, 256, int(offs[-1]) + 16, dtype=np.uint8)
     sigs, pubs = e.sign_arrays(seeds, msgs, offs)
-    base = port.verify_batch(pubs, sigs, msgs, offs.astype(np.uint64), 16, zip215=True)
+    base = port.verify_batch(pubs, sigs, msgs, offs.astype(np.uint64), 16, zip215=z)
     bad, t0 = 0, time.perf_counter()
     for c in range(calls):
         k = int(rng.integers(0, 7))
@@ -39,8 +41,8 @@ def main():
             sub_off = np.zeros(idx.size + 1, np.uint64)
             sub_off[1:] = 114 * np.arange(1, idx.size + 1)
             sub_msgs = np.concatenate([msgs[offs[i]:offs[i] + 114] for i in idx] + [np.zeros(16, np.uint8)])
-            exp[idx] = port.verify_batch(pubs[idx], sigs[idx], sub_msgs, sub_off, 1, zip215=True)
-        out = e.verify_zip215_arrays(pubs, sigs, msgs, offs)
+            exp[idx] = port.verify_batch(pubs[idx], sigs[idx], sub_msgs, sub_off, 1, zip215=z)
+        out = e.verify_zip215_arrays(pubs, sigs, msgs, offs) if z else e.verify_arrays(pubs, sigs, msgs, offs)
         diff = np.nonzero(out != exp)[0]
         if diff.size:
             bad += 1
