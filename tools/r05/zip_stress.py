@@ -2,7 +2,8 @@
 CSPRNG draw per call, bisection, single checks) on a 200k-signature batch with 0-6 fresh bit flips
 per call, repeated, every decision compared with the C port's ZIP-215 rule (the base batch checked
 once in full, the flipped signatures each call); "go" runs the default rule through the generic
-kernels the same way.  Usage: python tools/r05/zip_stress.py [calls] [go]"""
+kernels the same way, "keyed" through the key-cached kernels (1,000 keys).
+Usage: python tools/r05/zip_stress.py [calls] [go|keyed]"""
 import os
 import sys
 import time
@@ -20,14 +21,23 @@ from oracle import port  # noqa: E402
 
 def main():
     calls = int(sys.argv[1]) if len(sys.argv) > 1 else 100
-    z = "go" not in sys.argv[2:]  # "go": the default (Go 1.18) rule through the generic kernels instead
+    keyed = "keyed" in sys.argv[2:]  # the default rule through the key-cached kernels (1,000 keys)
+    z = "go" not in sys.argv[2:] and not keyed  # "go": the default (Go 1.18) rule, generic kernels
     e = engine_with_env()
     n = 200_000
     rng = np.random.default_rng(215)
     seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    vi = rng.integers(0, 1000, n).astype(np.uint32)
+    if keyed:
+        seeds = seeds[:1000][vi]
     offs = (np.arange(n + 1) * 114).astype(np.uint32)
     msgs = rng.integers(0, 256, int(offs[-1]) + 16, dtype=np.uint8)
     sigs, pubs = e.sign_arrays(seeds, msgs, offs)
+    ks = 0
+    if keyed:  # key j's encoding from its first signature (every key is used: 200k draws of 1,000)
+        u, first = np.unique(vi, return_index=True)
+        assert u.size == 1000
+        ks = e.keyset_load(np.ascontiguousarray(pubs[first]))
     base = port.verify_batch(pubs, sigs, msgs, offs.astype(np.uint64), 16, zip215=z)
     bad, t0 = 0, time.perf_counter()
     for c in range(calls):
@@ -42,7 +52,10 @@ def main():
             sub_off[1:] = 114 * np.arange(1, idx.size + 1)
             sub_msgs = np.concatenate([msgs[offs[i]:offs[i] + 114] for i in idx] + [np.zeros(16, np.uint8)])
             exp[idx] = port.verify_batch(pubs[idx], sigs[idx], sub_msgs, sub_off, 1, zip215=z)
-        out = e.verify_zip215_arrays(pubs, sigs, msgs, offs) if z else e.verify_arrays(pubs, sigs, msgs, offs)
+        if keyed:
+            out = e.verify_keyset_arrays(ks, vi, sigs, msgs, offs)
+        else:
+            out = e.verify_zip215_arrays(pubs, sigs, msgs, offs) if z else e.verify_arrays(pubs, sigs, msgs, offs)
         diff = np.nonzero(out != exp)[0]
         if diff.size:
             bad += 1
