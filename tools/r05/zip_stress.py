@@ -2,8 +2,9 @@
 CSPRNG draw per call, bisection, single checks) on a 200k-signature batch with 0-6 fresh bit flips
 per call, repeated, every decision compared with the C port's ZIP-215 rule (the base batch checked
 once in full, the flipped signatures each call); "go" runs the default rule through the generic
-kernels the same way, "keyed" through the key-cached kernels (1,000 keys).
-Usage: python tools/r05/zip_stress.py [calls] [go|keyed]"""
+kernels the same way, "keyed" through the key-cached kernels (1,000 keys), "small" with calls of
+1..4,096 signatures (the latency kernels), generic and keyed alternately.
+Usage: python tools/r05/zip_stress.py [calls] [go|keyed|small]"""
 import os
 import sys
 import time
@@ -21,7 +22,8 @@ from oracle import port  # noqa: E402
 
 def main():
     calls = int(sys.argv[1]) if len(sys.argv) > 1 else 100
-    keyed = "keyed" in sys.argv[2:]  # the default rule through the key-cached kernels (1,000 keys)
+    small = "small" in sys.argv[2:]  # calls of 1..4,096 signatures (latency kernels), generic and keyed alternately
+    keyed = "keyed" in sys.argv[2:] or small  # the default rule through the key-cached kernels (1,000 keys)
     z = "go" not in sys.argv[2:] and not keyed  # "go": the default (Go 1.18) rule, generic kernels
     e = engine_with_env()
     n = 200_000
@@ -42,7 +44,9 @@ def main():
     bad, t0 = 0, time.perf_counter()
     for c in range(calls):
         k = int(rng.integers(0, 7))
-        idx = np.unique(rng.integers(0, n, k))
+        m = int(rng.integers(1, 4097)) if small else n
+        lo = int(rng.integers(0, n - m)) if small else 0
+        idx = lo + np.unique(rng.integers(0, m, k))
         saved = sigs[idx].copy()
         for i in idx:
             sigs[i, int(rng.integers(0, 64))] ^= np.uint8(1 << int(rng.integers(0, 8)))
@@ -52,7 +56,13 @@ def main():
             sub_off[1:] = 114 * np.arange(1, idx.size + 1)
             sub_msgs = np.concatenate([msgs[offs[i]:offs[i] + 114] for i in idx] + [np.zeros(16, np.uint8)])
             exp[idx] = port.verify_batch(pubs[idx], sigs[idx], sub_msgs, sub_off, 1, zip215=z)
-        if keyed:
+        if small:
+            so = (offs[lo:lo + m + 1] - offs[lo]).astype(np.uint32)
+            sm = np.ascontiguousarray(msgs[offs[lo]:offs[lo + m] + 16])
+            out = (e.verify_keyset_arrays(ks, vi[lo:lo + m], sigs[lo:lo + m], sm, so) if c % 2 else
+                   e.verify_arrays(pubs[lo:lo + m], sigs[lo:lo + m], sm, so))
+            exp = exp[lo:lo + m]
+        elif keyed:
             out = e.verify_keyset_arrays(ks, vi, sigs, msgs, offs)
         else:
             out = e.verify_zip215_arrays(pubs, sigs, msgs, offs) if z else e.verify_arrays(pubs, sigs, msgs, offs)
