@@ -3,7 +3,7 @@ test_c3_many_sets_through_the_cache[40-2050-70000]) through the GENERIC pipeline
 one cache-off context, for each batch size in TMED_PIPE_SIGS-like steps, counting outcome
 mismatches against the oracle loops.  For every mismatch it prints the request, whether its
 Trusting/Light pair was split across two planning parts (16 parts per batch) and what a repeat of
-that request alone returns.  Usage: python tools/r05/c3_stress.py [calls_per_size] [sizes...] [cache]"""
+that request alone returns.  Usage: [C3_JITTER_US=us] [TMED_HOST_THREADS=k] python tools/r05/c3_stress.py [calls_per_size] [sizes...] [cache]"""
 import ctypes
 import os
 import sys
@@ -80,6 +80,8 @@ def main():
     calls = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     cache = "cache" in sys.argv[2:]  # the key-set cache on: the first call generic, then keyed (lane 0 / 1)
     sizes = [int(x) for x in sys.argv[2:] if x != "cache"] or [70000, 40000]
+    if os.environ.get("C3_JITTER_US"):  # host-pool jitter (tmed_test_pool_jitter) for the whole run
+        lib().tmed_test_pool_jitter(int(os.environ["C3_JITTER_US"]))
     base = engine_with_env()
     reqs, exp = workload(base)
     base.close()
