@@ -1,9 +1,10 @@
 // Package tmedgpu is the reference-side cgo binding of libtmed25519_hip.so
 // (include/tmed25519.h) for Tendermint Core v0.34.24.
 //
-// It is NOT compiled in this repository (no Go toolchain in the build image);
-// it is the shim a maintainer adds under github.com/tendermint/tendermint/crypto/
-// to route the commit-verification loops to the GPU.  See INTEGRATION.md.
+// It is NOT compiled in this repository (no Go toolchain in the build image); tools/go_cgo_check.py
+// type-checks it statically against include/tmed25519.h instead (tests/test_go_binding.py).  It is
+// the shim a maintainer adds under github.com/tendermint/tendermint/crypto/ to route the
+// commit-verification loops to the GPU.  See INTEGRATION.md.
 //
 // Seam (SURVEY.md §8b): ValidatorSet.VerifyCommit / VerifyCommitLight /
 // VerifyCommitLightTrusting (types/validator_set.go:667-826) call
@@ -663,13 +664,17 @@ func (e *Engine) BlocksyncWait() error {
 }
 
 // Results returns the window's outcomes and releases its memory.  Call it only after a later
-// BlocksyncSubmit or BlocksyncWait returned without error.
+// BlocksyncSubmit or BlocksyncWait returned without error.  A nil window (the one a failed
+// BlocksyncSubmit returns) has no results.
 func (p *PendingWindow) Results() []Result {
-	if p.n == 0 {
+	if p == nil {
 		return nil
 	}
-	out := toResults(unsafe.Slice(p.res, p.n))
-	p.free()
+	var out []Result
+	if p.n > 0 {
+		out = toResults(unsafe.Slice(p.res, p.n))
+	}
+	p.free() // an empty window still holds its arena (and a builder's pinned buffer)
 	return out
 }
 
@@ -823,7 +828,7 @@ func (e *Engine) batch(pubKeys []byte, msgs, sigs [][]byte, zip215 bool) ([]bool
 	}
 	a := e.getArena()
 	defer e.putArena(a)
-	pk, sg, sl, mg, mo := batchArgs(&a, pubKeys, msgs, sigs)
+	pk, sg, sl, mg, mo := batchArgs(a, pubKeys, msgs, sigs)
 	out := (*[1 << 28]C.uint8_t)(a.alloc(uintptr(n)))[:n:n]
 	var rc C.int
 	if zip215 {
