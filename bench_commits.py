@@ -493,6 +493,7 @@ def _c4_corrupt(commits, b0: int, every: int, upto: int):
 
 
 STREAM_CHUNK_WINDOWS = 13  # C4 stream mode: windows generated (pinned) at once: 13 x 1000 blocks x 10k x 64 B = 8.3 GB per rank
+OVERLAP_RING = 3  # C4 overlapped pass: Go-object windows held per rank (~1.6 GB each)
 
 
 def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, batch: int, corrupt_every: int = 0,
@@ -521,7 +522,7 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
     import torch.distributed as dist
     import tmed.types as T
     from tmed import PinnedBuffer, TmedError
-    from tmed.dist import aggregate_blocksync, block_range
+    from tmed.dist import aggregate_blocksync, block_range, overlapped_figures
     if stream:
         pregen = True  # every window exists before the timed stream starts (nothing generated inside it)
     from tmed.launch import gpu_count_fields
@@ -593,9 +594,11 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
             return np.array([self.res[h].verified for h in range(self.n)], np.int64)
 
     marshals = []  # one shim context per window held at once (a window in flight keeps its arrays)
-    # the overlapped pass keeps each window's Go objects until both of its flattens ran (~1.6 GB per
-    # 1000-block window, 13 per shard): one rank per node only, so an 8-rank node does not hold 8x that
-    overlap = marshal == "compiled" and stream and pregen and world == 1
+    # the overlapped pass (every rank): the windows of a chunk flattened again from a RING of the Go
+    # objects of its first OVERLAP_RING windows (~1.6 GB each), so the Go memory per rank stays bounded
+    # (3 windows, not 13) and an 8-rank node holds 8 x 4.8 GB, not 8 x 21 GB
+    overlap = marshal == "compiled" and stream and pregen
+    ring = []  # (go tuple, expected outcomes, blocks) of the chunk's first OVERLAP_RING windows
 
     def to_arena(commits, k):
         if k == len(arenas):
@@ -632,12 +635,18 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
                     arenas.append(_Pageable(window * nvals * 64))
             cw = _CompiledWindow(marshals[k], None, len(commits),
                                  (heap, si, ci, [c.height for c in commits], arenas[k].ptr if pinned else None))
-            if not overlap:  # marshalled here; otherwise inside the stream's overlapped pass
-                tm = time.perf_counter()
+            if overlap:
+                # a first flatten, untimed: a reactor reuses its contexts, so the timed flattens below
+                # and in the overlapped pass measure the steady state, not each context's first touch
                 cw.marshal()
-                t_marshal += time.perf_counter() - tm
-                cw.go = None
+            tm = time.perf_counter()
+            cw.marshal()  # the flatten the stream pass verifies (value_incl_marshal: the serial sum)
+            t_marshal += time.perf_counter() - tm
+            if overlap and k < OVERLAP_RING:
+                ring.append((cw.go, exp, len(commits)))
+            else:
                 heap.free()
+            cw.go = None
             return cw, exp, None
         tm = time.perf_counter()
         if pinned:
@@ -647,10 +656,11 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
         t_marshal += time.perf_counter() - tm
         return win, exp, commits
 
-    def check(w0, w1, win, exp):
-        """(verifies, outcome mismatches) of a collected window; its ok bits into ok_bits"""
+    def check(w0, w1, win, exp, record=True):
+        """(verifies, outcome mismatches) of a collected window; its ok bits into ok_bits (record)"""
         codes, vers = win.codes(), win.verified()
-        ok_bits[w0 - lo:w1 - lo] = codes == 0
+        if record:
+            ok_bits[w0 - lo:w1 - lo] = codes == 0
         bad = 0
         for h, (ec, ei, ev) in enumerate(exp):
             if codes[h] != ec or vers[h] != ev or (ec == 4 and win.res[h].idx != ei):
@@ -670,6 +680,59 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
     sync_pass = [0.0, 0, 0]  # the per-window calls of stream mode: seconds, verifies, mismatches
     ov_pass = [0.0, 0, 0, 0.0]  # the stream with the shim's flattens beside it (+ their summed seconds)
 
+    def overlapped_pass(wins):
+        """The drop-in's pipeline: each window flattened by the shim right before
+        its submit, on a producer thread (the ctypes calls release the GIL), as a reactor's marshalling
+        goroutine would beside the one that submits (tmed_blocksync_submit blocks while the device frees
+        pipeline slots, so a flatten on the submitting thread would not overlap).  Window i is flattened
+        from ring slot i % OVERLAP_RING (the Go objects of one of the chunk's first windows: same shape,
+        same cost) into its own shim context and pinned arena, after the stream pass has used them; its
+        outcomes are checked against that slot's known answers.  Timed from the first flatten to the
+        wait, the flattens summed beside it."""
+        import threading
+        ows = []
+        for i, (w0, w1, win, exp, _) in enumerate(wins):
+            go, sexp, n = ring[i % len(ring)]
+            ows.append((_CompiledWindow(marshals[i], None, n, go[:4] + (arenas[i].ptr if pinned else None,)), sexp))
+        ready = [threading.Event() for _ in ows]
+        tmar = [0.0] * len(ows)
+        perr = []
+
+        def producer():
+            try:
+                for i, (ow, _) in enumerate(ows):
+                    tq = time.perf_counter()
+                    ow.marshal()
+                    tmar[i] = time.perf_counter() - tq
+                    ready[i].set()
+            except BaseException as e:  # wake the submitting thread; it re-raises
+                perr.append(e)
+                for ev in ready:
+                    ev.set()
+
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        th = threading.Thread(target=producer)
+        th.start()
+        try:
+            for i, (ow, _) in enumerate(ows):
+                ready[i].wait()
+                if perr:
+                    break
+                ow.submit(eng, batch)
+            T.blocksync_wait(eng)
+        finally:
+            th.join()  # the producer writes into the shim contexts: never leave it running
+        if perr:
+            raise perr[0]
+        ov_pass[0] += time.perf_counter() - t0
+        ov_pass[3] += sum(tmar)
+        for ow, sexp in ows:
+            v, m = check(0, 0, ow, sexp, record=False)
+            ov_pass[1] += v
+            ov_pass[2] += m
+
     if pregen:  # the windows generated first (in chunks of STREAM_CHUNK_WINDOWS), then all ranks verify together
         starts = list(range(lo, hi, window))
         chunk_w = STREAM_CHUNK_WINDOWS if stream else max(1, len(starts))
@@ -683,73 +746,10 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
             t_gen += time.perf_counter() - tg
             if world > 1:
                 dist.barrier()
-            if overlap and first:
-                # every context flattened once, untimed (a reactor reuses its contexts: the timed
-                # passes then measure the steady state, not the first touch of each context's arrays)
-                for w in wins:
-                    w[2].marshal()
             for _ in range(2 if first else 0):  # untimed warmup (see below)
                 wins[0][2].run(eng, batch)
                 eng.keycache_wait()
             first = False
-            if overlap:
-                # the drop-in's pipeline: each window flattened by the shim right before its submit,
-                # so the flatten of window k+1 runs while the device verifies window k (submit is
-                # asynchronous); timed from the first flatten to the wait.  The flattens alone are
-                # timed too (t_marshal: value_incl_marshal, the serial sum).
-                # The flattens run on a producer thread (the ctypes calls release the GIL), as a
-                # reactor's marshalling goroutine would beside the one that submits: tmed_blocksync_submit
-                # blocks while the device frees pipeline slots, so a flatten on the submitting thread
-                # would not overlap.
-                import threading
-                ready = [threading.Event() for _ in wins]
-                tmar = [0.0] * len(wins)
-
-                perr = []
-
-                def producer():
-                    try:
-                        for i, (_, _, pw, _, _) in enumerate(wins):
-                            tq = time.perf_counter()
-                            pw.marshal()
-                            tmar[i] = time.perf_counter() - tq
-                            ready[i].set()
-                    except BaseException as e:  # wake the submitting thread; it re-raises
-                        perr.append(e)
-                        for ev in ready:
-                            ev.set()
-
-                if world > 1:
-                    dist.barrier()
-                t0 = time.perf_counter()
-                th = threading.Thread(target=producer)
-                th.start()
-                try:
-                    for i, (w0, w1, win, exp, _) in enumerate(wins):
-                        ready[i].wait()
-                        if perr:
-                            break
-                        win.submit(eng, batch)
-                    T.blocksync_wait(eng)
-                finally:
-                    th.join()  # the producer writes into the shim contexts: never leave it running
-                if perr:
-                    raise perr[0]
-                ov_pass[0] += time.perf_counter() - t0
-                ov_pass[3] += sum(tmar)
-                for w0, w1, win, exp, _ in wins:
-                    v, m = check(w0, w1, win, exp)
-                    ov_pass[1] += v
-                    ov_pass[2] += m
-                    win.res = type(win.res)()
-                # the flattens alone, one after another with nothing else running (value_incl_marshal:
-                # their sum added to the stream's seam time)
-                for w0, w1, win, exp, _ in wins:
-                    tm = time.perf_counter()
-                    win.marshal()
-                    t_marshal += time.perf_counter() - tm
-                    win.go[0].free()
-                    win.go = None
             if not stream:
                 for w0, w1, win, exp, _ in wins:  # a call per window (tmed_blocksync_verify)
                     run(w0, w1, win, exp)
@@ -779,6 +779,11 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
                 v, m = check(w0, w1, win, exp)
                 ver += v
                 mism += m
+            if overlap:
+                overlapped_pass(wins)
+            for go, _, _ in ring:
+                go[0].free()
+            ring.clear()
             del wins
     else:
         for w0 in range(lo, hi, window):
@@ -799,12 +804,17 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
     odt, over, omism, omar = ov_pass
     from tmed.launch import BINDING
     mine = [BINDING.get("numa_node", -1), BINDING.get("cpus", 0), int(os.environ.get("TMED_HOST_THREADS", "16")),
-            len(arenas) - len(pinned_failed) if pinned else 0, len(pinned_failed) if pinned else len(arenas)]
+            len(arenas) - len(pinned_failed) if pinned else 0, len(pinned_failed) if pinned else len(arenas),
+            odt, over, omism]
     agg = aggregate_blocksync(ok_bits, blocks, rank, world, ver, mism + smism + omism, dt,
                               extra_max=[t_marshal, sdt, odt, omar],
                               phases=list(phase) + [nbatch], device=dev, per_rank=mine)
+    ov_value, ov_each = overlapped_figures(agg["per_rank"], 5, 6)
     ranks = [{"rank": r, "numa_node": int(p[0]), "cpus": int(p[1]), "host_threads": int(p[2]),
-              "pinned_arenas": int(p[3]), "pageable_arenas": int(p[4])} for r, p in enumerate(agg["per_rank"])]
+              "pinned_arenas": int(p[3]), "pageable_arenas": int(p[4]),
+              "value_incl_marshal_overlapped": ov_each[r], "overlapped_seconds": round(p[5], 4),
+              "overlapped_mismatches": int(p[7])}
+             for r, p in enumerate(agg["per_rank"])]
     n_pageable = sum(x["pageable_arenas"] for x in ranks)
     n_arenas = sum(x["pinned_arenas"] + x["pageable_arenas"] for x in ranks)
     ok, nb, ver, mism, dt = agg["blocks_ok"], agg["blocks"], agg["verified"], agg["mismatches"], agg["seconds"]
@@ -821,15 +831,17 @@ def c4(eng, blocks: int, nvals: int, rank: int, world: int, dev, window: int, ba
     return {"metric": "blocksync replay verifies/s (VerifyCommitLight per block)", "value": round(ver / dt, 1),
             "unit": "verifies/s", "blocks_per_s": round(nb / dt, 1), "blocks": nb,
             "value_incl_marshal": round(ver / (dt + t_marshal_max), 1),
-            "value_incl_marshal_overlapped": (round(ver / odt_max, 1) if odt_max > 0 else None),
-            "overlapped_note": ("the same windows as one stream, each flattened by the shim on a producer "
+            "value_incl_marshal_overlapped": ov_value,
+            "overlapped_note": ("every rank: its windows as one stream, each flattened by the shim on a producer "
                                 "thread and submitted (tmed_blocksync_submit) as soon as it is ready, so the "
                                 "flatten of window k+1 runs while window k is submitted and verified; first "
-                                "flatten to tmed_blocksync_wait; outcome mismatches counted with the stream's. "
-                                "Every shim context is flattened once, untimed, before it (a reactor reuses its "
-                                "contexts: no first-touch page faults in either timed pass); "
-                                "marshal_seconds_max_rank is the serial pass over the same contexts, "
-                                "marshal_seconds_overlapped_pass the overlapped pass's flattens summed"
+                                "flatten to tmed_blocksync_wait, all ranks' verifies / the slowest rank's time "
+                                "(config.ranks[] per rank). Window k is flattened from the Go objects of window "
+                                "k mod %d of its chunk (a ring bounding the Go memory per rank) and checked "
+                                "against that window's known answers; outcome mismatches counted with the "
+                                "stream's. Every shim context is flattened once, untimed, first (a reactor "
+                                "reuses its contexts); marshal_seconds_max_rank is the serial flattens' sum, "
+                                "marshal_seconds_overlapped_pass the overlapped pass's flattens summed" % OVERLAP_RING
                                 if odt_max > 0 else None),
             "marshal_seconds_max_rank": round(t_marshal_max, 4),
             "marshal_seconds_overlapped_pass": (round(omar_max, 4) if odt_max > 0 else None),

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "ge25519.h"
+#include "signbytes.h"
 
 namespace tmed {
 
@@ -205,8 +206,7 @@ hipError_t launch_verify_glat(const uint8_t *pub, const uint8_t *sig, const uint
 // ([pre_len, bid_len, cid_len, 0] + bytes); message i is written to out + i * kVoteSlot
 // and its length to out_len[i].  With msg_slots = true the verify launchers read
 // messages that way (off = lengths).
-constexpr uint32_t kVoteTmplBytes = 256;
-constexpr uint32_t kVoteSlot = 256;
+// (kVoteTmplBytes, kVoteSlot: signbytes.h, shared with the host seam)
 hipError_t launch_assemble_votes(const uint8_t *tmpl, const uint32_t *tmpl_idx, const uint8_t *flags,
                                  const int64_t *ts_sec, const int32_t *ts_nanos, uint32_t n, uint8_t *out,
                                  uint32_t *out_len, hipStream_t stream);

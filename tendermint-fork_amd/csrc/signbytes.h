@@ -7,6 +7,11 @@
 
 namespace tmed {
 
+// f1: on-device CanonicalVote assembly (kernels.h launch_assemble_votes): templates are
+// kVoteTmplBytes records, message i is written at i * kVoteSlot.
+constexpr uint32_t kVoteTmplBytes = 256;
+constexpr uint32_t kVoteSlot = 256;
+
 // Everything but the per-vote flag/timestamp is encoded once per commit.
 struct VoteEncoder {
   uint8_t pre[32];

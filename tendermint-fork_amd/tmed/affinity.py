@@ -99,6 +99,17 @@ def gpu_numa_node(local_rank: int, sysfs: str = "/sys", env: dict | None = None)
     return (bdf, node) if node >= 0 else None
 
 
+def visible_gpu_count(sysfs: str = "/sys", env: dict | None = None):
+    """GPUs this process will see (KFD agents narrowed by the visibility variables), read without
+    touching the HIP runtime; None when the topology or the variables cannot be resolved."""
+    env = os.environ if env is None else env
+    agents = gpu_agents(sysfs)
+    vis = _visible(env, len(agents))
+    if not agents or vis is None:
+        return None
+    return len(vis)
+
+
 def node_cpus(node: int, sysfs: str = "/sys") -> list:
     s = _read(os.path.join(sysfs, "devices", "system", "node", "node%d" % node, "cpulist"))
     return parse_cpulist(s) if s else []

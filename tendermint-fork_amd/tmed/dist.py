@@ -152,3 +152,14 @@ def aggregate_blocksync(ok_bits: np.ndarray, blocks: int, rank: int, world: int,
     return {"blocks_ok": ok, "blocks": nb, "verified": ver, "mismatches": mism, "seconds": tm[0],
             "extra_max": tm[1:], "ok_bits": np.concatenate(full) if full else np.zeros(0, np.uint8),
             "phases": [g.tolist() for g in gp], "per_rank": [g.tolist()[:-1] for g in gr]}
+
+
+def overlapped_figures(per_rank, seconds_idx: int, verifies_idx: int):
+    """The drop-in's host cost at N ranks (bench_commits.c4, the overlapped-marshal pass every rank
+    runs): (whole-job verifies/s = every rank's verifies / the slowest rank's seconds, [each rank's own
+    verifies/s]) from aggregate_blocksync's per_rank rows.  None values where a rank ran no pass."""
+    secs = [float(p[seconds_idx]) for p in per_rank]
+    vers = [float(p[verifies_idx]) for p in per_rank]
+    each = [round(v / t, 1) if t > 0 else None for v, t in zip(vers, secs)]
+    tmax = max(secs) if secs else 0.0
+    return (round(sum(vers) / tmax, 1) if tmax > 0 else None), each

@@ -16,16 +16,28 @@ def dist_setup():
     result is kept in BINDING)."""
     import torch
     import torch.distributed as dist
-    from .affinity import bind_rank
+    from .affinity import bind_rank, visible_gpu_count
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     backend = os.environ.get("TMED_DIST_BACKEND", "nccl")
-    ndev = max(1, torch.cuda.device_count())  # counts devices without initialising HIP (this image)
-    local = local % ndev if backend == "gloo" else local
+    # the device count comes from the KFD topology, so the binding happens before any torch.cuda
+    # call: on a stock ROCm torch device_count() starts the HIP runtime's threads, which would keep
+    # the old CPU mask (sched_setaffinity only rebinds the calling thread and its later children)
+    ndev = visible_gpu_count()
+    counted = "kfd"
+    if ndev is None:
+        ndev, counted = None, "unresolved"
+    if ndev is not None:
+        ndev = max(1, ndev)
+        local = local % ndev if backend == "gloo" else local
     BINDING.clear()
     BINDING.update(bind_rank(local, local_world, ndev))
+    if ndev is None:  # topology unreadable: nothing was bound, so counting through HIP is harmless now
+        ndev = max(1, torch.cuda.device_count())
+        local = local % ndev if backend == "gloo" else local
+    BINDING["device_count_from"] = counted
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     coll = dev

@@ -89,3 +89,27 @@ def test_missing_topology_binds_nothing(tmp_path, monkeypatch):
     before = os.sched_getaffinity(0)
     r = A.bind_rank(0, 1)
     assert r["bound"] is False and os.sched_getaffinity(0) == before
+
+
+def test_visible_gpu_count_without_hip(sysfs):
+    """The device count dist_setup binds with comes from the KFD topology and the visibility
+    variables, so no torch.cuda call (which starts the HIP runtime's threads) precedes the binding."""
+    assert A.visible_gpu_count(sysfs, env={}) == 8
+    assert A.visible_gpu_count(sysfs, env={"HIP_VISIBLE_DEVICES": "2,5"}) == 2
+    assert A.visible_gpu_count(sysfs, env={"ROCR_VISIBLE_DEVICES": "0,1,2,3", "CUDA_VISIBLE_DEVICES": "1"}) == 1
+    assert A.visible_gpu_count(sysfs, env={"HIP_VISIBLE_DEVICES": "GPU-abc"}) is None
+    assert A.visible_gpu_count(os.path.join(sysfs, "missing"), env={}) is None
+
+
+def test_dist_setup_binds_before_any_device_call(monkeypatch):
+    """launch.dist_setup: bind_rank runs before torch.cuda.device_count / set_device."""
+    import torch
+    from tmed import launch
+    calls = []
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: calls.append("device_count") or 1)
+    monkeypatch.setattr(torch.cuda, "set_device", lambda d: calls.append("set_device"))
+    monkeypatch.setattr(A, "bind_rank", lambda *a, **k: calls.append("bind_rank") or {"bound": False})
+    monkeypatch.setattr(A, "visible_gpu_count", lambda *a, **k: 1)
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    launch.dist_setup()
+    assert calls[0] == "bind_rank" and "device_count" not in calls

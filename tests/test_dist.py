@@ -133,7 +133,7 @@ def _blocksync_worker(rank, world, port, q):
     ok_bits = np.array([e is None for e in errs], np.uint8)
     agg = aggregate_blocksync(ok_bits, len(reqs), rank, world, sum(stats), mismatches=rank,
                               seconds=1.0 + rank, extra_max=[0.25 * (rank + 1)], phases=[10.0 * rank, 1.0, 2.0],
-                              per_rank=[rank % 2, 64, 8, 13 - rank, rank])
+                              per_rank=[rank % 2, 64, 8, 13 - rank, rank, 0.5 + rank, 1000.0 * (rank + 1), 0])
     q.put((rank, agg["blocks_ok"], agg["blocks"], agg["verified"], agg["mismatches"], agg["seconds"],
            agg["extra_max"], agg["ok_bits"].tolist(), agg["phases"], agg["per_rank"]))
     dist.barrier()
@@ -175,8 +175,13 @@ def test_blocksync_aggregation_matches_single_process(world):
         assert mism == sum(range(world)) and sec == 1.0 + (world - 1) and extra == [0.25 * world]
         assert bits == single.tolist()
         assert [p[0] for p in phases] == [10.0 * r for r in range(world)] and all(p[-1] == 1.0 + r for r, p in enumerate(phases))
-        # every rank's placement and memory mode reaches every rank (C4's per-rank report)
-        assert per_rank == [[r % 2, 64, 8, 13 - r, r] for r in range(world)]
+        # every rank's placement, memory mode and overlapped-marshal pass reach every rank (C4's
+        # per-rank report): the whole-job overlapped rate is all ranks' verifies / the slowest rank
+        assert per_rank == [[r % 2, 64, 8, 13 - r, r, 0.5 + r, 1000.0 * (r + 1), 0] for r in range(world)]
+        from tmed.dist import overlapped_figures
+        value, each = overlapped_figures(per_rank, 5, 6)
+        assert value == round(sum(1000.0 * (r + 1) for r in range(world)) / (0.5 + world - 1), 1)
+        assert each == [round(1000.0 * (r + 1) / (0.5 + r), 1) for r in range(world)]
 
 
 def test_rehearsal_lines_name_simulated_gpus(monkeypatch):

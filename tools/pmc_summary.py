@@ -13,6 +13,10 @@ import glob
 import json
 import os
 import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tendermint-fork_amd"))
+from tmed.srcdigest import kernel_src_digest  # noqa: E402
 
 KERNELS = ("verify_main_hs_kernel", "verify_prep_r_kernel", "verify_main_kernel", "verify_prep_kernel", "verify_finish_kernel",
            "verify_keyset_main_kernel", "verify_keyset_prep_kernel", "verify_keyset_lat_kernel", "verify_lat_finish_kernel",
@@ -80,9 +84,13 @@ def main():
             d["wait_any_frac"] = d.get("SQ_WAIT_ANY", 0) / wc
             d["valu_active_frac"] = d.get("SQ_ACTIVE_INST_VALU", 0) / wc
         res[k] = d
+    # the kernel sources these counters belong to: bench.py leaves the summary out once they change
+    res["_meta"] = {"kernel_src_sha16": kernel_src_digest(), "collected": time.strftime("%Y-%m-%d %H:%M:%S UTC", time.gmtime())}
     with open(out_path, "w") as fh:
         json.dump(res, fh, indent=1, sort_keys=True)
     for k, d in res.items():
+        if k == "_meta":
+            continue
         print(k, {x: round(d[x], 3) for x in ("hbm_bytes_per_sig", "valu_insts_per_wave", "dispatch_ms_mean",
                                               "effective_clock_ghz", "active_inst_any_frac", "wait_inst_any_frac",
                                               "wait_any_frac") if x in d})
