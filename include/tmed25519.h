@@ -43,6 +43,11 @@ extern "C" {
 #define TMED_EHIP (-3)      /* HIP runtime error (device lost, launch failure) */
 #define TMED_ENOMEM (-4)    /* device or pinned-host allocation failed */
 #define TMED_ENOKEYSET (-5) /* unknown key-set handle */
+#define TMED_EINTERNAL (-6) /* internal error: a host-side exception inside the library (a bug, never a
+                               decision); the call's outputs are unusable.  A seam call that fails this
+                               way (or any other way) while blocksync windows are in flight on the
+                               context drops those windows: their results are not final, and
+                               tmed_blocksync_wait reports the error */
 
 typedef struct tmed_ctx tmed_ctx;
 

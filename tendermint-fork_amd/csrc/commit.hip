@@ -940,8 +940,11 @@ static int bs_window(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t bat
 
 // The seam's C entry points: no C++ exception may cross into the caller (a cgo caller would abort).
 // A host allocation that fails inside a call (the per-part plan vectors, a window's copies) returns
-// TMED_ENOMEM; the context's batch stream is then dropped like after any other error (bs_abort), so
-// no queued batch still reads the caller's buffers.
+// TMED_ENOMEM, any other exception TMED_EINTERNAL (never TMED_EHIP: the device is fine).  When the
+// context's blocksync stream still holds work (batches in flight, windows not collected), it is
+// dropped (bs_abort), so no queued batch still reads the caller's buffers, and its windows' callers
+// get the error from tmed_blocksync_wait; an idle stream is left alone, so the failure of one
+// synchronous call is not reported to a later, unrelated window.
 template <class F>
 static int c_guard(tmed_ctx *ctx, F &&f) {
   int rc;
@@ -950,12 +953,12 @@ static int c_guard(tmed_ctx *ctx, F &&f) {
   } catch (const std::bad_alloc &) {
     rc = TMED_ENOMEM;
   } catch (...) {
-    rc = TMED_EHIP;
+    rc = TMED_EINTERNAL;
   }
   if (ctx) {
     try {
       std::lock_guard<std::mutex> lk(ctx->mu);
-      if (ctx->bs) bs_abort(ctx, *ctx->bs, rc);
+      if (ctx->bs && (!ctx->bs->empty() || !ctx->bs->wins.empty())) bs_abort(ctx, *ctx->bs, rc);
     } catch (...) {
     }
   }

@@ -76,15 +76,18 @@ struct Keyset {
   // memory -> the radix-256 comb).
   std::vector<int4 *> comb, comba;
   std::vector<uint32_t> comb_keys, comba_keys;
-  // device: the chunk bases, kKeyChunksMax of the radix-256 comb then kKeyChunksMax of the
-  // radix-2^12 comb (the kernels' tables); entries are set on the set's stream as chunks appear
+  // device: the chunk bases, tab_chunks of the radix-256 comb then tab_chunks of the radix-2^12
+  // comb (the kernels' tables); entries are set on the set's stream as chunks appear.  tab_chunks:
+  // kKeyChunksMax for the cache's pool, else the chunks the set's keys need (rounded up to a power
+  // of two, grown with the set: keyset_reserve)
   int4 **d_tab = nullptr;
   int4 **h_tab = nullptr;  // pinned mirror (the source of the entries' copies)
+  size_t tab_chunks = 0;
   size_t comba_n = 0;
   bool comba_failed = false;
   bool pooled = false;  // the context's key-set cache pool: not reachable through the public handles
   const int4 *const *comb_tab() const { return d_tab; }
-  const int4 *const *comba_tab() const { return d_tab + kKeyChunksMax; }
+  const int4 *const *comba_tab() const { return d_tab + tab_chunks; }
   size_t comb_room() const { return comb.empty() ? 0 : (comb.size() - 1) * (size_t)kKeyChunkKeys + comb_keys.back(); }
   size_t comba_room() const { return comba.empty() ? 0 : (comba.size() - 1) * (size_t)kKeyChunkKeys + comba_keys.back(); }
   // the row of entry (window w, j) of key v: radix-256 / radix-2^12

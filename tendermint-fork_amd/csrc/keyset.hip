@@ -130,7 +130,7 @@ static void comba_drop(Keyset &k) {
 static void comba_extend(tmed_ctx *c, Keyset &k, hipStream_t s) {
   if (!c->acomb_on || k.comba_failed || k.comba_n >= k.n) return;
   std::vector<void *> retired;
-  hipError_t e = chunks_grow(c, k.comba, k.comba_keys, k.h_tab + kKeyChunksMax, k.d_tab + kKeyChunksMax, k.n,
+  hipError_t e = chunks_grow(c, k.comba, k.comba_keys, k.h_tab + k.tab_chunks, k.d_tab + k.tab_chunks, k.n,
                              k.comb_room(), kCombABytesPerKey, k.comba_n, s, retired);
   int32_t *bases = nullptr;
   const size_t m = k.n - k.comba_n;
@@ -167,27 +167,56 @@ Keyset *find_keyset(tmed_ctx *c, uint64_t handle) {
 // (chunks_grow: nothing built moves, except the keys of a partial last chunk); a synchronisation of
 // s and the second lane only when a replaced buffer is freed.  The radix-2^12 comb follows at the
 // next throughput batch (comba_extend).
+// The set's chunk tables (device + pinned mirror) with room for `chunks` chunks per comb: the
+// cache's pool takes kKeyChunksMax at once (512 KB), an explicit set what its keys need (a
+// 175-key set: 8 entries), doubled when tmed_keyset_extend outgrows it — the new tables take the
+// old entries, the old device table is freed with the other replaced buffers (retired), the old
+// pinned mirror after s has finished the copies made from it.
+static hipError_t tables_reserve(tmed_ctx *c, Keyset &k, size_t chunks, hipStream_t s,
+                                 std::vector<void *> &retired) {
+  if (k.d_tab && chunks <= k.tab_chunks) return hipSuccess;
+  size_t cap = 8;
+  while (cap < chunks) cap <<= 1;
+  cap = std::min<size_t>(cap, kKeyChunksMax);
+  const size_t bytes = 2 * cap * sizeof(int4 *);
+  int4 **d = nullptr, **h = nullptr;
+  hipError_t e = ks_malloc(c, (void **)&d, bytes);
+  if (e == hipSuccess) e = hipHostMalloc((void **)&h, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    if (d) (void)hipFree(d);
+    return e;
+  }
+  memset(h, 0, bytes);
+  if (k.h_tab) {  // the old entries: radix-256 half, then the radix-2^12 half at its new offset
+    memcpy(h, k.h_tab, k.tab_chunks * sizeof(int4 *));
+    memcpy(h + cap, k.h_tab + k.tab_chunks, k.tab_chunks * sizeof(int4 *));
+  }
+  e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) {
+    (void)hipFree(d);
+    (void)hipHostFree(h);
+    return e;
+  }
+  if (k.h_tab) {
+    (void)hipStreamSynchronize(s);  // earlier entry copies read the old mirror
+    (void)hipHostFree(k.h_tab);
+  }
+  if (k.d_tab) retired.push_back(k.d_tab);
+  k.d_tab = d;
+  k.h_tab = h;
+  k.tab_chunks = cap;
+  return hipSuccess;
+}
+
 static int keyset_reserve(tmed_ctx *c, Keyset &k, size_t want, size_t limit, hipStream_t s) {
   hipError_t e = hipSuccess;
-  const size_t tab_bytes = 2 * (size_t)kKeyChunksMax * sizeof(int4 *);
-  if (!k.d_tab) {
-    e = ks_malloc(c, (void **)&k.d_tab, tab_bytes);
-    if (e == hipSuccess) e = hipMemsetAsync(k.d_tab, 0, tab_bytes, s);
-    if (e != hipSuccess) {
-      if (k.d_tab) (void)hipFree(k.d_tab);
-      k.d_tab = nullptr;
-      return map_err(e);
-    }
-  }
-  if (!k.h_tab) {
-    e = hipHostMalloc((void **)&k.h_tab, tab_bytes, hipHostMallocDefault);
-    if (e != hipSuccess) {
-      k.h_tab = nullptr;
-      return map_err(e);
-    }
-    memset(k.h_tab, 0, tab_bytes);
-  }
   std::vector<void *> retired;
+  e = tables_reserve(c, k, k.pooled ? (size_t)kKeyChunksMax : (limit + kKeyChunkKeys - 1) / kKeyChunkKeys, s,
+                     retired);
+  if (e != hipSuccess) {
+    (void)free_retired(c, retired, s);
+    return map_err(e);
+  }
   if (want > k.cap) {
     const size_t cap = std::max(want, std::min(2 * k.cap, limit));
     uint8_t *pub = nullptr, *ok = nullptr;

@@ -624,6 +624,9 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
   const bool skew = nt > 1 && getenv("TMED_TEST_MERGE_SKEW") != nullptr;
   auto merge_part = [&](size_t t) {
     if (skew && (t & 1)) std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    // reads from outside part t: part[t], pc, lo_of / hi_of (the planning region, finished), rbase /
+    // cbase (the serial prefix sums above); everything else read below is part t's own output of
+    // this same body (its runs, offsets and plans, written before pair_request / add_run read them)
     size_t c = cbase[t];
     Run *dst = cands.runs.data() + rbase[t];
     size_t *off = cands.off.data() + rbase[t];
@@ -724,6 +727,8 @@ static int seam_plan(const tmed_commit_request *reqs, size_t n, tmed_commit_resu
   }
   if (aliases || rows_here) {
     auto join = [&](size_t t) {
+      // reads ps.aparts / gparts / trows (the merge region, finished) and the prefix sums above;
+      // writes only part t's slices of the joined arrays
       if (rows_here) {
         std::copy(ps.trows[t].begin(), ps.trows[t].end(), tp->rows.begin() + tbase[t] * tmed::kVoteTmplBytes);
         for (size_t q = lo_of[t]; q < hi_of[t]; q++)
@@ -814,7 +819,9 @@ static void pair_request(const tmed_commit_request *reqs, const std::vector<Plan
       if (kp)
         for (size_t b = 0; b < kb; b += 64) __builtin_prefetch(kp + b);
     }
-    // o's candidates are its qualifying signatures in order, as runs sorted by signature
+    // o's candidates are its qualifying signatures in order, as runs sorted by signature.  pq lies in
+    // [lo, hi), the calling merge part's own requests: plans[pq], its runs and their offsets were
+    // written by this part's merge before this call, never by another part
     size_t ro = po.run_lo;
     for (size_t ri = pl.run_lo; ri < pl.run_hi; ri++) {
       const Run &run = cands.runs[ri];
@@ -979,6 +986,7 @@ static void build_group(const Cands &c, Group &g) {
   parallel_ranges(nr, nt, [&](size_t lo, size_t hi, unsigned t) {
     Group mine;  // (a header of its own: see seam_plan)
     mine.start();
+    // c (runs, off, alias) is complete before this region (seam_plan returned): no part writes it
     const auto a0 = std::lower_bound(c.alias.begin(), c.alias.end(), std::make_pair((uint32_t)c.off[lo], 0u));
     size_t ap = (size_t)(a0 - c.alias.begin());
     for (size_t r = lo; r < hi; r++) mine.add_run(c, (uint32_t)r, c.alias, ap);

@@ -38,6 +38,7 @@ const char *tmed_strerror(int code) {
     case TMED_EHIP: return "HIP runtime error";
     case TMED_ENOMEM: return "out of memory";
     case TMED_ENOKEYSET: return "unknown key-set handle";
+    case TMED_EINTERNAL: return "internal error (host-side exception in the library)";
     default: return "unknown error";
   }
 }

@@ -18,6 +18,7 @@ TMED_ENODEV = -2
 TMED_EHIP = -3
 TMED_ENOMEM = -4
 TMED_ENOKEYSET = -5
+TMED_EINTERNAL = -6
 
 _lib = None
 

@@ -34,6 +34,10 @@ def test_strerror_and_no_fallback_without_gpu():
     import torch
     from tmed import Engine, TmedError, lib
     assert lib().tmed_strerror(-2).decode().startswith("no usable")
+    # a host-side exception is its own code, never reported as a HIP (device) error
+    from tmed import _native
+    assert lib().tmed_strerror(_native.TMED_EINTERNAL).decode().startswith("internal error")
+    assert lib().tmed_strerror(_native.TMED_EHIP).decode() == "HIP runtime error"
     if torch.cuda.is_available():
         pytest.skip("GPU present: covered by the gpu tests")
     assert lib().tmed_device_count() == 0

@@ -71,6 +71,28 @@ def test_key_set_across_chunks(engine):
         engine.keyset_free(h)
 
 
+def test_key_set_table_growth(engine):
+    """An explicit set's chunk tables are sized to its keys (8 entries per comb for up to 4,096 keys,
+    not the pool's 32,768): extending a 600-key set to 4,700 keys (10 chunks) moves both tables into
+    larger ones, the radix-2^12 half at its new offset.  Batches over every key through both combs
+    and the latency kernels equal the port before and after; comb rows at the far chunks read back."""
+    seeds, pubs = _keys(4700, 78)
+    h = engine.keyset_load(pubs[:600])
+    try:
+        big = _batch(seeds, pubs, 600, 30000, 11)  # > TMED_LAT_MAX (24,576): the throughput kernels
+        assert (engine.verify_keyset_arrays(h, *big[:4]) == big[4]).all()
+        assert engine.keyset_a_window_bits(h) == 12
+        assert engine.keyset_extend(h, pubs[600:]) == 600
+        big2 = _batch(seeds, pubs, 4700, 40000, 12)
+        assert (engine.verify_keyset_arrays(h, *big2[:4]) == big2[4]).all()
+        assert engine.keyset_a_window_bits(h) == 12
+        small2 = _batch(seeds, pubs, 4700, 700, 13)
+        assert (engine.verify_keyset_arrays(h, *small2[:4]) == small2[4]).all()
+        _rows_match(engine, h, pubs, (599, 4095, 4096, 4699), (8, 12))
+    finally:
+        engine.keyset_free(h)
+
+
 def test_full_size_keyed_property(engine):
     """BASELINE's key-cached C2 variant at full size: 2^20 GPU-signed signatures by 10,000 keys (20
     comb chunks, 64 GB of combs) through the throughput kernels on the radix-2^12 comb: every
