@@ -132,3 +132,12 @@ def test_header_change_is_caught(header):
 def test_snippet_mutation_is_caught(header, old, new, expect):
     errs = check(header, md=mutate(MD, old, new))
     assert errs and any(expect in e for e in errs), errs
+
+
+def test_cgo_preamble_paths():
+    """The binding's #cgo -I / -L directories resolve from ${SRCDIR} to include/ (holding the header it
+    includes) and to the library's build directory."""
+    go_dir = os.path.dirname(gc.GO_FILE)
+    assert gc.check_preamble(GO, go_dir) == []
+    bad = GO.replace("-I${SRCDIR}/../../../include", "-I${SRCDIR}/../../include")
+    assert any("tmed25519.h" in e or "does not exist" in e for e in gc.check_preamble(bad, go_dir))

@@ -1359,6 +1359,34 @@ def parse_go(src: str):
     return Parser(lex(src)).file()
 
 
+def check_preamble(go_src: str, go_dir: str, where="tmedgpu.go"):
+    """The cgo preamble's -I / -L directories (relative to ${SRCDIR}) exist and hold the header it
+    includes and the library it links."""
+    errs = []
+    m = re.search(r"/\*(.*?)\*/\s*import \"C\"", go_src, re.S)
+    if not m:
+        return ["%s: no cgo preamble before import \"C\"" % where]
+    pre = m.group(1)
+    incs = re.findall(r"#include \"([^\"]+)\"", pre)
+    for flag, kind in (("-I", "include"), ("-L", "lib")):
+        for d in re.findall(r"%s\$\{SRCDIR\}(\S+)" % flag, pre):
+            path = os.path.normpath(go_dir + d)
+            if not os.path.isdir(path):
+                errs.append("%s: cgo %s directory %s does not exist" % (where, flag, path))
+            elif kind == "include":
+                for h in incs:
+                    if not os.path.exists(os.path.join(path, h)):
+                        errs.append("%s: %s not found in the cgo include directory %s" % (where, h, path))
+    for lib in re.findall(r"-l(\w+)", pre):
+        dirs = [os.path.normpath(go_dir + d) for d in re.findall(r"-L\$\{SRCDIR\}(\S+)", pre)]
+        srcs = [os.path.join(d, "lib%s.so" % lib) for d in dirs]
+        # the library is a build product (make -C tendermint-fork_amd); its Makefile target must exist
+        if not any(os.path.exists(x) for x in srcs) and not any(
+                os.path.exists(os.path.join(os.path.dirname(d), "Makefile")) for d in dirs):
+            errs.append("%s: -l%s: neither built nor buildable from the -L directories" % (where, lib))
+    return errs
+
+
 def check_binding(go_src: str, header: Header, where="tmedgpu.go"):
     decls = parse_go(go_src)
     pkg = Pkg(decls)
@@ -1435,8 +1463,9 @@ def run(go_src=None, md_src=None, header_text=None):
     if md_src is None:
         with open(INTEGRATION) as f:
             md_src = f.read()
-    errs, pkg = check_binding(go_src, header)
-    errs += check_snippets(md_src, header, pkg)
+    errs = check_preamble(go_src, os.path.dirname(GO_FILE))
+    e2, pkg = check_binding(go_src, header)
+    errs += e2 + check_snippets(md_src, header, pkg)
     return errs
 
 
