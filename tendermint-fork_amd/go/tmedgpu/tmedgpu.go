@@ -786,6 +786,44 @@ func (e *Engine) MerkleRoots(trees [][][]byte) ([][32]byte, error) {
 	return append([][32]byte(nil), out...), nil
 }
 
+// VoteSignBytes returns Commit.VoteSignBytes for n votes of one commit (tmed_vote_sign_bytes;
+// types/block.go:807-810 -> types/vote.go:93-101): vote i has flag flags[i] and timestamp
+// (tsSec[i], tsNanos[i]).  The seam builds these itself (on the device); this is for callers and
+// tests that sign synthetic commits.
+func (e *Engine) VoteSignBytes(chainID string, height int64, round int32, bid *BlockID, flags []byte,
+	tsSec []int64, tsNanos []int32) ([][]byte, error) {
+	n := len(flags)
+	if len(tsSec) != n || len(tsNanos) != n {
+		return nil, errors.New("tmedgpu: one flag and one timestamp per vote")
+	}
+	if n == 0 {
+		return nil, nil
+	}
+	a := e.getArena()
+	defer e.putArena(a)
+	t := (*C.tmed_vote_template)(a.alloc(unsafe.Sizeof(C.tmed_vote_template{})))
+	*t = C.tmed_vote_template{chain_id: a.cstring(chainID), chain_id_len: C.uint32_t(len(chainID)),
+		height: C.int64_t(height), round: C.int32_t(round), block_hash: a.bytes(bid.Hash),
+		block_hash_len: C.uint32_t(len(bid.Hash)), psh_total: C.uint32_t(bid.PSHTotal), psh_hash: a.bytes(bid.PSHHash),
+		psh_hash_len: C.uint32_t(len(bid.PSHHash))}
+	fl, sec, ns := a.bytes(flags), a.i64(tsSec), a.i32(tsNanos)
+	off := (*[1 << 26]C.uint32_t)(a.alloc(uintptr(n+1) * 4))[: n+1 : n+1]
+	var total C.size_t
+	if rc := C.tmed_vote_sign_bytes(t, C.size_t(n), fl, sec, ns, nil, 0, &off[0], &total); rc != 0 {
+		return nil, errors.New(C.GoString(C.tmed_strerror(rc)))
+	}
+	buf := (*C.uint8_t)(a.alloc(uintptr(total) + 1))
+	if rc := C.tmed_vote_sign_bytes(t, C.size_t(n), fl, sec, ns, buf, total, &off[0], &total); rc != 0 {
+		return nil, errors.New(C.GoString(C.tmed_strerror(rc)))
+	}
+	flat := unsafe.Slice((*byte)(unsafe.Pointer(buf)), int(total))
+	out := make([][]byte, n)
+	for i := range out {
+		out[i] = append([]byte(nil), flat[off[i]:off[i+1]]...)
+	}
+	return out, nil
+}
+
 // batchArgs packs n (pubkey, message, signature) tuples for tmed_verify_batch(_zip215):
 // pubKeys n x 32, sigs as given (the lengths travel so a wrong-length signature is rejected
 // exactly as ed25519.Verify rejects it), messages concatenated with offsets.

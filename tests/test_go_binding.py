@@ -30,8 +30,12 @@ def header():
         pytest.skip(str(e))
 
 
-def check(header, go=GO, md=MD):
-    errs, pkg = gc.check_binding(go, header)
+with open(gc.GO_FILE[:-3] + "_test.go") as _f:
+    GOTEST = _f.read()
+
+
+def check(header, go=GO, md=MD, gotest=GOTEST):
+    errs, pkg = gc.check_binding(go, header, extra=[("tmedgpu_test.go", gotest)])
     return errs + gc.check_snippets(md, header, pkg)
 
 
@@ -141,3 +145,15 @@ def test_cgo_preamble_paths():
     assert gc.check_preamble(GO, go_dir) == []
     bad = GO.replace("-I${SRCDIR}/../../../include", "-I${SRCDIR}/../../include")
     assert any("tmed25519.h" in e or "does not exist" in e for e in gc.check_preamble(bad, go_dir))
+
+
+@pytest.mark.parametrize("old,new,expect", [
+    ("c.Height, c.Round, &bid, c.Flags", "c.Height, c.Round, bid, c.Flags", "argument 4 of method Engine.VoteSignBytes"),
+    ("res, err := b.Verify()", "res, err := b.Verify(1)", "takes 0 arguments"),
+    ("vs.Powers[i] = 10", "vs.Power[i] = 10", "no field or method Power"),
+])
+def test_go_test_file_mutation_is_caught(header, old, new, expect):
+    """The binding's Go tests (tmedgpu_test.go, what a maintainer runs on a GPU box) are checked
+    with the package's own declarations."""
+    errs = check(header, gotest=mutate(GOTEST, old, new))
+    assert errs and any(expect in e for e in errs), errs

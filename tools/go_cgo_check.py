@@ -664,7 +664,8 @@ class Parser:
                     self.eat("]")
                     x = ("index", t.line, x, lo)
                 self.no_lit = saved
-            elif self.at("{") and _litable(x) and self.no_lit == 0:
+            elif self.at("{") and _litable(x) and (self.no_lit == 0 or x[0] == "type"):
+                # (in an if/for/switch header only a literal of a TypeName needs parentheses)
                 x = ("complit", t.line, type_of_typeexpr(x), self.litbody())
             else:
                 return x
@@ -1387,18 +1388,24 @@ def check_preamble(go_src: str, go_dir: str, where="tmedgpu.go"):
     return errs
 
 
-def check_binding(go_src: str, header: Header, where="tmedgpu.go"):
-    decls = parse_go(go_src)
-    pkg = Pkg(decls)
-    ck = Checker(header, pkg, where)
-    for d in decls:
-        if d[0] == "func":
-            ck.check_func(d)
-        elif d[0] == "vardecl":
-            for v in d[4]:
-                ck.expr(v, [{}], {})
-    check_binding.stats = ck.stats
-    return ck.errors, pkg
+def check_binding(go_src: str, header: Header, where="tmedgpu.go", extra=()):
+    """The package's main file plus `extra` [(name, source)] files of the same package (its
+    _test.go): one declaration set, every function checked, errors named by file."""
+    files = [(where, parse_go(go_src))] + [(w, parse_go(src)) for w, src in extra]
+    pkg = Pkg([d for _, ds in files for d in ds])
+    errors = []
+    for w, decls in files:
+        ck = Checker(header, pkg, w)
+        for d in decls:
+            if d[0] == "func":
+                ck.check_func(d)
+            elif d[0] == "vardecl":
+                for v in d[4]:
+                    ck.expr(v, [{}], {})
+        if w == where:
+            check_binding.stats = ck.stats
+        errors += ck.errors
+    return errors, pkg
 
 
 def go_blocks(md: str):
@@ -1464,7 +1471,12 @@ def run(go_src=None, md_src=None, header_text=None):
         with open(INTEGRATION) as f:
             md_src = f.read()
     errs = check_preamble(go_src, os.path.dirname(GO_FILE))
-    e2, pkg = check_binding(go_src, header)
+    extra = []
+    test_file = GO_FILE[:-3] + "_test.go"
+    if os.path.exists(test_file):
+        with open(test_file) as f:
+            extra.append((os.path.basename(test_file), f.read()))
+    e2, pkg = check_binding(go_src, header, extra=extra)
     errs += e2 + check_snippets(md_src, header, pkg)
     return errs
 
