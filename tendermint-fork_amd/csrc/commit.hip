@@ -266,7 +266,7 @@ struct KcStore {
   std::vector<SetRef> sets;
   std::vector<int32_t> set_of, tval;
   std::vector<const tmed_valset *> tkey;
-  std::vector<uint32_t> nsig, slot, first;
+  std::vector<uint32_t> slot;
   std::vector<uint8_t> is_first;
 };
 struct KcCall {
@@ -365,7 +365,6 @@ static const tmed_commit_request *keycache_resolve(tmed_ctx *ctx, const tmed_com
     }
   clk.lap("sets");
   // request -> set and signatures per set (the policy's amortisation and the counters)
-  S.nsig.resize(n);
   parallel_ranges(n, nt, [&](size_t lo, size_t hi, unsigned) {
     for (size_t q = lo; q < hi; q++) {
       const int32_t s_ = slot[q] == kNoSet ? -1 : -1 - tval[slot[q]];
