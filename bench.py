@@ -719,6 +719,31 @@ def _cpu_model():
 HOST_SHARE_THREADS = 16  # one GPU's share of the box's CPUs (the pool's rule for worker pools)
 
 
+def _cgroup_cpus():
+    """The CPU bandwidth this process's cgroup allows, in CPUs (cgroup v2 cpu.max / v1 cfs quota), or
+    None when unlimited or unreadable: beside os.cpu_count(), what an all-threads run could use."""
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", lambda t: [t.strip(), None])):
+        try:
+            with open(path) as fh:
+                q, per = parse(fh.read())
+        except (OSError, ValueError):
+            continue
+        if q in ("max", "-1"):
+            return None
+        if per is None:
+            try:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+                    per = fh.read().strip()
+            except OSError:
+                return None
+        try:
+            return round(int(q) / int(per), 2)
+        except (ValueError, ZeroDivisionError):
+            return None
+    return None
+
+
 def cpu_baseline_threads(d_pub, d_sig, msgs, offs, m, d_out, one_thread_value, gpu_value):
     """The port on many host threads: the embarrassingly parallel upper bound SURVEY.md §8d and
     BASELINE.md:28-30 ask for beside the 1-core figure (the reference itself verifies on one
@@ -753,7 +778,7 @@ def cpu_baseline_threads(d_pub, d_sig, msgs, offs, m, d_out, one_thread_value, g
                       % (m, nt, runs[nt]["seconds"], _cpu_model()),
             "threads_runs": {str(k): r for k, r in sorted(runs.items())},
             "parallel_efficiency_vs_1_thread": round(per_thread / one_thread_value, 3) if one_thread_value else None,
-            "box_cpus": box, "node_cpus": node,
+            "box_cpus": box, "node_cpus": node, "cgroup_cpu_quota": _cgroup_cpus(),
             "all_cores_extrapolated": {
                 "value": round(extrap, 1), "cores": box,
                 "basis": "per-thread rate at %d threads x %d CPUs (linear: the port shares nothing between "
