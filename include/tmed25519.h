@@ -265,7 +265,7 @@ void tmed_test_stream_delay(int us);
  * With TMED_DEBUG_ZERO set at the first pipelined generic batch: every staged candidate whose
  * device bit is 0 is recorded (request, signature, staging position, the staged and the device
  * copies of its key and signature, the assembled sign-bytes).  Copies up to cap records into out
- * and removes them; *n = records copied; returns the record size in bytes (tools/r05/c3_stress.py).
+ * and removes them; *n = records copied; returns the record size in bytes (tools/stress/c3_stress.py).
  */
 int tmed_debug_zero_bits(void *out, size_t cap, size_t *n);
 

@@ -11,6 +11,6 @@ case $rc in 124|134|137|139) exit $rc;; esac
 timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
 rc=$?; echo "gpu tests rc=$rc"; tail -3 $O/gpu_tests.log
 case $rc in 124|134|137|139) exit $rc;; esac
-bash tools/r04/c4_trace.sh
+bash profiles/r04/recipes/c4_trace.sh
 timeout -k 10 600 python bench.py > $O/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -c 600 $O/bench.log

@@ -10,7 +10,7 @@ rc=$?; echo "gpu tests rc=$rc"; tail -3 $O/gpu_tests.log
 case $rc in 0) ;; *) exit $rc;; esac
 for r in 1 2 3; do
   for L in 2 1; do
-    TMED_LANES=$L timeout -k 10 120 python tools/r04/ab_keyed.py >> $O/ab_keyed_lanes.jsonl 2>> $O/ab_keyed.err || { echo "ab failed rc=$?"; exit 1; }
+    TMED_LANES=$L timeout -k 10 120 python profiles/r04/recipes/ab_keyed.py >> $O/ab_keyed_lanes.jsonl 2>> $O/ab_keyed.err || { echo "ab failed rc=$?"; exit 1; }
   done
 done
 cat $O/ab_keyed_lanes.jsonl

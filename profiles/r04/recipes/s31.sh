@@ -7,7 +7,7 @@ O=gpurun_out/s31
 mkdir -p $O
 for rep in 1 2 3; do
   for L in tendermint-fork_amd/lib/libtmed25519_hip.so tendermint-fork_amd/lib/ab/libtmed_fin131k.so tendermint-fork_amd/lib/ab/libtmed_fin262k.so; do
-    TMED_LIB=$PWD/$L timeout -k 10 200 python tools/r04/ab_keyed.py >> $O/ab_keyed.jsonl 2>> $O/ab_keyed.err
+    TMED_LIB=$PWD/$L timeout -k 10 200 python profiles/r04/recipes/ab_keyed.py >> $O/ab_keyed.jsonl 2>> $O/ab_keyed.err
     rc=$?; [ $rc -eq 0 ] || { echo "ab rc=$rc"; exit $rc; }
   done
 done

@@ -18,7 +18,7 @@ echo "probe rc=$?"
 # keyed C2 A/B: old batched finish / pipelined finish (default) / + 4-wave keyed prep
 for r in 1 2 3; do
   for L in tendermint-fork_amd/lib/ab/libtmed_finold.so tendermint-fork_amd/lib/libtmed25519_hip.so tendermint-fork_amd/lib/ab/libtmed_prep4.so; do
-    TMED_LIB=$PWD/$L timeout -k 10 120 python tools/r04/ab_keyed.py >> $O/ab_keyed.jsonl 2>> $O/ab_keyed.err || { echo "ab failed rc=$?"; exit 1; }
+    TMED_LIB=$PWD/$L timeout -k 10 120 python profiles/r04/recipes/ab_keyed.py >> $O/ab_keyed.jsonl 2>> $O/ab_keyed.err || { echo "ab failed rc=$?"; exit 1; }
   done
 done
 cat $O/ab_keyed.jsonl

@@ -20,6 +20,6 @@ print(" ".join(out))')" | tee -a $O/ab.txt
     case $rc in 124|134|137|139) exit $rc;; esac
   done
 done
-bash tools/r05/s16.sh; rc=$?
+bash profiles/r05/recipes/s16.sh; rc=$?
 cp -r gpurun_out/r05s16 $O/ 2>/dev/null
 exit $rc

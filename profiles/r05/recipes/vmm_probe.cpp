@@ -1,7 +1,7 @@
 // Probe of the HIP virtual-memory calls on the box (round 5, the key pool grown in place): which
 // of hipMemCreate / hipMemMap / hipMemSetAccess accepts a second physical chunk mapped at an offset
 // inside one reserved range, for small and multi-GB chunks, and whether a kernel then sees the data.
-// Build: hipcc --offload-arch=gfx950 -O2 tools/r05/vmm_probe.cpp -o tools/r05/vmm_probe
+// Build: hipcc --offload-arch=gfx950 -O2 profiles/r05/recipes/vmm_probe.cpp -o profiles/r05/recipes/vmm_probe
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>

@@ -249,7 +249,7 @@ def test_c3_pipelined_parts_merged_out_of_order(engine, monkeypatch):
     before it is written.  Before round 5's fix the merge took the end of a part's last run from
     the next part's first offset: the last request of a part then lost or borrowed candidates (a
     false "wrong signature" about once in 250 light-client calls, always the last request of a
-    part: tools/r05/c3_stress.py, profiles/r05/s28/).  Three calls of ~1,750-request batches on 16
+    part: tools/stress/c3_stress.py, profiles/r05/s28/).  Three calls of ~1,750-request batches on 16
     planning parts, slot 0's offsets left over from another batch on the second and third."""
     monkeypatch.setenv("TMED_PIPE_SIGS", "70000")
     monkeypatch.setenv("TMED_TEST_MERGE_SKEW", "1")

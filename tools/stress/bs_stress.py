@@ -3,7 +3,7 @@ one context, key-cached (batches alternating the two kernel lanes) and generic, 
 codes and verified counts compared with a per-window run on a second, generic context.  The
 workload is tests/test_gpu_commit.py's stream test (1,500 validators, windows of 12, 1, 5, 12 and
 7 blocks, pinned and pageable signatures, bad signatures before and after the crossing).
-Usage: python tools/r05/bs_stress.py [iterations]"""
+Usage: python tools/stress/bs_stress.py [iterations]"""
 import hashlib
 import os
 import sys

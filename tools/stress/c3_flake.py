@@ -2,7 +2,7 @@
 (test_c3_many_sets_through_the_cache[40-2050-70000]) run several times in ONE process, on fresh
 cache-on and cache-off contexts, counting outcome mismatches against the oracle loops per call.
 One closing session saw a single false "wrong signature" in the first (generic) call; this
-measures how often, and on which path.  Usage: python tools/r05/c3_flake.py [trials]"""
+measures how often, and on which path.  Usage: python tools/stress/c3_flake.py [trials]"""
 import os
 import sys
 import time

@@ -3,7 +3,7 @@ test_c3_many_sets_through_the_cache[40-2050-70000]) through the GENERIC pipeline
 one cache-off context, for each batch size in TMED_PIPE_SIGS-like steps, counting outcome
 mismatches against the oracle loops.  For every mismatch it prints the request, whether its
 Trusting/Light pair was split across two planning parts (16 parts per batch) and what a repeat of
-that request alone returns.  Usage: [C3_JITTER_US=us] [TMED_HOST_THREADS=k] python tools/r05/c3_stress.py [calls_per_size] [sizes...] [cache]"""
+that request alone returns.  Usage: [C3_JITTER_US=us] [TMED_HOST_THREADS=k] python tools/stress/c3_stress.py [calls_per_size] [sizes...] [cache]"""
 import ctypes
 import os
 import sys

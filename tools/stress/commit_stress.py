@@ -1,7 +1,7 @@
 """Diagnostic (round 5): random commit scenarios (tests/commit_cases.py: 1-31 validators, every
 flag, wrong BlockIDs / heights, double votes, bad signatures before and after the crossings, three
 chain IDs, the three loops) through tmed_verify_commits on a cache-off and a cache-on context, for
-many seeds, against the oracle loops.  Usage: python tools/r05/commit_stress.py [seeds]"""
+many seeds, against the oracle loops.  Usage: python tools/stress/commit_stress.py [seeds]"""
 import os
 import sys
 import time

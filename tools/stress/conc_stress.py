@@ -3,7 +3,7 @@ point of one cache-off context from seven threads, device-pointer batches on the
 tests/test_gpu_product_default.py::test_concurrent_callers_cache_on (blocksync windows, single
 commits on sets changing every three calls while the key-cache worker builds, a light client) —
 repeated on fresh contexts, each run checked against the port / the oracle loops as in the tests.
-Usage: python tools/r05/conc_stress.py [rounds]"""
+Usage: python tools/stress/conc_stress.py [rounds]"""
 import os
 import sys
 import time

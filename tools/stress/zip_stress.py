@@ -4,7 +4,7 @@ per call, repeated, every decision compared with the C port's ZIP-215 rule (the 
 once in full, the flipped signatures each call); "go" runs the default rule through the generic
 kernels the same way, "keyed" through the key-cached kernels (1,000 keys), "small" with calls of
 1..4,096 signatures (the latency kernels), generic and keyed alternately.
-Usage: python tools/r05/zip_stress.py [calls] [go|keyed|small]"""
+Usage: python tools/stress/zip_stress.py [calls] [go|keyed|small]"""
 import os
 import sys
 import time
