@@ -240,20 +240,24 @@ def _timed_runs(eng, pb, runs: int):
     phase times of tmed_seam_phase_us as fractions of the median call).  A large call is
     pipelined by the seam: then plan = host plan + staging and replay = host scatter + replay
     (both overlapping device work) and verify = the time the host sat waiting for the device."""
+    from tmed.affinity import cgroup_cpu_stat, cgroup_delta
     from tmed.types import seam_phase_us
     ts, ph = [], []
+    cg0, w0 = cgroup_cpu_stat(), time.perf_counter()
     for _ in range(runs):
         t0 = time.perf_counter()
         pb.run(eng)
         ts.append(time.perf_counter() - t0)
         ph.append(seam_phase_us())
+    cg = cgroup_delta(cg0, cgroup_cpu_stat(), time.perf_counter() - w0)
     ph = np.median(np.array(ph), axis=0)
     med = float(np.median(ts))
     frac = ph / 1e6 / med
     return (med, float(min(ts)), float(max(ts)),
             {"plan_host_ms": round(float(ph[0]) / 1e3, 3), "wait_or_verify_ms": round(float(ph[1]) / 1e3, 3),
              "replay_host_ms": round(float(ph[2]) / 1e3, 3), "plan_frac": round(float(frac[0]), 3),
-             "wait_or_verify_frac": round(float(frac[1]), 3), "replay_frac": round(float(frac[2]), 3)})
+             "wait_or_verify_frac": round(float(frac[1]), 3), "replay_frac": round(float(frac[2]), 3),
+             "host_cgroup": cg})
 
 
 def _c3_corrupt(sets, commits, headers: int, gap: int, every: int):

@@ -159,6 +159,35 @@ def bind_rank(local_rank: int, local_world: int, ndev: int | None = None) -> dic
     return {"bound": True, **_brief(plan), "host_threads_env": os.environ["TMED_HOST_THREADS"]}
 
 
+def cgroup_cpu_stat(path: str = "/sys/fs/cgroup/cpu.stat") -> dict | None:
+    """The cgroup v2 CPU counters of this process's group ({"usage_usec", "nr_periods",
+    "nr_throttled", "throttled_usec", ...} as ints), or None where the file is missing.  A GPU box
+    grants a job CPU bandwidth (cpu.max), not a CPU set: threads may run on any CPU, and once the
+    group has used its quota in a period ALL its threads stop until the next one."""
+    s = _read(path)
+    if s is None:
+        return None
+    out = {}
+    for line in s.splitlines():
+        k, _, v = line.partition(" ")
+        try:
+            out[k] = int(v)
+        except ValueError:
+            pass
+    return out
+
+
+def cgroup_delta(before: dict | None, after: dict | None, wall_s: float) -> dict | None:
+    """What a timed region cost the group: CPUs in use on average, throttled periods and the time
+    the group stood throttled (None without cgroup counters)."""
+    if not before or not after:
+        return None
+    d = {k: after.get(k, 0) - before.get(k, 0) for k in ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec")}
+    return {"cpus_used": round(d["usage_usec"] / 1e6 / wall_s, 2) if wall_s > 0 else None,
+            "periods": d["nr_periods"], "throttled_periods": d["nr_throttled"],
+            "throttled_ms": round(d["throttled_usec"] / 1e3, 3)}
+
+
 def _brief(plan: dict) -> dict:
     c = plan["cpus"]
     return {"gpu_bdf": plan["gpu_bdf"], "numa_node": plan["numa_node"], "cpus": len(c),

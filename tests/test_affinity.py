@@ -113,3 +113,17 @@ def test_dist_setup_binds_before_any_device_call(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "1")
     launch.dist_setup()
     assert calls[0] == "bind_rank" and "device_count" not in calls
+
+
+def test_cgroup_cpu_counters(tmp_path):
+    """cpu.stat deltas over a timed region: CPUs in use, throttled periods and time; None without
+    the file (a host outside a cgroup v2 CPU controller)."""
+    f = tmp_path / "cpu.stat"
+    f.write_text("usage_usec 1000000\nuser_usec 900000\nnr_periods 10\nnr_throttled 1\nthrottled_usec 5000\n")
+    a = A.cgroup_cpu_stat(str(f))
+    assert a["usage_usec"] == 1000000 and a["nr_throttled"] == 1
+    f.write_text("usage_usec 9000000\nuser_usec 8000000\nnr_periods 15\nnr_throttled 4\nthrottled_usec 20000\n")
+    d = A.cgroup_delta(a, A.cgroup_cpu_stat(str(f)), 0.5)
+    assert d == {"cpus_used": 16.0, "periods": 5, "throttled_periods": 3, "throttled_ms": 15.0}
+    assert A.cgroup_cpu_stat(str(tmp_path / "missing")) is None
+    assert A.cgroup_delta(None, a, 1.0) is None
