@@ -242,14 +242,20 @@ def _timed_runs(eng, pb, runs: int):
     (both overlapping device work) and verify = the time the host sat waiting for the device."""
     from tmed.affinity import cgroup_cpu_stat, cgroup_delta
     from tmed.types import seam_phase_us
-    ts, ph = [], []
+    import resource
+    ts, ph, flt = [], [], []
     cg0, w0 = cgroup_cpu_stat(), time.perf_counter()
     for _ in range(runs):
+        f0 = resource.getrusage(resource.RUSAGE_SELF).ru_minflt
         t0 = time.perf_counter()
         pb.run(eng)
         ts.append(time.perf_counter() - t0)
+        flt.append(resource.getrusage(resource.RUSAGE_SELF).ru_minflt - f0)
         ph.append(seam_phase_us())
     cg = cgroup_delta(cg0, cgroup_cpu_stat(), time.perf_counter() - w0)
+    if cg is not None:
+        cg["minor_faults_per_call"] = int(np.median(flt))  # page faults of the whole process
+        cg["call_ms"] = [round(t * 1e3, 2) for t in ts]
     ph = np.median(np.array(ph), axis=0)
     med = float(np.median(ts))
     frac = ph / 1e6 / med
