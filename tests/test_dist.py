@@ -148,7 +148,7 @@ def _light_blocks():
             for mode, vs, pv, chain, bid, h, cm, pc, num, den in scenarios(seed=23, count=60) if mode == T.MODE_LIGHT]
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 8])  # 8: the driver's node (21 blocks: uneven shards of 2 and 3)
 def test_blocksync_aggregation_matches_single_process(world):
     """bench.py's C4 collectives (tmed.dist.aggregate_blocksync): contiguous block ranges per rank,
     ONE int64 all-reduce of (blocks ok, blocks, verified, mismatches), a MAX of the seam (and
