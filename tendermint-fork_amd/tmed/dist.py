@@ -13,6 +13,16 @@ from typing import Sequence
 import numpy as np
 
 
+def _collectives(world: int) -> bool:
+    """Whether the ranks exchange: always at world > 1, and at world 1 when a process group exists
+    (a one-rank RCCL group runs the same collectives, dtypes and devices as an N-rank one:
+    tests/test_gpu_rccl.py)."""
+    if world > 1:
+        return True
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
 def shard(n: int, rank: int, world: int) -> list:
     """Commit indices owned by `rank` (round-robin keeps every rank's load equal for uniform commits)."""
     return list(range(rank, n, world))
@@ -43,7 +53,7 @@ def verify_sharded(engine, requests: Sequence[tuple], rank: int, world: int, dev
     full = torch.full((len(requests),), -1, dtype=torch.int32, device=dev)
     if mine:
         full[torch.tensor(mine, device=dev)] = torch.from_numpy(codes.astype(np.int32)).to(dev)
-    if world > 1:
+    if _collectives(world):
         dist.all_reduce(tally)
         gathered = [torch.empty_like(full) for _ in range(world)]
         dist.all_gather(gathered, full)
@@ -93,7 +103,7 @@ def verify_commit_sliced(engine, request: tuple, rank: int, world: int, device=N
             if bad.size:
                 first = lo + int(bad[0])
         f = torch.tensor([first], dtype=torch.int64, device=dev)
-        if world > 1:
+        if _collectives(world):
             dist.all_reduce(f, op=dist.ReduceOp.MIN)
         f = int(f.item())
         out = np.ones(m, np.uint8)
@@ -132,7 +142,7 @@ def aggregate_blocksync(ok_bits: np.ndarray, blocks: int, rank: int, world: int,
     bits = torch.from_numpy(np.packbits(np.pad(ok_bits.astype(np.uint8), (0, per - (hi - lo))))).to(dev)
     ph = torch.tensor([float(x) for x in phases] + [float(seconds)], dtype=torch.float64, device=dev)
     pr = torch.tensor([float(x) for x in per_rank] + [float(rank)], dtype=torch.float64, device=dev)
-    if world > 1:
+    if _collectives(world):
         dist.all_reduce(tally)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         gb = [torch.empty_like(bits) for _ in range(world)]
