@@ -974,9 +974,24 @@ static int bs_window(tmed_ctx *ctx, const tmed_blocksync_window *w, uint32_t bat
 // dropped (bs_abort), so no queued batch still reads the caller's buffers, and its windows' callers
 // get the error from tmed_blocksync_wait; an idle stream is left alone, so the failure of one
 // synchronous call is not reported to a later, unrelated window.
+// The calling thread is bound to the context's device for the call and given its own device back
+// on return: a cgo call may run on any OS thread (goroutines migrate), and the _multi entry points
+// call in from fresh threads (device 0).
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(const tmed_ctx *ctx) {
+    if (ctx && hipGetDevice(&prev) == hipSuccess && prev != ctx->device) (void)hipSetDevice(ctx->device);
+    else prev = -1;
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 template <class F>
 static int c_guard(tmed_ctx *ctx, F &&f) {
   int rc;
+  DeviceScope dev(ctx);
   try {
     return f();
   } catch (const std::bad_alloc &) {
